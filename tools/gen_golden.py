@@ -1,0 +1,162 @@
+#!/usr/bin/env python3 -B
+"""Generate golden vectors by running the REFERENCE implementation on CPU.
+
+Runs only in the build container, where /root/reference exists; exits 0 with a
+message elsewhere.  Must be run with ``python3 -B`` (importing the reference
+would otherwise write __pycache__ into the read-only tree).  Two modules the
+reference imports but never calls on this path are stubbed: ``cv2``
+(lib/utils/transforms.py:11; only get_affine_transform uses it and the 2x3
+matrix is supplied here) and nothing else -- the layers are built from a plain
+attribute-dict cfg, so lib/core/config.py (easydict) is not imported.
+
+Outputs: tests/golden/*.npz (inputs that cannot be regenerated bit-exactly
+elsewhere are stored; uniform-random inputs are regenerated from torch seeds).
+
+    python3 -B tools/gen_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
+
+STRIDE_SUB = 31  # sampled-voxel stride for large outputs
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    sys.path.insert(0, os.path.join(REF, "lib"))
+    import models.project_whole as pw  # noqa: E402
+    import models.project_individual as pi  # noqa: E402
+    import core.proposal as prop  # noqa: E402
+    import utils.cameras as ucam  # noqa: E402
+    return pw, pi, prop, ucam
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("gen_golden: /root/reference absent; nothing to do")
+        return 0
+    import torch
+    from fvp import geometry, synthetic
+    from fvp.workloads import WORKLOADS
+    from fvp.config import make_cfg
+
+    pw, pi, prop, ucam = import_reference()
+    torch.set_num_threads(8)
+
+    def whole_case(name, wname, batch, uniform_batch=0, full=False):
+        w = WORKLOADS[wname]
+        cfg = make_cfg(w, device="cpu")
+        cams, seq = w.cameras()
+        trans = geometry.resize_transform(w.ori_image_size, w.image_size)
+        rt = torch.as_tensor(trans, dtype=torch.float)
+        layer = pw.ProjectLayer(cfg)
+        hm = synthetic.gaussian_heatmaps(w, batch)
+        cube = layer(torch.from_numpy(hm), {"seq": [seq] * batch}, cams, rt)
+        X, Y, Z = w.voxels_per_axis
+        N = X * Y * Z
+        sg = layer.sample_grid[seq][:, 0].numpy()  # [V,N,2]
+        sub = np.arange(0, N, STRIDE_SUB)
+        d = {
+            "trans": trans, "resize_f32": rt.numpy(),
+            "grid_ref": layer.grid.numpy()[sub], "sub": sub,
+            "sample_grid_sub": sg[:, sub], "sample_grid_sum": sg.astype(np.float64).sum(axis=(1, 2)),
+            "heatmaps": hm,
+            "cube_sub": cube.numpy().reshape(batch, w.num_joints, N)[:, :, sub],
+            "cube_sum": cube.numpy().astype(np.float64).sum(axis=(2, 3, 4)),
+            "xy": torch.max(cube, dim=4)[0].numpy(),
+        }
+        if full:
+            d["cube"] = cube.numpy()
+            d["sample_grid"] = sg
+        # proposals: NMS on the root-joint xy plane as a stand-in for CenterNet's map
+        root = 2 if w.num_joints > 2 else 0
+        prob = torch.max(cube, dim=4)[0][:, root:root + 1].contiguous()
+        vals, idx2, flat = prop.nms2D(prob, w.max_people)
+        d.update(nms_vals=vals.numpy(), nms_xy=idx2.numpy(), nms_flat=flat.numpy())
+        # column gather exactly as human_detection_net.py:199-200
+        B, J = batch, w.num_joints
+        f1d = torch.gather(torch.flatten(cube, 2, 3).permute(0, 2, 1, 3), dim=1,
+                           index=flat.view(B, -1, 1, 1).repeat(1, 1, J, cube.shape[4]))
+        d["columns"] = f1d.numpy()
+        if uniform_batch:
+            layer_u = pw.ProjectLayer(cfg)
+            hu = synthetic.uniform_heatmaps(w, uniform_batch, seed=0)
+            cu = layer_u(hu, {"seq": [seq] * uniform_batch}, cams, rt)
+            d["u_cube_sub"] = cu.numpy().reshape(uniform_batch, J, N)[:, :, sub]
+            d["u_xy"] = torch.max(cu, dim=4)[0].numpy()
+            d["u_cube_sum"] = cu.numpy().astype(np.float64).sum(axis=(2, 3, 4))
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **d)
+        print("wrote", name, {k: v.shape for k, v in d.items()})
+
+    whole_case("whole_c1", "c1", batch=2, uniform_batch=1, full=True)
+    whole_case("whole_c2", "c2", batch=1, uniform_batch=1)
+    whole_case("whole_c3", "c3", batch=2)
+    whole_case("whole_shelf_native", "shelf_native", batch=1)
+
+    # ---- NMS / top-K on tie-free random maps, incl. the non-square divisor quirk
+    g = torch.Generator().manual_seed(7)
+    d = {}
+    for tag, shape, K in (("sq", (4, 1, 80, 80), 10), ("nonsq", (2, 1, 8, 6), 5), ("big", (2, 1, 128, 128), 10)):
+        p = torch.rand(shape, generator=g)
+        v, i2, fl = prop.nms2D(p, K)
+        d.update({f"{tag}_prob": p.numpy(), f"{tag}_vals": v.numpy(), f"{tag}_xy": i2.numpy(), f"{tag}_flat": fl.numpy()})
+    np.savez_compressed(os.path.join(OUT, "nms.npz"), **d)
+    print("wrote nms")
+
+    # ---- cameras.project_pose on a known point set (A2) incl. distortion
+    w = WORKLOADS["c3"]
+    cams, seq = w.cameras()
+    pts = torch.tensor(synthetic.skeletons(w, 0, 4).reshape(-1, 3), dtype=torch.float)
+    proj = np.stack([ucam.project_pose(pts, c).numpy() for c in cams[seq]])
+    np.savez_compressed(os.path.join(OUT, "project_pose.npz"), pts=pts.numpy(), proj=proj)
+    print("wrote project_pose")
+
+    # ---- per-person layer (JLN), demo cameras, J=5 heatmap channels
+    w = WORKLOADS["c3"]
+    cfg = make_cfg(w, device="cpu")
+    cams, seq = w.cameras()
+    trans = geometry.resize_transform(w.ori_image_size, w.image_size)
+    rt = torch.as_tensor(trans, dtype=torch.float)
+    layer = pi.ProjectLayer(cfg)
+    hm = synthetic.gaussian_heatmaps(w, 1)[:, :, :5].copy()
+    props = synthetic.proposals_for_frame(w, 0, 4)
+    extra = np.array([
+        [3900.0, 300.0, 900.0, 0, 0.9, 0.45, 0.55],    # clipped at +x end
+        [-3900.0, -4200.0, 900.0, 0, 0.9, 1.2, 0.3],   # clipped at -x/-y start, negative bbox margin
+        [4500.0, 0.0, 900.0, 0, 0.9, 0.45, 0.55],      # start >= end -> skipped (zeros)
+    ], dtype=np.float32)
+    props = np.concatenate([props, extra], axis=0)
+    cubes, offset = layer(torch.from_numpy(hm), 0, {"seq": [seq]}, torch.from_numpy(props), cams, rt)
+    planes = torch.cat([torch.max(cubes, dim=4)[0], torch.max(cubes, dim=3)[0], torch.max(cubes, dim=2)[0]])
+    fsg = layer.sample_grid[seq].numpy()  # [V,FX,FY,FZ,2]
+    fine_n = fsg.shape[1] * fsg.shape[2] * fsg.shape[3]
+    sub = np.arange(0, fine_n, 997)
+    d = {
+        "heatmaps": hm, "proposals": props, "resize_f32": rt.numpy(),
+        "planes": planes.numpy(), "offset": offset.numpy(),
+        "cube_sum": cubes.numpy().astype(np.float64).sum(axis=(2, 3, 4)),
+        "cube0_sub": cubes[0].numpy().reshape(5, -1)[:, ::53],
+        "fine": layer.fine_voxels_per_axis.numpy(), "scale": layer.scale.numpy(), "bias": layer.bias.numpy(),
+        "center_grid": layer.center_grid.numpy(),
+        "fine_grid_sub": layer.fine_grid.numpy()[sub], "fine_sub": sub,
+        "fine_sample_grid_sub": fsg.reshape(fsg.shape[0], -1, 2)[:, sub],
+        "fine_sample_grid_sum": fsg.astype(np.float64).sum(axis=(1, 2, 3, 4)),
+    }
+    np.savez_compressed(os.path.join(OUT, "individual_c3.npz"), **d)
+    print("wrote individual_c3", {k: v.shape for k, v in d.items()})
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Voxelize+project throughput benchmark (BASELINE.json metric).
+
+One step = the hot path over one batch of B synthetic frames per GPU, inputs
+resident in HBM:
+  fvp_voxelize (cube [B,J,X,Y,Z] + xy max-plane, one launch)
+  -> fvp_nms_topk on the root-joint xy plane (stand-in for CenterNet's map;
+     the dense CNN is out of scope) -> fvp_gather_columns [B,K,J,Z]
+  -> (N > 1) one RCCL all_gather of the compact proposals.
+Frames are sharded across ranks (weak scaling).  Default workload: C2 =
+BASELINE configs[1] (Shelf calibration, 5 cams, J=15, 128x240 -> 80x80x20).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
+
+METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VOX_KERNEL = "voxelize_kernel"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
+                    help="collect FETCH_SIZE/WRITE_SIZE with rocprofv3 child runs (N=1, rank 0)")
+    ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+def collect_traffic(args):
+    """Run this benchmark twice under rocprofv3 (one counter pass each, as
+    MI355X_MICROARCH.md prescribes) BEFORE this process touches the GPU, and
+    return per-launch HBM bytes of the voxelize kernel."""
+    res = {}
+    out_root = os.path.join(REPO, "gpurun_out", "bench_pmc")
+    os.makedirs(out_root, exist_ok=True)
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=out_root)
+        cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--child", "--steps", "3", "--warmup", "1",
+               "--batch", str(args.batch), "--workload", args.workload, "--traffic", "off", "--cpu-baseline", "off"]
+        try:
+            subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           cwd=REPO)
+        except Exception as e:  # profiler unavailable or failed: report null, never fake
+            return None, f"rocprofv3 {counter} failed: {e}"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        vals = []
+        for f in files:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if VOX_KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None, f"no {counter} rows for {VOX_KERNEL}"
+        res[counter] = sum(vals) / len(vals)
+    # rocprofv3 reports KB; gfx950 FETCH_SIZE counts half of a wide streaming
+    # read (MI355X_MICROARCH.md §HBM) -> the guide's correction doubles it.
+    fetch = res["FETCH_SIZE"] * 1024.0
+    write = res["WRITE_SIZE"] * 1024.0
+    return {"fetch_raw": fetch, "write": write, "corrected": 2.0 * fetch + write}, None
+
+
+def cpu_baseline(w, sample_grid_cpu, seconds):
+    """Reference op sequence on the host cores (oracle/torch_cpu.py), bounded."""
+    import torch
+    from fvp import synthetic
+    from oracle import torch_cpu
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    frames = 4
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, frames, first_frame=10_000))
+    torch_cpu.hot_path(hm, sample_grid_cpu, w.voxels_per_axis, w.max_people)  # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        torch_cpu.hot_path(hm, sample_grid_cpu, w.voxels_per_axis, w.max_people)
+        done += frames
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{done} frames of {w.name} in {el:.1f} s: torch-CPU restatement of project_whole.forward "
+                      f"(per-frame F.grid_sample, mean, clamp) + max(dim=4) + nms2D + column gather "
+                      f"(oracle/torch_cpu.py), sample grid prebuilt"}
+
+
+# ---------------------------------------------------------------------------
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    traffic, traffic_note = None, None
+    if args.traffic == "auto" and world == 1 and not args.child:
+        traffic, traffic_note = collect_traffic(args)  # before any GPU use in this process
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from fvp import geometry, synthetic
+    from fvp.project_whole import ProjectLayer
+    from fvp.proposal import nms2D, gather_columns
+    from fvp.workloads import WORKLOADS
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    w = WORKLOADS[args.workload]
+    B = args.batch
+    cams, seq = w.cameras()
+    V = len(cams[seq])
+    J = w.num_joints
+    X, Y, Z = w.voxels_per_axis
+    Wd, Hd = w.heatmap_size
+    K = w.max_people
+    root = 2 if J > 2 else 0
+
+    layer = ProjectLayer(w.cfg(str(dev)))
+    layer.verbose = False
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
+    hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=rank * B)
+    hm = torch.from_numpy(hm_host).to(dev)
+    del hm_host
+    meta = {"seq": [seq] * B}
+
+    # once-per-sequence cache build, timed separately (excluded from the step)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    layer._grids_for_batch(hm, meta, cams, rt)
+    torch.cuda.synchronize()
+    cache_ms = (time.perf_counter() - t0) * 1e3
+
+    stream = torch.cuda.current_stream(dev)
+    ev = []
+
+    def step(record):
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        cube, xy = layer.forward_fused(hm, meta, cams, rt, want_cube=True, want_xy=True)
+        if record:
+            e1.record(stream)
+            ev.append((e0, e1))
+        vals, idx, flat = nms2D(xy[:, root:root + 1], K)
+        cols = gather_columns(cube, flat)
+        if world > 1:
+            local = torch.cat([flat, vals.view(torch.int32).to(torch.int64)], dim=1)
+            out = torch.empty((world * B, 2 * K), dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(out, local)
+        return cols
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if args.child:
+        return
+
+    vox_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    frames = world * B * args.steps
+    fps = frames / el
+    per_frame = V * J * Hd * Wd * 4 + J * X * Y * Z * 4 + J * X * Y * 4
+    alg_bytes = B * per_frame
+    achieved = alg_bytes / (vox_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline == "on":
+        sg_cpu = layer.sample_grid[seq].cpu()
+        cpu = cpu_baseline(w, sg_cpu, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(fps, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{w.name}: BASELINE configs[1] Shelf jln64 geometry, {V} cams, J={J}, "
+                            f"{Hd}x{Wd} heatmaps -> {X}x{Y}x{Z} voxels, K={K} proposals",
+                "frames_per_gpu_step": B,
+                "global_batch": world * B,
+                "parallelism": f"frame-sharded x{world}" + (" + RCCL all_gather of proposals" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": VOX_KERNEL,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else round(traffic["corrected"]),
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "kernel_ms": round(vox_ms, 4),
+            },
+            "cpu_baseline": cpu,
+            "cache_build_ms": round(cache_ms, 2),
+        }
+        if traffic is not None:
+            line["roofline"]["traffic_detail"] = {k: round(v, 1) for k, v in traffic.items()}
+        elif traffic_note:
+            line["roofline"]["traffic_note"] = traffic_note
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,170 @@
+// Proposal selection on the 2-D detection map and the per-proposal gathers
+// (A9, A10 of SURVEY.md §8(a)).
+//
+// nms_topk: one 256-thread block per frame.  The 3x3/stride-1/pad-1 max-pool
+// keep mask (proposal.py:34-52) is evaluated once into LDS, then K rounds of
+// a block-wide arg-max (value descending, flat index ascending -- a total
+// order, so the result is deterministic) pick the top-K (proposal.py:73).
+// Indices decode as get_index2D does, dividing by shape[1] == X
+// (proposal.py:27-29,75).
+#include "fvp_device.h"
+
+namespace fvp {
+
+struct Cand {
+    float v;
+    int i;
+};
+
+// a precedes b: larger value first, then smaller index.  NaN sorts first, as
+// torch.topk treats NaN as the largest value.
+__device__ __forceinline__ bool before(const Cand &a, const Cand &b) {
+    const bool an = a.v != a.v, bn = b.v != b.v;
+    if (an != bn) return an;
+    if (!an && a.v != b.v) return a.v > b.v;
+    return a.i < b.i;
+}
+
+__device__ __forceinline__ Cand wave_best(Cand c) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        Cand o;
+        o.v = __shfl_xor(c.v, off);
+        o.i = __shfl_xor(c.i, off);
+        if (before(o, c)) c = o;
+    }
+    return c;
+}
+
+constexpr int kNmsThreads = 256;
+
+__global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__restrict__ prob, int X, int Y, int K,
+                                                               float *__restrict__ vals, int64_t *__restrict__ flat,
+                                                               int64_t *__restrict__ xy) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int M = X * Y;
+    float *nmsv = reinterpret_cast<float *>(smem);                           // [M]
+    unsigned *taken = reinterpret_cast<unsigned *>(smem + (size_t)M * 4);    // [ceil(M/32)]
+    __shared__ Cand red[kNmsThreads / kWave];
+    __shared__ Cand winner;
+    const int b = blockIdx.x;
+    const float *__restrict__ p = prob + (size_t)b * M;
+    const int tid = threadIdx.x;
+
+    for (int e = tid; e < M; e += kNmsThreads) {
+        const int ex = e / Y, ey = e - (e / Y) * Y;
+        const float c = p[e];
+        float m = -INFINITY;
+        bool nan = false;
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = ex + dx;
+            if (xx < 0 || xx >= X) continue;
+            for (int dy = -1; dy <= 1; ++dy) {
+                const int yy = ey + dy;
+                if (yy < 0 || yy >= Y) continue;
+                const float q = p[xx * Y + yy];
+                nan |= (q != q);
+                m = fmaxf(m, q);
+            }
+        }
+        // max_pool2d propagates NaN; (c == NaN) is false -> keep = 0 -> 0*c.
+        const float keep = (!nan && c == m) ? 1.0f : 0.0f;
+        nmsv[e] = keep * c;
+    }
+    for (int w = tid; w < (M + 31) / 32; w += kNmsThreads) taken[w] = 0u;
+    __syncthreads();
+
+    for (int k = 0; k < K; ++k) {
+        Cand best{-INFINITY, 0x7fffffff};
+        bool have = false;
+        for (int e = tid; e < M; e += kNmsThreads) {
+            if (taken[e >> 5] & (1u << (e & 31))) continue;
+            const Cand c{nmsv[e], e};
+            if (!have || before(c, best)) {
+                best = c;
+                have = true;
+            }
+        }
+        if (!have) best = Cand{-INFINITY, 0x7fffffff};
+        best = wave_best(best);
+        if ((tid & 63) == 0) red[tid >> 6] = best;
+        __syncthreads();
+        if (tid == 0) {
+            Cand w = red[0];
+            for (int i = 1; i < kNmsThreads / kWave; ++i)
+                if (before(red[i], w)) w = red[i];
+            winner = w;
+            if (w.i < M) taken[w.i >> 5] |= (1u << (w.i & 31));
+            vals[(size_t)b * K + k] = w.v;
+            flat[(size_t)b * K + k] = w.i;
+            if (xy) {
+                xy[((size_t)b * K + k) * 2 + 0] = (int64_t)(w.i / X);
+                xy[((size_t)b * K + k) * 2 + 1] = (int64_t)(w.i % X);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// columns[b,k,j,z] = cube[b,j,flat[b,k],z]; one thread per output element,
+// z fastest so reads and writes are contiguous runs of Z floats.
+__global__ __launch_bounds__(256) void gather_columns_kernel(const float *__restrict__ cube,
+                                                             const int64_t *__restrict__ flat,
+                                                             float *__restrict__ out, int J, int XY, int Z, int K,
+                                                             long long total) {
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= total) return;
+    const int z = (int)(gid % Z);
+    long long r = gid / Z;
+    const int j = (int)(r % J);
+    r /= J;
+    const int k = (int)(r % K);
+    const long long b = r / K;
+    const int64_t f = flat[b * K + k];
+    out[gid] = cube[((b * J + j) * XY + f) * Z + z];
+}
+
+__global__ __launch_bounds__(256) void gather_bbox_kernel(const float *__restrict__ size,
+                                                          const int64_t *__restrict__ flat, float *__restrict__ out,
+                                                          int XY, int K, long long total) {
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= total) return;
+    const int c = (int)(gid & 1);
+    const long long bk = gid >> 1;
+    const long long b = bk / K;
+    out[gid] = size[(b * 2 + c) * XY + flat[bk]];
+}
+
+}  // namespace fvp
+
+extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, int K, float *vals, int64_t *flat, int64_t *xy,
+                            void *stream) {
+    if (!prob || !vals || !flat) return FVP_ERR_NULL;
+    if (B <= 0 || X <= 0 || Y <= 0 || K <= 0 || K > X * Y) return FVP_ERR_SHAPE;
+    const size_t M = (size_t)X * Y;
+    const size_t lds = M * 4 + ((M + 31) / 32) * 4;
+    if (lds > 150 * 1024) return FVP_ERR_SHAPE;
+    hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob, X, Y, K,
+                       vals, flat, xy);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z, const int64_t *flat, int K,
+                                  float *columns, void *stream) {
+    if (!cube || !flat || !columns) return FVP_ERR_NULL;
+    if (B <= 0 || J <= 0 || X <= 0 || Y <= 0 || Z <= 0 || K <= 0) return FVP_ERR_SHAPE;
+    const long long total = (long long)B * K * J * Z;
+    hipLaunchKernelGGL(fvp::gather_columns_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, cube, flat, columns, J, X * Y, Z, K, total);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_gather_bbox(const float *size, int B, int X, int Y, const int64_t *flat, int K, float *out,
+                               void *stream) {
+    if (!size || !flat || !out) return FVP_ERR_NULL;
+    if (B <= 0 || X <= 0 || Y <= 0 || K <= 0) return FVP_ERR_SHAPE;
+    const long long total = (long long)B * K * 2;
+    hipLaunchKernelGGL(fvp::gather_bbox_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, size, flat, out, X * Y, K, total);
+    return (int)hipGetLastError();
+}

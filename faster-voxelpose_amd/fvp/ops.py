@@ -1,0 +1,196 @@
+"""torch.ops.fvp.* custom ops over the C ABI (include/fvp.h).
+
+Each op allocates its outputs on the input's device and launches on the
+current HIP stream; nothing synchronises.  Only a device ("cuda" = HIP on
+ROCm) implementation is registered: a CPU tensor raises, there is no CPU
+fallback.  The ops are forward-only -- the reference's projection layers have
+no parameters and no gradient flows through them -- so an
+input that requires grad under grad mode is rejected instead of being
+silently detached.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import GridSpec, ImageSpec, PersonSpec
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _f3(v):
+    return (ctypes.c_float * 3)(*[float(x) for x in v])
+
+
+def _i3(v):
+    return (ctypes.c_int32 * 3)(*[int(x) for x in v])
+
+
+def _stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dev_f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: {name} must be on a HIP device, got {t.device}")
+    if torch.is_grad_enabled() and t.requires_grad:
+        raise _lib.FvpError(f"fvp: {name} requires grad; the projection path is forward-only")
+    return t.to(torch.float32).contiguous() if t.dtype != torch.float32 else t.contiguous()
+
+
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("fvp::project_grid", mutates_args=(), device_types="cuda")
+def project_grid(cams: torch.Tensor, resize_t: torch.Tensor, start: list[float], end: list[float],
+                 center: list[float], bins: list[int], ori_max: float, img_w: float, img_h: float,
+                 hm_w: int, hm_h: int) -> torch.Tensor:
+    cams = _dev_f32(cams, "cams")
+    resize_t = _dev_f32(resize_t, "resize_transform")
+    V = cams.shape[0]
+    N = bins[0] * bins[1] * bins[2]
+    out = torch.empty((V, N, 2), dtype=torch.float32, device=cams.device)
+    g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
+    im = ImageSpec(ori_max, img_w, img_h, hm_w, hm_h)
+    _lib.call("fvp_project_grid", _ptr(cams), V, _ptr(resize_t), g, im, _ptr(out), _stream(cams))
+    return out
+
+
+@project_grid.register_fake
+def _(cams, resize_t, start, end, center, bins, ori_max, img_w, img_h, hm_w, hm_h):
+    return cams.new_empty((cams.shape[0], bins[0] * bins[1] * bins[2], 2))
+
+
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("fvp::voxelize", mutates_args=(), device_types="cuda")
+def voxelize(heatmaps: torch.Tensor, sample_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
+             X: int, Y: int, Z: int, want_cube: bool, want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    hm = _dev_f32(heatmaps, "heatmaps")
+    sg = _dev_f32(sample_grids, "sample_grids")
+    B, V, J, H, W = hm.shape
+    N = X * Y * Z
+    if sg.dim() == 3:
+        sg = sg.unsqueeze(0)
+    if sg.shape[1:] != (V, N, 2):
+        raise _lib.FvpError(f"fvp: sample grid {tuple(sg.shape)} does not match V={V}, N={N}")
+    gi = None
+    if grid_index is not None:
+        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
+        if gi.numel() != B:
+            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
+    xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
+    _lib.call("fvp_voxelize", _ptr(hm), B, V, J, H, W, _ptr(sg), _ptr(gi), X, Y, Z,
+              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _stream(hm))
+    return cube, xy
+
+
+@voxelize.register_fake
+def _(heatmaps, sample_grids, grid_index, X, Y, Z, want_cube, want_xy):
+    B, V, J = heatmaps.shape[:3]
+    return (heatmaps.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
+            heatmaps.new_empty((B, J, X, Y) if want_xy else (0,)))
+
+
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("fvp::nms_topk", mutates_args=(), device_types="cuda")
+def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    p = _dev_f32(prob, "prob_map")
+    B, X, Y = p.shape[0], p.shape[-2], p.shape[-1]
+    if p.numel() != B * X * Y:
+        raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map")
+    vals = torch.empty((B, K), dtype=torch.float32, device=p.device)
+    flat = torch.empty((B, K), dtype=torch.int64, device=p.device)
+    xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
+    _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
+    return vals, xy, flat
+
+
+@nms_topk.register_fake
+def _(prob, K):
+    B = prob.shape[0]
+    return (prob.new_empty((B, K)), prob.new_empty((B, K, 2), dtype=torch.int64),
+            prob.new_empty((B, K), dtype=torch.int64))
+
+
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("fvp::gather_columns", mutates_args=(), device_types="cuda")
+def gather_columns(cube: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
+    c = _dev_f32(cube, "feature_cubes")
+    B, J, X, Y, Z = c.shape
+    f = flat.to(device=c.device, dtype=torch.int64).contiguous()
+    K = f.shape[1]
+    out = torch.empty((B, K, J, Z), dtype=torch.float32, device=c.device)
+    _lib.call("fvp_gather_columns", _ptr(c), B, J, X, Y, Z, _ptr(f), K, _ptr(out), _stream(c))
+    return out
+
+
+@gather_columns.register_fake
+def _(cube, flat):
+    B, J, X, Y, Z = cube.shape
+    return cube.new_empty((B, flat.shape[1], J, Z))
+
+
+@torch.library.custom_op("fvp::gather_bbox", mutates_args=(), device_types="cuda")
+def gather_bbox(size: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
+    s = _dev_f32(size, "bbox_preds")
+    B, _, X, Y = s.shape
+    f = flat.to(device=s.device, dtype=torch.int64).contiguous()
+    K = f.shape[1]
+    out = torch.empty((B, K, 2), dtype=torch.float32, device=s.device)
+    _lib.call("fvp_gather_bbox", _ptr(s), B, X, Y, _ptr(f), K, _ptr(out), _stream(s))
+    return out
+
+
+@gather_bbox.register_fake
+def _(size, flat):
+    return size.new_empty((size.shape[0], flat.shape[1], 2))
+
+
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("fvp::person_cubes", mutates_args=(), device_types="cuda")
+def person_cubes(heatmaps_frame: torch.Tensor, fine_grid: torch.Tensor, proposals: torch.Tensor,
+                 fine: list[int], scale: list[float], bias: list[float], whole_size: list[float],
+                 ind_size: list[float], bins: list[int]) -> tuple[torch.Tensor, torch.Tensor]:
+    hm = _dev_f32(heatmaps_frame, "heatmaps")
+    fg = _dev_f32(fine_grid, "fine sample grid")
+    pc = _dev_f32(proposals, "proposal_centers")
+    V, J, H, W = hm.shape
+    P = pc.shape[0]
+    if fg.numel() != V * fine[0] * fine[1] * fine[2] * 2:
+        raise _lib.FvpError("fvp: fine sample grid does not match fine_voxels_per_axis")
+    cubes = torch.empty((P, J, bins[0], bins[1], bins[2]), dtype=torch.float32, device=hm.device)
+    offset = torch.empty((P, 3), dtype=torch.float32, device=hm.device)
+    if P > 0:
+        spec = PersonSpec(_i3(fine), _f3(scale), _f3(bias), _f3(whole_size), _f3(ind_size), _i3(bins))
+        _lib.call("fvp_person_cubes", _ptr(hm), V, J, H, W, _ptr(fg), spec, _ptr(pc), P, _ptr(cubes), _ptr(offset),
+                  _stream(hm))
+    return cubes, offset
+
+
+@person_cubes.register_fake
+def _(heatmaps_frame, fine_grid, proposals, fine, scale, bias, whole_size, ind_size, bins):
+    P = proposals.shape[0]
+    return (heatmaps_frame.new_empty((P, heatmaps_frame.shape[1], bins[0], bins[1], bins[2])),
+            heatmaps_frame.new_empty((P, 3)))
+
+
+@torch.library.custom_op("fvp::max_planes", mutates_args=(), device_types="cuda")
+def max_planes(cubes: torch.Tensor) -> torch.Tensor:
+    c = _dev_f32(cubes, "cubes")
+    P, J, S = c.shape[0], c.shape[1], c.shape[2]
+    if not (c.shape[3] == S and c.shape[4] == S):
+        raise _lib.FvpError("fvp: max planes need cubic person volumes (X == Y == Z)")
+    planes = torch.empty((3 * P, J, S, S), dtype=torch.float32, device=c.device)
+    if P > 0:
+        _lib.call("fvp_max_planes", _ptr(c), P, J, S, _ptr(planes), _stream(c))
+    return planes
+
+
+@max_planes.register_fake
+def _(cubes):
+    P, J, S = cubes.shape[:3]
+    return cubes.new_empty((3 * P, J, S, S))

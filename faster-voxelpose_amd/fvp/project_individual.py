@@ -1,0 +1,107 @@
+"""Drop-in for ``models.project_individual.ProjectLayer``
+(lib/models/project_individual.py).
+
+Same constructor and ``forward(heatmaps, index, meta, proposal_centers,
+cameras, resize_transform) -> (cubes[P,J,64,64,64], offset[P,3])``, same public
+attributes (``center_grid`` is read by JointLocalizationNet's soft-argmax,
+joint_localization_net.py:165; ``fine_voxels_per_axis``, ``scale``, ``bias``,
+``fine_grid``, ``sample_grid``).  The per-sequence fine sample grid is built
+by ``fvp_project_grid`` over the fine whole-space grid; all proposals of the
+frame are voxelised by ONE ``fvp_person_cubes`` launch that evaluates each
+proposal's window on the device (no per-proposal loop, no host syncs --
+project_individual.py:272-275 read ``torch.sum(start >= end)`` back per
+proposal).  ``forward_planes`` additionally returns the xy/xz/yz
+max-projections JointLocalizationNet concatenates (joint_localization_net.py:158-160).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import geometry, ops
+
+
+class ProjectLayer(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.device = torch.device(cfg.DEVICE)
+        self.image_size = cfg.DATASET.IMAGE_SIZE
+        self.heatmap_size = cfg.DATASET.HEATMAP_SIZE
+        self.ori_image_size = cfg.DATASET.ORI_IMAGE_SIZE
+        c = geometry.individual_constants(cfg.CAPTURE_SPEC.SPACE_SIZE, cfg.CAPTURE_SPEC.SPACE_CENTER,
+                                          cfg.INDIVIDUAL_SPEC.SPACE_SIZE, cfg.INDIVIDUAL_SPEC.VOXELS_PER_AXIS)
+        self._const = c
+        dev = self.device
+        self.whole_space_center = torch.from_numpy(c["whole_center"]).to(dev)
+        self.whole_space_size = torch.from_numpy(c["whole_size"]).to(dev)
+        self.ind_space_size = torch.from_numpy(c["ind_size"]).to(dev)
+        self.voxels_per_axis = torch.from_numpy(c["ind_bins"]).to(dev)
+        self.fine_voxels_per_axis = torch.from_numpy(c["fine"]).to(dev)
+        self.scale = torch.from_numpy(c["scale"]).to(dev)
+        self.bias = torch.from_numpy(c["bias"]).to(dev)
+        self.center_grid = self._center_grid().to(dev)  # project_individual.py:101-107
+        self._fine_grid = None
+        self.sample_grid = {}  # seq -> [V, FX, FY, FZ, 2]
+        self.verbose = True
+
+    @staticmethod
+    def _axis(size, centre, n):
+        s = float(size)
+        return torch.linspace(float(np.float32(-s / 2)), float(np.float32(s / 2)), int(n)) + float(centre)
+
+    def _grid3(self, size, centre, bins):
+        axes = [self._axis(size[a], centre[a], bins[a]) for a in range(3)]
+        gx, gy, gz = torch.meshgrid(*axes, indexing="ij")
+        return torch.stack([gx.reshape(-1), gy.reshape(-1), gz.reshape(-1)], dim=1)
+
+    def _center_grid(self):
+        c = self._const
+        b = [int(v) for v in c["ind_bins"]]
+        g = self._grid3(c["ind_size"], c["whole_center"], b).view(b[0], b[1], b[2], 3)
+        return torch.stack([g[:, :, 0, :2].reshape(-1, 2), g[:, 0, :, ::2].reshape(-1, 2),
+                            g[0, :, :, 1:].reshape(-1, 2)])
+
+    @property
+    def fine_grid(self) -> torch.Tensor:
+        """Fine whole-space voxel centres [FX*FY*FZ, 3] (project_individual.py:110).
+        Built lazily: the kernels rebuild centres on the fly and never read it."""
+        if self._fine_grid is None:
+            c = self._const
+            self._fine_grid = self._grid3(c["whole_size"], c["whole_center"], c["fine"]).to(self.device)
+        return self._fine_grid
+
+    def build_sample_grid(self, cameras, seq, resize_transform, device) -> torch.Tensor:
+        """compute_sample_grid (project_individual.py:192-220) on device -> [V,FX,FY,FZ,2]."""
+        c = self._const
+        cams = torch.from_numpy(geometry.pack_cameras(cameras, seq)).to(device)
+        start = [float(np.float32(-float(s) / 2)) for s in c["whole_size"]]
+        end = [float(np.float32(float(s) / 2)) for s in c["whole_size"]]
+        fine = [int(v) for v in c["fine"]]
+        w, h = self.heatmap_size
+        sg = ops.project_grid(cams, resize_transform.to(device=device, dtype=torch.float32), start, end,
+                              [float(v) for v in c["whole_center"]], fine,
+                              float(max(self.ori_image_size[0], self.ori_image_size[1])),
+                              float(self.image_size[0]), float(self.image_size[1]), int(w), int(h))
+        return sg.view(sg.shape[0], fine[0], fine[1], fine[2], 2)
+
+    def _seq_grid(self, heatmaps, index, meta, cameras, resize_transform):
+        curr_seq = meta["seq"][index]
+        if curr_seq not in self.sample_grid:
+            if self.verbose:
+                print("=> save the sampling grid in JLN for sequence", curr_seq)
+            self.sample_grid[curr_seq] = self.build_sample_grid(cameras, curr_seq, resize_transform, heatmaps.device)
+        return self.sample_grid[curr_seq]
+
+    def forward(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
+        grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
+        c = self._const
+        return ops.person_cubes(heatmaps[index], grid, proposal_centers,
+                                [int(v) for v in c["fine"]], [float(v) for v in c["scale"]],
+                                [float(v) for v in c["bias"]], [float(v) for v in c["whole_size"]],
+                                [float(v) for v in c["ind_size"]], [int(v) for v in c["ind_bins"]])
+
+    def forward_planes(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
+        """(planes[3P,J,S,S], offset[P,3]): the JLN input at joint_localization_net.py:158-160."""
+        cubes, offset = self.forward(heatmaps, index, meta, proposal_centers, cameras, resize_transform)
+        return ops.max_planes(cubes), offset

@@ -1,0 +1,99 @@
+"""Drop-in for ``models.project_whole.ProjectLayer`` (lib/models/project_whole.py).
+
+Same constructor ``ProjectLayer(cfg)``, same ``forward(heatmaps, meta,
+cameras, resize_transform) -> cube[B,J,X,Y,Z]``, same public attributes
+(``grid``, ``sample_grid`` cache keyed by sequence, the cfg copies), same two
+assertions (project_whole.py:147-148).  The arithmetic runs in two HIP
+kernels (faster-voxelpose_amd/csrc): ``fvp_project_grid`` builds a sequence's
+sample grid once (project_whole.py:151-156), ``fvp_voxelize`` samples, averages
+over cameras, clamps and (optionally) emits the xy max-plane in the same pass
+for every frame of the batch in one launch -- no Python loop over frames.
+
+Registers no parameters or buffers, so checkpoints load unchanged.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import geometry, ops
+
+
+def _as_list3(v, kind=float):
+    if isinstance(v, (int, float)):
+        return [kind(v)] * 3
+    return [kind(x) for x in v]
+
+
+class ProjectLayer(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.device = torch.device(cfg.DEVICE)
+        self.image_size = cfg.DATASET.IMAGE_SIZE
+        self.heatmap_size = cfg.DATASET.HEATMAP_SIZE
+        self.ori_image_size = cfg.DATASET.ORI_IMAGE_SIZE
+        self.space_size = cfg.CAPTURE_SPEC.SPACE_SIZE
+        self.space_center = cfg.CAPTURE_SPEC.SPACE_CENTER
+        self.voxels_per_axis = cfg.CAPTURE_SPEC.VOXELS_PER_AXIS
+        self._grid = None
+        self.sample_grid = {}  # seq -> [V, 1, N, 2] fp32 (the reference's cache layout)
+        self.verbose = True
+
+    # -- reference attribute: voxel centres [N,3] (compute_grid, :43-79) -------------
+    @property
+    def grid(self) -> torch.Tensor:
+        if self._grid is None:
+            S = _as_list3(self.space_size)
+            C = _as_list3(self.space_center)
+            nb = _as_list3(self.voxels_per_axis, int)
+            axes = [torch.linspace(-S[a] / 2, S[a] / 2, nb[a]) + C[a] for a in range(3)]
+            gx, gy, gz = torch.meshgrid(*axes, indexing="ij")
+            self._grid = torch.stack([gx.reshape(-1), gy.reshape(-1), gz.reshape(-1)], dim=1).to(self.device)
+        return self._grid
+
+    def grid_spec(self):
+        S = _as_list3(self.space_size)
+        C = _as_list3(self.space_center)
+        nb = _as_list3(self.voxels_per_axis, int)
+        start = [float(np.float32(-s / 2)) for s in S]
+        end = [float(np.float32(s / 2)) for s in S]
+        return start, end, [float(np.float32(c)) for c in C], nb
+
+    def build_sample_grid(self, cameras, seq, resize_transform, device) -> torch.Tensor:
+        """project_grid x V for one sequence (project_whole.py:81-117,151-156) on device."""
+        cams = torch.from_numpy(geometry.pack_cameras(cameras, seq)).to(device)
+        start, end, center, nb = self.grid_spec()
+        w, h = self.heatmap_size
+        sg = ops.project_grid(cams, resize_transform.to(device=device, dtype=torch.float32), start, end, center, nb,
+                              float(max(self.ori_image_size[0], self.ori_image_size[1])),
+                              float(self.image_size[0]), float(self.image_size[1]), int(w), int(h))
+        return sg.view(sg.shape[0], 1, sg.shape[1], 2)
+
+    def _grids_for_batch(self, heatmaps, meta, cameras, resize_transform):
+        device = heatmaps.device
+        n = heatmaps.shape[1]
+        seqs = list(meta["seq"])[: heatmaps.shape[0]]
+        for curr_seq in seqs:
+            assert curr_seq in cameras.keys(), "missing camera parameters for the current sequence"
+            assert len(cameras[curr_seq]) == n, "inconsistent number of cameras"
+            if curr_seq not in self.sample_grid:
+                if self.verbose:
+                    print("=> save the sampling grid in HDN for sequence", curr_seq)
+                self.sample_grid[curr_seq] = self.build_sample_grid(cameras, curr_seq, resize_transform, device)
+        uniq = list(dict.fromkeys(seqs))
+        if len(uniq) == 1:
+            return self.sample_grid[uniq[0]][:, 0].unsqueeze(0), None
+        grids = torch.stack([self.sample_grid[s][:, 0] for s in uniq])
+        index = torch.tensor([uniq.index(s) for s in seqs], dtype=torch.int32).to(device, non_blocking=True)
+        return grids, index
+
+    def forward_fused(self, heatmaps, meta, cameras, resize_transform, want_cube=True, want_xy=True):
+        """One launch for the whole batch: (cube[B,J,X,Y,Z] or empty, xy[B,J,X,Y] or empty)."""
+        grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
+        X, Y, Z = _as_list3(self.voxels_per_axis, int)
+        return ops.voxelize(heatmaps, grids, index, X, Y, Z, want_cube, want_xy)
+
+    def forward(self, heatmaps, meta, cameras, resize_transform):
+        cube, _ = self.forward_fused(heatmaps, meta, cameras, resize_transform, want_cube=True, want_xy=False)
+        return cube

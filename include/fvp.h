@@ -1,0 +1,134 @@
+/*
+ * fvp.h -- C ABI of the MI355X-native Faster-VoxelPose voxel-projection path.
+ *
+ * One shared library (libfvp.so, built from faster-voxelpose_amd/csrc) exports
+ * these entry points.  They are plain C: device pointers, sizes and a HIP
+ * stream handle (hipStream_t passed as void*).  Every call is asynchronous on
+ * that stream, allocates nothing, never synchronises, and returns a status
+ * (0 = success, otherwise a hipError_t value; FVP_ERR_* for argument errors).
+ *
+ * The reference has no FFI: its boundary is Python nn.Module classes reached
+ * by module path.  Each entry point below names the
+ * reference code it replaces (paths relative to the reference repo).  The
+ * Python mirror of the reference interface (faster-voxelpose_amd/fvp) binds
+ * these with ctypes and registers them as torch.ops.fvp.* custom ops.
+ *
+ * Layouts (all row-major, fp32 unless noted):
+ *   heatmaps      [B][V][J][H][W]      (as handed to ProjectLayer.forward)
+ *   cams          [V][FVP_CAM_STRIDE]  packed camera records (see below)
+ *   sample_grid   [V][N][2]            N = X*Y*Z, voxel n = (ix*Y+iy)*Z+iz
+ *   cube          [B][J][X][Y][Z]
+ *   xy            [B][J][X][Y]
+ */
+#ifndef FVP_H
+#define FVP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FVP_ABI_VERSION 1
+#define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
+
+/* Argument errors (distinct from hipError_t values, which are < 1000). */
+#define FVP_OK 0
+#define FVP_ERR_NULL 1001     /* a required pointer is NULL */
+#define FVP_ERR_SHAPE 1002    /* a size is <= 0 or exceeds a kernel limit */
+
+/* Voxel-grid description: centre_i = linspace(start, end, bins)[i] + center
+ * per axis, fp32, exactly as compute_grid (lib/models/project_whole.py:43-79). */
+typedef struct fvp_grid_spec {
+    float start[3];  /* -SPACE_SIZE/2 */
+    float end[3];    /* +SPACE_SIZE/2 */
+    float center[3]; /* SPACE_CENTER */
+    int32_t bins[3]; /* VOXELS_PER_AXIS (or fine_voxels_per_axis) */
+} fvp_grid_spec;
+
+/* Image geometry used when building a sample grid (project_whole.py:81-117). */
+typedef struct fvp_image_spec {
+    float ori_max;  /* max(ORI_IMAGE_SIZE): the upper clamp, project_whole.py:100 */
+    float img_w, img_h; /* IMAGE_SIZE */
+    int32_t hm_w, hm_h; /* HEATMAP_SIZE */
+} fvp_image_spec;
+
+/* Per-person layer constants (lib/models/project_individual.py:43-85). */
+typedef struct fvp_person_spec {
+    int32_t fine[3];      /* fine_voxels_per_axis, e.g. 253,253,64 */
+    float scale[3];       /* (fine-1)/whole_space_size */
+    float bias[3];
+    float whole_size[3];  /* CAPTURE_SPEC.SPACE_SIZE */
+    float ind_size[3];    /* INDIVIDUAL_SPEC.SPACE_SIZE */
+    int32_t bins[3];      /* INDIVIDUAL_SPEC.VOXELS_PER_AXIS, e.g. 64,64,64 */
+} fvp_person_spec;
+
+int fvp_abi_version(void);
+const char *fvp_status_string(int status);
+
+/* Sample grid of one sequence: for each camera v and voxel n, project the
+ * voxel centre (lib/utils/cameras.py:30-56), clamp to [-1, ori_max], apply
+ * resize_transform (lib/utils/transforms.py:59-63), scale to heatmap pixels,
+ * normalise to [-1,1] and clamp to +-1.1.
+ * Replaces ProjectLayer.project_grid x V (project_whole.py:81-117, :151-156)
+ * and compute_sample_grid (project_individual.py:192-220).
+ *   cams        device [V][FVP_CAM_STRIDE]
+ *   resize_t    device [2][3]
+ *   sample_grid device [V][N][2] (output) */
+int fvp_project_grid(const float *cams, int V, const float *resize_t,
+                     const fvp_grid_spec *grid, const fvp_image_spec *img,
+                     float *sample_grid, void *stream);
+
+/* Whole-space voxelisation fused with the xy max-projection:
+ *   cube[b,j,n] = clamp(mean_v grid_sample(heatmaps[b,v,j], sample_grid[g(b),v,n]), 0, 1)
+ *   xy[b,j,x,y] = max_z cube[b,j,x,y,z]
+ * Replaces ProjectLayer.forward (project_whole.py:119-168) and the first line
+ * of CenterNet.forward (lib/models/cnns_2d.py:291).
+ *   sample_grids device [n_grids][V][N][2]
+ *   grid_index   device int32 [B] (grid of frame b) or NULL (all frames use grid 0)
+ *   cube, xy     device outputs; either may be NULL to skip it */
+int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W,
+                 const float *sample_grids, const int32_t *grid_index,
+                 int X, int Y, int Z, float *cube, float *xy, void *stream);
+
+/* Peak NMS + top-K on prob [B][X*Y] (a [B,1,X,Y] map): 3x3 max-pool keep mask,
+ * top-K of the masked map (value descending, flat index ascending on ties),
+ * and get_index2D's (flat // X, flat % X) decode.
+ * Replaces nms2D / max_pool2D / get_index2D (lib/core/proposal.py:13-76).
+ *   vals [B][K] fp32, flat [B][K] int64, xy [B][K][2] int64 (xy may be NULL) */
+int fvp_nms_topk(const float *prob, int B, int X, int Y, int K,
+                 float *vals, int64_t *flat, int64_t *xy, void *stream);
+
+/* z-columns of the top-K proposals: columns[b,k,j,:] = cube[b,j,flat[b,k],:]
+ * Replaces the torch.gather at lib/models/human_detection_net.py:199-200. */
+int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z,
+                       const int64_t *flat, int K, float *columns, void *stream);
+
+/* bbox sizes at the top-K: out[b,k,c] = size[b,c,flat[b,k]] (c = 0,1)
+ * Replaces the torch.gather at lib/models/human_detection_net.py:191-192. */
+int fvp_gather_bbox(const float *size, int B, int X, int Y,
+                    const int64_t *flat, int K, float *out, void *stream);
+
+/* Per-person cubes of one frame from its cached fine sample grid.
+ * Replaces project_individual.ProjectLayer.forward (project_individual.py:222-293).
+ *   heatmaps    device [V][J][H][W] (the frame `index` of the batch)
+ *   fine_grid   device [V][FX][FY][FZ][2]
+ *   proposals   device [P][7] (x,y,z mm, gt, conf, bbox_w, bbox_h)
+ *   cubes       device [P][J][SX][SY][SZ] (output, fully written)
+ *   offset      device [P][3] (output) */
+int fvp_person_cubes(const float *heatmaps, int V, int J, int H, int W,
+                     const float *fine_grid, const fvp_person_spec *spec,
+                     const float *proposals, int P,
+                     float *cubes, float *offset, void *stream);
+
+/* xy / xz / yz max-projections of per-person cubes [P][J][S][S][S] into
+ * planes [3P][J][S][S] (xy block first, then xz, then yz).
+ * Replaces torch.cat([max(c,4), max(c,3), max(c,2)]) at
+ * lib/models/joint_localization_net.py:158-160.  S <= 64. */
+int fvp_max_planes(const float *cubes, int P, int J, int S, float *planes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FVP_H */

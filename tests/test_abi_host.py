@@ -1,0 +1,102 @@
+"""CPU tests: the C-ABI library loads and exports what include/fvp.h declares,
+argument validation happens before any launch, and the host-side mirror of
+the reference interface (geometry, config, layer construction) is correct."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from fvp import geometry, synthetic
+from fvp.workloads import WORKLOADS
+
+HEADER = os.path.join(REPO, "include", "fvp.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(fvp_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from fvp import _lib
+
+    lib = _lib.load()
+    names = _declared()
+    assert len(names) >= 9
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
+    assert lib.fvp_abi_version() == 1
+    assert lib.fvp_status_string(0) == b"success"
+
+
+def test_argument_validation_without_gpu():
+    """NULL / bad sizes are rejected on the host, before any HIP call."""
+    from fvp import _lib
+
+    lib = _lib.load()
+    assert lib.fvp_voxelize(None, 1, 5, 15, 128, 240, None, None, 80, 80, 20, None, None, None) == 1001
+    assert lib.fvp_voxelize(1, 0, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None) == 1002
+    assert lib.fvp_nms_topk(None, 1, 80, 80, 10, None, None, None, None) == 1001
+    assert lib.fvp_nms_topk(1, 1, 2, 2, 10, 1, 1, None, None) == 1002  # K > X*Y
+    assert lib.fvp_max_planes(1, 1, 1, 65, 1, None) == 1002            # S > 64
+    assert lib.fvp_gather_columns(None, 1, 1, 1, 1, 1, None, 1, None, None) == 1001
+    with pytest.raises(_lib.FvpError, match="NULL"):
+        _lib.check(1001, "fvp_voxelize")
+
+
+def test_ops_refuse_cpu_tensors():
+    from fvp import ops  # noqa: F401  (registers torch.ops.fvp.*)
+
+    hm = torch.zeros(1, 1, 1, 4, 4)
+    sg = torch.zeros(1, 8, 2)
+    with pytest.raises(Exception):
+        torch.ops.fvp.voxelize(hm, sg, None, 2, 2, 2, True, True)
+
+
+def test_pack_camera_layout():
+    cams, seq = WORKLOADS["c3"].cameras()
+    c = cams[seq][0]
+    rec = geometry.pack_camera(c)
+    assert rec.shape == (geometry.CAM_STRIDE,) and rec.dtype == np.float32
+    assert np.array_equal(rec[0:9], np.asarray(c["R"], np.float64).astype(np.float32).reshape(9))
+    assert np.array_equal(rec[9:12], np.asarray(c["T"], np.float64).astype(np.float32).reshape(3))
+    assert rec[12] == np.float32(c["fx"]) and rec[15] == np.float32(c["cy"])
+    assert np.array_equal(rec[16:19], np.asarray(c["k"]).astype(np.float32).reshape(3))
+    assert np.array_equal(rec[19:21], np.asarray(c["p"]).astype(np.float32).reshape(2))
+    # dict-of-int (shelf) and list (panoptic) camera containers
+    shelf, s2 = WORKLOADS["c2"].cameras()
+    assert geometry.pack_cameras(shelf, s2).shape == (5, geometry.CAM_STRIDE)
+
+
+def test_resize_transform_closed_forms():
+    """r = 0 closed forms quoted in SURVEY.md §8(a) A3."""
+    pan = geometry.resize_transform((1920, 1080), (960, 512))
+    np.testing.assert_allclose(pan, [[0.474074, 0, 24.8889], [0, 0.474074, 0]], atol=1e-4)
+    shelf = geometry.resize_transform((1032, 776), (800, 608))
+    np.testing.assert_allclose(shelf, [[0.775194, 0, 0], [0, 0.775194, 3.22481]], atol=1e-5)
+
+
+def test_layers_construct_without_state():
+    from fvp.project_whole import ProjectLayer as PW
+    from fvp.project_individual import ProjectLayer as PI
+
+    cfg = WORKLOADS["c3"].cfg("cpu")
+    pw, pi = PW(cfg), PI(cfg)
+    assert len(pw.state_dict()) == 0 and len(pi.state_dict()) == 0  # checkpoints load unchanged
+    assert pw.grid.shape == (128000, 3)
+    assert tuple(pi.fine_voxels_per_axis.tolist()) == (253, 253, 64)
+    assert pi.center_grid.shape == (3, 4096, 2)
+
+
+def test_synthetic_inputs_deterministic_and_peaked():
+    w = WORKLOADS["c2"]
+    a = synthetic.gaussian_heatmaps(w, 2)
+    b = synthetic.gaussian_heatmaps(w, 2)
+    assert np.array_equal(a, b)
+    assert a.shape == (2, 5, 15, 128, 240)
+    assert 0.0 <= a.min() and a.max() <= 1.0 and a.max() > 0.9
+    assert 0.001 < (a > 0).mean() < 0.2

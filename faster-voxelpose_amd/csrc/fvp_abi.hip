@@ -11,6 +11,8 @@ extern "C" const char *fvp_status_string(int status) {
             return "fvp: a required pointer argument is NULL";
         case FVP_ERR_SHAPE:
             return "fvp: a size argument is out of range for this kernel";
+        case FVP_ERR_WORKSPACE:
+            return "fvp: workspace missing or smaller than fvp_voxelize_workspace_bytes()";
         default:
             return hipGetErrorString((hipError_t)status);
     }

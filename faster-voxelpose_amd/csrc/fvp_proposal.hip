@@ -38,7 +38,8 @@ __device__ __forceinline__ Cand wave_best(Cand c) {
 
 constexpr int kNmsThreads = 256;
 
-__global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__restrict__ prob, int X, int Y, int K,
+__global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__restrict__ prob, long long stride, int X,
+                                                               int Y, int K,
                                                                float *__restrict__ vals, int64_t *__restrict__ flat,
                                                                int64_t *__restrict__ xy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -48,7 +49,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__re
     __shared__ Cand red[kNmsThreads / kWave];
     __shared__ Cand winner;
     const int b = blockIdx.x;
-    const float *__restrict__ p = prob + (size_t)b * M;
+    const float *__restrict__ p = prob + (size_t)b * stride;
     const int tid = threadIdx.x;
 
     for (int e = tid; e < M; e += kNmsThreads) {
@@ -137,15 +138,17 @@ __global__ __launch_bounds__(256) void gather_bbox_kernel(const float *__restric
 
 }  // namespace fvp
 
-extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, int K, float *vals, int64_t *flat, int64_t *xy,
-                            void *stream) {
+extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
+                            int64_t *flat, int64_t *xy, void *stream) {
     if (!prob || !vals || !flat) return FVP_ERR_NULL;
     if (B <= 0 || X <= 0 || Y <= 0 || K <= 0 || K > X * Y) return FVP_ERR_SHAPE;
     const size_t M = (size_t)X * Y;
     const size_t lds = M * 4 + ((M + 31) / 32) * 4;
     if (lds > 150 * 1024) return FVP_ERR_SHAPE;
-    hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob, X, Y, K,
-                       vals, flat, xy);
+    if (frame_stride == 0) frame_stride = (long long)M;
+    if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
+    hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob,
+                       frame_stride, X, Y, K, vals, flat, xy);
     return (int)hipGetLastError();
 }
 

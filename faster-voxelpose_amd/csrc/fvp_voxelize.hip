@@ -3,120 +3,245 @@
 // Reference: project_whole.py:119-168 (grid_sample per frame, mean over all V
 // cameras, clamp(0,1)) and cnns_2d.py:291 (max over z).
 //
-// Work decomposition (gfx950, wave64):
-//   * a wave owns a 4x4 block of (x,y) voxel columns; its 64 lanes are
-//     (x4, y4, z4) so one load instruction touches a compact 3-D voxel block,
-//     whose projections are a compact pixel patch (L1/L2 line reuse between
-//     the four bilinear taps and between neighbouring lanes);
-//   * the wave walks the z axis in steps of 4; each lane accumulates all J
-//     joints of its voxel in registers (coordinates and weights computed once
-//     per voxel-camera, reused for every joint plane);
-//   * the xy max over z is a running register max per lane plus two
-//     cross-lane steps (lanes differing in z4) at the end -- no LDS, no atomics;
-//   * a 256-thread block = 2x2 waves = an 8x8 column tile of one frame; the
-//     blockIdx is remapped so each XCD processes whole frames (its L2 holds the
-//     frame's heatmap planes while its tiles sample them).
-// Voxel-cameras whose four taps are all outside the image (clamped +-1.1
-// coordinates) contribute exactly 0 and issue no loads.
+// Why two kernels.  A bilinear tap of all J joints touches J separate
+// [H][W] planes in the reference layout.  On gfx950 the texture addresser
+// only merges ADJACENT lanes that fall in one 128-B line (a quad per clock);
+// scattered per-joint taps cost ~64 clocks per wave load (tools/ta_probe.py),
+// and a voxel-camera needs 2 rows x J planes of lines.  So each chunk of
+// frames is first re-laid out channels-last:
+//   heatmaps_to_cl : [B][V][J][H][W]  ->  [b][V][H][W][JP]   (JP = 4*LPV >= J, zero padded)
+// a pure streaming pass, then
+//   voxelize_cl    : LPV lanes share one voxel; lane q loads 16 B = joints
+//                    4q..4q+3 of each tap with one buffer_load_dwordx4, so a
+//                    quad reads one 64-B pixel in one clock; out-of-image taps
+//                    use an out-of-range offset and read 0 through the buffer
+//                    descriptor's range check (= grid_sample's zero padding).
+// The chunk's channels-last copy is sized to stay in the 256 MB Infinity
+// Cache between the two launches.
+//
+// voxelize_cl work decomposition: a 256-thread block owns COLS whole voxel
+// columns (x, y..y+COLS, all z) of one frame -- a contiguous range of the
+// cube -- processed in passes of 256/LPV voxels; results are staged in LDS
+// so the cube is written as contiguous runs per joint and the xy max over z
+// is read back from LDS.  Arithmetic per tap and the camera/sum order are the
+// reference's (fvp_device.h), so the result is bit-exact.
 #include "fvp_device.h"
 
 namespace fvp {
 
-template <int JT, typename T>
-__global__ __launch_bounds__(256) void voxelize_kernel(const T *__restrict__ hm, const float2 *__restrict__ grids,
-                                                       const int32_t *__restrict__ grid_index,
-                                                       float *__restrict__ cube, float *__restrict__ xy, int V,
-                                                       int J, int H, int W, int X, int Y, int Z, int tiles_y,
-                                                       int tiles_per_frame) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+constexpr unsigned kOOB = 0x80000000u;  // beyond any descriptor range -> loads return 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base, unsigned bytes) {
+    const unsigned long long p = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+    void *b = (void *)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// -- layout pass ----------------------------------------------------------------
+// thread = (pixel, joint quad q): reads joints 4q..4q+3 of one pixel (the lanes
+// of a wave cover 64/LPV consecutive pixels -> coalesced plane reads), writes
+// one float4 (a wave writes a contiguous 1 KiB run).
+template <int LPV, typename T>
+__global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict__ hm, float4 *__restrict__ cl, int J,
+                                                             int HW, long long total_px) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long pxg = gid / LPV;
+    const int q = (int)(gid - pxg * LPV);
+    if (pxg >= total_px) return;
+    const long long bv = pxg / HW;
+    const int pix = (int)(pxg - bv * HW);
+    const T *__restrict__ src = hm + (size_t)bv * J * HW + pix;
+    const int j = 4 * q;
+    float4 o;
+    o.x = (j + 0 < J) ? to_f32(src[(size_t)(j + 0) * HW]) : 0.f;
+    o.y = (j + 1 < J) ? to_f32(src[(size_t)(j + 1) * HW]) : 0.f;
+    o.z = (j + 2 < J) ? to_f32(src[(size_t)(j + 2) * HW]) : 0.f;
+    o.w = (j + 3 < J) ? to_f32(src[(size_t)(j + 3) * HW]) : 0.f;
+    cl[pxg * LPV + q] = o;
+}
+
+// -- gather pass ----------------------------------------------------------------
+template <int LPV>
+__global__ __launch_bounds__(256) void voxelize_cl_kernel(const float *__restrict__ cl, const float2 *__restrict__ grids,
+                                                          const int32_t *__restrict__ grid_index, int frame0,
+                                                          float *__restrict__ cube, float *__restrict__ xy, int V,
+                                                          int J, int H, int W, int X, int Y, int Z, int cols,
+                                                          int col_blocks) {
+    constexpr int JP = 4 * LPV;
+    constexpr int VPP = 256 / LPV;  // voxels per pass
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [JP][SP]
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int b = L / tiles_per_frame;
-    const int t = L - b * tiles_per_frame;
-    const int tx = t / tiles_y, ty = t - (t / tiles_y) * tiles_y;
-    const int x = tx * 8 + (wave >> 1) * 4 + (lane >> 4);
-    const int y = ty * 8 + (wave & 1) * 4 + ((lane >> 2) & 3);
-    const int zi = lane & 3;
-    const bool col_ok = (x < X) && (y < Y);
-
-    const long long N = (long long)X * Y * Z;
-    const size_t HW = (size_t)H * W;
-    const int gsel = grid_index ? grid_index[b] : 0;
-    const float2 *__restrict__ g = grids + (size_t)gsel * V * N;
-    const T *__restrict__ hmb = hm + (size_t)b * V * J * HW;
+    const int bl = L / col_blocks;   // frame within the chunk
+    const int b = frame0 + bl;       // frame within the batch (outputs, grid_index)
+    const int XY = X * Y;
+    const int c0 = (L - bl * col_blocks) * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const int SP = cols * Z + 1;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const unsigned HW = (unsigned)(H * W);
+    const unsigned pix_bytes = JP * 4u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
     const float fV = (float)V;
+    const int gsel = grid_index ? grid_index[b] : 0;
+    const float2 *__restrict__ g = grids + (size_t)gsel * V * N + n0;
 
-    for (int j0 = 0; j0 < J; j0 += JT) {
-        float xymax[JT];
+    for (int i0 = 0; i0 < T; i0 += VPP) {
+        const int i = i0 + threadIdx.x / LPV;
+        const bool valid = i < T;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int v = 0; v < V; ++v) {
+            float2 gg = g[(size_t)v * N + min(i, T - 1)];
+            if (!valid) gg = make_float2(-2.f, -2.f);
+            const float ix = (gg.x + 1.0f) * sxs;
+            const float iy = (gg.y + 1.0f) * sys;
+            const bool isnan_ = (ix != ix) || (iy != iy);
+            if (isnan_) {  // grid_sample of a NaN coordinate is NaN (0 * NaN weights)
 #pragma unroll
-        for (int jj = 0; jj < JT; ++jj) xymax[jj] = -INFINITY;
-
-        for (int z0 = 0; z0 < Z; z0 += 4) {
-            const int z = z0 + zi;
-            const bool valid = col_ok && (z < Z);
-            const long long n = ((long long)x * Y + y) * Z + z;
-            float acc[JT];
-#pragma unroll
-            for (int jj = 0; jj < JT; ++jj) acc[jj] = 0.0f;
-            if (valid) {
-                for (int v = 0; v < V; ++v) {
-                    const float2 gg = g[(size_t)v * N + n];
-                    const Taps tp = make_taps(gg.x, gg.y, H, W);
-                    if (tp.nan) {
-#pragma unroll
-                        for (int jj = 0; jj < JT; ++jj) acc[jj] = acc[jj] + NAN;
-                    } else if (tp.any) {
-                        const T *__restrict__ base = hmb + ((size_t)v * J + j0) * HW;
-#pragma unroll
-                        for (int jj = 0; jj < JT; ++jj) {
-                            if (j0 + jj < J) acc[jj] = acc[jj] + sample(base + (size_t)jj * HW, tp);
-                        }
-                    }
-                }
+                for (int k = 0; k < 4; ++k) acc[k] = acc[k] + NAN;
             }
+            const float x0f = floorf(ix), y0f = floorf(iy);
+            const float wx = ix - x0f, ex = 1.0f - wx;
+            const float ny = iy - y0f, syw = 1.0f - ny;
+            const float nw = syw * ex, ne = syw * wx, sw = ny * ex, se = ny * wx;
+            const int x0 = isnan_ ? -4 : (int)x0f, y0 = isnan_ ? -4 : (int)y0f;
+            const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
+            const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
+            const bool any = (vx0 | vx1) & (vy0 | vy1);
+            if (!__builtin_amdgcn_ballot_w64(any)) continue;  // whole wave off-image: contributes exactly 0
+            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(cl + ((size_t)bl * V + v) * HW * JP, HW * pix_bytes);
+            const unsigned pix = (unsigned)(y0 * W + x0);
+            const unsigned qo = (unsigned)q * 16u;
+            const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx0) ? pix * pix_bytes + qo : kOOB, 0, 0);
+            const auto bq =
+                __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx1) ? (pix + 1u) * pix_bytes + qo : kOOB, 0, 0);
+            const auto c = __builtin_amdgcn_raw_buffer_load_b128(
+                rs, (vy1 & vx0) ? (pix + (unsigned)W) * pix_bytes + qo : kOOB, 0, 0);
+            const auto d = __builtin_amdgcn_raw_buffer_load_b128(
+                rs, (vy1 & vx1) ? (pix + (unsigned)W + 1u) * pix_bytes + qo : kOOB, 0, 0);
+            if (!isnan_) {
 #pragma unroll
-            for (int jj = 0; jj < JT; ++jj) {
-                if (j0 + jj < J) {
-                    const float o = clampf(acc[jj] / fV, 0.0f, 1.0f);
-                    if (valid) {
-                        if (cube) cube[((size_t)b * J + j0 + jj) * N + n] = o;
-                        xymax[jj] = nanmax(xymax[jj], o);
-                    }
+                for (int k = 0; k < 4; ++k) {
+                    const float fa = __builtin_bit_cast(float, (unsigned)a[k]);
+                    const float fb = __builtin_bit_cast(float, (unsigned)bq[k]);
+                    const float fc = __builtin_bit_cast(float, (unsigned)c[k]);
+                    const float fd = __builtin_bit_cast(float, (unsigned)d[k]);
+                    acc[k] = acc[k] + __builtin_fmaf(fd, se, __builtin_fmaf(fc, sw, __builtin_fmaf(fb, ne, fa * nw)));
                 }
             }
         }
-        if (xy) {
+        if (valid) {
 #pragma unroll
-            for (int jj = 0; jj < JT; ++jj) {
-                float m = xymax[jj];
-                m = nanmax(m, __shfl_xor(m, 1));
-                m = nanmax(m, __shfl_xor(m, 2));
-                if (j0 + jj < J && zi == 0 && col_ok) xy[(((size_t)b * J + j0 + jj) * X + x) * Y + y] = m;
-            }
+            for (int k = 0; k < 4; ++k) stage[(4 * q + k) * SP + i] = clampf(acc[k] / fV, 0.0f, 1.0f);
+        }
+    }
+    __syncthreads();
+    if (cube) {
+        for (int j = 0; j < J; ++j) {
+            float *__restrict__ dst = cube + ((size_t)b * J + j) * N + n0;
+            for (int e = threadIdx.x; e < T; e += 256) dst[e] = stage[j * SP + e];
+        }
+    }
+    if (xy) {
+        for (int e = threadIdx.x; e < J * ncols; e += 256) {
+            const int j = e / ncols, cc = e - (e / ncols) * ncols;
+            const float *s = stage + j * SP + cc * Z;
+            float m = -INFINITY;
+            for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+            xy[((size_t)b * J + j) * XY + c0 + cc] = m;
         }
     }
 }
 
-template <typename T>
-static int launch_voxelize(const T *hm, int B, int V, int J, int H, int W, const float *grids,
-                           const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, hipStream_t s) {
-    const int tiles_x = (X + 7) / 8, tiles_y = (Y + 7) / 8;
-    const long long tiles = (long long)tiles_x * tiles_y;
-    const long long blocks = tiles * B;
-    if (blocks > 0x7fffffffLL) return FVP_ERR_SHAPE;
-    hipLaunchKernelGGL((voxelize_kernel<16, T>), dim3((unsigned)blocks), dim3(256), 0, s, hm,
-                       reinterpret_cast<const float2 *>(grids), grid_index, cube, xy, V, J, H, W, X, Y, Z, tiles_y,
-                       (int)tiles);
+static int lanes_per_voxel(int J) { return J <= 4 ? 1 : J <= 8 ? 2 : J <= 16 ? 4 : 8; }
+
+static int cols_per_block(int Z) { return Z >= 320 ? 1 : 320 / Z; }
+
+static size_t cl_frame_bytes(int V, int J, int H, int W) {
+    return (size_t)V * H * W * 4 * lanes_per_voxel(J) * sizeof(float);
+}
+
+// Frames per chunk: keep the channels-last copy of a chunk well inside the
+// 256 MB Infinity Cache (measured best at ~64-80 MB for C2: 8 frames).
+static int chunk_frames(int B, int V, int J, int H, int W) {
+    const size_t per = cl_frame_bytes(V, J, H, W);
+    long long c = (long long)((80ull << 20) / (per ? per : 1));
+    if (c < 1) c = 1;
+    if (c > B) c = B;
+    return (int)c;
+}
+
+template <int LPV, typename T>
+static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const float *grids, const int32_t *grid_index,
+                      int X, int Y, int Z, float *cube, float *xy, float *ws, hipStream_t s) {
+    const int chunk = chunk_frames(B, V, J, H, W);
+    const int cols = cols_per_block(Z);
+    const int col_blocks = (X * Y + cols - 1) / cols;
+    const size_t lds = (size_t)4 * LPV * (cols * Z + 1) * sizeof(float);
+    const size_t frame_elems = (size_t)V * J * H * W;
+    for (int f0 = 0; f0 < B; f0 += chunk) {
+        const int nb = min(chunk, B - f0);
+        const long long px = (long long)nb * V * H * W;
+        const long long threads = px * LPV;
+        hipLaunchKernelGGL((heatmaps_to_cl_kernel<LPV, T>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                           hm + (size_t)f0 * frame_elems, reinterpret_cast<float4 *>(ws), J, H * W, px);
+        hipLaunchKernelGGL((voxelize_cl_kernel<LPV>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s, ws,
+                           reinterpret_cast<const float2 *>(grids), grid_index, f0, cube, xy, V, J, H, W, X, Y, Z,
+                           cols, col_blocks);
+    }
     return (int)hipGetLastError();
+}
+
+template <typename T>
+static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const float *grids, const int32_t *grid_index,
+                        int X, int Y, int Z, float *cube, float *xy, void *ws, size_t ws_bytes, hipStream_t s) {
+    const size_t need = (size_t)chunk_frames(B, V, J, H, W) * cl_frame_bytes(V, J, H, W);
+    if (!ws || ws_bytes < need) return FVP_ERR_WORKSPACE;
+    if ((long long)V * H * W * 4 * lanes_per_voxel(J) * 4 > 0x7fffffffLL) return FVP_ERR_SHAPE;  // 32-bit offsets
+    float *w = reinterpret_cast<float *>(ws);
+    switch (lanes_per_voxel(J)) {
+        case 1: return run_chunks<1, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
+        case 2: return run_chunks<2, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
+        case 4: return run_chunks<4, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
+        default: return run_chunks<8, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
+    }
+}
+
+static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, const float *grids, int X, int Y, int Z) {
+    if (!heatmaps || !grids) return FVP_ERR_NULL;
+    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2 || X <= 0 || Y <= 0 || Z <= 0)
+        return FVP_ERR_SHAPE;
+    if ((long long)X * Y * Z > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    return FVP_OK;
 }
 
 }  // namespace fvp
 
+extern "C" size_t fvp_voxelize_workspace_bytes(int B, int V, int J, int H, int W) {
+    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
+    return (size_t)fvp::chunk_frames(B, V, J, H, W) * fvp::cl_frame_bytes(V, J, H, W);
+}
+
 extern "C" int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W, const float *sample_grids,
-                            const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *stream) {
-    if (!heatmaps || !sample_grids) return FVP_ERR_NULL;
-    if (B <= 0 || V <= 0 || J <= 0 || H < 2 || W < 2 || X <= 0 || Y <= 0 || Z <= 0) return FVP_ERR_SHAPE;
+                            const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *workspace,
+                            size_t workspace_bytes, void *stream) {
+    const int st = fvp::check_args(heatmaps, B, V, J, H, W, sample_grids, X, Y, Z);
+    if (st != FVP_OK) return st;
     if (!cube && !xy) return FVP_OK;
-    return fvp::launch_voxelize<float>(heatmaps, B, V, J, H, W, sample_grids, grid_index, X, Y, Z, cube, xy,
-                                       (hipStream_t)stream);
+    return fvp::voxelize_any<float>(heatmaps, B, V, J, H, W, sample_grids, grid_index, X, Y, Z, cube, xy, workspace,
+                                    workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W, const float *sample_grids,
+                                const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy,
+                                void *workspace, size_t workspace_bytes, void *stream) {
+    const int st = fvp::check_args(heatmaps, B, V, J, H, W, sample_grids, X, Y, Z);
+    if (st != FVP_OK) return st;
+    if (!cube && !xy) return FVP_OK;
+    return fvp::voxelize_any<_Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, sample_grids,
+                                       grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
 }

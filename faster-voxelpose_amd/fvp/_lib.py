@@ -38,9 +38,12 @@ SIGNATURES = {
     "fvp_status_string": [c_int],
     "fvp_project_grid": [c_void_p, c_int, c_void_p, ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p,
                          c_void_p],
+    "fvp_voxelize_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
     "fvp_voxelize": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
-                     c_void_p, c_void_p],
-    "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+                     c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
+    "fvp_voxelize_f16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                         c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
+    "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_person_cubes": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, ctypes.POINTER(PersonSpec), c_void_p, c_int,
@@ -48,7 +51,7 @@ SIGNATURES = {
     "fvp_max_planes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _LIB = None
 
 
@@ -67,7 +70,7 @@ def load():
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = c_char_p if name == "fvp_status_string" else c_int
+        fn.restype = {"fvp_status_string": c_char_p, "fvp_voxelize_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
     if lib.fvp_abi_version() != ABI_VERSION:
         raise FvpError(f"fvp: ABI version mismatch ({lib.fvp_abi_version()} != {ABI_VERSION})")
     _LIB = lib

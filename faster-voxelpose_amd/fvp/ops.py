@@ -35,11 +35,18 @@ def _stream(t: torch.Tensor):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def forward_only(*tensors) -> None:
+    """Reject autograd inputs: the ops have no backward (called by the layers
+    before dispatch, where requires_grad is still visible)."""
+    if torch.is_grad_enabled():
+        for t in tensors:
+            if isinstance(t, torch.Tensor) and t.requires_grad:
+                raise _lib.FvpError("fvp: input requires grad; the projection path is forward-only")
+
+
 def _dev_f32(t: torch.Tensor, name: str) -> torch.Tensor:
     if t.device.type != "cuda":
         raise _lib.FvpError(f"fvp: {name} must be on a HIP device, got {t.device}")
-    if torch.is_grad_enabled() and t.requires_grad:
-        raise _lib.FvpError(f"fvp: {name} requires grad; the projection path is forward-only")
     return t.to(torch.float32).contiguous() if t.dtype != torch.float32 else t.contiguous()
 
 
@@ -68,7 +75,10 @@ def _(cams, resize_t, start, end, center, bins, ori_max, img_w, img_h, hm_w, hm_
 @torch.library.custom_op("fvp::voxelize", mutates_args=(), device_types="cuda")
 def voxelize(heatmaps: torch.Tensor, sample_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
              X: int, Y: int, Z: int, want_cube: bool, want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
-    hm = _dev_f32(heatmaps, "heatmaps")
+    if heatmaps.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps.device}")
+    half = heatmaps.dtype == torch.float16
+    hm = heatmaps.contiguous() if half else _dev_f32(heatmaps, "heatmaps")
     sg = _dev_f32(sample_grids, "sample_grids")
     B, V, J, H, W = hm.shape
     N = X * Y * Z
@@ -83,8 +93,12 @@ def voxelize(heatmaps: torch.Tensor, sample_grids: torch.Tensor, grid_index: Opt
             raise _lib.FvpError("fvp: grid_index must have one entry per frame")
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
-    _lib.call("fvp_voxelize", _ptr(hm), B, V, J, H, W, _ptr(sg), _ptr(gi), X, Y, Z,
-              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _stream(hm))
+    ws_bytes = _lib.load().fvp_voxelize_workspace_bytes(B, V, J, H, W)
+    if ws_bytes == 0:
+        raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
+    _lib.call("fvp_voxelize_f16" if half else "fvp_voxelize", _ptr(hm), B, V, J, H, W, _ptr(sg), _ptr(gi), X, Y, Z,
+              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _ptr(ws), ws_bytes, _stream(hm))
     return cube, xy
 
 
@@ -98,14 +112,20 @@ def _(heatmaps, sample_grids, grid_index, X, Y, Z, want_cube, want_xy):
 # ---------------------------------------------------------------------------
 @torch.library.custom_op("fvp::nms_topk", mutates_args=(), device_types="cuda")
 def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    p = _dev_f32(prob, "prob_map")
-    B, X, Y = p.shape[0], p.shape[-2], p.shape[-1]
-    if p.numel() != B * X * Y:
+    if prob.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: prob_map must be on a HIP device, got {prob.device}")
+    B, X, Y = prob.shape[0], prob.shape[-2], prob.shape[-1]
+    if prob.numel() != B * X * Y:
         raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map")
+    p = prob
+    # a channel slice of a contiguous [B,C,X,Y] tensor is passed by frame stride, without a copy
+    if not (p.dtype == torch.float32 and p.stride()[-1] == 1 and p.stride()[-2] == Y):
+        p = p.to(torch.float32).contiguous()
+    stride = p.stride()[0] if B > 1 else X * Y
     vals = torch.empty((B, K), dtype=torch.float32, device=p.device)
     flat = torch.empty((B, K), dtype=torch.int64, device=p.device)
     xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
-    _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
+    _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
     return vals, xy, flat
 
 

@@ -94,6 +94,7 @@ class ProjectLayer(nn.Module):
         return self.sample_grid[curr_seq]
 
     def forward(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
+        ops.forward_only(heatmaps, proposal_centers)
         grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
         c = self._const
         return ops.person_cubes(heatmaps[index], grid, proposal_centers,

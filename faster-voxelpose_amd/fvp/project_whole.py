@@ -90,6 +90,7 @@ class ProjectLayer(nn.Module):
 
     def forward_fused(self, heatmaps, meta, cameras, resize_transform, want_cube=True, want_xy=True):
         """One launch for the whole batch: (cube[B,J,X,Y,Z] or empty, xy[B,J,X,Y] or empty)."""
+        ops.forward_only(heatmaps)
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         return ops.voxelize(heatmaps, grids, index, X, Y, Z, want_cube, want_xy)

@@ -24,6 +24,7 @@ def get_index2D(indices: torch.Tensor, shape) -> torch.Tensor:
 
 
 def nms2D(prob_map: torch.Tensor, max_num: int):
+    prob_map = prob_map.detach()  # human_detection_net.py:188 passes .detach(); the op is forward-only
     vals, xy, flat = ops.nms_topk(prob_map, int(max_num))
     return vals, xy, flat
 

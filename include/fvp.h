@@ -23,19 +23,22 @@
 #ifndef FVP_H
 #define FVP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 1
+#define FVP_ABI_VERSION 2
+#define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
 #define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
 
 /* Argument errors (distinct from hipError_t values, which are < 1000). */
 #define FVP_OK 0
 #define FVP_ERR_NULL 1001     /* a required pointer is NULL */
 #define FVP_ERR_SHAPE 1002    /* a size is <= 0 or exceeds a kernel limit */
+#define FVP_ERR_WORKSPACE 1003 /* workspace missing or smaller than fvp_voxelize_workspace_bytes() */
 
 /* Voxel-grid description: centre_i = linspace(start, end, bins)[i] + center
  * per axis, fp32, exactly as compute_grid (lib/models/project_whole.py:43-79). */
@@ -86,17 +89,28 @@ int fvp_project_grid(const float *cams, int V, const float *resize_t,
  * of CenterNet.forward (lib/models/cnns_2d.py:291).
  *   sample_grids device [n_grids][V][N][2]
  *   grid_index   device int32 [B] (grid of frame b) or NULL (all frames use grid 0)
- *   cube, xy     device outputs; either may be NULL to skip it */
+ *   cube, xy     device outputs; either may be NULL to skip it
+ *   workspace    device scratch of >= fvp_voxelize_workspace_bytes(B,V,J,H,W)
+ *                bytes (channels-last copy of a chunk of frames); J <= FVP_MAX_JOINTS */
+size_t fvp_voxelize_workspace_bytes(int B, int V, int J, int H, int W);
 int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W,
                  const float *sample_grids, const int32_t *grid_index,
-                 int X, int Y, int Z, float *cube, float *xy, void *stream);
+                 int X, int Y, int Z, float *cube, float *xy,
+                 void *workspace, size_t workspace_bytes, void *stream);
+/* Same with fp16 heatmaps (IEEE binary16), computed in fp32 (exact upcast). */
+int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W,
+                     const float *sample_grids, const int32_t *grid_index,
+                     int X, int Y, int Z, float *cube, float *xy,
+                     void *workspace, size_t workspace_bytes, void *stream);
 
-/* Peak NMS + top-K on prob [B][X*Y] (a [B,1,X,Y] map): 3x3 max-pool keep mask,
- * top-K of the masked map (value descending, flat index ascending on ties),
- * and get_index2D's (flat // X, flat % X) decode.
+/* Peak NMS + top-K on a [B,1,X,Y] map: 3x3 max-pool keep mask, top-K of the
+ * masked map (value descending, flat index ascending on ties), and
+ * get_index2D's (flat // X, flat % X) decode.
  * Replaces nms2D / max_pool2D / get_index2D (lib/core/proposal.py:13-76).
+ *   prob         frame b's X*Y map starts at prob + b*frame_stride (0 = X*Y),
+ *                so one channel of the xy planes can be passed without a copy
  *   vals [B][K] fp32, flat [B][K] int64, xy [B][K][2] int64 (xy may be NULL) */
-int fvp_nms_topk(const float *prob, int B, int X, int Y, int K,
+int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K,
                  float *vals, int64_t *flat, int64_t *xy, void *stream);
 
 /* z-columns of the top-K proposals: columns[b,k,j,:] = cube[b,j,flat[b,k],:]

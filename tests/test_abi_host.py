@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == 1
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 2
     assert lib.fvp_status_string(0) == b"success"
 
 
@@ -38,10 +38,17 @@ def test_argument_validation_without_gpu():
     from fvp import _lib
 
     lib = _lib.load()
-    assert lib.fvp_voxelize(None, 1, 5, 15, 128, 240, None, None, 80, 80, 20, None, None, None) == 1001
-    assert lib.fvp_voxelize(1, 0, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None) == 1002
-    assert lib.fvp_nms_topk(None, 1, 80, 80, 10, None, None, None, None) == 1001
-    assert lib.fvp_nms_topk(1, 1, 2, 2, 10, 1, 1, None, None) == 1002  # K > X*Y
+    assert lib.fvp_voxelize(None, 1, 5, 15, 128, 240, None, None, 80, 80, 20, None, None, None, 0, None) == 1001
+    assert lib.fvp_voxelize(1, 0, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1002
+    assert lib.fvp_voxelize(1, 1, 5, 33, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1002  # J > 32
+    assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1003  # no workspace
+    need = lib.fvp_voxelize_workspace_bytes(256, 5, 15, 128, 240)
+    assert need == 8 * 5 * 128 * 240 * 16 * 4  # channels-last chunk of 8 frames (J padded to 16)
+    assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, 1, 100, None) == 1003
+    assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 0
+    assert lib.fvp_nms_topk(None, 1, 80, 80, 0, 10, None, None, None, None) == 1001
+    assert lib.fvp_nms_topk(1, 1, 2, 2, 0, 10, 1, 1, None, None) == 1002  # K > X*Y
+    assert lib.fvp_nms_topk(1, 2, 8, 8, 10, 5, 1, 1, None, None) == 1002  # frame stride < X*Y
     assert lib.fvp_max_planes(1, 1, 1, 65, 1, None) == 1002            # S > 64
     assert lib.fvp_gather_columns(None, 1, 1, 1, 1, 1, None, 1, None, None) == 1001
     with pytest.raises(_lib.FvpError, match="NULL"):

@@ -182,7 +182,7 @@ def _custom_workload(**kw):
     return dataclasses.replace(WORKLOADS[kw.pop("base", "c3")], **kw)
 
 
-@pytest.mark.parametrize("bins,J,hm_size", [((13, 11, 7), 3, (240, 128)), ((8, 8, 1), 33, (64, 48)),
+@pytest.mark.parametrize("bins,J,hm_size", [((13, 11, 7), 3, (240, 128)), ((8, 8, 1), 32, (64, 48)),
                                             ((24, 16, 5), 17, (200, 152)), ((1, 1, 9), 2, (2, 2))])
 def test_ragged_shapes_vs_oracle(gpu_device, bins, J, hm_size):
     from fvp import geometry, synthetic
@@ -294,3 +294,47 @@ def test_reference_assertions_and_errors(gpu_device):
         layer(hm.cpu(), {"seq": [seq]}, cams, rt)  # no CPU fallback
     with pytest.raises(_lib.FvpError, match="forward-only"):
         layer(hm.clone().requires_grad_(True), {"seq": [seq]}, cams, rt)
+
+
+def test_fp16_heatmaps_computed_in_fp32(gpu_device):
+    """C5 input dtype: fp16 heatmaps are upcast exactly and computed in fp32
+    (oracle on hm.half().float())."""
+    from fvp import geometry, synthetic
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c3"]
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+    hm = synthetic.uniform_heatmaps(w, 2, seed=9).half()
+    cube, xy = layer.forward_fused(hm.to(gpu_device), {"seq": [seq] * 2}, cams, rt.to(gpu_device))
+    c32, x32 = layer.forward_fused(hm.float().to(gpu_device), {"seq": [seq] * 2}, cams, rt.to(gpu_device))
+    assert torch.equal(cube, c32) and torch.equal(xy, x32)
+    grid = O.compute_grid(w.space_size, w.space_center, w.voxels_per_axis)
+    sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, w.heatmap_size, rt.numpy())
+                   for c in geometry.camera_list(cams, seq)])
+    ref = O.voxelize(hm[1].float().numpy(), sg).reshape(cube.shape[1:])
+    _assert_same(cube[1].cpu().numpy(), ref, "fp16 frame")
+
+
+def test_nms_on_channel_slice_without_copy(gpu_device):
+    from fvp.proposal import nms2D
+
+    g = torch.Generator().manual_seed(21)
+    planes = torch.rand((3, 15, 80, 80), generator=g).to(gpu_device)
+    v1, i1, f1 = nms2D(planes[:, 2:3], 10)
+    v2, i2, f2 = nms2D(planes[:, 2:3].contiguous(), 10)
+    assert torch.equal(v1, v2) and torch.equal(f1, f2) and torch.equal(i1, i2)
+    ov, oxy, ofl = O.nms2d(planes[:, 2:3].cpu().numpy(), 10)
+    assert np.array_equal(v1.cpu().numpy(), ov) and np.array_equal(f1.cpu().numpy(), ofl)
+
+
+def test_more_than_32_joints_rejected(gpu_device):
+    from fvp import _lib
+
+    hm = torch.zeros((1, 1, 33, 8, 8), device=gpu_device)
+    sg = torch.zeros((1, 8, 2), device=gpu_device)
+    with pytest.raises(_lib.FvpError, match="J <= 32"):
+        torch.ops.fvp.voxelize(hm, sg, None, 2, 2, 2, True, True)

@@ -127,7 +127,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from fvp import geometry, synthetic
+    from fvp import geometry, parallel, synthetic
     from fvp.project_whole import ProjectLayer
     from fvp.proposal import nms2D, gather_columns
     from fvp.workloads import WORKLOADS
@@ -176,10 +176,8 @@ def main():
             ev.append((e0, e1))
         vals, idx, flat = nms2D(xy[:, root:root + 1], K)
         cols = gather_columns(cube, flat)
-        if world > 1:
-            local = torch.cat([flat, vals.view(torch.int32).to(torch.int64)], dim=1)
-            out = torch.empty((world * B, 2 * K), dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(out, local)
+        if world > 1:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
+            parallel.gather_proposals(vals, flat)
         return cols
 
     for _ in range(args.warmup):

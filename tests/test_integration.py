@@ -1,0 +1,139 @@
+"""Drop-in integration (fvp/integration.py): install() rebinds the reference's
+names, and the fused HumanDetectionNet.forward returns what the reference's
+forward (human_detection_net.py:157-220) returns for the same modules.  The
+dense CNNs are out of scope, so seeded stand-ins with the reference's
+attribute names are used; the reference flow is restated with plain torch ops
+(torch.max / max_pool2d+topk / torch.gather) around them."""
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from fvp import integration
+
+
+def test_install_patches_reference_names():
+    mods = {}
+    for name in ("models.project_whole", "models.project_individual", "models.human_detection_net",
+                 "models.joint_localization_net", "core.proposal"):
+        m = types.ModuleType(name)
+        mods[name] = m
+    mods["models.project_whole"].ProjectLayer = object
+    mods["models.project_individual"].ProjectLayer = object
+    mods["models.human_detection_net"].ProjectLayer = object
+    mods["models.human_detection_net"].nms2D = None
+    mods["models.joint_localization_net"].ProjectLayer = object
+    mods["core.proposal"].nms2D = None
+
+    class HDN:
+        def forward(self):
+            return "reference"
+
+    mods["models.human_detection_net"].HumanDetectionNet = HDN
+    patched = integration.install(fused=True, modules=mods)
+    from fvp import project_individual, project_whole, proposal
+
+    assert mods["models.project_whole"].ProjectLayer is project_whole.ProjectLayer
+    assert mods["models.human_detection_net"].ProjectLayer is project_whole.ProjectLayer
+    assert mods["models.project_individual"].ProjectLayer is project_individual.ProjectLayer
+    assert mods["models.joint_localization_net"].ProjectLayer is project_individual.ProjectLayer
+    assert mods["core.proposal"].nms2D is proposal.nms2D
+    assert mods["models.human_detection_net"].nms2D is proposal.nms2D
+    assert HDN.forward is integration.fused_hdn_forward
+    assert len(patched) == 7
+
+
+class _CenterNet(nn.Module):
+    """Stand-in with CenterNet's attribute names (cnns_2d.py:235-295)."""
+
+    def __init__(self, J):
+        super().__init__()
+        self.front_layers = nn.Sequential(nn.Conv2d(J, 8, 3, padding=1), nn.ReLU())
+        self.encoder_decoder = nn.Conv2d(8, 8, 3, padding=1)
+        self.output_hm = nn.Conv2d(8, 1, 1)
+        self.output_size = nn.Conv2d(8, 2, 1)
+
+    def forward(self, x):
+        x, _ = torch.max(x, dim=4)
+        x = self.encoder_decoder(self.front_layers(x))
+        return self.output_hm(x), self.output_size(x)
+
+
+class _Proposal(nn.Module):
+    """Test-mode ProposalLayer semantics (human_detection_net.py:36-37,99-124)."""
+
+    def __init__(self, w):
+        super().__init__()
+        self.scale = torch.tensor(w.space_size) / (torch.tensor(w.voxels_per_axis) - 1)
+        self.bias = torch.tensor(w.space_center) - torch.tensor(w.space_size) / 2.0
+        self.min_score = w.min_score
+
+    def forward(self, topk_index, topk_confs, match_bbox, meta):
+        B, K = topk_confs.shape
+        out = torch.zeros(B, K, 7, device=topk_confs.device)
+        out[:, :, 0:3] = topk_index.float() * self.scale.to(out.device) + self.bias.to(out.device)
+        out[:, :, 4] = topk_confs
+        out[:, :, 3] = (topk_confs > self.min_score).float() - 1.0
+        out[:, :, 5:7] = match_bbox
+        return out
+
+
+def _reference_flow(net, heatmaps, meta, cameras, rt):
+    """human_detection_net.py:177-220 with plain torch ops (reference semantics)."""
+    B, J = heatmaps.shape[0], heatmaps.shape[2]
+    cubes = net.project_layer(heatmaps, meta, cameras, rt)
+    hm2d, bbox = net.center_net(cubes)
+    mx = F.max_pool2d(hm2d, 3, 1, 1)
+    nms = ((hm2d == mx).float() * hm2d).reshape(B, -1)
+    confs, flat = nms.topk(net.max_people)
+    idx2d = torch.stack([torch.div(flat, hm2d.shape[2], rounding_mode="trunc"), flat % hm2d.shape[2]], dim=2)
+    bbox_f = torch.flatten(bbox, 2, 3).permute(0, 2, 1)
+    match = torch.gather(bbox_f, 1, flat.unsqueeze(2).repeat(1, 1, 2))
+    f1d = torch.gather(torch.flatten(cubes, 2, 3).permute(0, 2, 1, 3), 1,
+                       flat.view(B, -1, 1, 1).repeat(1, 1, J, cubes.shape[4]))
+    hm1d = net.c2c_net(torch.flatten(f1d, 0, 1)).view(B, net.max_people, -1)
+    c1, i1 = hm1d.detach().topk(1)
+    centers = net.proposal_layer(torch.cat([idx2d, i1], dim=2), confs * c1.squeeze(2), match, meta)
+    return hm2d, hm1d, centers, bbox_f
+
+
+@pytest.mark.gpu
+def test_fused_hdn_forward_matches_reference_flow(gpu_device):
+    from fvp import geometry, synthetic
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    torch.manual_seed(0)
+    w = WORKLOADS["c3"]
+    net = types.SimpleNamespace()
+    net.project_layer = ProjectLayer(w.cfg(str(gpu_device)))
+    net.project_layer.verbose = False
+    net.center_net = _CenterNet(w.num_joints).to(gpu_device).eval()
+    net.c2c_net = nn.Conv1d(w.num_joints, 1, 1).to(gpu_device).eval()
+    net.proposal_layer = _Proposal(w)
+    net.max_people = w.max_people
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 3)).to(gpu_device)
+    meta = {"seq": [seq] * 3}
+    with torch.no_grad():
+        ref = _reference_flow(net, hm, meta, cams, rt)
+        got = integration.fused_hdn_forward(net, hm, meta, cams, rt)
+    assert torch.equal(got[0], ref[0])           # CenterNet heatmap: same conv on the same xy plane
+    assert torch.equal(got[3], ref[3])           # bbox preds
+    from oracle import fvp_oracle as O
+
+    rc, gc = ref[2].cpu().numpy(), got[2].cpu().numpy()
+    v2d, _, _ = O.nms2d(ref[0].cpu().numpy(), w.max_people)
+    tie_free = 0
+    for b in range(3):  # proposals identical wherever the 2-D peak value is tie-free (topk tie order unspecified)
+        for k in range(w.max_people):
+            if np.sum(v2d[b] == v2d[b, k]) == 1:
+                assert np.array_equal(gc[b, k], rc[b, k])
+                tie_free += 1
+    assert tie_free > 0
+    if tie_free == 3 * w.max_people:
+        assert torch.equal(got[1], ref[1])

@@ -55,6 +55,9 @@ class _CenterNet(nn.Module):
         self.encoder_decoder = nn.Conv2d(8, 8, 3, padding=1)
         self.output_hm = nn.Conv2d(8, 1, 1)
         self.output_size = nn.Conv2d(8, 2, 1)
+        with torch.no_grad():  # positive weights: peaks of the xy plane stay peaks (tie-free proposals)
+            for m in (self.front_layers[0], self.encoder_decoder, self.output_hm):
+                m.weight.abs_()
 
     def forward(self, x):
         x, _ = torch.max(x, dim=4)

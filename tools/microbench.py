@@ -192,6 +192,50 @@ def main():
         print(f"cl3 region={region} {rx}x{ry}: rc={rc} {'ok' if good else 'MISMATCH'} {t:8.3f} ms "
               f"{B / (t * 1e-3):10.0f} FPS-eq", flush=True)
 
+    lib.voxvar_cl4.argtypes = [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p] + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3
+    lib.voxvar_cl5.argtypes = lib.voxvar_cl4.argtypes
+    for cols in (8, 16):
+        cube.fill_(-7.0)
+        xy.fill_(-7.0)
+        rc = lib.voxvar_cl5(cols, cl.data_ptr(), B, V, J, H, W, grids.data_ptr(), X, Y, Z, cube.data_ptr(),
+                            xy.data_ptr(), stream)
+        torch.cuda.synchronize()
+        good = torch.equal(xy, ref_xy) and torch.equal(cube, ref_cube)
+        ts = []
+        for r in range(args.rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                lib.voxvar_cl5(cols, cl.data_ptr(), B, V, J, H, W, grids.data_ptr(), X, Y, Z, cube.data_ptr(),
+                               xy.data_ptr(), stream)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / args.iters)
+        t = float(np.median(ts))
+        print(f"cl5 prefetch cols={cols}: rc={rc} {'ok' if good else 'MISMATCH'} {t:8.3f} ms "
+              f"{B / (t * 1e-3):10.0f} FPS-eq", flush=True)
+    for cols in (8, 16, 32):
+        cube.fill_(-7.0)
+        xy.fill_(-7.0)
+        rc = lib.voxvar_cl4(cols, cl.data_ptr(), B, V, J, H, W, grids.data_ptr(), X, Y, Z, cube.data_ptr(),
+                            xy.data_ptr(), stream)
+        torch.cuda.synchronize()
+        good = torch.equal(xy, ref_xy) and torch.equal(cube, ref_cube)
+        ts = []
+        for r in range(args.rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                lib.voxvar_cl4(cols, cl.data_ptr(), B, V, J, H, W, grids.data_ptr(), X, Y, Z, cube.data_ptr(),
+                               xy.data_ptr(), stream)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / args.iters)
+        t = float(np.median(ts))
+        print(f"cl4 cam-outer cols={cols}: rc={rc} {'ok' if good else 'MISMATCH'} {t:8.3f} ms "
+              f"{B / (t * 1e-3):10.0f} FPS-eq", flush=True)
+
     cl_tags = ["to_cl", (16, 1), (16, 0), (32, 1), (8, 1)]
     cl_times = {str(t): [] for t in cl_tags}
     for r in range(args.rounds):

@@ -562,3 +562,218 @@ extern "C" int voxvar_cl3(int region, int rx, int ry, const float *cl, int B, in
     }
     return (int)hipGetLastError();
 }
+
+// v4: camera-outer loop (all passes of a block for camera v, then v+1), so the
+// blocks resident on an XCD tend to sample the same camera image at the same
+// time (L2 working set ~ one camera instead of all V).  Accumulators for every
+// pass live in registers; the per-voxel sum order over cameras is unchanged.
+namespace fvpx {
+template <int MAXP>
+__global__ __launch_bounds__(256) void vox_cl4(const float *__restrict__ cl, const float2 *__restrict__ grids,
+                                               float *__restrict__ cube, float *__restrict__ xy, int V, int J, int H,
+                                               int W, int X, int Y, int Z, int cols, int col_blocks) {
+    constexpr int LPV = 4, JP = 16, VPP = 64;
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = L / col_blocks;
+    const int c0 = (L - b * col_blocks) * cols;
+    const int XY = X * Y;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const int SP = cols * Z + 1;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const unsigned HW = (unsigned)(H * W);
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    float acc[MAXP][4];
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[p][k] = 0.f;
+    for (int v = 0; v < V; ++v) {
+        const __amdgpu_buffer_rsrc_t rs = rsrc_for(cl + ((size_t)b * V + v) * HW * JP, HW * JP * 4u);
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) {
+            const int i = p * VPP + threadIdx.x / LPV;
+            const bool valid = i < T;
+            float2 gg = grids[(size_t)v * N + n0 + min(i, T - 1)];
+            if (!valid) gg = make_float2(-2.f, -2.f);
+            const float ix = (gg.x + 1.0f) * sxs;
+            const float iy = (gg.y + 1.0f) * sys;
+            const float x0f = floorf(ix), y0f = floorf(iy);
+            const float wx = ix - x0f, ex = 1.0f - wx;
+            const float ny = iy - y0f, syw = 1.0f - ny;
+            const float nw = syw * ex, ne = syw * wx, sw = ny * ex, se = ny * wx;
+            const bool isnan_ = (ix != ix) || (iy != iy);
+            const int x0 = isnan_ ? -4 : (int)x0f, y0 = isnan_ ? -4 : (int)y0f;
+            const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
+            const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
+            const unsigned pix = (unsigned)(y0 * W + x0);
+            const unsigned qo = (unsigned)q * 16u;
+            const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx0) ? pix * (JP * 4u) + qo : kOOB, 0, 0);
+            const auto bq = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx1) ? (pix + 1u) * (JP * 4u) + qo : kOOB, 0, 0);
+            const auto c = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy1 & vx0) ? (pix + (unsigned)W) * (JP * 4u) + qo : kOOB, 0, 0);
+            const auto d = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy1 & vx1) ? (pix + (unsigned)W + 1u) * (JP * 4u) + qo : kOOB, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float fa = __builtin_bit_cast(float, (unsigned)a[k]);
+                const float fb = __builtin_bit_cast(float, (unsigned)bq[k]);
+                const float fc = __builtin_bit_cast(float, (unsigned)c[k]);
+                const float fd = __builtin_bit_cast(float, (unsigned)d[k]);
+                const float val = isnan_ ? NAN : __builtin_fmaf(fd, se, __builtin_fmaf(fc, sw, __builtin_fmaf(fb, ne, fa * nw)));
+                acc[p][k] = acc[p][k] + val;
+            }
+        }
+    }
+    const float fV = (float)V;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+        const int i = p * VPP + threadIdx.x / LPV;
+        if (i < T) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stage[(4 * q + k) * SP + i] = clampf(acc[p][k] / fV, 0.f, 1.f);
+        }
+    }
+    __syncthreads();
+    for (int j = 0; j < J; ++j)
+        for (int e = threadIdx.x; e < T; e += 256) cube[((size_t)b * J + j) * N + n0 + e] = stage[j * SP + e];
+    for (int e = threadIdx.x; e < J * ncols; e += 256) {
+        const int j = e / ncols, cc = e - (e / ncols) * ncols;
+        float m = -INFINITY;
+        const float *s = stage + j * SP + cc * Z;
+        for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+        xy[((size_t)b * J + j) * XY + c0 + cc] = m;
+    }
+}
+}  // namespace fvpx
+
+extern "C" int voxvar_cl4(int cols, const float *cl, int B, int V, int J, int H, int W, const float *grids, int X,
+                          int Y, int Z, float *cube, float *xy, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int XY = X * Y;
+    const int cb = (XY + cols - 1) / cols;
+    const size_t lds = (size_t)16 * (cols * Z + 1) * 4;
+    const int passes = (cols * Z + 63) / 64;
+    if (J > 16) return -1;
+#define CL4(P) hipLaunchKernelGGL((fvpx::vox_cl4<P>), dim3(cb * B), dim3(256), lds, s, cl, \
+                                  reinterpret_cast<const float2 *>(grids), cube, xy, V, J, H, W, X, Y, Z, cols, cb)
+    if (passes <= 3) CL4(3);
+    else if (passes <= 5) CL4(5);
+    else if (passes <= 10) CL4(10);
+    else return -2;
+#undef CL4
+    return (int)hipGetLastError();
+}
+
+// v5: cl + all cameras' grid coordinates loaded up front (one latency instead
+// of V), tap loads of camera v+1 issued before camera v is consumed (2 deep),
+// ballot skip kept.
+namespace fvpx {
+template <int VMAX>
+__global__ __launch_bounds__(256) void vox_cl5(const float *__restrict__ cl, const float2 *__restrict__ grids,
+                                               float *__restrict__ cube, float *__restrict__ xy, int V, int J, int H,
+                                               int W, int X, int Y, int Z, int cols, int col_blocks) {
+    constexpr int LPV = 4, JP = 16, VPP = 64;
+    using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = L / col_blocks;
+    const int c0 = (L - b * col_blocks) * cols;
+    const int XY = X * Y;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const int SP = cols * Z + 1;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const unsigned HW = (unsigned)(H * W);
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    const unsigned qo = (unsigned)q * 16u;
+    for (int i0 = 0; i0 < T; i0 += VPP) {
+        const int i = i0 + threadIdx.x / LPV;
+        const bool valid = i < T;
+        float2 g[VMAX];
+#pragma unroll
+        for (int u = 0; u < VMAX; ++u) {
+            g[u] = grids[(size_t)min(u, V - 1) * N + n0 + min(i, T - 1)];
+            if (!valid) g[u] = make_float2(-2.f, -2.f);
+        }
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        // per camera: weights, tap data, flags
+        float wt[2][4];
+        u32x4 d[2][4];
+        bool nanv[2], act[2];
+        auto issue = [&](int u, int slot) {
+            const float ix = (g[u].x + 1.0f) * sxs;
+            const float iy = (g[u].y + 1.0f) * sys;
+            const float x0f = floorf(ix), y0f = floorf(iy);
+            const float wx = ix - x0f, ex = 1.0f - wx;
+            const float ny = iy - y0f, syw = 1.0f - ny;
+            wt[slot][0] = syw * ex; wt[slot][1] = syw * wx; wt[slot][2] = ny * ex; wt[slot][3] = ny * wx;
+            nanv[slot] = (ix != ix) || (iy != iy);
+            const int x0 = nanv[slot] ? -4 : (int)x0f, y0 = nanv[slot] ? -4 : (int)y0f;
+            const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
+            const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
+            act[slot] = __builtin_amdgcn_ballot_w64((vx0 | vx1) & (vy0 | vy1)) != 0;
+            if (act[slot]) {
+                const __amdgpu_buffer_rsrc_t rs = rsrc_for(cl + ((size_t)b * V + u) * HW * JP, HW * JP * 4u);
+                const unsigned pix = (unsigned)(y0 * W + x0);
+                d[slot][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx0) ? pix * (JP * 4u) + qo : kOOB, 0, 0);
+                d[slot][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx1) ? (pix + 1u) * (JP * 4u) + qo : kOOB, 0, 0);
+                d[slot][2] = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy1 & vx0) ? (pix + (unsigned)W) * (JP * 4u) + qo : kOOB, 0, 0);
+                d[slot][3] = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy1 & vx1) ? (pix + (unsigned)W + 1u) * (JP * 4u) + qo : kOOB, 0, 0);
+            }
+        };
+        auto consume = [&](int slot) {
+            if (nanv[slot]) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] = acc[k] + NAN;
+            } else if (act[slot]) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float fa = __builtin_bit_cast(float, d[slot][0][k]);
+                    const float fb = __builtin_bit_cast(float, d[slot][1][k]);
+                    const float fc = __builtin_bit_cast(float, d[slot][2][k]);
+                    const float fd = __builtin_bit_cast(float, d[slot][3][k]);
+                    acc[k] = acc[k] + __builtin_fmaf(fd, wt[slot][3], __builtin_fmaf(fc, wt[slot][2],
+                                                     __builtin_fmaf(fb, wt[slot][1], fa * wt[slot][0])));
+                }
+            }
+        };
+        issue(0, 0);
+#pragma unroll
+        for (int u = 0; u < VMAX; ++u) {
+            if (u + 1 < VMAX && u + 1 < V) issue(u + 1, (u + 1) & 1);
+            if (u < V) consume(u & 1);
+        }
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stage[(4 * q + k) * SP + i] = clampf(acc[k] / fV, 0.f, 1.f);
+        }
+    }
+    __syncthreads();
+    for (int j = 0; j < J; ++j)
+        for (int e = threadIdx.x; e < T; e += 256) cube[((size_t)b * J + j) * N + n0 + e] = stage[j * SP + e];
+    for (int e = threadIdx.x; e < J * ncols; e += 256) {
+        const int j = e / ncols, cc = e - (e / ncols) * ncols;
+        float m = -INFINITY;
+        const float *s = stage + j * SP + cc * Z;
+        for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+        xy[((size_t)b * J + j) * XY + c0 + cc] = m;
+    }
+}
+}  // namespace fvpx
+
+extern "C" int voxvar_cl5(int cols, const float *cl, int B, int V, int J, int H, int W, const float *grids, int X,
+                          int Y, int Z, float *cube, float *xy, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int XY = X * Y;
+    const int cb = (XY + cols - 1) / cols;
+    const size_t lds = (size_t)16 * (cols * Z + 1) * 4;
+    if (J > 16 || V != 5) return -1;
+    hipLaunchKernelGGL((fvpx::vox_cl5<5>), dim3(cb * B), dim3(256), lds, s, cl, reinterpret_cast<const float2 *>(grids),
+                       cube, xy, V, J, H, W, X, Y, Z, cols, cb);
+    return (int)hipGetLastError();
+}

@@ -1,19 +1,19 @@
 // Per-person voxel cubes from the cached fine sample grid (A11-A13) and the
 // JLN xy/xz/yz max-projections (A8).
 //
-// person_cubes replaces project_individual.ProjectLayer.forward
-// (project_individual.py:222-293) without its host syncs: every block
-// recomputes its proposal's window (centers_tl, margins, start/end, skip
-// flag, :255-275) from the proposal row, so no per-proposal launch or
-// torch.sum(...) readback is needed.  One thread per output voxel (x, y, z),
-// all joints in registers; lanes run along z so grid reads and cube writes
-// are contiguous.
+// fvp_person_planes replaces project_individual.ProjectLayer.forward
+// (project_individual.py:222-293) and, fused, the max-projections of
+// joint_localization_net.py:158-160, for every proposal of a batch in one
+// launch and without host syncs: each block recomputes its proposal's window
+// (centers_tl, margins, start/end, skip flag, :255-275) from the proposal
+// row.  The frames are first re-laid out channels-last (fvp_layout.h) so the
+// taps are quad-coalesced (see fvp_voxelize.hip).
 //
-// max_planes replaces torch.cat([max(c,4), max(c,3), max(c,2)])
+// max_planes (planes of an already materialised cube) replaces torch.cat([max(c,4), max(c,3), max(c,2)])
 // (joint_localization_net.py:158-160): one block per (person, joint) reads the
 // S^3 cube once; lane = z, each wave owns S/4 y-rows; yz is a register max
 // over x, xz a register + LDS max over y, xy a wave reduction over z.
-#include "fvp_device.h"
+#include "fvp_layout.h"
 
 namespace fvp {
 
@@ -46,68 +46,6 @@ __device__ __forceinline__ Window person_window(const float *__restrict__ pc, co
         w.skip |= (w.start[a] >= w.end[a]);              // :274-275
     }
     return w;
-}
-
-template <int JT>
-__global__ __launch_bounds__(256) void person_cubes_kernel(const float *__restrict__ hm,
-                                                           const float2 *__restrict__ fgrid,
-                                                           const float *__restrict__ props, fvp_person_spec s,
-                                                           float *__restrict__ cubes, float *__restrict__ offset,
-                                                           int V, int J, int H, int W) {
-    const int p = blockIdx.z;
-    const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
-    const int ox = blockIdx.y;
-    const int oz = threadIdx.x % SZ;  // SZ <= 256 and divides blockDim handled below
-    const int oy = blockIdx.x * (blockDim.x / SZ) + threadIdx.x / SZ;
-    const bool inside = (oy < SY) && (threadIdx.x < (blockDim.x / SZ) * SZ);
-    const Window w = person_window(props + (size_t)p * 7, s);
-
-    if (offset && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 3) {
-        const int a = threadIdx.x;
-        // offset = ctl.float() / (fine - 1) * ws - ws / 2 + isz / 2   (:258)
-        offset[(size_t)p * 3 + a] =
-            ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f +
-            s.ind_size[a] / 2.0f;
-    }
-    if (!inside) return;
-
-    const int gx = w.ctl[0] + ox, gy = w.ctl[1] + oy, gz = w.ctl[2] + oz;
-    const bool valid = !w.skip && gx >= w.start[0] && gx < w.end[0] && gy >= w.start[1] && gy < w.end[1] &&
-                       gz >= w.start[2] && gz < w.end[2];
-    const size_t HW = (size_t)H * W;
-    const long long FN = (long long)s.fine[0] * s.fine[1] * s.fine[2];
-    const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
-    const size_t S3 = (size_t)SX * SY * SZ;
-    const size_t cell = ((size_t)ox * SY + oy) * SZ + oz;
-    const float fV = (float)V;
-
-    for (int j0 = 0; j0 < J; j0 += JT) {
-        float acc[JT];
-#pragma unroll
-        for (int jj = 0; jj < JT; ++jj) acc[jj] = 0.0f;
-        if (valid) {
-            for (int v = 0; v < V; ++v) {
-                const float2 gg = fgrid[(size_t)v * FN + gn];
-                const Taps tp = make_taps(gg.x, gg.y, H, W);
-                if (tp.nan) {
-#pragma unroll
-                    for (int jj = 0; jj < JT; ++jj) acc[jj] = acc[jj] + NAN;
-                } else if (tp.any) {
-                    const float *__restrict__ base = hm + ((size_t)v * J + j0) * HW;
-#pragma unroll
-                    for (int jj = 0; jj < JT; ++jj)
-                        if (j0 + jj < J) acc[jj] = acc[jj] + sample(base + (size_t)jj * HW, tp);
-                }
-            }
-        }
-#pragma unroll
-        for (int jj = 0; jj < JT; ++jj) {
-            if (j0 + jj < J) {
-                const float o = valid ? clampf(acc[jj] / fV, 0.0f, 1.0f) : 0.0f;
-                cubes[((size_t)p * J + j0 + jj) * S3 + cell] = o;
-            }
-        }
-    }
 }
 
 // planes: [3P][J][S][S]; block (p, j); 256 threads = 4 waves, lane = z.
@@ -160,25 +98,187 @@ __global__ __launch_bounds__(256) void max_planes_kernel(const float *__restrict
     }
 }
 
-}  // namespace fvp
+// Channels-last per-person kernel (batched over frames, optional fused planes).
+// Block = (proposal p, group of YG y-rows); threads = 64 z-lanes x LPV joint
+// quads.  The block walks x = 0..S-1 and, for each x, its YG rows:
+//   xy[x][y] = max_z   -> wave shuffles over z + one LDS combine per x
+//   yz[y][z] = max_x   -> registers (the block owns its y rows), stored at the end
+//   xz[x][z] = max_y   -> max over the block's rows, then one atomicMax per
+//                         (x, z, joint) into the pre-zeroed plane (values are
+//                         clamped to [0,1] or NaN, so unsigned order == float order)
+// Outside-window voxels are 0 exactly as in the reference cube.
+template <int LPV, int YG>
+__global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
+                                                             const float2 *__restrict__ fgrid,
+                                                             const float *__restrict__ props,
+                                                             const int32_t *__restrict__ frame_of, fvp_person_spec s,
+                                                             float *__restrict__ cubes, float *__restrict__ planes,
+                                                             float *__restrict__ offset, int P, int V, int J, int H,
+                                                             int W) {
+    constexpr int JP = 4 * LPV;
+    constexpr int NW = LPV;  // waves per block (64*LPV threads)
+    __shared__ float xy_part[NW][YG][JP];
+    const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
+    const int ngroups = (SY + YG - 1) / YG;
+    const int p = blockIdx.x / ngroups;
+    const int yg0 = (blockIdx.x - p * ngroups) * YG;
+    const Window w = person_window(props + (size_t)p * 7, s);
+    if (offset && yg0 == 0 && threadIdx.x < 3) {
+        const int a = threadIdx.x;
+        offset[(size_t)p * 3 + a] =
+            ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int zl = threadIdx.x / LPV, q = threadIdx.x % LPV;
+    const int b = frame_of ? frame_of[p] : 0;
+    const unsigned HW = (unsigned)(H * W);
+    const unsigned pix_bytes = JP * 4u;
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    const long long FN = (long long)s.fine[0] * s.fine[1] * s.fine[2];
+    const size_t SS = (size_t)SY * SZ;
+    const size_t S3 = (size_t)SX * SS;
+    float *xy_pl = planes ? planes + (size_t)p * J * SX * SY : nullptr;
+    float *xz_pl = planes ? planes + ((size_t)P + p) * J * SX * SZ : nullptr;
+    float *yz_pl = planes ? planes + ((size_t)2 * P + p) * J * SY * SZ : nullptr;
+    const bool zok = zl < SZ;
+    const int gz = w.ctl[2] + zl;
+    const bool zin = zok && gz >= w.start[2] && gz < w.end[2];
 
-extern "C" int fvp_person_cubes(const float *heatmaps, int V, int J, int H, int W, const float *fine_grid,
-                                const fvp_person_spec *spec, const float *proposals, int P, float *cubes,
-                                float *offset, void *stream) {
-    if (!heatmaps || !fine_grid || !spec || !cubes) return FVP_ERR_NULL;
-    if (P <= 0) return FVP_OK;
-    if (!proposals) return FVP_ERR_NULL;
-    if (V <= 0 || J <= 0 || H < 2 || W < 2) return FVP_ERR_SHAPE;
-    const int SX = spec->bins[0], SY = spec->bins[1], SZ = spec->bins[2];
-    if (SX <= 0 || SY <= 0 || SZ <= 0 || SZ > 256 || spec->fine[0] <= 1 || spec->fine[1] <= 1 ||
-        spec->fine[2] <= 1)
-        return FVP_ERR_SHAPE;
-    const int rows = 256 / SZ;  // y rows per block
-    dim3 grid((SY + rows - 1) / rows, SX, P);
-    hipLaunchKernelGGL((fvp::person_cubes_kernel<16>), grid, dim3(256), 0, (hipStream_t)stream, heatmaps,
-                       reinterpret_cast<const float2 *>(fine_grid), proposals, *spec, cubes, offset, V, J, H, W);
-    return (int)hipGetLastError();
+    float yzacc[YG][4];
+#pragma unroll
+    for (int r = 0; r < YG; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) yzacc[r][k] = 0.0f;
+
+    for (int x = 0; x < SX; ++x) {
+        const int gx = w.ctl[0] + x;
+        const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
+        float xzacc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < YG; ++r) {
+            const int y = yg0 + r;
+            const int gy = w.ctl[1] + y;
+            const bool valid = xin && zin && y < SY && gy >= w.start[1] && gy < w.end[1];
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            if (__builtin_amdgcn_ballot_w64(valid)) {
+                const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
+                for (int v = 0; v < V; ++v) {
+                    float2 gg = fgrid[(size_t)v * FN + gn];
+                    if (!valid) gg = make_float2(-2.f, -2.f);
+                    const float ix = (gg.x + 1.0f) * sxs;
+                    const float iy = (gg.y + 1.0f) * sys;
+                    const bool isnan_ = (ix != ix) || (iy != iy);
+                    const float x0f = floorf(ix), y0f = floorf(iy);
+                    const float wx = ix - x0f, ex = 1.0f - wx;
+                    const float ny = iy - y0f, syw = 1.0f - ny;
+                    const float nw = syw * ex, ne = syw * wx, sw = ny * ex, se = ny * wx;
+                    const int x0 = isnan_ ? -4 : (int)x0f, y0 = isnan_ ? -4 : (int)y0f;
+                    const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
+                    const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
+                    if (isnan_) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) acc[k] = acc[k] + NAN;
+                    }
+                    if (!__builtin_amdgcn_ballot_w64((vx0 | vx1) & (vy0 | vy1))) continue;
+                    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(cl + ((size_t)b * V + v) * HW * JP, HW * pix_bytes);
+                    const unsigned pix = (unsigned)(y0 * W + x0);
+                    const auto ta = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx0) ? pix * pix_bytes + qo : kOOB, 0, 0);
+                    const auto tb = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (vy0 & vx1) ? (pix + 1u) * pix_bytes + qo : kOOB, 0, 0);
+                    const auto tc = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (vy1 & vx0) ? (pix + (unsigned)W) * pix_bytes + qo : kOOB, 0, 0);
+                    const auto td = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (vy1 & vx1) ? (pix + (unsigned)W + 1u) * pix_bytes + qo : kOOB, 0, 0);
+                    if (!isnan_) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const float fa = __builtin_bit_cast(float, (unsigned)ta[k]);
+                            const float fb = __builtin_bit_cast(float, (unsigned)tb[k]);
+                            const float fc = __builtin_bit_cast(float, (unsigned)tc[k]);
+                            const float fd = __builtin_bit_cast(float, (unsigned)td[k]);
+                            acc[k] = acc[k] + __builtin_fmaf(fd, se, __builtin_fmaf(fc, sw, __builtin_fmaf(fb, ne, fa * nw)));
+                        }
+                    }
+                }
+            }
+            float o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                // clamp(0,1) of the mean; +0.0f turns a -0 into +0 (unsigned max order below)
+                o[k] = valid ? clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f : 0.0f;
+                if (!zok || y >= SY) o[k] = -INFINITY;  // lanes/rows beyond the cube take no part
+            }
+            if (cubes && zok && y < SY) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * q + k < J) cubes[((size_t)p * J + 4 * q + k) * S3 + ((size_t)x * SY + y) * SZ + zl] = o[k];
+            }
+            if (planes) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    yzacc[r][k] = nanmax(yzacc[r][k], o[k]);
+                    xzacc[k] = nanmax(xzacc[k], o[k]);
+                    float m = o[k];
+#pragma unroll
+                    for (int off = LPV; off < 64; off <<= 1) m = nanmax(m, __shfl_xor(m, off));
+                    if (lane < LPV) xy_part[wave][r][4 * q + k] = m;
+                }
+            }
+        }
+        if (planes) {
+            __syncthreads();
+            for (int e = threadIdx.x; e < YG * JP; e += 64 * LPV) {
+                const int r = e / JP, j = e - (e / JP) * JP;
+                const int y = yg0 + r;
+                if (j < J && y < SY) {
+                    float m = xy_part[0][r][j];
+#pragma unroll
+                    for (int ww = 1; ww < NW; ++ww) m = nanmax(m, xy_part[ww][r][j]);
+                    xy_pl[((size_t)j * SX + x) * SY + y] = m;
+                }
+            }
+            if (zok) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * q + k < J)
+                        atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl,
+                                  __builtin_bit_cast(unsigned, xzacc[k]));
+            }
+            __syncthreads();
+        }
+    }
+    if (planes && zok) {
+#pragma unroll
+        for (int r = 0; r < YG; ++r) {
+            const int y = yg0 + r;
+            if (y < SY) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * q + k < J) yz_pl[((size_t)(4 * q + k) * SY + y) * SZ + zl] = yzacc[r][k];
+            }
+        }
+    }
 }
+
+template <int LPV>
+static void launch_person_cl(const float *cl, const float2 *fgrid, const float *props, const int32_t *frame_of,
+                             const fvp_person_spec &s, float *cubes, float *planes, float *offset, int P, int V, int J,
+                             int H, int W, hipStream_t st) {
+    const int SY = s.bins[1];
+    if (P >= 64) {
+        const int ng = (SY + 7) / 8;
+        hipLaunchKernelGGL((person_cl_kernel<LPV, 8>), dim3((unsigned)(P * ng)), dim3(64 * LPV), 0, st, cl, fgrid,
+                           props, frame_of, s, cubes, planes, offset, P, V, J, H, W);
+    } else {
+        const int ng = (SY + 3) / 4;
+        hipLaunchKernelGGL((person_cl_kernel<LPV, 4>), dim3((unsigned)(P * ng)), dim3(64 * LPV), 0, st, cl, fgrid,
+                           props, frame_of, s, cubes, planes, offset, P, V, J, H, W);
+    }
+}
+
+}  // namespace fvp
 
 extern "C" int fvp_max_planes(const float *cubes, int P, int J, int S, float *planes, void *stream) {
     if (!cubes || !planes) return FVP_ERR_NULL;
@@ -186,5 +286,45 @@ extern "C" int fvp_max_planes(const float *cubes, int P, int J, int S, float *pl
     if (J <= 0 || S <= 0 || S > 64) return FVP_ERR_SHAPE;
     hipLaunchKernelGGL(fvp::max_planes_kernel, dim3(P * J), dim3(256), 0, (hipStream_t)stream, cubes, planes, P, J,
                        S);
+    return (int)hipGetLastError();
+}
+
+extern "C" size_t fvp_person_workspace_bytes(int B, int V, int J, int H, int W) {
+    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
+    return (size_t)B * fvp::cl_frame_bytes(V, J, H, W);
+}
+
+extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int H, int W, const float *fine_grid,
+                                 const fvp_person_spec *spec, const float *proposals, const int32_t *frame_of, int P,
+                                 float *cubes, float *planes, float *offset, void *workspace, size_t workspace_bytes,
+                                 void *stream) {
+    if (!heatmaps || !fine_grid || !spec) return FVP_ERR_NULL;
+    if (P <= 0) return FVP_OK;
+    if (!proposals) return FVP_ERR_NULL;
+    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2) return FVP_ERR_SHAPE;
+    const int SX = spec->bins[0], SY = spec->bins[1], SZ = spec->bins[2];
+    if (SX <= 0 || SY <= 0 || SZ <= 0 || SZ > 64 || spec->fine[0] <= 1 || spec->fine[1] <= 1 || spec->fine[2] <= 1)
+        return FVP_ERR_SHAPE;
+    if (planes && !(SX == SY && SY == SZ)) return FVP_ERR_SHAPE;  // torch.cat of the planes needs a cubic volume
+    const size_t need = (size_t)B * fvp::cl_frame_bytes(V, J, H, W);
+    if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    float *cl = reinterpret_cast<float *>(workspace);
+    if (planes) {  // xz is reduced with atomicMax over non-negative floats: start from +0
+        const hipError_t e = hipMemsetAsync(planes + (size_t)P * J * SX * SZ, 0, (size_t)P * J * SX * SZ * 4, st);
+        if (e != hipSuccess) return (int)e;
+    }
+    const float2 *fg = reinterpret_cast<const float2 *>(fine_grid);
+#define FVP_PERSON_CASE(L)                                                                                            \
+    fvp::launch_layout<L, float>(heatmaps, B, V, J, H, W, cl, st);                                                   \
+    fvp::launch_person_cl<L>(cl, fg, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, W, st);         \
+    break;
+    switch (fvp::lanes_per_voxel(J)) {
+        case 1: FVP_PERSON_CASE(1)
+        case 2: FVP_PERSON_CASE(2)
+        case 4: FVP_PERSON_CASE(4)
+        default: FVP_PERSON_CASE(8)
+    }
+#undef FVP_PERSON_CASE
     return (int)hipGetLastError();
 }

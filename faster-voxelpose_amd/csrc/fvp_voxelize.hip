@@ -25,42 +25,9 @@
 // so the cube is written as contiguous runs per joint and the xy max over z
 // is read back from LDS.  Arithmetic per tap and the camera/sum order are the
 // reference's (fvp_device.h), so the result is bit-exact.
-#include "fvp_device.h"
+#include "fvp_layout.h"
 
 namespace fvp {
-
-constexpr unsigned kOOB = 0x80000000u;  // beyond any descriptor range -> loads return 0
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base, unsigned bytes) {
-    const unsigned long long p = (unsigned long long)base;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
-    void *b = (void *)(((unsigned long long)hi << 32) | lo);
-    return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-// -- layout pass ----------------------------------------------------------------
-// thread = (pixel, joint quad q): reads joints 4q..4q+3 of one pixel (the lanes
-// of a wave cover 64/LPV consecutive pixels -> coalesced plane reads), writes
-// one float4 (a wave writes a contiguous 1 KiB run).
-template <int LPV, typename T>
-__global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict__ hm, float4 *__restrict__ cl, int J,
-                                                             int HW, long long total_px) {
-    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-    const long long pxg = gid / LPV;
-    const int q = (int)(gid - pxg * LPV);
-    if (pxg >= total_px) return;
-    const long long bv = pxg / HW;
-    const int pix = (int)(pxg - bv * HW);
-    const T *__restrict__ src = hm + (size_t)bv * J * HW + pix;
-    const int j = 4 * q;
-    float4 o;
-    o.x = (j + 0 < J) ? to_f32(src[(size_t)(j + 0) * HW]) : 0.f;
-    o.y = (j + 1 < J) ? to_f32(src[(size_t)(j + 1) * HW]) : 0.f;
-    o.z = (j + 2 < J) ? to_f32(src[(size_t)(j + 2) * HW]) : 0.f;
-    o.w = (j + 3 < J) ? to_f32(src[(size_t)(j + 3) * HW]) : 0.f;
-    cl[pxg * LPV + q] = o;
-}
 
 // -- gather pass ----------------------------------------------------------------
 template <int LPV>
@@ -157,13 +124,9 @@ __global__ __launch_bounds__(256) void voxelize_cl_kernel(const float *__restric
     }
 }
 
-static int lanes_per_voxel(int J) { return J <= 4 ? 1 : J <= 8 ? 2 : J <= 16 ? 4 : 8; }
 
 static int cols_per_block(int Z) { return Z >= 320 ? 1 : 320 / Z; }
 
-static size_t cl_frame_bytes(int V, int J, int H, int W) {
-    return (size_t)V * H * W * 4 * lanes_per_voxel(J) * sizeof(float);
-}
 
 // Frames per chunk: keep the channels-last copy of a chunk well inside the
 // 256 MB Infinity Cache (measured best at ~64-80 MB for C2: 8 frames).

@@ -171,31 +171,46 @@ def _(size, flat):
 
 
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("fvp::person_cubes", mutates_args=(), device_types="cuda")
-def person_cubes(heatmaps_frame: torch.Tensor, fine_grid: torch.Tensor, proposals: torch.Tensor,
-                 fine: list[int], scale: list[float], bias: list[float], whole_size: list[float],
-                 ind_size: list[float], bins: list[int]) -> tuple[torch.Tensor, torch.Tensor]:
-    hm = _dev_f32(heatmaps_frame, "heatmaps")
+@torch.library.custom_op("fvp::person_planes", mutates_args=(), device_types="cuda")
+def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: torch.Tensor,
+                  frame_of: Optional[torch.Tensor], fine: list[int], scale: list[float], bias: list[float],
+                  whole_size: list[float], ind_size: list[float], bins: list[int], want_cubes: bool,
+                  want_planes: bool) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    hm = _dev_f32(heatmaps, "heatmaps")
     fg = _dev_f32(fine_grid, "fine sample grid")
     pc = _dev_f32(proposals, "proposal_centers")
-    V, J, H, W = hm.shape
+    B, V, J, H, W = hm.shape
     P = pc.shape[0]
     if fg.numel() != V * fine[0] * fine[1] * fine[2] * 2:
         raise _lib.FvpError("fvp: fine sample grid does not match fine_voxels_per_axis")
-    cubes = torch.empty((P, J, bins[0], bins[1], bins[2]), dtype=torch.float32, device=hm.device)
+    fo = None
+    if frame_of is not None:
+        fo = frame_of.to(device=hm.device, dtype=torch.int32).contiguous()
+        if fo.numel() != P:
+            raise _lib.FvpError("fvp: frame_of must have one entry per proposal")
+    SX, SY, SZ = bins
+    cubes = torch.empty((P, J, SX, SY, SZ) if want_cubes else (0,), dtype=torch.float32, device=hm.device)
+    planes = torch.empty((3 * P, J, SX, SY) if want_planes else (0,), dtype=torch.float32, device=hm.device)
     offset = torch.empty((P, 3), dtype=torch.float32, device=hm.device)
     if P > 0:
+        ws_bytes = _lib.load().fvp_person_workspace_bytes(B, V, J, H, W)
+        if ws_bytes == 0:
+            raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
         spec = PersonSpec(_i3(fine), _f3(scale), _f3(bias), _f3(whole_size), _f3(ind_size), _i3(bins))
-        _lib.call("fvp_person_cubes", _ptr(hm), V, J, H, W, _ptr(fg), spec, _ptr(pc), P, _ptr(cubes), _ptr(offset),
-                  _stream(hm))
-    return cubes, offset
+        _lib.call("fvp_person_planes", _ptr(hm), B, V, J, H, W, _ptr(fg), spec, _ptr(pc), _ptr(fo), P,
+                  _ptr(cubes) if want_cubes else None, _ptr(planes) if want_planes else None, _ptr(offset),
+                  _ptr(ws), ws_bytes, _stream(hm))
+    return cubes, planes, offset
 
 
-@person_cubes.register_fake
-def _(heatmaps_frame, fine_grid, proposals, fine, scale, bias, whole_size, ind_size, bins):
-    P = proposals.shape[0]
-    return (heatmaps_frame.new_empty((P, heatmaps_frame.shape[1], bins[0], bins[1], bins[2])),
-            heatmaps_frame.new_empty((P, 3)))
+@person_planes.register_fake
+def _(heatmaps, fine_grid, proposals, frame_of, fine, scale, bias, whole_size, ind_size, bins, want_cubes,
+      want_planes):
+    P, J = proposals.shape[0], heatmaps.shape[2]
+    return (heatmaps.new_empty((P, J, bins[0], bins[1], bins[2]) if want_cubes else (0,)),
+            heatmaps.new_empty((3 * P, J, bins[0], bins[1]) if want_planes else (0,)),
+            heatmaps.new_empty((P, 3)))
 
 
 @torch.library.custom_op("fvp::max_planes", mutates_args=(), device_types="cuda")

@@ -7,11 +7,13 @@ attributes (``center_grid`` is read by JointLocalizationNet's soft-argmax,
 joint_localization_net.py:165; ``fine_voxels_per_axis``, ``scale``, ``bias``,
 ``fine_grid``, ``sample_grid``).  The per-sequence fine sample grid is built
 by ``fvp_project_grid`` over the fine whole-space grid; all proposals of the
-frame are voxelised by ONE ``fvp_person_cubes`` launch that evaluates each
+frame are voxelised by ONE ``fvp_person_planes`` launch that evaluates each
 proposal's window on the device (no per-proposal loop, no host syncs --
 project_individual.py:272-275 read ``torch.sum(start >= end)`` back per
-proposal).  ``forward_planes`` additionally returns the xy/xz/yz
-max-projections JointLocalizationNet concatenates (joint_localization_net.py:158-160).
+proposal).  ``forward_planes`` returns the xy/xz/yz max-projections
+JointLocalizationNet concatenates (joint_localization_net.py:158-160) without
+materialising the 64^3 cubes; ``forward_batch`` does that for every valid
+proposal of a batch of frames in one launch.
 """
 from __future__ import annotations
 
@@ -93,16 +95,41 @@ class ProjectLayer(nn.Module):
             self.sample_grid[curr_seq] = self.build_sample_grid(cameras, curr_seq, resize_transform, heatmaps.device)
         return self.sample_grid[curr_seq]
 
+    def _args(self):
+        c = self._const
+        return ([int(v) for v in c["fine"]], [float(v) for v in c["scale"]], [float(v) for v in c["bias"]],
+                [float(v) for v in c["whole_size"]], [float(v) for v in c["ind_size"]],
+                [int(v) for v in c["ind_bins"]])
+
     def forward(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
         ops.forward_only(heatmaps, proposal_centers)
         grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
-        c = self._const
-        return ops.person_cubes(heatmaps[index], grid, proposal_centers,
-                                [int(v) for v in c["fine"]], [float(v) for v in c["scale"]],
-                                [float(v) for v in c["bias"]], [float(v) for v in c["whole_size"]],
-                                [float(v) for v in c["ind_size"]], [int(v) for v in c["ind_bins"]])
+        cubes, _, offset = ops.person_planes(heatmaps[index:index + 1], grid, proposal_centers, None, *self._args(),
+                                             True, False)
+        return cubes, offset
 
     def forward_planes(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
-        """(planes[3P,J,S,S], offset[P,3]): the JLN input at joint_localization_net.py:158-160."""
-        cubes, offset = self.forward(heatmaps, index, meta, proposal_centers, cameras, resize_transform)
-        return ops.max_planes(cubes), offset
+        """(planes[3P,J,S,S], offset[P,3]) without materialising the cubes: the JLN
+        input at joint_localization_net.py:158-160 for frame ``index``."""
+        ops.forward_only(heatmaps, proposal_centers)
+        grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
+        _, planes, offset = ops.person_planes(heatmaps[index:index + 1], grid, proposal_centers, None, *self._args(),
+                                              False, True)
+        return planes, offset
+
+    def forward_batch(self, heatmaps, meta, proposal_centers, mask, cameras, resize_transform):
+        """Every valid proposal of the batch in ONE launch (the reference loops
+        frames and proposals with host syncs, joint_localization_net.py:148-151,
+        project_individual.py:272-275).  proposal_centers [B,K,7], mask [B,K] bool.
+        Returns (planes [3P,J,S,S] in (frame, proposal) order of ``mask``, offset
+        [P,3], frame_of [P]).  Frames must share one sequence's cameras."""
+        ops.forward_only(heatmaps, proposal_centers)
+        grid = self._seq_grid(heatmaps, 0, meta, cameras, resize_transform)
+        seqs = list(meta["seq"])[: heatmaps.shape[0]]
+        if len(set(seqs)) != 1:
+            raise ValueError("forward_batch: all frames must belong to one sequence")
+        idx = mask.nonzero()  # one host sync for the whole batch
+        frame_of = idx[:, 0].to(torch.int32)
+        props = proposal_centers[idx[:, 0], idx[:, 1]]
+        _, planes, offset = ops.person_planes(heatmaps, grid, props, frame_of, *self._args(), False, True)
+        return planes, offset, frame_of

@@ -123,17 +123,25 @@ int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z,
 int fvp_gather_bbox(const float *size, int B, int X, int Y,
                     const int64_t *flat, int K, float *out, void *stream);
 
-/* Per-person cubes of one frame from its cached fine sample grid.
- * Replaces project_individual.ProjectLayer.forward (project_individual.py:222-293).
- *   heatmaps    device [V][J][H][W] (the frame `index` of the batch)
+/* Per-person voxelisation of a batch of proposals from the cached fine
+ * sample grid, optionally fused with the JLN max-projections.
+ * Replaces project_individual.ProjectLayer.forward (project_individual.py:222-293)
+ * and torch.cat([max(c,4), max(c,3), max(c,2)]) (joint_localization_net.py:158-160).
+ *   heatmaps    device [B][V][J][H][W] (the frames the proposals refer to)
  *   fine_grid   device [V][FX][FY][FZ][2]
  *   proposals   device [P][7] (x,y,z mm, gt, conf, bbox_w, bbox_h)
- *   cubes       device [P][J][SX][SY][SZ] (output, fully written)
- *   offset      device [P][3] (output) */
-int fvp_person_cubes(const float *heatmaps, int V, int J, int H, int W,
-                     const float *fine_grid, const fvp_person_spec *spec,
-                     const float *proposals, int P,
-                     float *cubes, float *offset, void *stream);
+ *   frame_of    device int32 [P]: frame of each proposal in [0,B) (NULL: all frame 0)
+ *   cubes       device [P][J][SX][SY][SZ] or NULL (outside-window voxels are 0)
+ *   planes      device [3P][J][S][S] or NULL: xy (max over z) for p < P, then xz
+ *               (max over y), then yz (max over x); needs SX == SY == SZ <= 64
+ *   offset      device [P][3] or NULL
+ *   workspace   >= fvp_person_workspace_bytes(B,V,J,H,W) bytes (channels-last frames) */
+size_t fvp_person_workspace_bytes(int B, int V, int J, int H, int W);
+int fvp_person_planes(const float *heatmaps, int B, int V, int J, int H, int W,
+                      const float *fine_grid, const fvp_person_spec *spec,
+                      const float *proposals, const int32_t *frame_of, int P,
+                      float *cubes, float *planes, float *offset,
+                      void *workspace, size_t workspace_bytes, void *stream);
 
 /* xy / xz / yz max-projections of per-person cubes [P][J][S][S][S] into
  * planes [3P][J][S][S] (xy block first, then xz, then yz).

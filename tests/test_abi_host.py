@@ -50,6 +50,12 @@ def test_argument_validation_without_gpu():
     assert lib.fvp_nms_topk(1, 1, 2, 2, 0, 10, 1, 1, None, None) == 1002  # K > X*Y
     assert lib.fvp_nms_topk(1, 2, 8, 8, 10, 5, 1, 1, None, None) == 1002  # frame stride < X*Y
     assert lib.fvp_max_planes(1, 1, 1, 65, 1, None) == 1002            # S > 64
+    spec = _lib.PersonSpec((253, 253, 64), (0.03, 0.03, 0.03), (0, 0, 0), (8000, 8000, 2000), (2000,) * 3, (64,) * 3)
+    assert lib.fvp_person_planes(None, 1, 5, 15, 128, 240, 1, spec, 1, None, 1, None, 1, None, 1, 10, None) == 1001
+    assert lib.fvp_person_planes(1, 1, 5, 15, 128, 240, 1, spec, 1, None, 1, None, 1, None, None, 0, None) == 1003
+    assert lib.fvp_person_workspace_bytes(2, 5, 15, 128, 240) == 2 * 5 * 128 * 240 * 16 * 4
+    bad = _lib.PersonSpec((253, 253, 64), (0.03,) * 3, (0,) * 3, (8000,) * 3, (2000,) * 3, (64, 64, 32))
+    assert lib.fvp_person_planes(1, 1, 5, 15, 128, 240, 1, bad, 1, None, 1, None, 1, None, 1, 1 << 30, None) == 1002
     assert lib.fvp_gather_columns(None, 1, 1, 1, 1, 1, None, 1, None, None) == 1001
     with pytest.raises(_lib.FvpError, match="NULL"):
         _lib.check(1001, "fvp_voxelize")

@@ -338,3 +338,72 @@ def test_more_than_32_joints_rejected(gpu_device):
     sg = torch.zeros((1, 8, 2), device=gpu_device)
     with pytest.raises(_lib.FvpError, match="J <= 32"):
         torch.ops.fvp.voxelize(hm, sg, None, 2, 2, 2, True, True)
+
+
+def _jln_setup(gpu_device, J=15, frames=3):
+    from fvp import geometry, synthetic
+    from fvp.project_individual import ProjectLayer
+    from fvp.workloads import WORKLOADS
+    import dataclasses
+
+    w = dataclasses.replace(WORKLOADS["c3"], num_joints=J)
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, frames)).to(gpu_device)
+    return w, layer, cams, seq, rt, hm
+
+
+def _props(w, f, rng, n_extra):
+    from fvp import synthetic
+
+    base = synthetic.proposals_for_frame(w, f, 4)
+    extra = np.zeros((n_extra, 7), np.float32)
+    extra[:, 0] = rng.uniform(-4600, 4600, n_extra)
+    extra[:, 1] = -500 + rng.uniform(-4600, 4600, n_extra)
+    extra[:, 2] = rng.uniform(200, 1500, n_extra)
+    extra[:, 5:7] = rng.uniform(-0.2, 1.2, (n_extra, 2))
+    return np.concatenate([base, extra])
+
+
+@pytest.mark.parametrize("J", [15, 17])
+def test_person_planes_fused_vs_oracle(gpu_device, J):
+    """Fused planes (no cube) == max-projections of the oracle's cubes, incl.
+    clipped, skipped and negative-margin windows; J=17 takes the 8-lane path."""
+    from fvp import geometry
+
+    w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, J=J, frames=1)
+    props = _props(w, 0, np.random.default_rng(1), 6)
+    planes, offset = layer.forward_planes(hm, 0, {"seq": [seq]}, torch.from_numpy(props).to(gpu_device), cams, rt)
+    ind = O.Individual(w.space_size, w.space_center, w.ind_space_size, w.ind_voxels_per_axis)
+    fsg = layer.sample_grid[seq].cpu().numpy()
+    cubes, off = ind.person_cubes(hm[0].cpu().numpy(), fsg, props)
+    _assert_same(planes.cpu().numpy(), O.max_planes(cubes), "fused planes")
+    _assert_same(offset.cpu().numpy(), off, "offset")
+    c2, _ = layer(hm, 0, {"seq": [seq]}, torch.from_numpy(props).to(gpu_device), cams, rt)
+    _assert_same(c2.cpu().numpy(), cubes, "cubes")
+
+
+def test_person_planes_batched_matches_per_frame(gpu_device):
+    """forward_batch (one launch, >= 64 proposals -> 8-row blocks) == per-frame calls."""
+    w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, frames=8)
+    rng = np.random.default_rng(2)
+    props = torch.from_numpy(np.stack([_props(w, f, rng, 6) for f in range(8)])).to(gpu_device)  # [8,10,7]
+    mask = torch.rand((8, 10), generator=torch.Generator().manual_seed(3)).to(gpu_device) > 0.15
+    meta = {"seq": [seq] * 8}
+    planes, offset, frame_of = layer.forward_batch(hm, meta, props, mask, cams, rt)
+    P = int(mask.sum())
+    assert planes.shape[0] == 3 * P and P >= 64 // 2
+    k = 0
+    for f in range(8):
+        sel = props[f][mask[f]]
+        if sel.shape[0] == 0:
+            continue
+        pf, of = layer.forward_planes(hm, f, meta, sel, cams, rt)
+        n = sel.shape[0]
+        for part in range(3):
+            assert torch.equal(planes[part * P + k: part * P + k + n], pf[part * n:(part + 1) * n])
+        assert torch.equal(offset[k:k + n], of)
+        k += n
+    assert k == P

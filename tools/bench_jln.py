@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""JLN per-person line (SURVEY.md §8(d) "JLN, per proposal (separate line)"):
+project_individual.ProjectLayer.forward (64^3 cubes) + xy/xz/yz max planes for
+K proposals per frame, Panoptic demo geometry (configs/panoptic/jln64.yaml).
+
+    python tools/bench_jln.py [--frames 16] [--proposals 10] [--steps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--proposals", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--workload", default="c3")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from fvp import geometry, synthetic
+    from fvp.project_individual import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    dev = torch.device("cuda:0")
+    w = WORKLOADS[args.workload]
+    cams, seq = w.cameras()
+    layer = ProjectLayer(w.cfg("cuda:0"))
+    layer.verbose = False
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
+    F, P = args.frames, args.proposals
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, F)).to(dev)
+    rng = np.random.default_rng(5)
+    props = []
+    for f in range(F):
+        pr = synthetic.proposals_for_frame(w, f, 4)
+        extra = np.zeros((P - 4, 7), np.float32)
+        extra[:, 0] = w.space_center[0] + rng.uniform(-3500, 3500, P - 4)
+        extra[:, 1] = w.space_center[1] + rng.uniform(-3500, 3500, P - 4)
+        extra[:, 2] = 900.0
+        extra[:, 4] = 0.5
+        extra[:, 5:7] = 0.5
+        props.append(torch.from_numpy(np.concatenate([pr, extra])[:P]).to(dev))
+    meta = {"seq": [seq] * F}
+    t0 = time.perf_counter()
+    layer.forward_planes(hm, 0, meta, props[0], cams, rt)  # builds the fine sample grid (once per sequence)
+    torch.cuda.synchronize()
+    cache_ms = (time.perf_counter() - t0) * 1e3
+
+    allp = torch.stack(props)
+    mask = torch.ones((F, P), dtype=torch.bool, device=dev)
+
+    def per_frame():
+        for f in range(F):
+            layer.forward_planes(hm, f, meta, props[f], cams, rt)
+
+    def batched():
+        layer.forward_batch(hm, meta, allp, mask, cams, rt)
+
+    def timeit(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.steps
+
+    ms_frame = timeit(per_frame)
+    ms = timeit(batched)
+    J = w.num_joints
+    n_prop = F * P
+    print(json.dumps({
+        "metric": "JLN per-person voxelize + xy/xz/yz max planes", "unit": "proposals/s",
+        "value": round(n_prop / (ms * 1e-3), 1), "us_per_proposal": round(ms * 1e3 / n_prop, 2),
+        "frames_per_s_at_K": round(F / (ms * 1e-3), 1), "K": P, "frames": F,
+        "config": f"{w.name}: {len(cams[seq])} cams, J={J}, 64^3 person cubes from a 253x253x64 fine grid",
+        "cube_bytes_per_proposal": J * 64 ** 3 * 4, "plane_bytes_per_proposal": 3 * J * 64 * 64 * 4,
+        "per_frame_calls_us_per_proposal": round(ms_frame * 1e3 / n_prop, 2),
+        "path": "forward_batch: one fvp_person_planes launch for all frames' proposals (fused planes, no cubes)",
+        "cache_build_ms": round(cache_ms, 1)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -107,6 +107,86 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__re
     }
 }
 
+// Fast path for K <= KMAX: the map is staged in LDS with coalesced loads, each
+// thread keeps a sorted top-KMAX of its own elements in registers while it
+// evaluates the 3x3 peak mask, and K block-wide arg-max rounds merge the
+// per-thread heads (no rescans of the map).
+template <int KMAX>
+__global__ __launch_bounds__(kNmsThreads) void nms_topk_small_kernel(const float *__restrict__ prob, long long stride,
+                                                                     int X, int Y, int K, float *__restrict__ vals,
+                                                                     int64_t *__restrict__ flat,
+                                                                     int64_t *__restrict__ xy) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float *map = reinterpret_cast<float *>(smem);  // [X*Y]
+    __shared__ Cand red[kNmsThreads / kWave];
+    __shared__ int win_tid;
+    const int M = X * Y;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float *__restrict__ p = prob + (size_t)b * stride;
+    for (int e = tid; e < M; e += kNmsThreads) map[e] = p[e];
+    __syncthreads();
+
+    Cand top[KMAX];
+#pragma unroll
+    for (int t = 0; t < KMAX; ++t) top[t] = Cand{-INFINITY, 0x7fffffff};
+    int have = 0;
+    for (int e = tid; e < M; e += kNmsThreads) {
+        const int ex = e / Y, ey = e - (e / Y) * Y;
+        const float c = map[e];
+        float m = -INFINITY;
+        bool nan = false;
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = ex + dx;
+            if (xx < 0 || xx >= X) continue;
+            for (int dy = -1; dy <= 1; ++dy) {
+                const int yy = ey + dy;
+                if (yy < 0 || yy >= Y) continue;
+                const float q = map[xx * Y + yy];
+                nan |= (q != q);
+                m = fmaxf(m, q);
+            }
+        }
+        Cand cand{((!nan && c == m) ? 1.0f : 0.0f) * c, e};
+        // sorted insertion (descending by `before`), fully unrolled: registers only
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) {
+            if (t >= have || before(cand, top[t])) {
+                const Cand tmp = top[t];
+                top[t] = cand;
+                cand = tmp;
+            }
+        }
+        have = have < KMAX ? have + 1 : KMAX;
+    }
+    // merge: K rounds of block arg-max over the per-thread heads
+    for (int k = 0; k < K; ++k) {
+        Cand best = have > 0 ? top[0] : Cand{-INFINITY, 0x7fffffff};
+        best = wave_best(best);
+        if ((tid & 63) == 0) red[tid >> 6] = best;
+        __syncthreads();
+        if (tid == 0) {
+            Cand w = red[0];
+            for (int i = 1; i < kNmsThreads / kWave; ++i)
+                if (before(red[i], w)) w = red[i];
+            vals[(size_t)b * K + k] = w.v;
+            flat[(size_t)b * K + k] = w.i;
+            if (xy) {
+                xy[((size_t)b * K + k) * 2 + 0] = (int64_t)(w.i / X);
+                xy[((size_t)b * K + k) * 2 + 1] = (int64_t)(w.i % X);
+            }
+            win_tid = (w.i < M) ? (w.i % kNmsThreads) : -1;  // element e lives in thread e % threads
+        }
+        __syncthreads();
+        if (tid == win_tid) {  // pop the head
+#pragma unroll
+            for (int t = 0; t < KMAX - 1; ++t) top[t] = top[t + 1];
+            top[KMAX - 1] = Cand{-INFINITY, 0x7fffffff};
+            --have;
+        }
+    }
+}
+
 // columns[b,k,j,z] = cube[b,j,flat[b,k],z]; one thread per output element,
 // z fastest so reads and writes are contiguous runs of Z floats.
 __global__ __launch_bounds__(256) void gather_columns_kernel(const float *__restrict__ cube,
@@ -147,6 +227,11 @@ extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long fr
     if (lds > 150 * 1024) return FVP_ERR_SHAPE;
     if (frame_stride == 0) frame_stride = (long long)M;
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
+    if (K <= 16) {
+        hipLaunchKernelGGL(fvp::nms_topk_small_kernel<16>, dim3(B), dim3(fvp::kNmsThreads), M * 4, (hipStream_t)stream,
+                           prob, frame_stride, X, Y, K, vals, flat, xy);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob,
                        frame_stride, X, Y, K, vals, flat, xy);
     return (int)hipGetLastError();

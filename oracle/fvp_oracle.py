@@ -170,7 +170,7 @@ def max_planes(cubes: np.ndarray) -> np.ndarray:
 
 def nms2d(prob: np.ndarray, K: int):
     """proposal.py:34-76 for prob [B,1,X,Y]: 3x3/s1/p1 peak mask, flattened
-    top-K (value desc, flat index asc on ties), then get_index2D with the
+    top-K (NaN first, then value desc, flat index asc on ties), then get_index2D with the
     reference's divisor shape[1] == X (proposal.py:27-29,75)."""
     B, _, X, Y = prob.shape
     p = prob[:, 0]
@@ -185,7 +185,8 @@ def nms2d(prob: np.ndarray, K: int):
     vals = np.empty((B, K), F32)
     idx = np.empty((B, K), np.int64)
     for b in range(B):
-        order = np.lexsort((np.arange(X * Y), -nmsv[b]))[:K]
+        isn = np.isnan(nmsv[b])  # torch.topk ranks NaN above every number
+        order = np.lexsort((np.arange(X * Y), -np.where(isn, 0, nmsv[b]), ~isn))[:K]
         idx[b] = order
         vals[b] = nmsv[b][order]
     xy = np.stack([idx // X, idx % X], axis=2)

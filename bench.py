@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="frames per GPU per step (default per workload)")
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
                     help="collect FETCH_SIZE/WRITE_SIZE with rocprofv3 child runs (N=1, rank 0)")
@@ -51,6 +51,11 @@ def parse():
 
 # ---------------------------------------------------------------------------
 CHILD_OPS = 4  # warmup + steps of a profiled child run
+WORKLOAD_DESC = {"c1": "BASELINE configs[0] (1 demo camera)", "c2": "BASELINE configs[1] Shelf jln64 geometry",
+                 "c3": "BASELINE configs[2] Panoptic demo cameras", "c4": "BASELINE configs[3] Panoptic 128x128x32",
+                 "c5": "BASELINE configs[4] stress: 31 ring cameras, fp16 heatmaps",
+                 "shelf_native": "Shelf native J=17 152x200"}
+DEFAULT_BATCH = {"c1": 256, "c2": 256, "c3": 256, "c4": 64, "c5": 8, "shelf_native": 256}
 
 
 def collect_traffic(args):
@@ -138,7 +143,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     w = WORKLOADS[args.workload]
-    B = args.batch
+    B = args.batch or DEFAULT_BATCH.get(args.workload, 64)
     cams, seq = w.cameras()
     V = len(cams[seq])
     J = w.num_joints
@@ -152,6 +157,8 @@ def main():
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
     hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=rank * B)
     hm = torch.from_numpy(hm_host).to(dev)
+    if w.dtype == "float16":  # C5: fp16 heatmaps (computed in fp32 by the kernels)
+        hm = hm.half()
     del hm_host
     meta = {"seq": [seq] * B}
 
@@ -203,7 +210,7 @@ def main():
     vox_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     frames = world * B * args.steps
     fps = frames / el
-    per_frame = V * J * Hd * Wd * 4 + J * X * Y * Z * 4 + J * X * Y * 4
+    per_frame = V * J * Hd * Wd * hm.element_size() + J * X * Y * Z * 4 + J * X * Y * 4
     alg_bytes = B * per_frame
     achieved = alg_bytes / (vox_ms * 1e-3) / 1e9
 
@@ -224,10 +231,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if w.dtype == "float32" else "f16-in/f32",
             "data": "synthetic",
             "config": {
-                "workload": f"{w.name}: BASELINE configs[1] Shelf jln64 geometry, {V} cams, J={J}, "
+                "workload": f"{w.name}: {WORKLOAD_DESC.get(w.name, '')}, {V} cams, J={J}, "
                             f"{Hd}x{Wd} heatmaps -> {X}x{Y}x{Z} voxels, K={K} proposals",
                 "frames_per_gpu_step": B,
                 "global_batch": world * B,

@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
 
 METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "voxelize_cl_kernel")  # the fvp_voxelize op
+VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_pairs_kernel", "voxelize_kernel")  # the fvp_voxelize op
 
 
 def parse():
@@ -216,7 +216,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
-        sg_cpu = layer.sample_grid[seq].cpu()
+        sg_cpu = layer.sample_grid[seq].cpu().contiguous()
         cpu = cpu_baseline(w, sg_cpu, args.cpu_seconds)
 
     if rank == 0:
@@ -242,7 +242,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "fvp_voxelize op = heatmaps_to_cl_kernel + voxelize_cl_kernel per frame chunk",
+                "kernel": "fvp_voxelize op = layout pass (heatmaps_to_cl / heatmaps_to_pairs) + voxelize_kernel per frame chunk",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

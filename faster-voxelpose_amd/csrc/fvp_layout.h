@@ -4,6 +4,8 @@
 // range check.
 #pragma once
 
+#include <utility>
+
 #include "fvp_device.h"
 
 namespace fvp {
@@ -39,6 +41,70 @@ __global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict
     o.z = (j + 2 < J) ? to_f32(src[(size_t)(j + 2) * HW]) : 0.f;
     o.w = (j + 3 < J) ? to_f32(src[(size_t)(j + 3) * HW]) : 0.f;
     cl[pxg * LPV + q] = o;
+}
+
+// -- fp16 pixel-pair table ------------------------------------------------------
+// [b][V][H][W+1] entries of 64 B; entry (y, e) holds pixels x0 = e-1 and x0+1
+// of row y, lane q's 16 B = [x0: joints 4q..4q+3 | x0+1: joints 4q..4q+3] fp16,
+// zeros outside the image (J <= 16).  One thread per (entry, q).
+template <typename T>  // T = _Float16
+__global__ __launch_bounds__(256) void heatmaps_to_pairs_kernel(const T *__restrict__ hm,
+                                                                uint4 *__restrict__ tab, int J, int H, int W,
+                                                                long long total) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int q = (int)(gid & 3);
+    const long long ent = gid >> 2;
+    const int W1 = W + 1;
+    const long long row = ent / W1;
+    const int e = (int)(ent - row * W1);
+    const long long bv = row / H;
+    const int y = (int)(row - bv * H);
+    const size_t HW = (size_t)H * W;
+    const T *__restrict__ src = hm + (size_t)bv * J * HW + (size_t)y * W;
+    unsigned short h[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * q + k;
+        const T z = (T)0.0f;
+        const T a = (j < J && e >= 1) ? src[j * HW + e - 1] : z;
+        const T b = (j < J && e < W) ? src[j * HW + e] : z;
+        h[k] = __builtin_bit_cast(unsigned short, a);
+        h[4 + k] = __builtin_bit_cast(unsigned short, b);
+    }
+    tab[gid] = make_uint4(h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16), h[4] | ((unsigned)h[5] << 16),
+                          h[6] | ((unsigned)h[7] << 16));
+}
+
+inline size_t pair_frame_bytes(int V, int H, int W) { return (size_t)V * H * (W + 1) * 64; }
+
+// -- lane-group helpers -----------------------------------------------------------
+// Broadcast lane S of each LPV-lane voxel group to the whole group (DPP quad
+// permutes for LPV <= 4, ds_swizzle bit mode for 8-lane groups).
+template <int LPV, int S>
+__device__ __forceinline__ unsigned group_bcast(unsigned x) {
+    if constexpr (LPV == 1) {
+        return x;
+    } else if constexpr (LPV == 2) {
+        return (unsigned)__builtin_amdgcn_mov_dpp((int)x, S | (S << 2) | ((2 + S) << 4) | ((2 + S) << 6), 0xf, 0xf,
+                                                  false);
+    } else if constexpr (LPV == 4) {
+        return (unsigned)__builtin_amdgcn_mov_dpp((int)x, S | (S << 2) | (S << 4) | (S << 6), 0xf, 0xf, false);
+    } else {
+        static_assert(LPV == 8, "voxel groups of 1, 2, 4 or 8 lanes");
+        return (unsigned)__builtin_amdgcn_ds_swizzle((int)x, 0x18 | (S << 5));
+    }
+}
+
+template <int LPV, int S>
+__device__ __forceinline__ float group_bcast(float x) {
+    return __builtin_bit_cast(float, group_bcast<LPV, S>(__builtin_bit_cast(unsigned, x)));
+}
+
+// Compile-time loop: f(std::integral_constant<int, K>) for K in the sequence.
+template <int... K, typename F>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, K...>, F &&f) {
+    (f(std::integral_constant<int, K>{}), ...);
 }
 
 inline int lanes_per_voxel(int J) { return J <= 4 ? 1 : J <= 8 ? 2 : J <= 16 ? 4 : 8; }

@@ -3,45 +3,104 @@
 // Reference: project_whole.py:119-168 (grid_sample per frame, mean over all V
 // cameras, clamp(0,1)) and cnns_2d.py:291 (max over z).
 //
-// Why two kernels.  A bilinear tap of all J joints touches J separate
+// Why a layout pass.  A bilinear tap of all J joints touches J separate
 // [H][W] planes in the reference layout.  On gfx950 the texture addresser
 // only merges ADJACENT lanes that fall in one 128-B line (a quad per clock);
 // scattered per-joint taps cost ~64 clocks per wave load (tools/ta_probe.py),
 // and a voxel-camera needs 2 rows x J planes of lines.  So each chunk of
-// frames is first re-laid out channels-last:
-//   heatmaps_to_cl : [B][V][J][H][W]  ->  [b][V][H][W][JP]   (JP = 4*LPV >= J, zero padded)
-// a pure streaming pass, then
-//   voxelize_cl    : LPV lanes share one voxel; lane q loads 16 B = joints
-//                    4q..4q+3 of each tap with one buffer_load_dwordx4, so a
-//                    quad reads one 64-B pixel in one clock; out-of-image taps
-//                    use an out-of-range offset and read 0 through the buffer
-//                    descriptor's range check (= grid_sample's zero padding).
-// The chunk's channels-last copy is sized to stay in the 256 MB Infinity
-// Cache between the two launches.
+// frames is first re-laid out, a pure streaming pass:
+//   fp32: heatmaps_to_cl    [B][V][J][H][W] -> [b][V][H][W][JP] (JP = 4*LPV >= J, zero padded)
+//         LPV lanes share one voxel; lane q loads 16 B = joints 4q..4q+3 of a
+//         tap with one buffer_load_dwordx4, so a quad reads one 64-B pixel in
+//         one clock: 4 loads per voxel-camera.
+//   fp16: heatmaps_to_pairs [B][V][J][H][W] -> [b][V][H][W+1] 64-B entries
+//         holding pixels x0 and x0+1 of a row (J <= 16): 2 loads per
+//         voxel-camera, half the bytes through L1 (fp16 -> fp32 is exact).
+// Out-of-image taps use an out-of-range offset and read 0 through the buffer
+// descriptor's range check (= grid_sample's zero padding).  The chunk's copy
+// stays in the 256 MB Infinity Cache between the two launches.
 //
-// voxelize_cl work decomposition: a 256-thread block owns COLS whole voxel
-// columns (x, y..y+COLS, all z) of one frame -- a contiguous range of the
-// cube -- processed in passes of 256/LPV voxels; results are staged in LDS
-// so the cube is written as contiguous runs per joint and the xy max over z
-// is read back from LDS.  Arithmetic per tap and the camera/sum order are the
-// reference's (fvp_device.h), so the result is bit-exact.
+// Gather work decomposition: a 256-thread block owns COLS whole voxel columns
+// (x, y..y+COLS, all z) of one frame -- a contiguous range of the cube --
+// processed in passes of 256/LPV voxels; results are staged in LDS so the
+// cube is written as contiguous runs per joint and the xy max over z is read
+// back from LDS.  The sample grid is read voxel-major (fvp_pack_grid): each
+// lane of a voxel group loads 2 cameras' coordinates with one 16-B load,
+// computes their bilinear offsets/weights once, and the group picks them up
+// per camera through lane broadcasts -- one grid load and one tap setup per
+// 2*LPV voxel-cameras instead of per voxel-camera and lane.  Arithmetic per
+// tap and the camera/sum order are the reference's (fvp_device.h), so the
+// result is bit-exact.
 #include "fvp_layout.h"
 
 namespace fvp {
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float h_lo(unsigned u) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu));
+}
+__device__ __forceinline__ float h_hi(unsigned u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)); }
+
+// Bilinear setup of one voxel-camera (aten grid_sampler_2d, align_corners=True,
+// zeros padding): weights nw, ne, sw, se and the byte offsets of the taps
+// (kOOB when outside).  CL: 4 pixel offsets.  PAIR: 2 row-entry offsets.
+template <bool PAIR>
+struct Taps4 {
+    static constexpr int NO = PAIR ? 2 : 4;
+    unsigned o[NO];
+    float w[4];
+};
+
+template <bool PAIR>
+__device__ __forceinline__ Taps4<PAIR> setup_taps(float gx, float gy, float sxs, float sys, int W, int H,
+                                                  unsigned unit) {
+    Taps4<PAIR> t;
+    const float ix = (gx + 1.0f) * sxs;
+    const float iy = (gy + 1.0f) * sys;
+    const bool nan_ = (ix != ix) || (iy != iy);
+    const float x0f = floorf(ix), y0f = floorf(iy);
+    const float wx = ix - x0f, ex = 1.0f - wx;
+    const float ny = iy - y0f, syw = 1.0f - ny;
+    t.w[0] = syw * ex;
+    t.w[1] = syw * wx;
+    t.w[2] = ny * ex;
+    t.w[3] = ny * wx;
+    // NaN coordinates read in-image taps so the NaN weights propagate (as in
+    // grid_sample); far-off coordinates are clamped before the int conversion.
+    const int x0 = nan_ ? 0 : (int)fminf(fmaxf(x0f, -4.0f), (float)W + 4.0f);
+    const int y0 = nan_ ? 0 : (int)fminf(fmaxf(y0f, -4.0f), (float)H + 4.0f);
+    const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
+    if constexpr (PAIR) {
+        const bool vx = (x0 >= -1) & (x0 < W);
+        const unsigned e0 = (unsigned)(y0 * (W + 1) + x0 + 1) * unit;
+        t.o[0] = (vx & vy0) ? e0 : kOOB;
+        t.o[1] = (vx & vy1) ? e0 + (unsigned)(W + 1) * unit : kOOB;
+    } else {
+        const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
+        const unsigned p = (unsigned)(y0 * W + x0) * unit;
+        t.o[0] = (vy0 & vx0) ? p : kOOB;
+        t.o[1] = (vy0 & vx1) ? p + unit : kOOB;
+        t.o[2] = (vy1 & vx0) ? p + (unsigned)W * unit : kOOB;
+        t.o[3] = (vy1 & vx1) ? p + (unsigned)(W + 1) * unit : kOOB;
+    }
+    return t;
+}
+
 // -- gather pass ----------------------------------------------------------------
-template <int LPV>
-__global__ __launch_bounds__(256) void voxelize_cl_kernel(const float *__restrict__ cl, const float2 *__restrict__ grids,
-                                                          const int32_t *__restrict__ grid_index, int frame0,
-                                                          float *__restrict__ cube, float *__restrict__ xy, int V,
-                                                          int J, int H, int W, int X, int Y, int Z, int cols,
-                                                          int col_blocks) {
+template <int LPV, bool PAIR>
+__global__ __launch_bounds__(256) void voxelize_kernel(const void *__restrict__ tab, const float *__restrict__ grids,
+                                                       const int32_t *__restrict__ grid_index, int frame0,
+                                                       float *__restrict__ cube, float *__restrict__ xy, int V, int J,
+                                                       int H, int W, int X, int Y, int Z, int cols, int col_blocks) {
+    static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
+    constexpr int CPG = 2 * LPV;    // cameras per grid load (2 per lane)
     extern __shared__ __attribute__((aligned(16))) float stage[];  // [JP][SP]
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int bl = L / col_blocks;   // frame within the chunk
-    const int b = frame0 + bl;       // frame within the batch (outputs, grid_index)
+    const int bl = L / col_blocks;  // frame within the chunk
+    const int b = frame0 + bl;      // frame within the batch (outputs, grid_index)
     const int XY = X * Y;
     const int c0 = (L - bl * col_blocks) * cols;
     const int ncols = min(cols, XY - c0);
@@ -50,60 +109,86 @@ __global__ __launch_bounds__(256) void voxelize_cl_kernel(const float *__restric
     const long long N = (long long)XY * Z;
     const long long n0 = (long long)c0 * Z;
     const int q = threadIdx.x % LPV;
-    const unsigned HW = (unsigned)(H * W);
-    const unsigned pix_bytes = JP * 4u;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
     const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
     const float fV = (float)V;
     const int gsel = grid_index ? grid_index[b] : 0;
-    const float2 *__restrict__ g = grids + (size_t)gsel * V * N + n0;
+    const __amdgpu_buffer_rsrc_t grs =
+        uniform_rsrc(grids + (size_t)gsel * N * GV * 2, (unsigned)(N * GV * 8));
+    // per-camera image of this frame in the workspace
+    const unsigned unit = PAIR ? 64u : JP * 4u;                               // bytes per pixel / entry
+    const unsigned img = PAIR ? (unsigned)(H * (W + 1)) * 64u : (unsigned)(H * W) * unit;  // bytes per camera
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
 
     for (int i0 = 0; i0 < T; i0 += VPP) {
         const int i = i0 + threadIdx.x / LPV;
         const bool valid = i < T;
+        const int ii = min(i, T - 1);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int v = 0; v < V; ++v) {
-            float2 gg = g[(size_t)v * N + min(i, T - 1)];
-            if (!valid) gg = make_float2(-2.f, -2.f);
-            const float ix = (gg.x + 1.0f) * sxs;
-            const float iy = (gg.y + 1.0f) * sys;
-            const bool isnan_ = (ix != ix) || (iy != iy);
-            if (isnan_) {  // grid_sample of a NaN coordinate is NaN (0 * NaN weights)
+        for (int v0 = 0; v0 < V; v0 += CPG) {
+            // slots v0+2q, v0+2q+1 of voxel n0+ii (past the row: next voxel's or 0, unused)
+            const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(
+                grs, (unsigned)(((n0 + ii) * GV + v0 + 2 * q) * 8), 0, 0);
+            float g[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) acc[k] = acc[k] + NAN;
-            }
-            const float x0f = floorf(ix), y0f = floorf(iy);
-            const float wx = ix - x0f, ex = 1.0f - wx;
-            const float ny = iy - y0f, syw = 1.0f - ny;
-            const float nw = syw * ex, ne = syw * wx, sw = ny * ex, se = ny * wx;
-            const int x0 = isnan_ ? -4 : (int)x0f, y0 = isnan_ ? -4 : (int)y0f;
-            const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
-            const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
-            const bool any = (vx0 | vx1) & (vy0 | vy1);
-            if (!__builtin_amdgcn_ballot_w64(any)) continue;  // whole wave off-image: contributes exactly 0
-            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(cl + ((size_t)bl * V + v) * HW * JP, HW * pix_bytes);
-            const unsigned pix = (unsigned)(y0 * W + x0);
-            const unsigned qo = (unsigned)q * 16u;
-            const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx0) ? pix * pix_bytes + qo : kOOB, 0, 0);
-            const auto bq =
-                __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx1) ? (pix + 1u) * pix_bytes + qo : kOOB, 0, 0);
-            const auto c = __builtin_amdgcn_raw_buffer_load_b128(
-                rs, (vy1 & vx0) ? (pix + (unsigned)W) * pix_bytes + qo : kOOB, 0, 0);
-            const auto d = __builtin_amdgcn_raw_buffer_load_b128(
-                rs, (vy1 & vx1) ? (pix + (unsigned)W + 1u) * pix_bytes + qo : kOOB, 0, 0);
-            if (!isnan_) {
+            for (int k = 0; k < 4; ++k) g[k] = valid ? __builtin_bit_cast(float, (unsigned)graw[k]) : -2.0f;
+            const Taps4<PAIR> t0 = setup_taps<PAIR>(g[0], g[1], sxs, sys, W, H, unit);
+            const Taps4<PAIR> t1 = setup_taps<PAIR>(g[2], g[3], sxs, sys, W, H, unit);
+            static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = k >> 1;  // lane of the group that set this camera up
+                const int v = v0 + k;
+                if (v >= V) return;
+                const Taps4<PAIR> &src = (k & 1) ? t1 : t0;
+                unsigned o[Taps4<PAIR>::NO];
+                unsigned all = kOOB;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float fa = __builtin_bit_cast(float, (unsigned)a[k]);
-                    const float fb = __builtin_bit_cast(float, (unsigned)bq[k]);
-                    const float fc = __builtin_bit_cast(float, (unsigned)c[k]);
-                    const float fd = __builtin_bit_cast(float, (unsigned)d[k]);
-                    acc[k] = acc[k] + __builtin_fmaf(fd, se, __builtin_fmaf(fc, sw, __builtin_fmaf(fb, ne, fa * nw)));
+                for (int m = 0; m < Taps4<PAIR>::NO; ++m) {
+                    o[m] = group_bcast<LPV, S>(src.o[m]);
+                    all &= o[m];
                 }
-            }
+                // whole wave off-image (every tap's kOOB bit set): contributes exactly 0
+                if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+                float w[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(src.w[m]);
+                const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+                if constexpr (PAIR) {
+                    // r0 = [a j0 j1 | a j2 j3 | b j0 j1 | b j2 j3] (row y0), r1 likewise (c, d; row y1)
+                    const u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                    const u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const unsigned ua = r0[m >> 1], ub = r0[2 + (m >> 1)];
+                        const unsigned uc = r1[m >> 1], ud = r1[2 + (m >> 1)];
+                        const float fa = (m & 1) ? h_hi(ua) : h_lo(ua);
+                        const float fb = (m & 1) ? h_hi(ub) : h_lo(ub);
+                        const float fc = (m & 1) ? h_hi(uc) : h_lo(uc);
+                        const float fd = (m & 1) ? h_hi(ud) : h_lo(ud);
+                        acc[m] = acc[m] +
+                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                    }
+                } else {
+                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                    const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                    const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
+                    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
+                        const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
+                        const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
+                        const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
+                        acc[m] = acc[m] +
+                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                    }
+                }
+            });
         }
         if (valid) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) stage[(4 * q + k) * SP + i] = clampf(acc[k] / fV, 0.0f, 1.0f);
+            for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf(acc[m] / fV, 0.0f, 1.0f);
         }
     }
     __syncthreads();
@@ -124,37 +209,57 @@ __global__ __launch_bounds__(256) void voxelize_cl_kernel(const float *__restric
     }
 }
 
+// [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
+__global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict__ g, float2 *__restrict__ out, int V,
+                                                        int GV, long long N) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= N * GV) return;
+    const long long n = t / GV;
+    const int v = (int)(t - n * GV);
+    out[t] = v < V ? g[(size_t)v * N + n] : make_float2(-2.f, -2.f);
+}
 
 static int cols_per_block(int Z) { return Z >= 320 ? 1 : 320 / Z; }
 
+static bool use_pairs(int J, bool half) { return half && J <= 16; }
 
-// Frames per chunk: keep the channels-last copy of a chunk well inside the
-// 256 MB Infinity Cache (measured best at ~64-80 MB for C2: 8 frames).
-static int chunk_frames(int B, int V, int J, int H, int W) {
-    const size_t per = cl_frame_bytes(V, J, H, W);
-    long long c = (long long)((80ull << 20) / (per ? per : 1));
+static size_t frame_bytes(int V, int J, int H, int W, bool half) {
+    return use_pairs(J, half) ? pair_frame_bytes(V, H, W) : cl_frame_bytes(V, J, H, W);
+}
+
+// Frames per chunk: keep a chunk's re-laid-out copy inside the 256 MB Infinity
+// Cache (measured best: ~80 MB for the fp32 layout, C2: 8 frames; 2 frames
+// (~122 MB) of the fp16 pair table at C5).
+static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
+    const size_t per = frame_bytes(V, J, H, W, half);
+    const size_t budget = use_pairs(J, half) ? (128ull << 20) : (80ull << 20);
+    long long c = (long long)(budget / (per ? per : 1));
     if (c < 1) c = 1;
     if (c > B) c = B;
     return (int)c;
 }
 
-template <int LPV, typename T>
+template <int LPV, bool PAIR, typename T>
 static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const float *grids, const int32_t *grid_index,
-                      int X, int Y, int Z, float *cube, float *xy, float *ws, hipStream_t s) {
-    const int chunk = chunk_frames(B, V, J, H, W);
+                      int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
+    const bool half = sizeof(T) == 2;
+    const int chunk = chunk_frames(B, V, J, H, W, half);
     const int cols = cols_per_block(Z);
     const int col_blocks = (X * Y + cols - 1) / cols;
     const size_t lds = (size_t)4 * LPV * (cols * Z + 1) * sizeof(float);
     const size_t frame_elems = (size_t)V * J * H * W;
     for (int f0 = 0; f0 < B; f0 += chunk) {
         const int nb = min(chunk, B - f0);
-        const long long px = (long long)nb * V * H * W;
-        const long long threads = px * LPV;
-        hipLaunchKernelGGL((heatmaps_to_cl_kernel<LPV, T>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                           hm + (size_t)f0 * frame_elems, reinterpret_cast<float4 *>(ws), J, H * W, px);
-        hipLaunchKernelGGL((voxelize_cl_kernel<LPV>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s, ws,
-                           reinterpret_cast<const float2 *>(grids), grid_index, f0, cube, xy, V, J, H, W, X, Y, Z,
-                           cols, col_blocks);
+        const T *src = hm + (size_t)f0 * frame_elems;
+        if constexpr (PAIR) {
+            const long long total = (long long)nb * V * H * (W + 1) * 4;
+            hipLaunchKernelGGL(heatmaps_to_pairs_kernel<_Float16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                               reinterpret_cast<const _Float16 *>(src), reinterpret_cast<uint4 *>(ws), J, H, W, total);
+        } else {
+            launch_layout<LPV, T>(src, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
+        }
+        hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s, ws,
+                           grids, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks);
     }
     return (int)hipGetLastError();
 }
@@ -162,15 +267,17 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const floa
 template <typename T>
 static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const float *grids, const int32_t *grid_index,
                         int X, int Y, int Z, float *cube, float *xy, void *ws, size_t ws_bytes, hipStream_t s) {
-    const size_t need = (size_t)chunk_frames(B, V, J, H, W) * cl_frame_bytes(V, J, H, W);
+    const bool half = sizeof(T) == 2;
+    const size_t need = (size_t)chunk_frames(B, V, J, H, W, half) * frame_bytes(V, J, H, W, half);
     if (!ws || ws_bytes < need) return FVP_ERR_WORKSPACE;
-    if ((long long)V * H * W * 4 * lanes_per_voxel(J) * 4 > 0x7fffffffLL) return FVP_ERR_SHAPE;  // 32-bit offsets
-    float *w = reinterpret_cast<float *>(ws);
+    if (frame_bytes(1, J, H, W, half) > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets
+    if (use_pairs(J, half))
+        return run_chunks<4, true, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
     switch (lanes_per_voxel(J)) {
-        case 1: return run_chunks<1, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
-        case 2: return run_chunks<2, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
-        case 4: return run_chunks<4, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
-        default: return run_chunks<8, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, w, s);
+        case 1: return run_chunks<1, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 2: return run_chunks<2, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 4: return run_chunks<4, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
+        default: return run_chunks<8, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
     }
 }
 
@@ -178,33 +285,52 @@ static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, c
     if (!heatmaps || !grids) return FVP_ERR_NULL;
     if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2 || X <= 0 || Y <= 0 || Z <= 0)
         return FVP_ERR_SHAPE;
-    if ((long long)X * Y * Z > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    // packed grid of one sequence addressed with 32-bit byte offsets
+    if ((long long)X * Y * Z * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL) return FVP_ERR_SHAPE;
     return FVP_OK;
+}
+
+static size_t workspace_bytes(int B, int V, int J, int H, int W, bool half) {
+    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
+    return (size_t)chunk_frames(B, V, J, H, W, half) * frame_bytes(V, J, H, W, half);
 }
 
 }  // namespace fvp
 
-extern "C" size_t fvp_voxelize_workspace_bytes(int B, int V, int J, int H, int W) {
-    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
-    return (size_t)fvp::chunk_frames(B, V, J, H, W) * fvp::cl_frame_bytes(V, J, H, W);
+extern "C" int fvp_pack_grid(const float *sample_grid, int V, long long N, float *packed, void *stream) {
+    if (!sample_grid || !packed) return FVP_ERR_NULL;
+    if (V <= 0 || N <= 0) return FVP_ERR_SHAPE;
+    const int GV = FVP_GRID_SLOTS(V);
+    const long long tot = N * GV;
+    hipLaunchKernelGGL(fvp::pack_grid_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float2 *>(sample_grid), reinterpret_cast<float2 *>(packed), V, GV, N);
+    return (int)hipGetLastError();
 }
 
-extern "C" int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W, const float *sample_grids,
+extern "C" size_t fvp_voxelize_workspace_bytes(int B, int V, int J, int H, int W) {
+    return fvp::workspace_bytes(B, V, J, H, W, false);
+}
+
+extern "C" size_t fvp_voxelize_f16_workspace_bytes(int B, int V, int J, int H, int W) {
+    return fvp::workspace_bytes(B, V, J, H, W, true);
+}
+
+extern "C" int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W, const float *packed_grids,
                             const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *workspace,
                             size_t workspace_bytes, void *stream) {
-    const int st = fvp::check_args(heatmaps, B, V, J, H, W, sample_grids, X, Y, Z);
+    const int st = fvp::check_args(heatmaps, B, V, J, H, W, packed_grids, X, Y, Z);
     if (st != FVP_OK) return st;
     if (!cube && !xy) return FVP_OK;
-    return fvp::voxelize_any<float>(heatmaps, B, V, J, H, W, sample_grids, grid_index, X, Y, Z, cube, xy, workspace,
+    return fvp::voxelize_any<float>(heatmaps, B, V, J, H, W, packed_grids, grid_index, X, Y, Z, cube, xy, workspace,
                                     workspace_bytes, (hipStream_t)stream);
 }
 
-extern "C" int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W, const float *sample_grids,
+extern "C" int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W, const float *packed_grids,
                                 const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy,
                                 void *workspace, size_t workspace_bytes, void *stream) {
-    const int st = fvp::check_args(heatmaps, B, V, J, H, W, sample_grids, X, Y, Z);
+    const int st = fvp::check_args(heatmaps, B, V, J, H, W, packed_grids, X, Y, Z);
     if (st != FVP_OK) return st;
     if (!cube && !xy) return FVP_OK;
-    return fvp::voxelize_any<_Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, sample_grids,
+    return fvp::voxelize_any<_Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, packed_grids,
                                        grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
 }

@@ -38,7 +38,9 @@ SIGNATURES = {
     "fvp_status_string": [c_int],
     "fvp_project_grid": [c_void_p, c_int, c_void_p, ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p,
                          c_void_p],
+    "fvp_pack_grid": [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p],
     "fvp_voxelize_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
+    "fvp_voxelize_f16_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
     "fvp_voxelize": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                      c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_voxelize_f16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -52,7 +54,7 @@ SIGNATURES = {
     "fvp_max_planes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _LIB = None
 
 
@@ -72,6 +74,7 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = {"fvp_status_string": c_char_p, "fvp_voxelize_workspace_bytes": ctypes.c_size_t,
+                      "fvp_voxelize_f16_workspace_bytes": ctypes.c_size_t,
                       "fvp_person_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
     if lib.fvp_abi_version() != ABI_VERSION:
         raise FvpError(f"fvp: ABI version mismatch ({lib.fvp_abi_version()} != {ABI_VERSION})")

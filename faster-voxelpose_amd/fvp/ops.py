@@ -72,20 +72,48 @@ def _(cams, resize_t, start, end, center, bins, ori_max, img_w, img_h, hm_w, hm_
 
 
 # ---------------------------------------------------------------------------
+def grid_slots(V: int) -> int:
+    """Camera slots per voxel of a packed grid (FVP_GRID_SLOTS: V rounded up to even)."""
+    return V + (V & 1)
+
+
+@torch.library.custom_op("fvp::pack_grid", mutates_args=(), device_types="cuda")
+def pack_grid(sample_grid: torch.Tensor) -> torch.Tensor:
+    """[V,N,2] (the reference's per-camera layout) -> voxel-major [N,GV,2] read by fvp_voxelize."""
+    sg = _dev_f32(sample_grid, "sample_grid")
+    V, N = sg.shape[0], sg.shape[1]
+    out = torch.empty((N, grid_slots(V), 2), dtype=torch.float32, device=sg.device)
+    _lib.call("fvp_pack_grid", _ptr(sg), V, N, _ptr(out), _stream(sg))
+    return out
+
+
+@pack_grid.register_fake
+def _(sample_grid):
+    V, N = sample_grid.shape[0], sample_grid.shape[1]
+    return sample_grid.new_empty((N, grid_slots(V), 2))
+
+
+def packed_as_reference(packed: torch.Tensor, V: int) -> torch.Tensor:
+    """View [V,1,N,2] of a packed grid [N,GV,2]: the reference's sample_grid layout, no copy."""
+    return packed.permute(1, 0, 2)[:V].unsqueeze(1)
+
+
 @torch.library.custom_op("fvp::voxelize", mutates_args=(), device_types="cuda")
-def voxelize(heatmaps: torch.Tensor, sample_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
+def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
              X: int, Y: int, Z: int, want_cube: bool, want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """packed_grids: [S,N,GV,2] (or [N,GV,2]) from pack_grid; grid_index: int [B] sequence of frame b."""
     if heatmaps.device.type != "cuda":
         raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps.device}")
     half = heatmaps.dtype == torch.float16
     hm = heatmaps.contiguous() if half else _dev_f32(heatmaps, "heatmaps")
-    sg = _dev_f32(sample_grids, "sample_grids")
+    pg = _dev_f32(packed_grids, "packed_grids")
     B, V, J, H, W = hm.shape
     N = X * Y * Z
-    if sg.dim() == 3:
-        sg = sg.unsqueeze(0)
-    if sg.shape[1:] != (V, N, 2):
-        raise _lib.FvpError(f"fvp: sample grid {tuple(sg.shape)} does not match V={V}, N={N}")
+    if pg.dim() == 3:
+        pg = pg.unsqueeze(0)
+    if pg.shape[1:] != (N, grid_slots(V), 2):
+        raise _lib.FvpError(f"fvp: packed grid {tuple(pg.shape)} does not match V={V}, N={N} "
+                            f"(expected [S,{N},{grid_slots(V)},2] from pack_grid)")
     gi = None
     if grid_index is not None:
         gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
@@ -93,17 +121,18 @@ def voxelize(heatmaps: torch.Tensor, sample_grids: torch.Tensor, grid_index: Opt
             raise _lib.FvpError("fvp: grid_index must have one entry per frame")
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
-    ws_bytes = _lib.load().fvp_voxelize_workspace_bytes(B, V, J, H, W)
+    lib = _lib.load()
+    ws_bytes = (lib.fvp_voxelize_f16_workspace_bytes if half else lib.fvp_voxelize_workspace_bytes)(B, V, J, H, W)
     if ws_bytes == 0:
         raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
     ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
-    _lib.call("fvp_voxelize_f16" if half else "fvp_voxelize", _ptr(hm), B, V, J, H, W, _ptr(sg), _ptr(gi), X, Y, Z,
+    _lib.call("fvp_voxelize_f16" if half else "fvp_voxelize", _ptr(hm), B, V, J, H, W, _ptr(pg), _ptr(gi), X, Y, Z,
               _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _ptr(ws), ws_bytes, _stream(hm))
     return cube, xy
 
 
 @voxelize.register_fake
-def _(heatmaps, sample_grids, grid_index, X, Y, Z, want_cube, want_xy):
+def _(heatmaps, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
     B, V, J = heatmaps.shape[:3]
     return (heatmaps.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
             heatmaps.new_empty((B, J, X, Y) if want_xy else (0,)))

@@ -37,7 +37,8 @@ class ProjectLayer(nn.Module):
         self.space_center = cfg.CAPTURE_SPEC.SPACE_CENTER
         self.voxels_per_axis = cfg.CAPTURE_SPEC.VOXELS_PER_AXIS
         self._grid = None
-        self.sample_grid = {}  # seq -> [V, 1, N, 2] fp32 (the reference's cache layout)
+        self.sample_grid = {}  # seq -> [V, 1, N, 2] fp32 (the reference's cache layout; a view of _packed)
+        self._packed = {}      # seq -> [N, GV, 2] voxel-major copy read by the voxelize kernel
         self.verbose = True
 
     # -- reference attribute: voxel centres [N,3] (compute_grid, :43-79) -------------
@@ -61,14 +62,28 @@ class ProjectLayer(nn.Module):
         return start, end, [float(np.float32(c)) for c in C], nb
 
     def build_sample_grid(self, cameras, seq, resize_transform, device) -> torch.Tensor:
-        """project_grid x V for one sequence (project_whole.py:81-117,151-156) on device."""
+        """project_grid x V for one sequence (project_whole.py:81-117,151-156) on device.
+
+        Returns the reference's [V,1,N,2] layout as a view of the voxel-major
+        packed grid (fvp_pack_grid) that the voxelize kernel reads."""
         cams = torch.from_numpy(geometry.pack_cameras(cameras, seq)).to(device)
         start, end, center, nb = self.grid_spec()
         w, h = self.heatmap_size
         sg = ops.project_grid(cams, resize_transform.to(device=device, dtype=torch.float32), start, end, center, nb,
                               float(max(self.ori_image_size[0], self.ori_image_size[1])),
                               float(self.image_size[0]), float(self.image_size[1]), int(w), int(h))
-        return sg.view(sg.shape[0], 1, sg.shape[1], 2)
+        packed = ops.pack_grid(sg)
+        self._packed[seq] = packed
+        return ops.packed_as_reference(packed, sg.shape[0])
+
+    def _packed_grid(self, seq) -> torch.Tensor:
+        sg = self.sample_grid[seq]
+        pg = self._packed.get(seq)
+        if pg is None or ops.packed_as_reference(pg, sg.shape[0]).data_ptr() != sg.data_ptr():
+            # a grid assigned from outside (e.g. a reference-layout tensor): pack it once
+            pg = ops.pack_grid(sg[:, 0].to(torch.float32).contiguous())
+            self._packed[seq] = pg
+        return pg
 
     def _grids_for_batch(self, heatmaps, meta, cameras, resize_transform):
         device = heatmaps.device
@@ -83,8 +98,8 @@ class ProjectLayer(nn.Module):
                 self.sample_grid[curr_seq] = self.build_sample_grid(cameras, curr_seq, resize_transform, device)
         uniq = list(dict.fromkeys(seqs))
         if len(uniq) == 1:
-            return self.sample_grid[uniq[0]][:, 0].unsqueeze(0), None
-        grids = torch.stack([self.sample_grid[s][:, 0] for s in uniq])
+            return self._packed_grid(uniq[0]), None
+        grids = torch.stack([self._packed_grid(s) for s in uniq])
         index = torch.tensor([uniq.index(s) for s in seqs], dtype=torch.int32).to(device, non_blocking=True)
         return grids, index
 

@@ -17,6 +17,7 @@
  *   heatmaps      [B][V][J][H][W]      (as handed to ProjectLayer.forward)
  *   cams          [V][FVP_CAM_STRIDE]  packed camera records (see below)
  *   sample_grid   [V][N][2]            N = X*Y*Z, voxel n = (ix*Y+iy)*Z+iz
+ *   packed grid   [N][FVP_GRID_SLOTS(V)][2]  voxel-major copy read by fvp_voxelize
  *   cube          [B][J][X][Y][Z]
  *   xy            [B][J][X][Y]
  */
@@ -30,9 +31,11 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 2
+#define FVP_ABI_VERSION 3
 #define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
 #define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
+/* Camera slots per voxel in a packed grid (V rounded up to even). */
+#define FVP_GRID_SLOTS(V) ((V) + ((V) & 1))
 
 /* Argument errors (distinct from hipError_t values, which are < 1000). */
 #define FVP_OK 0
@@ -82,24 +85,35 @@ int fvp_project_grid(const float *cams, int V, const float *resize_t,
                      const fvp_grid_spec *grid, const fvp_image_spec *img,
                      float *sample_grid, void *stream);
 
+/* Voxel-major copy of a sample grid, the layout fvp_voxelize reads:
+ *   packed[n][v][:] = sample_grid[v][n][:] for v < V; padding slots = (-2,-2)
+ * (off-image).  Built once per sequence, like the grid itself.  The LPV lanes
+ * that share a voxel read 2*LPV cameras' coordinates with one 16-B load each.
+ *   sample_grid device [V][N][2];  packed device [N][FVP_GRID_SLOTS(V)][2] */
+int fvp_pack_grid(const float *sample_grid, int V, long long N, float *packed, void *stream);
+
 /* Whole-space voxelisation fused with the xy max-projection:
  *   cube[b,j,n] = clamp(mean_v grid_sample(heatmaps[b,v,j], sample_grid[g(b),v,n]), 0, 1)
  *   xy[b,j,x,y] = max_z cube[b,j,x,y,z]
  * Replaces ProjectLayer.forward (project_whole.py:119-168) and the first line
  * of CenterNet.forward (lib/models/cnns_2d.py:291).
- *   sample_grids device [n_grids][V][N][2]
+ *   packed_grids device [n_grids][N][FVP_GRID_SLOTS(V)][2] (fvp_pack_grid)
  *   grid_index   device int32 [B] (grid of frame b) or NULL (all frames use grid 0)
  *   cube, xy     device outputs; either may be NULL to skip it
  *   workspace    device scratch of >= fvp_voxelize_workspace_bytes(B,V,J,H,W)
  *                bytes (channels-last copy of a chunk of frames); J <= FVP_MAX_JOINTS */
 size_t fvp_voxelize_workspace_bytes(int B, int V, int J, int H, int W);
 int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W,
-                 const float *sample_grids, const int32_t *grid_index,
+                 const float *packed_grids, const int32_t *grid_index,
                  int X, int Y, int Z, float *cube, float *xy,
                  void *workspace, size_t workspace_bytes, void *stream);
-/* Same with fp16 heatmaps (IEEE binary16), computed in fp32 (exact upcast). */
+/* Same with fp16 heatmaps (IEEE binary16), computed in fp32 (exact upcast).
+ * For J <= 16 the chunk is re-laid out as an fp16 pixel-pair table (each
+ * 64-B entry holds pixels x and x+1 of a row), so a voxel-camera is 2 loads;
+ * the workspace size differs from the fp32 one. */
+size_t fvp_voxelize_f16_workspace_bytes(int B, int V, int J, int H, int W);
 int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W,
-                     const float *sample_grids, const int32_t *grid_index,
+                     const float *packed_grids, const int32_t *grid_index,
                      int X, int Y, int Z, float *cube, float *xy,
                      void *workspace, size_t workspace_bytes, void *stream);
 

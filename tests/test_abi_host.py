@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 3
     assert lib.fvp_status_string(0) == b"success"
 
 
@@ -46,6 +46,14 @@ def test_argument_validation_without_gpu():
     assert need == 8 * 5 * 128 * 240 * 16 * 4  # channels-last chunk of 8 frames (J padded to 16)
     assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, 1, 100, None) == 1003
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 0
+    # fp16, J <= 16: pixel-pair table [V][H][W+1] x 64 B, 2 frames of C5 per chunk
+    assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 2 * 31 * 128 * 241 * 64
+    # fp16, J > 16: the fp32 channels-last copy
+    assert lib.fvp_voxelize_f16_workspace_bytes(1, 5, 17, 128, 240) == 5 * 128 * 240 * 32 * 4
+    assert lib.fvp_pack_grid(None, 5, 100, None, None) == 1001
+    assert lib.fvp_pack_grid(1, 0, 100, 1, None) == 1002
+    # packed grid of one sequence beyond 32-bit byte offsets
+    assert lib.fvp_voxelize(1, 1, 32, 15, 128, 240, 1, None, 1024, 1024, 512, 1, None, 1, 1 << 40, None) == 1002
     assert lib.fvp_nms_topk(None, 1, 80, 80, 0, 10, None, None, None, None) == 1001
     assert lib.fvp_nms_topk(1, 1, 2, 2, 0, 10, 1, 1, None, None) == 1002  # K > X*Y
     assert lib.fvp_nms_topk(1, 2, 8, 8, 10, 5, 1, 1, None, None) == 1002  # frame stride < X*Y

@@ -205,6 +205,63 @@ def test_ragged_shapes_vs_oracle(gpu_device, bins, J, hm_size):
         _assert_same(xy[b].cpu().numpy(), O.xy_plane(ref), f"xy frame {b}")
 
 
+@pytest.mark.parametrize("half", [False, True], ids=["f32", "f16"])
+@pytest.mark.parametrize("V,J", [(1, 3), (2, 6), (4, 1), (7, 15), (31, 15), (31, 24), (7, 32), (3, 16)])
+def test_camera_and_joint_counts_vs_oracle(gpu_device, V, J, half):
+    """Every lane-group size (J -> 1/2/4/8 lanes per voxel), odd/even and
+    >2*LPV camera counts (packed-grid groups), the fp16 pixel-pair table
+    (J <= 16) and the fp16 -> fp32 layout fallback (J > 16)."""
+    from fvp import geometry, synthetic
+    from fvp.project_whole import ProjectLayer
+
+    bins, hm_size = (12, 10, 6), (64, 48)
+    w = _custom_workload(base="c5", voxels_per_axis=bins, num_joints=J, heatmap_size=hm_size, extra={"views": V})
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+    hm = synthetic.uniform_heatmaps(w, 3, seed=V * 100 + J)
+    if half:
+        hm = hm.half()
+    cube, xy = layer.forward_fused(hm.to(gpu_device), {"seq": [seq] * 3}, cams, rt.to(gpu_device))
+    grid = O.compute_grid(w.space_size, w.space_center, bins)
+    sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, hm_size, rt.numpy())
+                   for c in geometry.camera_list(cams, seq)])
+    assert sg.shape[0] == V
+    for b in range(3):
+        ref = O.voxelize(hm[b].float().numpy(), sg).reshape(J, *bins)
+        _assert_same(cube[b].cpu().numpy(), ref, f"cube frame {b}")
+        _assert_same(xy[b].cpu().numpy(), O.xy_plane(ref), f"xy frame {b}")
+
+
+def test_sample_grid_is_view_of_packed_grid(gpu_device):
+    """sample_grid[seq] keeps the reference's [V,1,N,2] layout as a view of the
+    voxel-major packed grid; a grid assigned from outside is packed on use."""
+    from fvp import geometry, synthetic, ops
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c3"]
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 2)).to(gpu_device)
+    cube, _ = layer.forward_fused(hm, {"seq": [seq] * 2}, cams, rt)
+    sg = layer.sample_grid[seq]
+    N = 80 * 80 * 20
+    assert sg.shape == (5, 1, N, 2)
+    packed = layer._packed[seq]
+    assert packed.shape == (N, ops.grid_slots(5), 2)
+    assert torch.equal(packed[:, :5].permute(1, 0, 2), sg[:, 0])
+    assert torch.equal(packed[:, 5:], torch.full_like(packed[:, 5:], -2.0))
+    other = ProjectLayer(w.cfg(str(gpu_device)))
+    other.verbose = False
+    other.sample_grid[seq] = sg.contiguous().clone()  # reference-layout tensor from outside
+    cube2, _ = other.forward_fused(hm, {"seq": [seq] * 2}, cams, rt)
+    assert torch.equal(cube, cube2)
+
+
 def test_mixed_sequences_in_one_batch(gpu_device):
     """Frames of different sequences (different cameras) in one launch."""
     from fvp import geometry, synthetic
@@ -335,7 +392,7 @@ def test_more_than_32_joints_rejected(gpu_device):
     from fvp import _lib
 
     hm = torch.zeros((1, 1, 33, 8, 8), device=gpu_device)
-    sg = torch.zeros((1, 8, 2), device=gpu_device)
+    sg = torch.zeros((8, 2, 2), device=gpu_device)  # packed [N, GV, 2]
     with pytest.raises(_lib.FvpError, match="J <= 32"):
         torch.ops.fvp.voxelize(hm, sg, None, 2, 2, 2, True, True)
 

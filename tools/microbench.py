@@ -67,7 +67,7 @@ def main():
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, B)).to(dev)
     meta = {"seq": [seq] * B}
     ref_cube, ref_xy = layer.forward_fused(hm, meta, cams, rt)
-    grids = layer.sample_grid[seq]
+    grids = layer.sample_grid[seq].contiguous()
     B_, V, J, H, W = hm.shape
     X, Y, Z = w.voxels_per_axis
     stream = torch.cuda.current_stream().cuda_stream

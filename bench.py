@@ -69,7 +69,9 @@ def collect_traffic(args):
         d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=out_root)
         cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--child", "--steps", str(CHILD_OPS - 1), "--warmup", "1",
-               "--batch", str(args.batch), "--workload", args.workload, "--traffic", "off", "--cpu-baseline", "off"]
+               "--workload", args.workload, "--traffic", "off", "--cpu-baseline", "off"]
+        if args.batch:
+            cmd += ["--batch", str(args.batch)]
         try:
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            cwd=REPO)
@@ -165,7 +167,7 @@ def main():
     # once-per-sequence cache build, timed separately (excluded from the step)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    layer._grids_for_batch(hm, meta, cams, rt)
+    layer.prepare(hm, meta, cams, rt)
     torch.cuda.synchronize()
     cache_ms = (time.perf_counter() - t0) * 1e3
 
@@ -214,9 +216,50 @@ def main():
     alg_bytes = B * per_frame
     achieved = alg_bytes / (vox_ms * 1e-3) / 1e9
 
+    # secondary bound: the bilinear tap rate, N*V*J*4 joint-taps
+    # per frame, against the per-CU vector-memory (texture addresser / L1) rate of
+    # 64 B/clk: 16 fp32 joint-taps/clk/CU, 32 with the fp16 pixel-pair table.
+    taps = B * X * Y * Z * V * J * 4
+    tap_bytes = 2 if (hm.element_size() == 2 and J <= 16) else 4
+    tap_peak = 256 * 2.4e9 * 64 / tap_bytes / 1e12
+    tap_rate = taps / (vox_ms * 1e-3) / 1e12
+
+    extra = {}
+    if rank == 0:
+        # measured copy bandwidth (float4-style device copy, 1 GiB each way) and
+        # the one-frame latency of the step; both outside the timed region
+        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dst.copy_(src)
+        e1.record()
+        torch.cuda.synchronize()
+        extra["copy_gbs"] = 2 * src.numel() * 4 * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        del src, dst
+        hm1, meta1 = hm[:1], {"seq": [seq]}
+
+        def step1():
+            cube, xy = layer.forward_fused(hm1, meta1, cams, rt, want_cube=True, want_xy=True)
+            vals, idx, flat = nms2D(xy[:, root:root + 1], K)
+            return gather_columns(cube, flat)
+
+        for _ in range(3):
+            step1()
+        torch.cuda.synchronize()
+        lat = []
+        for _ in range(20):
+            t1 = time.perf_counter()
+            step1()
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - t1) * 1e3)
+        extra["latency_b1_ms"] = float(np.median(lat))
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
-        sg_cpu = layer.sample_grid[seq].cpu().contiguous()
+        sg_cpu = layer.build_sample_grid(cams, seq, rt, dev).cpu().contiguous()
         cpu = cpu_baseline(w, sg_cpu, args.cpu_seconds)
 
     if rank == 0:
@@ -250,7 +293,13 @@ def main():
                 "traffic": None if traffic is None else round(traffic["corrected"]),
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": round(vox_ms, 4),
+                "measured_copy_gbs": round(extra.get("copy_gbs", 0.0), 1),
+                "frac_of_measured_copy": round(achieved / extra["copy_gbs"], 4) if extra.get("copy_gbs") else None,
+                "tap_rate": {"bound": "vector-memory 64 B/clk/CU", "achieved": round(tap_rate, 3),
+                             "peak": round(tap_peak, 3), "unit": "T joint-taps/s",
+                             "frac": round(tap_rate / tap_peak, 4), "joint_taps_per_launch": taps},
             },
+            "latency_b1_ms": round(extra["latency_b1_ms"], 3) if "latency_b1_ms" in extra else None,
             "cpu_baseline": cpu,
             "cache_build_ms": round(cache_ms, 2),
         }

@@ -88,16 +88,29 @@ __device__ __forceinline__ Taps4<PAIR> setup_taps(float gx, float gy, float sxs,
 }
 
 // -- gather pass ----------------------------------------------------------------
-template <int LPV, bool PAIR>
-__global__ __launch_bounds__(256) void voxelize_kernel(const void *__restrict__ tab, const float *__restrict__ grids,
+// Where the sampling coordinates come from: a packed per-sequence grid
+// (OTF = false), or the camera records, projected on the fly with the exact
+// fp32 sequence of project_grid_kernel (OTF = true; used when the grid would
+// not stay cache-resident, e.g. 31 cameras x 160x160x64 = 420 MB).
+struct CoordSource {
+    const float *grids;     // packed grids [S][N][GV][2]            (!OTF)
+    const float *cams;      // camera records [S][V][FVP_CAM_STRIDE] (OTF)
+    const float *resize_t;  // [2][3]                                (OTF)
+    fvp_grid_spec gs;
+    fvp_image_spec im;
+};
+
+template <int LPV, bool PAIR, bool OTF>
+__device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
-                                                       int H, int W, int X, int Y, int Z, int cols, int col_blocks) {
+                                                       int H, int W, int X, int Y, int Z, int cols, int col_blocks,
+                                                       int SP) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
     constexpr int CPG = 2 * LPV;    // cameras per grid load (2 per lane)
-    extern __shared__ __attribute__((aligned(16))) float stage[];  // [JP][SP]
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [JP][SP] (+ OTF camera records)
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int bl = L / col_blocks;  // frame within the chunk
     const int b = frame0 + bl;      // frame within the batch (outputs, grid_index)
@@ -105,7 +118,6 @@ __global__ __launch_bounds__(256) void voxelize_kernel(const void *__restrict__ 
     const int c0 = (L - bl * col_blocks) * cols;
     const int ncols = min(cols, XY - c0);
     const int T = ncols * Z;
-    const int SP = cols * Z + 1;
     const long long N = (long long)XY * Z;
     const long long n0 = (long long)c0 * Z;
     const int q = threadIdx.x % LPV;
@@ -114,8 +126,18 @@ __global__ __launch_bounds__(256) void voxelize_kernel(const void *__restrict__ 
     const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
     const float fV = (float)V;
     const int gsel = grid_index ? grid_index[b] : 0;
-    const __amdgpu_buffer_rsrc_t grs =
-        uniform_rsrc(grids + (size_t)gsel * N * GV * 2, (unsigned)(N * GV * 8));
+    __amdgpu_buffer_rsrc_t grs;
+    float *lcam = stage + ((JP * SP + 3) & ~3);  // OTF: camera records [GV][FVP_CAM_STRIDE] after the stage
+    float rt[6];
+    if constexpr (OTF) {
+        const float *cams = src_.cams + (size_t)gsel * V * FVP_CAM_STRIDE;
+        for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256) lcam[e] = e < V * FVP_CAM_STRIDE ? cams[e] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) rt[k] = src_.resize_t[k];
+        __syncthreads();
+    } else {
+        grs = uniform_rsrc(src_.grids + (size_t)gsel * N * GV * 2, (unsigned)(N * GV * 8));
+    }
     // per-camera image of this frame in the workspace
     const unsigned unit = PAIR ? 64u : JP * 4u;                               // bytes per pixel / entry
     const unsigned img = PAIR ? (unsigned)(H * (W + 1)) * 64u : (unsigned)(H * W) * unit;  // bytes per camera
@@ -126,13 +148,36 @@ __global__ __launch_bounds__(256) void voxelize_kernel(const void *__restrict__ 
         const bool valid = i < T;
         const int ii = min(i, T - 1);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        float wx_ = 0.f, wy_ = 0.f, wz_ = 0.f;  // OTF: voxel centre (compute_grid, project_whole.py:43-79)
+        if constexpr (OTF) {
+            const long long n = n0 + ii;
+            const int iz = (int)(n % Z);
+            const long long r = n / Z;
+            wx_ = axis_coord(src_.gs.start[0], src_.gs.end[0], X, (int)(r / Y), src_.gs.center[0]);
+            wy_ = axis_coord(src_.gs.start[1], src_.gs.end[1], Y, (int)(r % Y), src_.gs.center[1]);
+            wz_ = axis_coord(src_.gs.start[2], src_.gs.end[2], Z, iz, src_.gs.center[2]);
+        }
         for (int v0 = 0; v0 < V; v0 += CPG) {
-            // slots v0+2q, v0+2q+1 of voxel n0+ii (past the row: next voxel's or 0, unused)
-            const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(
-                grs, (unsigned)(((n0 + ii) * GV + v0 + 2 * q) * 8), 0, 0);
+            // cameras v0+2q, v0+2q+1 of voxel n0+ii (past V: padding, unused)
             float g[4];
+            if constexpr (OTF) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) g[k] = valid ? __builtin_bit_cast(float, (unsigned)graw[k]) : -2.0f;
+                for (int h = 0; h < 2; ++h) {
+                    const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
+                    float px, py;
+                    project_point(c, wx_, wy_, wz_, px, py);
+                    pixel_to_sample(px, py, rt, src_.im.ori_max, src_.im.img_w, src_.im.img_h, (float)src_.im.hm_w,
+                                    (float)src_.im.hm_h, g[2 * h], g[2 * h + 1]);
+                }
+            } else {
+                // slots v0+2q, v0+2q+1 (past the row: the next voxel's or 0)
+                const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(
+                    grs, (unsigned)(((n0 + ii) * GV + v0 + 2 * q) * 8), 0, 0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
             const Taps4<PAIR> t0 = setup_taps<PAIR>(g[0], g[1], sxs, sys, W, H, unit);
             const Taps4<PAIR> t1 = setup_taps<PAIR>(g[2], g[3], sxs, sys, W, H, unit);
             static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
@@ -209,6 +254,28 @@ __global__ __launch_bounds__(256) void voxelize_kernel(const void *__restrict__ 
     }
 }
 
+// Cached-grid gather: <= 64 VGPRs so 8 waves/SIMD fit (32 waves/CU with the
+// 20 KB stage); the on-the-fly variant keeps its registers (no spills).
+template <int LPV, bool PAIR, bool OTF>
+__global__ __launch_bounds__(256, 8) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
+                                                          const int32_t *__restrict__ grid_index, int frame0,
+                                                          float *__restrict__ cube, float *__restrict__ xy, int V,
+                                                          int J, int H, int W, int X, int Y, int Z, int cols,
+                                                          int col_blocks, int SP) {
+    static_assert(!OTF, "grid kernel");
+    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+}
+
+template <int LPV, bool PAIR, bool OTF>
+__global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restrict__ tab, CoordSource src,
+                                                            const int32_t *__restrict__ grid_index, int frame0,
+                                                            float *__restrict__ cube, float *__restrict__ xy, int V,
+                                                            int J, int H, int W, int X, int Y, int Z, int cols,
+                                                            int col_blocks, int SP) {
+    static_assert(OTF, "on-the-fly kernel");
+    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+}
+
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
 __global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict__ g, float2 *__restrict__ out, int V,
                                                         int GV, long long N) {
@@ -220,6 +287,14 @@ __global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict
 }
 
 static int cols_per_block(int Z) { return Z >= 320 ? 1 : 320 / Z; }
+
+// LDS row pitch of the stage: one float of padding against bank conflicts,
+// unless dropping it lets 8 blocks (32 waves, full occupancy) share a CU's 160 KB.
+static int stage_pitch(int LPV, int cols, int Z) {
+    const int T = cols * Z;
+    const size_t padded = (size_t)16 * LPV * (T + 1), tight = (size_t)16 * LPV * T;
+    return (padded > 20480 && tight <= 20480) ? T : T + 1;
+}
 
 static bool use_pairs(int J, bool half) { return half && J <= 16; }
 
@@ -239,45 +314,54 @@ static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     return (int)c;
 }
 
-template <int LPV, bool PAIR, typename T>
-static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const float *grids, const int32_t *grid_index,
-                      int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
+template <int LPV, bool PAIR, bool OTF, typename T>
+static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
+                      const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
     const bool half = sizeof(T) == 2;
     const int chunk = chunk_frames(B, V, J, H, W, half);
     const int cols = cols_per_block(Z);
     const int col_blocks = (X * Y + cols - 1) / cols;
-    const size_t lds = (size_t)4 * LPV * (cols * Z + 1) * sizeof(float);
+    const int SP = stage_pitch(LPV, cols, Z);
+    size_t lds = (size_t)4 * LPV * SP * sizeof(float);
+    if (OTF) lds = ((lds / 4 + 3) & ~(size_t)3) * 4 + (size_t)FVP_GRID_SLOTS(V) * FVP_CAM_STRIDE * sizeof(float);
+    if (lds > 160 * 1024) return FVP_ERR_SHAPE;
     const size_t frame_elems = (size_t)V * J * H * W;
     for (int f0 = 0; f0 < B; f0 += chunk) {
         const int nb = min(chunk, B - f0);
-        const T *src = hm + (size_t)f0 * frame_elems;
+        const T *hsrc = hm + (size_t)f0 * frame_elems;
         if constexpr (PAIR) {
             const long long total = (long long)nb * V * H * (W + 1) * 4;
-            hipLaunchKernelGGL(heatmaps_to_pairs_kernel<_Float16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                               reinterpret_cast<const _Float16 *>(src), reinterpret_cast<uint4 *>(ws), J, H, W, total);
+            hipLaunchKernelGGL(heatmaps_to_pairs_kernel<_Float16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                               s, reinterpret_cast<const _Float16 *>(hsrc), reinterpret_cast<uint4 *>(ws), J, H, W,
+                               total);
         } else {
-            launch_layout<LPV, T>(src, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
+            launch_layout<LPV, T>(hsrc, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
         }
-        hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s, ws,
-                           grids, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks);
+        if constexpr (OTF)
+            hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true>), dim3((unsigned)(nb * col_blocks)), dim3(256),
+                               lds, s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+        else
+            hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds,
+                               s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
     }
     return (int)hipGetLastError();
 }
 
-template <typename T>
-static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const float *grids, const int32_t *grid_index,
-                        int X, int Y, int Z, float *cube, float *xy, void *ws, size_t ws_bytes, hipStream_t s) {
+template <bool OTF, typename T>
+static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
+                        const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws,
+                        size_t ws_bytes, hipStream_t s) {
     const bool half = sizeof(T) == 2;
     const size_t need = (size_t)chunk_frames(B, V, J, H, W, half) * frame_bytes(V, J, H, W, half);
     if (!ws || ws_bytes < need) return FVP_ERR_WORKSPACE;
     if (frame_bytes(1, J, H, W, half) > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets
     if (use_pairs(J, half))
-        return run_chunks<4, true, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
+        return run_chunks<4, true, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
     switch (lanes_per_voxel(J)) {
-        case 1: return run_chunks<1, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 2: return run_chunks<2, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 4: return run_chunks<4, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
-        default: return run_chunks<8, false, T>(hm, B, V, J, H, W, grids, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 1: return run_chunks<1, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 2: return run_chunks<2, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 4: return run_chunks<4, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        default: return run_chunks<8, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
     }
 }
 
@@ -321,8 +405,10 @@ extern "C" int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, i
     const int st = fvp::check_args(heatmaps, B, V, J, H, W, packed_grids, X, Y, Z);
     if (st != FVP_OK) return st;
     if (!cube && !xy) return FVP_OK;
-    return fvp::voxelize_any<float>(heatmaps, B, V, J, H, W, packed_grids, grid_index, X, Y, Z, cube, xy, workspace,
-                                    workspace_bytes, (hipStream_t)stream);
+    fvp::CoordSource src{};
+    src.grids = packed_grids;
+    return fvp::voxelize_any<false, float>(heatmaps, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, workspace,
+                                           workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W, const float *packed_grids,
@@ -331,6 +417,32 @@ extern "C" int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H
     const int st = fvp::check_args(heatmaps, B, V, J, H, W, packed_grids, X, Y, Z);
     if (st != FVP_OK) return st;
     if (!cube && !xy) return FVP_OK;
-    return fvp::voxelize_any<_Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, packed_grids,
-                                       grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
+    fvp::CoordSource src{};
+    src.grids = packed_grids;
+    return fvp::voxelize_any<false, _Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, src,
+                                              grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes,
+                                              (hipStream_t)stream);
+}
+
+extern "C" int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H, int W,
+                                 const float *cams, const int32_t *grid_index, const float *resize_t,
+                                 const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
+                                 void *workspace, size_t workspace_bytes, void *stream) {
+    if (!cams || !resize_t || !grid || !img) return FVP_ERR_NULL;
+    const int X = grid->bins[0], Y = grid->bins[1], Z = grid->bins[2];
+    const int st = fvp::check_args(heatmaps, B, V, J, H, W, cams, X, Y, Z);
+    if (st != FVP_OK) return st;
+    if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
+    if (!cube && !xy) return FVP_OK;
+    fvp::CoordSource src{};
+    src.cams = cams;
+    src.resize_t = resize_t;
+    src.gs = *grid;
+    src.im = *img;
+    if (half)
+        return fvp::voxelize_any<true, _Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, src,
+                                                 grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes,
+                                                 (hipStream_t)stream);
+    return fvp::voxelize_any<true, float>(reinterpret_cast<const float *>(heatmaps), B, V, J, H, W, src, grid_index,
+                                          X, Y, Z, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
 }

@@ -45,6 +45,9 @@ SIGNATURES = {
                      c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_voxelize_f16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
+    "fvp_voxelize_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                          ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p, c_void_p, c_void_p,
+                          ctypes.c_size_t, c_void_p],
     "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],

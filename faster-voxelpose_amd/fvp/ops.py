@@ -131,6 +131,50 @@ def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Opt
     return cube, xy
 
 
+@torch.library.custom_op("fvp::voxelize_cams", mutates_args=(), device_types="cuda")
+def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Optional[torch.Tensor],
+                  resize_t: torch.Tensor, start: list[float], end: list[float], center: list[float], bins: list[int],
+                  ori_max: float, img_w: float, img_h: float, want_cube: bool,
+                  want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """voxelize with the sampling coordinates projected on the fly from packed camera
+    records cams [S,V,FVP_CAM_STRIDE] (no cached grid; for grids too large to stay cached)."""
+    if heatmaps.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps.device}")
+    half = heatmaps.dtype == torch.float16
+    hm = heatmaps.contiguous() if half else _dev_f32(heatmaps, "heatmaps")
+    cm = _dev_f32(cams, "cams")
+    rt = _dev_f32(resize_t, "resize_transform")
+    B, V, J, H, W = hm.shape
+    if cm.dim() == 2:
+        cm = cm.unsqueeze(0)
+    if cm.shape[1] != V:
+        raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
+    X, Y, Z = bins
+    gi = None
+    if grid_index is not None:
+        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
+    cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
+    xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
+    lib = _lib.load()
+    ws_bytes = (lib.fvp_voxelize_f16_workspace_bytes if half else lib.fvp_voxelize_workspace_bytes)(B, V, J, H, W)
+    if ws_bytes == 0:
+        raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
+    g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
+    im = ImageSpec(ori_max, img_w, img_h, W, H)
+    _lib.call("fvp_voxelize_cams", _ptr(hm), int(half), B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im,
+              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _ptr(ws), ws_bytes, _stream(hm))
+    return cube, xy
+
+
+@voxelize_cams.register_fake
+def _(heatmaps, cams, grid_index, resize_t, start, end, center, bins, ori_max, img_w, img_h, want_cube, want_xy):
+    B, V, J = heatmaps.shape[:3]
+    X, Y, Z = bins
+    return (heatmaps.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
+            heatmaps.new_empty((B, J, X, Y) if want_xy else (0,)))
+
+
 @voxelize.register_fake
 def _(heatmaps, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
     B, V, J = heatmaps.shape[:3]

@@ -117,6 +117,19 @@ int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W,
                      int X, int Y, int Z, float *cube, float *xy,
                      void *workspace, size_t workspace_bytes, void *stream);
 
+/* Same operation with the sampling coordinates projected on the fly from the
+ * camera records (the exact fp32 sequence of fvp_project_grid) instead of read
+ * from a cached grid: for configurations whose grid would not stay
+ * cache-resident (e.g. 31 cameras x 160x160x64 = 420 MB per sequence).
+ *   half       0: heatmaps fp32, 1: fp16 (workspace as fvp_voxelize[_f16])
+ *   cams       device [n_seq][V][FVP_CAM_STRIDE]; grid_index selects the sequence
+ *   resize_t   device [2][3];  grid, img as for fvp_project_grid
+ *              (X,Y,Z = grid->bins; img->hm_w/hm_h must equal W/H) */
+int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H, int W,
+                      const float *cams, const int32_t *grid_index, const float *resize_t,
+                      const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
+                      void *workspace, size_t workspace_bytes, void *stream);
+
 /* Peak NMS + top-K on a [B,1,X,Y] map: 3x3 max-pool keep mask, top-K of the
  * masked map (value descending, flat index ascending on ties), and
  * get_index2D's (flat // X, flat % X) decode.

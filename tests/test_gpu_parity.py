@@ -205,12 +205,14 @@ def test_ragged_shapes_vs_oracle(gpu_device, bins, J, hm_size):
         _assert_same(xy[b].cpu().numpy(), O.xy_plane(ref), f"xy frame {b}")
 
 
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "onthefly"])
 @pytest.mark.parametrize("half", [False, True], ids=["f32", "f16"])
 @pytest.mark.parametrize("V,J", [(1, 3), (2, 6), (4, 1), (7, 15), (31, 15), (31, 24), (7, 32), (3, 16)])
-def test_camera_and_joint_counts_vs_oracle(gpu_device, V, J, half):
+def test_camera_and_joint_counts_vs_oracle(gpu_device, V, J, half, otf):
     """Every lane-group size (J -> 1/2/4/8 lanes per voxel), odd/even and
     >2*LPV camera counts (packed-grid groups), the fp16 pixel-pair table
-    (J <= 16) and the fp16 -> fp32 layout fallback (J > 16)."""
+    (J <= 16), the fp16 -> fp32 layout fallback (J > 16), and the cached-grid
+    and on-the-fly-projection coordinate sources."""
     from fvp import geometry, synthetic
     from fvp.project_whole import ProjectLayer
 
@@ -218,6 +220,7 @@ def test_camera_and_joint_counts_vs_oracle(gpu_device, V, J, half):
     w = _custom_workload(base="c5", voxels_per_axis=bins, num_joints=J, heatmap_size=hm_size, extra={"views": V})
     layer = ProjectLayer(w.cfg(str(gpu_device)))
     layer.verbose = False
+    layer.on_the_fly = otf
     cams, seq = w.cameras()
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
     hm = synthetic.uniform_heatmaps(w, 3, seed=V * 100 + J)
@@ -262,7 +265,8 @@ def test_sample_grid_is_view_of_packed_grid(gpu_device):
     assert torch.equal(cube, cube2)
 
 
-def test_mixed_sequences_in_one_batch(gpu_device):
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "onthefly"])
+def test_mixed_sequences_in_one_batch(gpu_device, otf):
     """Frames of different sequences (different cameras) in one launch."""
     from fvp import geometry, synthetic
     from fvp.project_whole import ProjectLayer
@@ -271,6 +275,7 @@ def test_mixed_sequences_in_one_batch(gpu_device):
     w = WORKLOADS["c3"]
     layer = ProjectLayer(w.cfg(str(gpu_device)))
     layer.verbose = False
+    layer.on_the_fly = otf
     cams, seq = w.cameras()
     cams2 = {"a": cams[seq], "b": list(reversed(cams[seq]))}
     trans = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
@@ -281,6 +286,11 @@ def test_mixed_sequences_in_one_batch(gpu_device):
         single, sxy = layer.forward_fused(hm[b:b + 1], {"seq": [s]}, cams2, trans.to(gpu_device))
         assert torch.equal(single[0], cube[b]) and torch.equal(sxy[0], xy[b])
     assert not torch.equal(cube[0], cube[1])
+    other = ProjectLayer(w.cfg(str(gpu_device)))
+    other.verbose = False
+    other.on_the_fly = not otf
+    c_o, x_o = other.forward_fused(hm, meta, cams2, trans.to(gpu_device))
+    assert torch.equal(c_o, cube) and torch.equal(x_o, xy)  # both coordinate sources agree bit-for-bit
 
 
 def test_batch_invariance_full_size(gpu_device):

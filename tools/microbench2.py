@@ -104,11 +104,36 @@ def main():
                                stream)
             assert rc == 0, rc
         return f
+    from fvp import _lib as fl
+    lib.voxnext_otf.argtypes = [vp, i_] + [i_] * 5 + [vp, vp, ctypes.POINTER(fl.GridSpec), ctypes.POINTER(fl.ImageSpec),
+                                                     vp, vp, vp, i_, i_, vp]
+    cams_t = torch.from_numpy(geometry.pack_cameras(cams, seq)).to(dev)
+    st_, en_, ce_, nb_ = layer.grid_spec()
+    gspec = fl.GridSpec((ctypes.c_float * 3)(*st_), (ctypes.c_float * 3)(*en_), (ctypes.c_float * 3)(*ce_),
+                        (ctypes.c_int32 * 3)(*nb_))
+    ispec = fl.ImageSpec(float(max(w.ori_image_size)), float(w.image_size[0]), float(w.image_size[1]),
+                         int(w.heatmap_size[0]), int(w.heatmap_size[1]))
+
+    def otf(chunk, cols):
+        def f():
+            rc = lib.voxnext_otf(hm.data_ptr(), int(hm.dtype == torch.float16), B, V, J, H, W, cams_t.data_ptr(),
+                                 rt.data_ptr(), ctypes.byref(gspec), ctypes.byref(ispec), cube.data_ptr(),
+                                 xy.data_ptr(), (wsh if hm.dtype == torch.float16 else ws).data_ptr(), chunk, cols, stream)
+            assert rc == 0, rc
+        return f
+    lib.voxnext_occ.argtypes = [vp] + [i_] * 5 + [vp] + [i_] * 3 + [vp, vp, vp, i_, i_, i_, vp]
+
+    def occ(chunk, cols, lds):
+        def f():
+            rc = lib.voxnext_occ(hm.data_ptr(), B, V, J, H, W, gq2.data_ptr(), X, Y, Z, cube.data_ptr(),
+                                 xy.data_ptr(), ws.data_ptr(), chunk, cols, lds, stream)
+            assert rc == 0, rc
+        return f
     cube = torch.empty_like(ref_cube)
     xy = torch.empty_like(ref_xy)
     per = V * H * W * 16 * 4
     chunk0 = max(1, min(B, (80 << 20) // per))
-    ws = torch.empty(max(chunk0, 16) * per // 4, device=dev)
+    ws = torch.empty(max(2 * chunk0, 16) * per // 4, device=dev)
 
     def product():
         layer.forward_fused(hm, meta, cams, rt)
@@ -125,16 +150,21 @@ def main():
 
     cols0 = 1 if Z >= 320 else 320 // Z
     cands = {"product": product}
-    cands[f"qg chunk={chunk0} cols={cols0} pf=1"] = qg(chunk0, cols0, 0, 1)
-    for F, pf in ((1, 1),):
-        for chunk in sorted({chunk0, max(F, chunk0 // 2)}):
-            cands[f"mf chunk={chunk} F={F} pf={pf}"] = mf(chunk, cols0, F, pf)
+
+    hchunk = max(1, (80 << 20) // hper)
     if hm.dtype == torch.float16:
-        hchunk = max(1, (80 << 20) // hper)
         for chunk in sorted({hchunk, 2 * hchunk}):
             for cols in sorted({cols0, max(1, cols0 // 2)}):
                 cands[f"fp16 pair chunk={chunk} cols={cols}"] = hvar(chunk, cols)
                 cands[f"fp16 pair qg chunk={chunk} cols={cols}"] = hvar(chunk, cols, True)
+    if hm.dtype == torch.float32:
+        for lds in (0, -1):
+            cands[f"occ chunk={chunk0} cols={cols0} lds={lds >> 10}K"] = occ(chunk0, cols0, lds)
+        cands[f"occ chunk={2 * chunk0} cols={cols0} lds=0"] = occ(2 * chunk0, cols0, 0)
+        cands[f"occ chunk={2 * chunk0} cols={cols0} lds=40K"] = occ(2 * chunk0, cols0, 40 << 10)
+    ochunk = hchunk * 2 if hm.dtype == torch.float16 else chunk0
+    for cols in sorted({cols0, max(1, cols0 // 2)}):
+        cands[f"otf chunk={ochunk} cols={cols}"] = otf(ochunk, cols)
     probes = {f"probe L1-taps chunk={chunk0}": qg(chunk0, cols0, 1)}
     lay = lambda: [lib.voxnext_layout(hm.data_ptr() + c * chunk0 * fbytes, int(hm.dtype == torch.float16),
                                       min(chunk0, B - c * chunk0), V, J, H, W, ws.data_ptr(), stream)

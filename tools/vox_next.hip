@@ -10,7 +10,7 @@
 // voxel-camera this removes a grid load and 3/4 of the coordinate VALU.
 #include <utility>
 
-#include "../faster-voxelpose_amd/csrc/fvp_layout.h"
+#include "../faster-voxelpose_amd/csrc/fvp_voxelize.hip"
 
 namespace fvp {
 namespace next {
@@ -30,10 +30,6 @@ __device__ __forceinline__ unsigned bcast(unsigned x) {
     }
 }
 
-template <int... K, typename F>
-__device__ __forceinline__ void static_for(std::integer_sequence<int, K...>, F &&f) {
-    (f(std::integral_constant<int, K>{}), ...);
-}
 
 struct Tap {
     unsigned o[4];  // byte offsets of the 4 taps' pixels (kOOB when outside)
@@ -548,6 +544,143 @@ __global__ __launch_bounds__(256) void gather_hq(const uint4 *__restrict__ tab, 
     }
 }
 
+// On-the-fly projection: no grid read.  Lane q of a voxel group projects the
+// voxel centre into cameras v0+2q, v0+2q+1 (camera records staged in LDS) with
+// the exact fp32 sequence of project_grid_kernel, then the product's tap code.
+template <int LPV, bool PAIR>
+__global__ __launch_bounds__(256) void gather_otf(const void *__restrict__ tab, const float *__restrict__ cams,
+                                                  const float *__restrict__ resize_t, fvp_grid_spec gs,
+                                                  fvp_image_spec im, int frame0, float *__restrict__ cube,
+                                                  float *__restrict__ xy, int V, int J, int H, int W, int X, int Y,
+                                                  int Z, int cols, int col_blocks) {
+    constexpr int JP = 4 * LPV;
+    constexpr int VPP = 256 / LPV;
+    constexpr int CPG = 2 * LPV;
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [JP][SP] then cams [GV][24], rt[6]
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int bl = L / col_blocks;
+    const int b = frame0 + bl;
+    const int XY = X * Y;
+    const int c0 = (L - bl * col_blocks) * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const int SP = cols * Z + 1;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    float *lcam = stage + JP * SP + 3;  // 16-B aligned enough for float reads
+    for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256)
+        lcam[e] = e < V * FVP_CAM_STRIDE ? cams[e] : 0.0f;
+    float rt[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rt[k] = resize_t[k];
+    __syncthreads();
+    const unsigned unit = PAIR ? 64u : JP * 4u;
+    const unsigned img = PAIR ? (unsigned)(H * (W + 1)) * 64u : (unsigned)(H * W) * unit;
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
+
+    for (int i0 = 0; i0 < T; i0 += VPP) {
+        const int i = i0 + threadIdx.x / LPV;
+        const bool valid = i < T;
+        const int ii = min(i, T - 1);
+        const long long n = n0 + ii;
+        const int iz = (int)(n % Z);
+        const long long r = n / Z;
+        const int iy = (int)(r % Y), ix = (int)(r / Y);
+        const float wx_ = axis_coord(gs.start[0], gs.end[0], gs.bins[0], ix, gs.center[0]);
+        const float wy_ = axis_coord(gs.start[1], gs.end[1], gs.bins[1], iy, gs.center[1]);
+        const float wz_ = axis_coord(gs.start[2], gs.end[2], gs.bins[2], iz, gs.center[2]);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int v0 = 0; v0 < V; v0 += CPG) {
+            float g[4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int vc = min(v0 + 2 * q + h, GV - 1);
+                const Cam c = load_cam(lcam + vc * FVP_CAM_STRIDE);
+                float px, py;
+                project_point(c, wx_, wy_, wz_, px, py);
+                pixel_to_sample(px, py, rt, im.ori_max, im.img_w, im.img_h, (float)im.hm_w, (float)im.hm_h, g[2 * h],
+                                g[2 * h + 1]);
+            }
+            if (!valid) g[0] = g[1] = g[2] = g[3] = -2.0f;
+            const Taps4<PAIR> t0 = setup_taps<PAIR>(g[0], g[1], sxs, sys, W, H, unit);
+            const Taps4<PAIR> t1 = setup_taps<PAIR>(g[2], g[3], sxs, sys, W, H, unit);
+            static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = k >> 1;
+                const int v = v0 + k;
+                if (v >= V) return;
+                const Taps4<PAIR> &src = (k & 1) ? t1 : t0;
+                unsigned o[Taps4<PAIR>::NO];
+                unsigned all = kOOB;
+#pragma unroll
+                for (int m = 0; m < Taps4<PAIR>::NO; ++m) {
+                    o[m] = group_bcast<LPV, S>(src.o[m]);
+                    all &= o[m];
+                }
+                if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+                float w[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(src.w[m]);
+                const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+                if constexpr (PAIR) {
+                    const u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                    const u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const unsigned ua = r0[m >> 1], ub = r0[2 + (m >> 1)];
+                        const unsigned uc = r1[m >> 1], ud = r1[2 + (m >> 1)];
+                        const float fa = (m & 1) ? h_hi(ua) : h_lo(ua);
+                        const float fb = (m & 1) ? h_hi(ub) : h_lo(ub);
+                        const float fc = (m & 1) ? h_hi(uc) : h_lo(uc);
+                        const float fd = (m & 1) ? h_hi(ud) : h_lo(ud);
+                        acc[m] = acc[m] +
+                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                    }
+                } else {
+                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                    const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                    const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
+                    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
+                        const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
+                        const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
+                        const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
+                        acc[m] = acc[m] +
+                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                    }
+                }
+            });
+        }
+        if (valid) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf(acc[m] / fV, 0.0f, 1.0f);
+        }
+    }
+    __syncthreads();
+    if (cube) {
+        for (int j = 0; j < J; ++j) {
+            float *__restrict__ dst = cube + ((size_t)b * J + j) * N + n0;
+            for (int e = threadIdx.x; e < T; e += 256) dst[e] = stage[j * SP + e];
+        }
+    }
+    if (xy) {
+        for (int e = threadIdx.x; e < J * ncols; e += 256) {
+            const int j = e / ncols, cc = e - (e / ncols) * ncols;
+            const float *s = stage + j * SP + cc * Z;
+            float m = -INFINITY;
+            for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+            xy[((size_t)b * J + j) * XY + c0 + cc] = m;
+        }
+    }
+}
+
 // [V][N][2] -> [N][GV][2], padded cameras (-2,-2) (off-image)
 __global__ void regrid_kernel(const float2 *__restrict__ g, float2 *__restrict__ out, int V, int GV, long long N) {
     const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -686,6 +819,55 @@ extern "C" int voxnext_h(const void *hm, int B, int V, int J, int H, int W, cons
         else
             hipLaunchKernelGGL(next::gather_h, dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s, (const uint4 *)ws,
                                (const float2 *)grids, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks);
+    }
+    return (int)hipGetLastError();
+}
+
+// On-the-fly op (fp32 CL or fp16 pairs per input dtype), per chunk.
+extern "C" int voxnext_otf(const void *hm, int half, int B, int V, int J, int H, int W, const float *cams,
+                           const float *rt, const fvp_grid_spec *gs, const fvp_image_spec *im, float *cube, float *xy,
+                           void *ws, int chunk, int cols, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (J > 16 || J < 9) return -1;
+    const int X = gs->bins[0], Y = gs->bins[1], Z = gs->bins[2];
+    const int col_blocks = (X * Y + cols - 1) / cols;
+    const size_t lds = ((size_t)16 * (cols * Z + 1) + 3 + (size_t)(V + 1) * FVP_CAM_STRIDE) * sizeof(float);
+    const size_t frame_elems = (size_t)V * J * H * W;
+    for (int f0 = 0; f0 < B; f0 += chunk) {
+        const int nb = min(chunk, B - f0);
+        const dim3 grid((unsigned)(nb * col_blocks));
+        if (half) {
+            const long long total = (long long)nb * V * H * (W + 1) * 4;
+            hipLaunchKernelGGL(heatmaps_to_pairs_kernel<_Float16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                               s, (const _Float16 *)hm + (size_t)f0 * frame_elems, (uint4 *)ws, J, H, W, total);
+            hipLaunchKernelGGL((next::gather_otf<4, true>), grid, dim3(256), lds, s, ws, cams, rt, *gs, *im, f0, cube,
+                               xy, V, J, H, W, X, Y, Z, cols, col_blocks);
+        } else {
+            launch_layout<4, float>((const float *)hm + (size_t)f0 * frame_elems, nb, V, J, H, W, (float *)ws, s);
+            hipLaunchKernelGGL((next::gather_otf<4, false>), grid, dim3(256), lds, s, ws, cams, rt, *gs, *im, f0,
+                               cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks);
+        }
+    }
+    return (int)hipGetLastError();
+}
+
+// Product kernel with a chosen dynamic-LDS size (occupancy limiter), chunk and cols.
+extern "C" int voxnext_occ(const float *hm, int B, int V, int J, int H, int W, const float *packed, int X, int Y, int Z,
+                           float *cube, float *xy, void *ws, int chunk, int cols, int lds_bytes, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (lanes_per_voxel(J) != 4) return -1;
+    const int col_blocks = (X * Y + cols - 1) / cols;
+    const int SP = lds_bytes < 0 ? cols * Z : cols * Z + 1;
+    size_t lds = (size_t)16 * SP * sizeof(float);
+    if (lds_bytes > 0 && (size_t)lds_bytes > lds) lds = lds_bytes;
+    CoordSource src{};
+    src.grids = packed;
+    const size_t frame_elems = (size_t)V * J * H * W;
+    for (int f0 = 0; f0 < B; f0 += chunk) {
+        const int nb = min(chunk, B - f0);
+        launch_layout<4, float>(hm + (size_t)f0 * frame_elems, nb, V, J, H, W, (float *)ws, s);
+        hipLaunchKernelGGL((voxelize_kernel<4, false, false>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s,
+                           ws, src, nullptr, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
     }
     return (int)hipGetLastError();
 }

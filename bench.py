@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
 
 METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_pairs_kernel", "voxelize_kernel")  # the fvp_voxelize op
+VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_pairs_kernel", "voxelize_kernel", "voxelize_cams_kernel")  # the fvp_voxelize op
 
 
 def parse():

@@ -107,6 +107,58 @@ __device__ __forceinline__ void static_for(std::integer_sequence<int, K...>, F &
     (f(std::integral_constant<int, K>{}), ...);
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float h_lo(unsigned u) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu));
+}
+__device__ __forceinline__ float h_hi(unsigned u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)); }
+
+// Bilinear setup of one voxel-camera (aten grid_sampler_2d, align_corners=True,
+// zeros padding): weights nw, ne, sw, se and the byte offsets of the taps
+// (kOOB when outside).  CL: 4 pixel offsets.  PAIR: 2 row-entry offsets.
+template <bool PAIR>
+struct Taps4 {
+    static constexpr int NO = PAIR ? 2 : 4;
+    unsigned o[NO];
+    float w[4];
+};
+
+template <bool PAIR>
+__device__ __forceinline__ Taps4<PAIR> setup_taps(float gx, float gy, float sxs, float sys, int W, int H,
+                                                  unsigned unit) {
+    Taps4<PAIR> t;
+    const float ix = (gx + 1.0f) * sxs;
+    const float iy = (gy + 1.0f) * sys;
+    const bool nan_ = (ix != ix) || (iy != iy);
+    const float x0f = floorf(ix), y0f = floorf(iy);
+    const float wx = ix - x0f, ex = 1.0f - wx;
+    const float ny = iy - y0f, syw = 1.0f - ny;
+    t.w[0] = syw * ex;
+    t.w[1] = syw * wx;
+    t.w[2] = ny * ex;
+    t.w[3] = ny * wx;
+    // NaN coordinates read in-image taps so the NaN weights propagate (as in
+    // grid_sample); far-off coordinates are clamped before the int conversion.
+    const int x0 = nan_ ? 0 : (int)fminf(fmaxf(x0f, -4.0f), (float)W + 4.0f);
+    const int y0 = nan_ ? 0 : (int)fminf(fmaxf(y0f, -4.0f), (float)H + 4.0f);
+    const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
+    if constexpr (PAIR) {
+        const bool vx = (x0 >= -1) & (x0 < W);
+        const unsigned e0 = (unsigned)(y0 * (W + 1) + x0 + 1) * unit;
+        t.o[0] = (vx & vy0) ? e0 : kOOB;
+        t.o[1] = (vx & vy1) ? e0 + (unsigned)(W + 1) * unit : kOOB;
+    } else {
+        const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
+        const unsigned p = (unsigned)(y0 * W + x0) * unit;
+        t.o[0] = (vy0 & vx0) ? p : kOOB;
+        t.o[1] = (vy0 & vx1) ? p + unit : kOOB;
+        t.o[2] = (vy1 & vx0) ? p + (unsigned)W * unit : kOOB;
+        t.o[3] = (vy1 & vx1) ? p + (unsigned)(W + 1) * unit : kOOB;
+    }
+    return t;
+}
+
 inline int lanes_per_voxel(int J) { return J <= 4 ? 1 : J <= 8 ? 2 : J <= 16 ? 4 : 8; }
 
 inline size_t cl_frame_bytes(int V, int J, int H, int W) {

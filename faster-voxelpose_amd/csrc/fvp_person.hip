@@ -109,14 +109,15 @@ __global__ __launch_bounds__(256) void max_planes_kernel(const float *__restrict
 // Outside-window voxels are 0 exactly as in the reference cube.
 template <int LPV, int YG>
 __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
-                                                             const float2 *__restrict__ fgrid,
+                                                             const float *__restrict__ fgrid,
                                                              const float *__restrict__ props,
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
                                                              float *__restrict__ cubes, float *__restrict__ planes,
                                                              float *__restrict__ offset, int P, int V, int J, int H,
                                                              int W) {
     constexpr int JP = 4 * LPV;
-    constexpr int NW = LPV;  // waves per block (64*LPV threads)
+    constexpr int NW = LPV;       // waves per block (64*LPV threads)
+    constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
     __shared__ float xy_part[NW][YG][JP];
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
     const int ngroups = (SY + YG - 1) / YG;
@@ -133,10 +134,14 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     const int b = frame_of ? frame_of[p] : 0;
     const unsigned HW = (unsigned)(H * W);
     const unsigned pix_bytes = JP * 4u;
+    const unsigned img = HW * pix_bytes;
     const unsigned qo = (unsigned)q * 16u;
     const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
     const float fV = (float)V;
+    const int GV = V + (V & 1);
     const long long FN = (long long)s.fine[0] * s.fine[1] * s.fine[2];
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(fgrid, (unsigned)(FN * GV * 8));
+    const char *__restrict__ frame_cl = (const char *)cl + (size_t)b * V * img;
     const size_t SS = (size_t)SY * SZ;
     const size_t S3 = (size_t)SX * SS;
     float *xy_pl = planes ? planes + (size_t)p * J * SX * SY : nullptr;
@@ -164,43 +169,47 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             if (__builtin_amdgcn_ballot_w64(valid)) {
                 const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
-                for (int v = 0; v < V; ++v) {
-                    float2 gg = fgrid[(size_t)v * FN + gn];
-                    if (!valid) gg = make_float2(-2.f, -2.f);
-                    const float ix = (gg.x + 1.0f) * sxs;
-                    const float iy = (gg.y + 1.0f) * sys;
-                    const bool isnan_ = (ix != ix) || (iy != iy);
-                    const float x0f = floorf(ix), y0f = floorf(iy);
-                    const float wx = ix - x0f, ex = 1.0f - wx;
-                    const float ny = iy - y0f, syw = 1.0f - ny;
-                    const float nw = syw * ex, ne = syw * wx, sw = ny * ex, se = ny * wx;
-                    const int x0 = isnan_ ? -4 : (int)x0f, y0 = isnan_ ? -4 : (int)y0f;
-                    const bool vx0 = (unsigned)x0 < (unsigned)W, vx1 = (unsigned)(x0 + 1) < (unsigned)W;
-                    const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
-                    if (isnan_) {
+                for (int v0 = 0; v0 < V; v0 += CPG) {
+                    // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
+                    const u32x4 graw =
+                        __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
+                    float g[4];
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) acc[k] = acc[k] + NAN;
-                    }
-                    if (!__builtin_amdgcn_ballot_w64((vx0 | vx1) & (vy0 | vy1))) continue;
-                    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(cl + ((size_t)b * V + v) * HW * JP, HW * pix_bytes);
-                    const unsigned pix = (unsigned)(y0 * W + x0);
-                    const auto ta = __builtin_amdgcn_raw_buffer_load_b128(rs, (vy0 & vx0) ? pix * pix_bytes + qo : kOOB, 0, 0);
-                    const auto tb = __builtin_amdgcn_raw_buffer_load_b128(
-                        rs, (vy0 & vx1) ? (pix + 1u) * pix_bytes + qo : kOOB, 0, 0);
-                    const auto tc = __builtin_amdgcn_raw_buffer_load_b128(
-                        rs, (vy1 & vx0) ? (pix + (unsigned)W) * pix_bytes + qo : kOOB, 0, 0);
-                    const auto td = __builtin_amdgcn_raw_buffer_load_b128(
-                        rs, (vy1 & vx1) ? (pix + (unsigned)W + 1u) * pix_bytes + qo : kOOB, 0, 0);
-                    if (!isnan_) {
+                    for (int k = 0; k < 4; ++k) g[k] = valid ? __builtin_bit_cast(float, (unsigned)graw[k]) : -2.0f;
+                    const Taps4<false> t0 = setup_taps<false>(g[0], g[1], sxs, sys, W, H, pix_bytes);
+                    const Taps4<false> t1 = setup_taps<false>(g[2], g[3], sxs, sys, W, H, pix_bytes);
+                    static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int S = k >> 1;
+                        const int v = v0 + k;
+                        if (v >= V) return;
+                        const Taps4<false> &src = (k & 1) ? t1 : t0;
+                        unsigned o[4];
+                        unsigned all = kOOB;
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const float fa = __builtin_bit_cast(float, (unsigned)ta[k]);
-                            const float fb = __builtin_bit_cast(float, (unsigned)tb[k]);
-                            const float fc = __builtin_bit_cast(float, (unsigned)tc[k]);
-                            const float fd = __builtin_bit_cast(float, (unsigned)td[k]);
-                            acc[k] = acc[k] + __builtin_fmaf(fd, se, __builtin_fmaf(fc, sw, __builtin_fmaf(fb, ne, fa * nw)));
+                        for (int m = 0; m < 4; ++m) {
+                            o[m] = group_bcast<LPV, S>(src.o[m]);
+                            all &= o[m];
                         }
-                    }
+                        if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+                        float wt[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) wt[m] = group_bcast<LPV, S>(src.w[m]);
+                        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_cl + (size_t)v * img, img);
+                        const u32x4 ta = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                        const u32x4 tb = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                        const u32x4 tc = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
+                        const u32x4 td = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const float fa = __builtin_bit_cast(float, (unsigned)ta[m]);
+                            const float fb = __builtin_bit_cast(float, (unsigned)tb[m]);
+                            const float fc = __builtin_bit_cast(float, (unsigned)tc[m]);
+                            const float fd = __builtin_bit_cast(float, (unsigned)td[m]);
+                            acc[m] = acc[m] + __builtin_fmaf(fd, wt[3], __builtin_fmaf(fc, wt[2],
+                                                                                      __builtin_fmaf(fb, wt[1], fa * wt[0])));
+                        }
+                    });
                 }
             }
             float o[4];
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
 }
 
 template <int LPV>
-static void launch_person_cl(const float *cl, const float2 *fgrid, const float *props, const int32_t *frame_of,
+static void launch_person_cl(const float *cl, const float *fgrid, const float *props, const int32_t *frame_of,
                              const fvp_person_spec &s, float *cubes, float *planes, float *offset, int P, int V, int J,
                              int H, int W, hipStream_t st) {
     const int SY = s.bins[1];
@@ -306,6 +315,9 @@ extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int
     if (SX <= 0 || SY <= 0 || SZ <= 0 || SZ > 64 || spec->fine[0] <= 1 || spec->fine[1] <= 1 || spec->fine[2] <= 1)
         return FVP_ERR_SHAPE;
     if (planes && !(SX == SY && SY == SZ)) return FVP_ERR_SHAPE;  // torch.cat of the planes needs a cubic volume
+    // packed fine grid addressed with 32-bit byte offsets
+    if ((long long)spec->fine[0] * spec->fine[1] * spec->fine[2] * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL)
+        return FVP_ERR_SHAPE;
     const size_t need = (size_t)B * fvp::cl_frame_bytes(V, J, H, W);
     if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
@@ -314,7 +326,7 @@ extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int
         const hipError_t e = hipMemsetAsync(planes + (size_t)P * J * SX * SZ, 0, (size_t)P * J * SX * SZ * 4, st);
         if (e != hipSuccess) return (int)e;
     }
-    const float2 *fg = reinterpret_cast<const float2 *>(fine_grid);
+    const float *fg = fine_grid;
 #define FVP_PERSON_CASE(L)                                                                                            \
     fvp::launch_layout<L, float>(heatmaps, B, V, J, H, W, cl, st);                                                   \
     fvp::launch_person_cl<L>(cl, fg, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, W, st);         \

@@ -254,8 +254,8 @@ def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: to
     pc = _dev_f32(proposals, "proposal_centers")
     B, V, J, H, W = hm.shape
     P = pc.shape[0]
-    if fg.numel() != V * fine[0] * fine[1] * fine[2] * 2:
-        raise _lib.FvpError("fvp: fine sample grid does not match fine_voxels_per_axis")
+    if tuple(fg.shape) != (fine[0] * fine[1] * fine[2], grid_slots(V), 2):
+        raise _lib.FvpError("fvp: packed fine grid must be [FX*FY*FZ, GV, 2] (pack_grid of the fine sample grid)")
     fo = None
     if frame_of is not None:
         fo = frame_of.to(device=hm.device, dtype=torch.int32).contiguous()

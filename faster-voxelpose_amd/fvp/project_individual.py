@@ -44,7 +44,8 @@ class ProjectLayer(nn.Module):
         self.bias = torch.from_numpy(c["bias"]).to(dev)
         self.center_grid = self._center_grid().to(dev)  # project_individual.py:101-107
         self._fine_grid = None
-        self.sample_grid = {}  # seq -> [V, FX, FY, FZ, 2]
+        self.sample_grid = {}  # seq -> [V, FX, FY, FZ, 2] (the reference's cache; a view of _packed)
+        self._packed = {}      # seq -> [FX*FY*FZ, GV, 2] voxel-major copy read by the person kernel
         self.verbose = True
 
     @staticmethod
@@ -85,15 +86,24 @@ class ProjectLayer(nn.Module):
                               [float(v) for v in c["whole_center"]], fine,
                               float(max(self.ori_image_size[0], self.ori_image_size[1])),
                               float(self.image_size[0]), float(self.image_size[1]), int(w), int(h))
-        return sg.view(sg.shape[0], fine[0], fine[1], fine[2], 2)
+        packed = ops.pack_grid(sg)  # voxel-major [FN, GV, 2], read by the person kernel
+        self._packed[seq] = packed
+        return ops.packed_as_reference(packed, sg.shape[0])[:, 0].view(sg.shape[0], fine[0], fine[1], fine[2], 2)
 
     def _seq_grid(self, heatmaps, index, meta, cameras, resize_transform):
+        """Packed fine grid of frame ``index``'s sequence (built once per sequence)."""
         curr_seq = meta["seq"][index]
         if curr_seq not in self.sample_grid:
             if self.verbose:
                 print("=> save the sampling grid in JLN for sequence", curr_seq)
             self.sample_grid[curr_seq] = self.build_sample_grid(cameras, curr_seq, resize_transform, heatmaps.device)
-        return self.sample_grid[curr_seq]
+        sg = self.sample_grid[curr_seq]
+        pg = self._packed.get(curr_seq)
+        if pg is None or pg.data_ptr() != sg.data_ptr():
+            # a grid assigned from outside (the reference's [V,FX,FY,FZ,2] layout): pack it once
+            pg = ops.pack_grid(sg.reshape(sg.shape[0], -1, 2).to(torch.float32).contiguous())
+            self._packed[curr_seq] = pg
+        return pg
 
     def _args(self):
         c = self._const

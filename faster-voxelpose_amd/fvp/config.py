@@ -52,6 +52,7 @@ def make_cfg(w, device: str = "cuda:0") -> AttrDict:
             "SPACE_SIZE": list(map(float, w.ind_space_size)),
             "VOXELS_PER_AXIS": list(map(int, w.ind_voxels_per_axis)),
         },
+        "NETWORK": {"BETA": 100},  # configs/*/jln64.yaml NETWORK.BETA
     })
 
 

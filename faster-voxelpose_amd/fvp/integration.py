@@ -10,7 +10,9 @@ implementations, in the modules that import them, BEFORE the model is built
     models.joint_localization_net.ProjectLayer -> fvp.project_individual.ProjectLayer  (:12)
     core.proposal.nms2D / human_detection_net.nms2D -> fvp.proposal.nms2D  (:12)
 
-With ``fused=True`` it also replaces HumanDetectionNet.forward
+With ``fused=True`` it also replaces JointLocalizationNet.forward by
+:func:`fvp.jln.fused_jln_forward` (every proposal of a batch at once, soft-argmax
+and fusion on fvp kernels; eval mode) and HumanDetectionNet.forward
 (human_detection_net.py:157-220) by :func:`fused_hdn_forward`, which takes the
 cube AND its xy max-plane from one voxelize launch (skipping CenterNet's
 ``torch.max(x, dim=4)``, cnns_2d.py:291) and uses the fvp gathers for the
@@ -24,7 +26,7 @@ import sys
 
 import torch
 
-from . import project_individual, project_whole, proposal
+from . import jln, project_individual, project_whole, proposal
 
 
 def install(fused: bool = True, modules=None) -> dict:
@@ -49,6 +51,13 @@ def install(fused: bool = True, modules=None) -> dict:
         if hdn is not None and hasattr(hdn, "HumanDetectionNet"):
             hdn.HumanDetectionNet.forward = fused_hdn_forward
             patched["models.human_detection_net.HumanDetectionNet.forward"] = fused_hdn_forward
+        jn = mods.get("models.joint_localization_net")
+        if jn is not None and hasattr(jn, "JointLocalizationNet"):
+            cls = jn.JointLocalizationNet
+            if not hasattr(cls, "_fvp_original_forward"):
+                cls._fvp_original_forward = cls.forward
+            cls.forward = jln.fused_jln_forward
+            patched["models.joint_localization_net.JointLocalizationNet.forward"] = jln.fused_jln_forward
     return patched
 
 

@@ -1,0 +1,83 @@
+"""JLN post-processing on the fvp kernels.
+
+* :class:`SoftArgmaxLayer` -- drop-in for
+  ``models.joint_localization_net.SoftArgmaxLayer`` (joint_localization_net.py:15-56):
+  same constructor (``cfg.NETWORK.BETA``), same ``forward(x, grids) -> (x, confs)``.
+* :func:`fuse_pose_preds` -- ``JointLocalizationNet.fuse_pose_preds`` (:83-120).
+* :func:`fused_jln_forward` -- ``JointLocalizationNet.forward`` (:122-182) for
+  every proposal of a batch at once: one per-person planes launch
+  (``project_layer.forward_batch``), the P2PNet / WeightNet CNNs on all
+  proposals together, the soft-argmax + offsets and the fusion as two fvp
+  launches; no per-frame loop and no per-frame host sync.  Eval mode only:
+  in training the CNNs' BatchNorm statistics are per frame in the reference,
+  so the original per-frame forward is kept.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+class SoftArgmaxLayer(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.beta = cfg.NETWORK.BETA
+
+    def forward(self, x, grids):
+        """x [3,B,C,H*W,1] or [3,B,C,H,W] -> (coords [3,B,C,2], confs [B])."""
+        ops.forward_only(x)
+        pose, maxprob = ops.soft_argmax(x, grids, None, float(self.beta))
+        C = x.shape[2]
+        confs = maxprob.sum(dim=(0, 2)) / (3 * C)
+        return pose, confs
+
+
+def fuse_pose_preds(pose_preds, weights):
+    """pose_preds [3,P,J,2], weights [3P,J,1] -> fused [P,J,3] (joint_localization_net.py:83-120)."""
+    P, J = pose_preds.shape[1], pose_preds.shape[2]
+    fused, _ = ops.fuse_poses(pose_preds, weights, pose_preds.new_zeros((3, P, J)))
+    return fused
+
+
+def fused_jln_forward(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform):
+    """JointLocalizationNet.forward (joint_localization_net.py:122-182), batched.
+
+    Same inputs and outputs: (all_fused_pose_preds [B,K,J,3],
+    all_pose_preds [3,B,K,J,2]); proposal_centers[..., 4] of valid proposals is
+    overwritten with the confidences, as in the reference (:180)."""
+    if self.training:
+        return self._fvp_original_forward(meta, heatmaps, proposal_centers, mask, cameras, resize_transform)
+    device = heatmaps.device
+    B, K = proposal_centers.shape[:2]
+    J = heatmaps.shape[2]
+    all_fused = torch.zeros((B, K, J, 3), device=device)
+    all_pose = torch.zeros((3, B, K, J, 2), device=device)
+    seqs = list(meta["seq"])[:B]
+    if len(set(seqs)) != 1:  # frames of several sequences: one batched call per sequence
+        for s in dict.fromkeys(seqs):
+            sel = torch.tensor([q == s for q in seqs], device=device)
+            _jln_batch(self, meta, heatmaps, proposal_centers, mask & sel[:, None], cameras, resize_transform,
+                       all_fused, all_pose, first=seqs.index(s))
+        return all_fused, all_pose
+    _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform, all_fused, all_pose, first=0)
+    return all_fused, all_pose
+
+
+def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform, all_fused, all_pose, first):
+    sub_meta = dict(meta)
+    sub_meta["seq"] = [meta["seq"][first]] * heatmaps.shape[0]
+    planes, offset, _ = self.project_layer.forward_batch(heatmaps, sub_meta, proposal_centers, mask, cameras,
+                                                         resize_transform)
+    P = planes.shape[0] // 3
+    if P == 0:
+        return
+    features = torch.stack(torch.chunk(self.conv_net(planes), 3), dim=0)          # [3,P,J,S,S]
+    pose, maxprob = ops.soft_argmax(features, self.project_layer.center_grid, offset,
+                                    float(self.soft_argmax_layer.beta))
+    weights = self.weight_net(features)                                             # [3P,J,1]
+    fused, confs = ops.fuse_poses(pose, weights, maxprob)
+    all_fused[mask] = fused
+    all_pose[:, mask] = pose
+    proposal_centers[mask, 4] = confs

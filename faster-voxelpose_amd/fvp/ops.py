@@ -302,3 +302,49 @@ def max_planes(cubes: torch.Tensor) -> torch.Tensor:
 def _(cubes):
     P, J, S = cubes.shape[:3]
     return cubes.new_empty((3 * P, J, S, S))
+
+
+# ---------------------------------------------------------------------------
+@torch.library.custom_op("fvp::soft_argmax", mutates_args=(), device_types="cuda")
+def soft_argmax(features: torch.Tensor, center_grid: torch.Tensor, offset: Optional[torch.Tensor],
+                beta: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """features [3,P,J,S,S] (or [3,P,J,S*S,1]) -> (pose [3,P,J,2] (+offset), maxprob [3,P,J])."""
+    f = _dev_f32(features, "features")
+    g = _dev_f32(center_grid, "center_grid")
+    P, J = f.shape[1], f.shape[2]
+    S2 = f[0, 0, 0].numel() if P > 0 else g.shape[1]
+    if g.numel() != 3 * S2 * 2:
+        raise _lib.FvpError(f"fvp: center_grid {tuple(g.shape)} does not match {S2} cells per plane")
+    off = None if offset is None else _dev_f32(offset, "offset")
+    pose = torch.empty((3, P, J, 2), dtype=torch.float32, device=f.device)
+    maxprob = torch.empty((3, P, J), dtype=torch.float32, device=f.device)
+    _lib.call("fvp_soft_argmax", _ptr(f), P, J, S2, _ptr(g), _ptr(off), float(beta), _ptr(pose), _ptr(maxprob),
+              _stream(f))
+    return pose, maxprob
+
+
+@soft_argmax.register_fake
+def _(features, center_grid, offset, beta):
+    P, J = features.shape[1], features.shape[2]
+    return features.new_empty((3, P, J, 2)), features.new_empty((3, P, J))
+
+
+@torch.library.custom_op("fvp::fuse_poses", mutates_args=(), device_types="cuda")
+def fuse_poses(pose: torch.Tensor, weights: torch.Tensor, maxprob: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """pose [3,P,J,2], weights [3P,J,1] (WeightNet), maxprob [3,P,J] -> (fused [P,J,3], confs [P])."""
+    pz = _dev_f32(pose, "pose")
+    w = _dev_f32(weights, "weights")
+    mp = _dev_f32(maxprob, "maxprob")
+    P, J = pz.shape[1], pz.shape[2]
+    if w.numel() != 3 * P * J:
+        raise _lib.FvpError(f"fvp: weights {tuple(w.shape)} must hold 3*P*J = {3 * P * J} values")
+    fused = torch.empty((P, J, 3), dtype=torch.float32, device=pz.device)
+    confs = torch.empty((P,), dtype=torch.float32, device=pz.device)
+    _lib.call("fvp_fuse_poses", _ptr(pz), _ptr(w), _ptr(mp), P, J, _ptr(fused), _ptr(confs), _stream(pz))
+    return fused, confs
+
+
+@fuse_poses.register_fake
+def _(pose, weights, maxprob):
+    P, J = pose.shape[1], pose.shape[2]
+    return pose.new_empty((P, J, 3)), pose.new_empty((P,))

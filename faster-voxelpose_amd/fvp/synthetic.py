@@ -149,3 +149,27 @@ def proposals_for_frame(w, frame: int, people: int = 4, bbox=(0.45, 0.55)) -> np
     out[:, 5] = bbox[0]
     out[:, 6] = bbox[1]
     return out
+
+
+def joint_features(P: int, J: int, S: int = 64, seed: int = 0) -> np.ndarray:
+    """Stand-in P2PNet output [3, P, J, S, S] (fp32): one Gaussian peak (height
+    0.15, sigma 3 cells) per (plane, proposal, joint) on N(0, 0.02) noise, so that
+    softmax(100 x) is peaked like a trained network's maps.  numpy RNG only, so
+    the test and the golden generator rebuild identical inputs."""
+    rng = np.random.default_rng(seed)
+    f = rng.normal(0.0, 0.02, (3, P, J, S, S)).astype(np.float32)
+    c = rng.uniform(8.0, S - 8.0, (3, P, J, 2))
+    yy, xx = np.mgrid[0:S, 0:S].astype(np.float64)
+    d2 = (xx[None, None, None] - c[..., 0, None, None]) ** 2 + (yy[None, None, None] - c[..., 1, None, None]) ** 2
+    f += (0.15 * np.exp(-d2 / (2 * 3.0 ** 2))).astype(np.float32)
+    return f
+
+
+def jln_weights(P: int, J: int, seed: int = 0) -> np.ndarray:
+    """Stand-in WeightNet output [3P, J, 1] in (0.05, 0.95) (a sigmoid's range)."""
+    return np.random.default_rng(seed + 1).uniform(0.05, 0.95, (3 * P, J, 1)).astype(np.float32)
+
+
+def jln_offsets(P: int, seed: int = 0) -> np.ndarray:
+    """Per-proposal cube offsets [P, 3] in mm."""
+    return np.random.default_rng(seed + 2).uniform(-3000.0, 3000.0, (P, 3)).astype(np.float32)

@@ -155,7 +155,7 @@ int fvp_gather_bbox(const float *size, int B, int X, int Y,
  * Replaces project_individual.ProjectLayer.forward (project_individual.py:222-293)
  * and torch.cat([max(c,4), max(c,3), max(c,2)]) (joint_localization_net.py:158-160).
  *   heatmaps    device [B][V][J][H][W] (the frames the proposals refer to)
- *   fine_grid   device [V][FX][FY][FZ][2]
+ *   fine_grid   device packed fine grid [FX*FY*FZ][FVP_GRID_SLOTS(V)][2] (fvp_pack_grid)
  *   proposals   device [P][7] (x,y,z mm, gt, conf, bbox_w, bbox_h)
  *   frame_of    device int32 [P]: frame of each proposal in [0,B) (NULL: all frame 0)
  *   cubes       device [P][J][SX][SY][SZ] or NULL (outside-window voxels are 0)
@@ -175,6 +175,27 @@ int fvp_person_planes(const float *heatmaps, int B, int V, int J, int H, int W,
  * Replaces torch.cat([max(c,4), max(c,3), max(c,2)]) at
  * lib/models/joint_localization_net.py:158-160.  S <= 64. */
 int fvp_max_planes(const float *cubes, int P, int J, int S, float *planes, void *stream);
+
+/* JLN soft-argmax of the per-plane joint maps plus the offset shift:
+ *   softmax(beta * x) over the S2 = S*S cells of each (plane, proposal, joint),
+ *   pose = expectation of center_grid[plane] + offset (xy: x,y; xz: x,z; yz: y,z)
+ *   maxprob = max of the softmax
+ * Replaces SoftArgmaxLayer.forward (lib/models/joint_localization_net.py:32-56)
+ * and the offset additions of JointLocalizationNet.forward (:170-174).
+ *   features    device [3][P][J][S2] (P2PNet output, chunked and stacked by plane)
+ *   center_grid device [3][S2][2] (project_individual.ProjectLayer.center_grid)
+ *   offset      device [P][3] or NULL;  pose [3][P][J][2], maxprob [3][P][J] outputs */
+int fvp_soft_argmax(const float *features, int P, int J, int S2, const float *center_grid,
+                    const float *offset, float beta, float *pose, float *maxprob, void *stream);
+
+/* Three-plane fusion and the per-proposal confidence:
+ *   fused[p,j] = weighted (x from xy/xz, y from xy/yz, z from xz/yz), weights
+ *   normalised per axis; confs[p] = mean over planes and joints of maxprob.
+ * Replaces fuse_pose_preds (joint_localization_net.py:83-120) and the confs
+ * mean of SoftArgmaxLayer.forward (:49-50).
+ *   weights device [3P][J] (WeightNet output);  fused [P][J][3], confs [P] (either may be NULL) */
+int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob, int P, int J,
+                   float *fused, float *confs, void *stream);
 
 #ifdef __cplusplus
 }

@@ -274,3 +274,49 @@ class Individual:
             o0, o1 = s - ctl[i], e - ctl[i]
             cubes[i, :, o0[0]:o1[0], o0[1]:o1[1], o0[2]:o1[2]] = acc
         return np.clip(cubes, F32(0), F32(1)), offset
+
+
+# ---------------------------------------------------------------------------
+# JLN post-processing.  Computed in float64: the
+# reference's fp32 softmax / 4096-term sums are matched within a tolerance,
+# not bit-for-bit (tests/test_jln_post.py states it).
+def soft_argmax(features: np.ndarray, center_grid: np.ndarray, beta: float):
+    """SoftArgmaxLayer.forward (joint_localization_net.py:32-56):
+    features [3,P,J,S,S] -> (coords [3,P,J,2], confs [P])."""
+    x = features.reshape(features.shape[0], features.shape[1], features.shape[2], -1).astype(np.float64)
+    y = np.float32(beta) * x
+    e = np.exp(y - y.max(axis=3, keepdims=True))
+    p = e / e.sum(axis=3, keepdims=True)
+    confs = p.max(axis=3).mean(axis=(0, 2))
+    g = center_grid.reshape(3, 1, 1, -1, 2).astype(np.float64)
+    coords = (p[..., None] * g).sum(axis=3)
+    return coords, confs
+
+
+def add_offsets(coords: np.ndarray, offset: np.ndarray) -> np.ndarray:
+    """joint_localization_net.py:170-174: xy += (x,y), xz += (x,z), yz += (y,z)."""
+    o = offset.reshape(-1, 1, 3).astype(np.float64)
+    out = coords.copy()
+    out[0] += o[:, :, :2]
+    out[1] += o[:, :, ::2]
+    out[2] += o[:, :, 1:]
+    return out
+
+
+def fuse_pose_preds(pose: np.ndarray, weights: np.ndarray) -> np.ndarray:
+    """JointLocalizationNet.fuse_pose_preds (joint_localization_net.py:83-120):
+    pose [3,P,J,2], weights [3P,J,1] -> [P,J,3]."""
+    P = pose.shape[1]
+    w = weights.astype(np.float64).reshape(3, P, -1, 1)
+    xy_w, xz_w, yz_w = w[0], w[1], w[2]
+    xy, xz, yz = pose[0], pose[1], pose[2]
+    xw = np.concatenate([xy_w, xz_w], 2)
+    yw = np.concatenate([xy_w, yz_w], 2)
+    zw = np.concatenate([xz_w, yz_w], 2)
+    xw = xw / xw.sum(2, keepdims=True)
+    yw = yw / yw.sum(2, keepdims=True)
+    zw = zw / zw.sum(2, keepdims=True)
+    x = xw[:, :, :1] * xy[:, :, :1] + xw[:, :, 1:] * xz[:, :, :1]
+    y = yw[:, :, :1] * xy[:, :, 1:] + yw[:, :, 1:] * yz[:, :, :1]
+    z = zw[:, :, :1] * xz[:, :, 1:] + zw[:, :, 1:] * yz[:, :, 1:]
+    return np.concatenate([x, y, z], axis=2)

@@ -140,3 +140,90 @@ def test_fused_hdn_forward_matches_reference_flow(gpu_device):
     assert tie_free > 0
     if tie_free == 3 * w.max_people:
         assert torch.equal(got[1], ref[1])
+
+
+class _WeightNet(nn.Module):
+    """Stand-in with WeightNet's I/O (weight_net.py:48-80): [3,P,J,S,S] -> [3P,J,1] in (0,1)."""
+
+    def __init__(self, J):
+        super().__init__()
+        self.lin = nn.Linear(1, 1)
+        self.J = J
+
+    def forward(self, x):
+        x = torch.flatten(x, 0, 1)
+        return torch.sigmoid(self.lin(x.mean(dim=(2, 3)).reshape(-1, 1))).view(x.shape[0], self.J, 1)
+
+
+def _jln_reference_flow(net, meta, heatmaps, pc, mask, cams, rt):
+    """joint_localization_net.py:122-182 with plain torch ops (reference semantics,
+    per-frame loop, SoftArgmaxLayer :32-56, fuse_pose_preds :83-120)."""
+    B, K, J = pc.shape[0], pc.shape[1], heatmaps.shape[2]
+    all_f = torch.zeros((B, K, J, 3), device=heatmaps.device)
+    all_p = torch.zeros((3, B, K, J, 2), device=heatmaps.device)
+    for i in range(B):
+        if torch.sum(mask[i]) == 0:
+            continue
+        cubes, offset = net.project_layer(heatmaps, i, meta, pc[i, mask[i]], cams, rt)
+        inp = torch.cat([torch.max(cubes, dim=4)[0], torch.max(cubes, dim=3)[0], torch.max(cubes, dim=2)[0]])
+        jf = torch.stack(torch.chunk(net.conv_net(inp), 3), dim=0)
+        P = jf.shape[1]
+        x = F.softmax(net.soft_argmax_layer.beta * jf.reshape(3, P, J, -1, 1), dim=3)
+        confs = torch.mean(torch.max(x, dim=3)[0].squeeze(3), dim=(0, 2))
+        pose = torch.sum(x * net.project_layer.center_grid.reshape(3, 1, 1, -1, 2), dim=3)
+        o = offset.reshape(-1, 1, 3)
+        pose[0] += o[:, :, :2]
+        pose[1] += o[:, :, ::2]
+        pose[2] += o[:, :, 1:]
+        wxy, wxz, wyz = torch.chunk(net.weight_net(jf), 3)
+        xw = torch.cat([wxy, wxz], 2)
+        yw = torch.cat([wxy, wyz], 2)
+        zw = torch.cat([wxz, wyz], 2)
+        xw, yw, zw = (t / torch.sum(t, dim=2).unsqueeze(2) for t in (xw, yw, zw))
+        fused = torch.cat([xw[:, :, :1] * pose[0][:, :, :1] + xw[:, :, 1:] * pose[1][:, :, :1],
+                           yw[:, :, :1] * pose[0][:, :, 1:] + yw[:, :, 1:] * pose[2][:, :, :1],
+                           zw[:, :, :1] * pose[1][:, :, 1:] + zw[:, :, 1:] * pose[2][:, :, 1:]], dim=2)
+        all_f[i, mask[i]] = fused
+        all_p[:, i, mask[i]] = pose
+        pc[i, mask[i], 4] = confs
+    return all_f, all_p
+
+
+@pytest.mark.gpu
+def test_fused_jln_forward_matches_reference_flow(gpu_device):
+    """Batched JLN forward (one planes launch, CNNs on all proposals, fvp
+    soft-argmax + fusion) vs the reference's per-frame flow.  Tolerance: the
+    stand-in CNNs run on a different batch shape (conv rounding) and the
+    softmax sums differ in order: poses within 0.5 mm, confidences 1e-4."""
+    from fvp import geometry, jln, synthetic
+    from fvp.config import AttrDict
+    from fvp.project_individual import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    torch.manual_seed(0)
+    w = WORKLOADS["c3"]
+    J = w.num_joints
+    net = types.SimpleNamespace(training=False)
+    net.project_layer = ProjectLayer(w.cfg(str(gpu_device)))
+    net.project_layer.verbose = False
+    net.conv_net = nn.Conv2d(J, J, 3, padding=1).to(gpu_device).eval()
+    net.weight_net = _WeightNet(J).to(gpu_device).eval()
+    net.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    B, K = 3, 5
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, B)).to(gpu_device)
+    pc = torch.from_numpy(np.stack([synthetic.proposals_for_frame(w, f, K) for f in range(B)])).to(gpu_device)
+    mask = torch.ones((B, K), dtype=torch.bool, device=gpu_device)
+    mask[1, 3:] = False
+    mask[2] = False  # a frame without proposals
+    meta = {"seq": [seq] * B}
+    pc_ref, pc_got = pc.clone(), pc.clone()
+    with torch.no_grad():
+        rf, rp = _jln_reference_flow(net, meta, hm, pc_ref, mask, cams, rt)
+        gf, gp = jln.fused_jln_forward(net, meta, hm, pc_got, mask, cams, rt)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(gp.cpu().numpy(), rp.cpu().numpy(), atol=0.5, rtol=0)
+    np.testing.assert_allclose(gf.cpu().numpy(), rf.cpu().numpy(), atol=0.5, rtol=0)
+    np.testing.assert_allclose(pc_got.cpu().numpy(), pc_ref.cpu().numpy(), atol=1e-4, rtol=0)
+    assert torch.count_nonzero(gf[2]) == 0 and torch.count_nonzero(gf[1, 3:]) == 0

@@ -79,6 +79,21 @@ def main():
 
     ms_frame = timeit(per_frame)
     ms = timeit(batched)
+
+    # JLN post-processing on device (soft-argmax + offsets + fusion) on stand-in
+    # CNN outputs of the same shape: reads 3*J*S*S*4 B of joint maps per proposal
+    from fvp import ops
+    n_prop0 = F * P
+    feats = torch.from_numpy(synthetic.joint_features(n_prop0, w.num_joints, 64, 3)).to(dev)
+    wts = torch.from_numpy(synthetic.jln_weights(n_prop0, w.num_joints, 3)).to(dev)
+    offs = torch.from_numpy(synthetic.jln_offsets(n_prop0, 3)).to(dev)
+
+    def post():
+        pose, mp = ops.soft_argmax(feats, layer.center_grid, offs, 100.0)
+        ops.fuse_poses(pose, wts, mp)
+
+    ms_post = timeit(post)
+    post_bytes = 3 * w.num_joints * 64 * 64 * 4 * n_prop0
     J = w.num_joints
     n_prop = F * P
     print(json.dumps({
@@ -89,7 +104,11 @@ def main():
         "cube_bytes_per_proposal": J * 64 ** 3 * 4, "plane_bytes_per_proposal": 3 * J * 64 * 64 * 4,
         "per_frame_calls_us_per_proposal": round(ms_frame * 1e3 / n_prop, 2),
         "path": "forward_batch: one fvp_person_planes launch for all frames' proposals (fused planes, no cubes)",
-        "cache_build_ms": round(cache_ms, 1)}))
+        "cache_build_ms": round(cache_ms, 1),
+        "post": {"op": "fvp_soft_argmax + fvp_fuse_poses (SoftArgmaxLayer, offsets, fuse_pose_preds)",
+                 "us_per_proposal": round(ms_post * 1e3 / n_prop0, 3),
+                 "hbm_gbs": round(post_bytes / (ms_post * 1e-3) / 1e9, 1),
+                 "hbm_frac": round(post_bytes / (ms_post * 1e-3) / 8e12, 4)}}))
 
 
 if __name__ == "__main__":

@@ -155,6 +155,26 @@ def main():
     }
     np.savez_compressed(os.path.join(OUT, "individual_c3.npz"), **d)
     print("wrote individual_c3", {k: v.shape for k, v in d.items()})
+
+    # ---- JLN post-processing: SoftArgmaxLayer + offsets + fuse_pose_preds on
+    # stand-in CNN outputs rebuilt from numpy seeds (fvp/synthetic.py)
+    import models.joint_localization_net as jl  # noqa: E402
+    P, J, seed = 6, 15, 7
+    feats = synthetic.joint_features(P, J, 64, seed)
+    weights = synthetic.jln_weights(P, J, seed)
+    offsets = synthetic.jln_offsets(P, seed)
+    sal = jl.SoftArgmaxLayer(types.SimpleNamespace(NETWORK=types.SimpleNamespace(BETA=100)))
+    x = torch.from_numpy(feats).reshape(3, P, J, -1, 1)
+    pose, confs = sal(x, layer.center_grid)
+    o = torch.from_numpy(offsets).reshape(-1, 1, 3)
+    pose[0] += o[:, :, :2]
+    pose[1] += o[:, :, ::2]
+    pose[2] += o[:, :, 1:]
+    fused = jl.JointLocalizationNet.fuse_pose_preds(None, pose, torch.from_numpy(weights))
+    d = {"P": P, "J": J, "seed": seed, "beta": 100.0, "center_grid": layer.center_grid.numpy(),
+         "pose": pose.numpy(), "confs": confs.numpy(), "fused": fused.numpy()}
+    np.savez_compressed(os.path.join(OUT, "jln_post.npz"), **d)
+    print("wrote jln_post", {k: np.shape(v) for k, v in d.items()})
     return 0
 
 

@@ -43,6 +43,8 @@ __device__ __forceinline__ float block_reduce_sum(float v, float *red) {
 
 // feat [3][P][J][S2], grids [3][S2][2], offset [P][3] (may be NULL)
 // pose [3][P][J][2], maxprob [3][P][J]
+// The row is read once: S2 <= 256*4*RV values stay in registers (float4 loads).
+template <int RV>
 __global__ __launch_bounds__(256) void softargmax_kernel(const float *__restrict__ feat,
                                                          const float *__restrict__ grids,
                                                          const float *__restrict__ offset, int P, int J, int S2,
@@ -53,17 +55,38 @@ __global__ __launch_bounds__(256) void softargmax_kernel(const float *__restrict
     const int plane = row / (P * J);
     const int p = (row / J) % P;
     const float *__restrict__ x = feat + (size_t)row * S2;
-    const float2 *__restrict__ g = reinterpret_cast<const float2 *>(grids) + (size_t)plane * S2;
+    const float *__restrict__ g = grids + (size_t)plane * S2 * 2;
+    const bool vec = (S2 & 3) == 0;
+    float y[RV][4];
     float m = -INFINITY;
-    for (int i = threadIdx.x; i < S2; i += 256) m = fmaxf(m, beta * x[i]);
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+        const int i = (r * 256 + threadIdx.x) * 4;
+        if (vec && i < S2) {
+            const float4 v = *reinterpret_cast<const float4 *>(x + i);
+            y[r][0] = beta * v.x; y[r][1] = beta * v.y; y[r][2] = beta * v.z; y[r][3] = beta * v.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[r][k] = (i + k < S2) ? beta * x[i + k] : -INFINITY;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m = fmaxf(m, y[r][k]);
+    }
     m = block_reduce_max(m, red);
     float s = 0.f, sx = 0.f, sy = 0.f;
-    for (int i = threadIdx.x; i < S2; i += 256) {
-        const float e = expf(beta * x[i] - m);
-        const float2 c = g[i];
-        s += e;
-        sx = __builtin_fmaf(e, c.x, sx);
-        sy = __builtin_fmaf(e, c.y, sy);
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+        const int i = (r * 256 + threadIdx.x) * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (i + k < S2) {
+                const float e = expf(y[r][k] - m);
+                const float2 c = reinterpret_cast<const float2 *>(g)[i + k];
+                s += e;
+                sx = __builtin_fmaf(e, c.x, sx);
+                sy = __builtin_fmaf(e, c.y, sy);
+            }
+        }
     }
     s = block_reduce_sum(s, red);
     sx = block_reduce_sum(sx, red);
@@ -114,8 +137,14 @@ extern "C" int fvp_soft_argmax(const float *features, int P, int J, int S2, cons
     if (!features || !center_grid || !pose || !maxprob) return FVP_ERR_NULL;
     if (P < 0 || J <= 0 || S2 <= 0) return FVP_ERR_SHAPE;
     if ((long long)3 * P * J > 0x7fffffffLL) return FVP_ERR_SHAPE;
-    hipLaunchKernelGGL(fvp::softargmax_kernel, dim3((unsigned)(3 * P * J)), dim3(256), 0, (hipStream_t)stream,
-                       features, center_grid, offset, P, J, S2, beta, pose, maxprob);
+    if (S2 > 256 * 4 * 8) return FVP_ERR_SHAPE;  // up to 8192 cells per plane (64x64 = 4096)
+    const dim3 grid((unsigned)(3 * P * J));
+    if (S2 <= 256 * 4 * 4)
+        hipLaunchKernelGGL(fvp::softargmax_kernel<4>, grid, dim3(256), 0, (hipStream_t)stream, features, center_grid,
+                           offset, P, J, S2, beta, pose, maxprob);
+    else
+        hipLaunchKernelGGL(fvp::softargmax_kernel<8>, grid, dim3(256), 0, (hipStream_t)stream, features, center_grid,
+                           offset, P, J, S2, beta, pose, maxprob);
     return (int)hipGetLastError();
 }
 

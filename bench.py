@@ -256,6 +256,19 @@ def main():
             torch.cuda.synchronize()
             lat.append((time.perf_counter() - t1) * 1e3)
         extra["latency_b1_ms"] = float(np.median(lat))
+        # the same one-frame step replayed from a captured hipGraph (fvp/graphs.py)
+        from fvp.graphs import CapturedStep
+
+        cap = CapturedStep(step1)
+        cap.replay()
+        torch.cuda.synchronize()
+        lat = []
+        for _ in range(20):
+            t1 = time.perf_counter()
+            cap.replay()
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - t1) * 1e3)
+        extra["latency_b1_graph_ms"] = float(np.median(lat))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
@@ -300,6 +313,7 @@ def main():
                              "frac": round(tap_rate / tap_peak, 4), "joint_taps_per_launch": taps},
             },
             "latency_b1_ms": round(extra["latency_b1_ms"], 3) if "latency_b1_ms" in extra else None,
+            "latency_b1_graph_ms": round(extra["latency_b1_graph_ms"], 3) if "latency_b1_graph_ms" in extra else None,
             "cpu_baseline": cpu,
             "cache_build_ms": round(cache_ms, 2),
         }

@@ -1,7 +1,9 @@
 // Proposal selection on the 2-D detection map and the per-proposal gathers
 // (A9, A10 of SURVEY.md §8(a)).
 //
-// nms_topk: one 256-thread block per frame.  The 3x3/stride-1/pad-1 max-pool
+// nms_topk (K <= 16): one 1024-thread block per frame, register top-K per
+// thread merged by K block arg-max rounds (below).  nms_topk (K > 16): one
+// 256-thread block per frame.  The 3x3/stride-1/pad-1 max-pool
 // keep mask (proposal.py:34-52) is evaluated once into LDS, then K rounds of
 // a block-wide arg-max (value descending, flat index ascending -- a total
 // order, so the result is deterministic) pick the top-K (proposal.py:73).
@@ -107,46 +109,55 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__re
     }
 }
 
-// Fast path for K <= KMAX: the map is staged in LDS with coalesced loads, each
-// thread keeps a sorted top-KMAX of its own elements in registers while it
-// evaluates the 3x3 peak mask, and K block-wide arg-max rounds merge the
+// Fast path for K <= KMAX: one NT-thread block per frame.  The map is staged
+// in LDS with unrolled (8 loads in flight per thread) coalesced reads, each
+// thread evaluates the 3x3 peak mask branch-free for its elements and keeps a
+// sorted top-KMAX in registers, and K block-wide arg-max rounds merge the
 // per-thread heads (no rescans of the map).
-template <int KMAX>
-__global__ __launch_bounds__(kNmsThreads) void nms_topk_small_kernel(const float *__restrict__ prob, long long stride,
-                                                                     int X, int Y, int K, float *__restrict__ vals,
-                                                                     int64_t *__restrict__ flat,
-                                                                     int64_t *__restrict__ xy) {
+template <int KMAX, int NT>
+__global__ __launch_bounds__(NT) void nms_topk_small_kernel(const float *__restrict__ prob, long long stride, int X,
+                                                            int Y, int K, float *__restrict__ vals,
+                                                            int64_t *__restrict__ flat, int64_t *__restrict__ xy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float *map = reinterpret_cast<float *>(smem);  // [X*Y]
-    __shared__ Cand red[kNmsThreads / kWave];
+    __shared__ Cand red[NT / kWave];
     __shared__ int win_tid;
     const int M = X * Y;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const float *__restrict__ p = prob + (size_t)b * stride;
-    for (int e = tid; e < M; e += kNmsThreads) map[e] = p[e];
+    constexpr int U = 8;
+    for (int e0 = tid; e0 < M; e0 += NT * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = (e0 + u * NT < M) ? p[e0 + u * NT] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (e0 + u * NT < M) map[e0 + u * NT] = v[u];
+    }
     __syncthreads();
 
     Cand top[KMAX];
 #pragma unroll
     for (int t = 0; t < KMAX; ++t) top[t] = Cand{-INFINITY, 0x7fffffff};
     int have = 0;
-    for (int e = tid; e < M; e += kNmsThreads) {
+    for (int e = tid; e < M; e += NT) {
         const int ex = e / Y, ey = e - (e / Y) * Y;
         const float c = map[e];
         float m = -INFINITY;
         bool nan = false;
+#pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
-            const int xx = ex + dx;
-            if (xx < 0 || xx >= X) continue;
+#pragma unroll
             for (int dy = -1; dy <= 1; ++dy) {
-                const int yy = ey + dy;
-                if (yy < 0 || yy >= Y) continue;
-                const float q = map[xx * Y + yy];
-                nan |= (q != q);
-                m = fmaxf(m, q);
+                const int xx = ex + dx, yy = ey + dy;
+                const bool ok = (unsigned)xx < (unsigned)X && (unsigned)yy < (unsigned)Y;
+                const float q = map[ok ? xx * Y + yy : e];  // max_pool2d's -inf padding: out-of-map taps ignored
+                nan |= ok && (q != q);
+                m = ok ? fmaxf(m, q) : m;
             }
         }
+        // max_pool2d propagates NaN; (c == NaN) is false -> keep = 0 -> 0*c.
         Cand cand{((!nan && c == m) ? 1.0f : 0.0f) * c, e};
         // sorted insertion (descending by `before`), fully unrolled: registers only
 #pragma unroll
@@ -167,7 +178,8 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_small_kernel(const float
         __syncthreads();
         if (tid == 0) {
             Cand w = red[0];
-            for (int i = 1; i < kNmsThreads / kWave; ++i)
+#pragma unroll
+            for (int i = 1; i < NT / kWave; ++i)
                 if (before(red[i], w)) w = red[i];
             vals[(size_t)b * K + k] = w.v;
             flat[(size_t)b * K + k] = w.i;
@@ -175,7 +187,7 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_small_kernel(const float
                 xy[((size_t)b * K + k) * 2 + 0] = (int64_t)(w.i / X);
                 xy[((size_t)b * K + k) * 2 + 1] = (int64_t)(w.i % X);
             }
-            win_tid = (w.i < M) ? (w.i % kNmsThreads) : -1;  // element e lives in thread e % threads
+            win_tid = (w.i < M) ? (w.i % NT) : -1;  // element e lives in thread e % NT
         }
         __syncthreads();
         if (tid == win_tid) {  // pop the head
@@ -228,7 +240,7 @@ extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long fr
     if (frame_stride == 0) frame_stride = (long long)M;
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
     if (K <= 16) {
-        hipLaunchKernelGGL(fvp::nms_topk_small_kernel<16>, dim3(B), dim3(fvp::kNmsThreads), M * 4, (hipStream_t)stream,
+        hipLaunchKernelGGL((fvp::nms_topk_small_kernel<16, 1024>), dim3(B), dim3(1024), M * 4, (hipStream_t)stream,
                            prob, frame_stride, X, Y, K, vals, flat, xy);
         return (int)hipGetLastError();
     }

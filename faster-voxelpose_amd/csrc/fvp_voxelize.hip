@@ -267,7 +267,8 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
                       const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
     const bool half = sizeof(T) == 2;
     const int chunk = chunk_frames(B, V, J, H, W, half);
-    const int cols = cols_per_block(Z);
+    // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
+    const int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
     const int col_blocks = (X * Y + cols - 1) / cols;
     const int SP = stage_pitch(LPV, cols, Z);
     size_t lds = (size_t)4 * LPV * SP * sizeof(float);

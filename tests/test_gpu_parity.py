@@ -493,3 +493,35 @@ def test_nms_topk_both_paths_vs_oracle(gpu_device, K):
     assert np.array_equal(np.nan_to_num(got, nan=7.0), np.nan_to_num(ov, nan=7.0))
     assert np.array_equal(fl.cpu().numpy()[1:], ofl[1:])  # frame 0 holds a NaN (ordering checked above)
     assert np.array_equal(xy.cpu().numpy()[1:], oxy[1:])
+
+
+def test_captured_graph_step_matches_eager(gpu_device):
+    """The hot-path step (voxelize -> NMS -> columns) captured as one hipGraph
+    replays to the eager results, and picks up new frames copied into its input."""
+    from fvp import geometry, synthetic
+    from fvp.graphs import CapturedStep
+    from fvp.project_whole import ProjectLayer
+    from fvp.proposal import gather_columns, nms2D
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c2"]
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    frames = torch.from_numpy(synthetic.gaussian_heatmaps(w, 3)).to(gpu_device)
+    hm = frames[0:1].clone()
+    meta = {"seq": [seq]}
+
+    def step():
+        cube, xy = layer.forward_fused(hm, meta, cams, rt)
+        vals, idx, flat = nms2D(xy[:, 2:3], 10)
+        return cube, xy, vals, flat, gather_columns(cube, flat)
+
+    cap = CapturedStep(step)
+    for f in (0, 2):
+        hm.copy_(frames[f:f + 1])
+        got = [t.clone() for t in cap.replay()]
+        ref = step()
+        for g, r in zip(got, ref):
+            assert torch.equal(g, r)

@@ -73,7 +73,7 @@ def main():
     meta = {"seq": [seq] * B}
     ref_cube, ref_xy = layer.forward_fused(hm, meta, cams, rt)
     torch.cuda.synchronize()
-    grids = layer.sample_grid[seq].contiguous()  # [V,1,N,2]
+    grids = layer.build_sample_grid(cams, seq, rt, dev).contiguous()  # [V,1,N,2]
     _, V, J, H, W = hm.shape
     X, Y, Z = w.voxels_per_axis
     N = X * Y * Z
@@ -129,6 +129,15 @@ def main():
                                  xy.data_ptr(), ws.data_ptr(), chunk, cols, lds, stream)
             assert rc == 0, rc
         return f
+    lib.voxnext_co.argtypes = lib.voxnext_otf.argtypes[:1] + lib.voxnext_otf.argtypes[2:]
+
+    def co(chunk, cols):
+        def f():
+            rc = lib.voxnext_co(hm.data_ptr(), B, V, J, H, W, cams_t.data_ptr(), rt.data_ptr(), ctypes.byref(gspec),
+                                ctypes.byref(ispec), cube.data_ptr(), xy.data_ptr(), wsh.data_ptr(), chunk, cols,
+                                stream)
+            assert rc == 0, rc
+        return f
     cube = torch.empty_like(ref_cube)
     xy = torch.empty_like(ref_xy)
     per = V * H * W * 16 * 4
@@ -165,6 +174,10 @@ def main():
     ochunk = hchunk * 2 if hm.dtype == torch.float16 else chunk0
     for cols in sorted({cols0, max(1, cols0 // 2)}):
         cands[f"otf chunk={ochunk} cols={cols}"] = otf(ochunk, cols)
+    if hm.dtype == torch.float16:
+        for chunk in (1, 2):
+            for cols in (1, 2, 4, 5):
+                cands[f"co chunk={chunk} cols={cols}"] = co(chunk, cols)
     probes = {f"probe L1-taps chunk={chunk0}": qg(chunk0, cols0, 1)}
     lay = lambda: [lib.voxnext_layout(hm.data_ptr() + c * chunk0 * fbytes, int(hm.dtype == torch.float16),
                                       min(chunk0, B - c * chunk0), V, J, H, W, ws.data_ptr(), stream)

@@ -681,6 +681,125 @@ __global__ __launch_bounds__(256) void gather_otf(const void *__restrict__ tab, 
     }
 }
 
+// Camera-outer C5 variant: fp16 pair table, on-the-fly coordinates; each block
+// keeps the accumulators of its NP passes (NP*64 voxels) in registers and walks
+// camera groups outermost, so concurrently resident blocks sweep the cameras
+// roughly in lockstep (L2 working set = a few cameras' footprints).
+template <int NP>
+__global__ __launch_bounds__(256) void gather_co(const void *__restrict__ tab, CoordSource src_, int frame0,
+                                                 float *__restrict__ cube, float *__restrict__ xy, int V, int J, int H,
+                                                 int W, int X, int Y, int Z, int cols, int col_blocks, int SP) {
+    constexpr int LPV = 4, JP = 16, VPP = 64, CPG = 8;
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int bl = L / col_blocks;
+    const int b = frame0 + bl;
+    const int XY = X * Y;
+    const int c0 = (L - bl * col_blocks) * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    float *lcam = stage + ((JP * SP + 3) & ~3);
+    for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256) lcam[e] = e < V * FVP_CAM_STRIDE ? src_.cams[e] : 0.0f;
+    float rt[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rt[k] = src_.resize_t[k];
+    __syncthreads();
+    const unsigned img = (unsigned)(H * (W + 1)) * 64u;
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
+    float acc[NP][4];
+    float wc[NP][3];
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[pp][m] = 0.f;
+        const int i = pp * VPP + threadIdx.x / LPV;
+        const long long n = n0 + min(i, T - 1);
+        const int iz = (int)(n % Z);
+        const long long r = n / Z;
+        wc[pp][0] = axis_coord(src_.gs.start[0], src_.gs.end[0], X, (int)(r / Y), src_.gs.center[0]);
+        wc[pp][1] = axis_coord(src_.gs.start[1], src_.gs.end[1], Y, (int)(r % Y), src_.gs.center[1]);
+        wc[pp][2] = axis_coord(src_.gs.start[2], src_.gs.end[2], Z, iz, src_.gs.center[2]);
+    }
+    for (int v0 = 0; v0 < V; v0 += CPG) {
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) {
+            const int i = pp * VPP + threadIdx.x / LPV;
+            const bool valid = i < T;
+            float g[4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
+                float px, py;
+                project_point(c, wc[pp][0], wc[pp][1], wc[pp][2], px, py);
+                pixel_to_sample(px, py, rt, src_.im.ori_max, src_.im.img_w, src_.im.img_h, (float)src_.im.hm_w,
+                                (float)src_.im.hm_h, g[2 * h], g[2 * h + 1]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
+            const Taps4<true> t0 = setup_taps<true>(g[0], g[1], sxs, sys, W, H, 64u);
+            const Taps4<true> t1 = setup_taps<true>(g[2], g[3], sxs, sys, W, H, 64u);
+            static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = k >> 1;
+                const int v = v0 + k;
+                if (v >= V) return;
+                const Taps4<true> &src = (k & 1) ? t1 : t0;
+                const unsigned o0 = group_bcast<LPV, S>(src.o[0]);
+                const unsigned o1 = group_bcast<LPV, S>(src.o[1]);
+                if (!__builtin_amdgcn_ballot_w64(((o0 & o1) & kOOB) == 0u)) return;
+                float w[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(src.w[m]);
+                const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+                const u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o0 + qo, 0, 0);
+                const u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o1 + qo, 0, 0);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const unsigned ua = r0[m >> 1], ub = r0[2 + (m >> 1)];
+                    const unsigned uc = r1[m >> 1], ud = r1[2 + (m >> 1)];
+                    const float fa = (m & 1) ? h_hi(ua) : h_lo(ua);
+                    const float fb = (m & 1) ? h_hi(ub) : h_lo(ub);
+                    const float fc = (m & 1) ? h_hi(uc) : h_lo(uc);
+                    const float fd = (m & 1) ? h_hi(ud) : h_lo(ud);
+                    acc[pp][m] = acc[pp][m] +
+                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                }
+            });
+        }
+    }
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+        const int i = pp * VPP + threadIdx.x / LPV;
+        if (i < T) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf(acc[pp][m] / fV, 0.0f, 1.0f);
+        }
+    }
+    __syncthreads();
+    if (cube) {
+        for (int j = 0; j < J; ++j) {
+            float *__restrict__ dst = cube + ((size_t)b * J + j) * N + n0;
+            for (int e = threadIdx.x; e < T; e += 256) dst[e] = stage[j * SP + e];
+        }
+    }
+    if (xy) {
+        for (int e = threadIdx.x; e < J * ncols; e += 256) {
+            const int j = e / ncols, cc = e - (e / ncols) * ncols;
+            const float *sp = stage + j * SP + cc * Z;
+            float m = -INFINITY;
+            for (int z = 0; z < Z; ++z) m = nanmax(m, sp[z]);
+            xy[((size_t)b * J + j) * XY + c0 + cc] = m;
+        }
+    }
+}
+
 // [V][N][2] -> [N][GV][2], padded cameras (-2,-2) (off-image)
 __global__ void regrid_kernel(const float2 *__restrict__ g, float2 *__restrict__ out, int V, int GV, long long N) {
     const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -868,6 +987,47 @@ extern "C" int voxnext_occ(const float *hm, int B, int V, int J, int H, int W, c
         launch_layout<4, float>(hm + (size_t)f0 * frame_elems, nb, V, J, H, W, (float *)ws, s);
         hipLaunchKernelGGL((voxelize_kernel<4, false, false>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds, s,
                            ws, src, nullptr, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+    }
+    return (int)hipGetLastError();
+}
+
+// camera-outer C5 op (fp16 pairs + on-the-fly), NP = cols*Z/64 passes
+extern "C" int voxnext_co(const void *hm, int B, int V, int J, int H, int W, const float *cams, const float *rt,
+                          const fvp_grid_spec *gs, const fvp_image_spec *im, float *cube, float *xy, void *ws,
+                          int chunk, int cols, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (J > 16 || J < 9) return -1;
+    const int X = gs->bins[0], Y = gs->bins[1], Z = gs->bins[2];
+    const int T = cols * Z;
+    if (T % 64) return -3;
+    const int NP = T / 64;
+    const int col_blocks = (X * Y + cols - 1) / cols;
+    const int SP = T + 1;
+    const size_t lds = (((size_t)16 * SP + 3) & ~(size_t)3) * 4 + (size_t)(V + 1) * FVP_CAM_STRIDE * 4;
+    CoordSource src{};
+    src.cams = cams;
+    src.resize_t = rt;
+    src.gs = *gs;
+    src.im = *im;
+    const size_t frame_elems = (size_t)V * J * H * W;
+    for (int f0 = 0; f0 < B; f0 += chunk) {
+        const int nb = min(chunk, B - f0);
+        const long long total = (long long)nb * V * H * (W + 1) * 4;
+        hipLaunchKernelGGL(heatmaps_to_pairs_kernel<_Float16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                           (const _Float16 *)hm + (size_t)f0 * frame_elems, (uint4 *)ws, J, H, W, total);
+        const dim3 grid((unsigned)(nb * col_blocks));
+#define CO(NPV) hipLaunchKernelGGL((next::gather_co<NPV>), grid, dim3(256), lds, s, ws, src, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP)
+        switch (NP) {
+            case 1: CO(1); break;
+            case 2: CO(2); break;
+            case 3: CO(3); break;
+            case 4: CO(4); break;
+            case 5: CO(5); break;
+            case 8: CO(8); break;
+            case 10: CO(10); break;
+            default: return -4;
+        }
+#undef CO
     }
     return (int)hipGetLastError();
 }

@@ -268,7 +268,10 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
     const bool half = sizeof(T) == 2;
     const int chunk = chunk_frames(B, V, J, H, W, half);
     // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
-    const int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
+    int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
+    // latency (few frames): one pass of 256/LPV voxels per block, so a single
+    // frame spreads over enough blocks to fill the CUs
+    if ((long long)min(chunk, B) * ((X * Y + cols - 1) / cols) < 4 * 256) cols = max(1, (256 / LPV) / Z);
     const int col_blocks = (X * Y + cols - 1) / cols;
     const int SP = stage_pitch(LPV, cols, Z);
     size_t lds = (size_t)4 * LPV * SP * sizeof(float);

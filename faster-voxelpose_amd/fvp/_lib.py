@@ -57,6 +57,11 @@ SIGNATURES = {
     "fvp_max_planes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_soft_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "fvp_fuse_poses": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "fvp_conv2d_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                        c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
 ABI_VERSION = 3

@@ -173,3 +173,39 @@ def jln_weights(P: int, J: int, seed: int = 0) -> np.ndarray:
 def jln_offsets(P: int, seed: int = 0) -> np.ndarray:
     """Per-proposal cube offsets [P, 3] in mm."""
     return np.random.default_rng(seed + 2).uniform(-3000.0, 3000.0, (P, 3)).astype(np.float32)
+
+
+def seeded_state_dict(module, seed: int = 0) -> dict:
+    """Deterministic weights for any module, keyed by parameter name (zlib.crc32),
+    so the reference's classes and a restatement with the same attribute names
+    get identical tensors: conv/linear weights N(0, sqrt(2/fan_in)), biases
+    N(0, 0.05), BatchNorm gamma U(0.5, 1.5), beta N(0, 0.1), running mean
+    N(0, 0.1), running var U(0.5, 1.5).  (The checkpoints are not available
+    offline)"""
+    import zlib
+
+    import torch
+
+    out = {}
+    for name, t in module.state_dict().items():
+        rng = np.random.default_rng((seed * 1000003 + zlib.crc32(name.encode())) & 0xFFFFFFFF)
+        shape = tuple(t.shape)
+        leaf = name.rsplit(".", 1)[-1]
+        if leaf == "num_batches_tracked":
+            out[name] = t.clone()
+            continue
+        if leaf == "weight" and len(shape) > 1:
+            fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else 1
+            v = rng.normal(0.0, np.sqrt(2.0 / fan_in), shape)
+        elif leaf == "weight":      # BatchNorm gamma
+            v = rng.uniform(0.5, 1.5, shape)
+        elif leaf == "bias":
+            v = rng.normal(0.0, 0.05, shape)
+        elif leaf == "running_mean":
+            v = rng.normal(0.0, 0.1, shape)
+        elif leaf == "running_var":
+            v = rng.uniform(0.5, 1.5, shape)
+        else:
+            v = rng.normal(0.0, 0.1, shape)
+        out[name] = torch.from_numpy(v.astype(np.float32))
+    return out

@@ -197,6 +197,27 @@ int fvp_soft_argmax(const float *features, int P, int J, int S2, const float *ce
 int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob, int P, int J,
                    float *fused, float *confs, void *stream);
 
+/* Dense 2-D convolution on the fp32 matrix cores (v_mfma_f32_32x32x2_f32),
+ * implicit GEMM over NHWC activations, for the HDN / JLN CNNs
+ * (lib/models/cnns_2d.py:12-295, weight_net.py:48-80):
+ *   out = act(conv(in, W) * scale + shift + res_pre) + res_post
+ * with eval-mode BatchNorm and the conv bias folded into scale/shift, act =
+ * ReLU when relu != 0.  Stride 1, zero padding (K-1)/2, odd KH/KW.
+ * upsample2 != 0: ConvTranspose2d(k=2, s=2) as a 1x1 conv with 4*Cpo packed
+ * outputs n = (dy*2+dx)*Cpo + co, scattered to the 2H x 2W output.
+ *   in        device [N][H][W][Cpi], Cpi % 16 == 0 (padding channels zero)
+ *   wpack     device [KH*KW*Cpi][Cpo_w], row (ky*KW+kx)*Cpi+ci, Cpo_w % 64 == 0
+ *   scale, shift device [Cpo];  res_pre, res_post device [N][Ho][Wo][Cpo] or NULL
+ *   out       device [N][Ho][Wo][Cpo], Cpo % 16 == 0 */
+int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
+                    int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                    const float *res_post, int relu, int upsample2, float *out, void *stream);
+/* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
+int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);
+/* NCHW [N][C][H][W] <-> NHWC [N][H][W][Cp] (Cp >= C, padding channels zero). */
+int fvp_nchw_to_nhwc(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream);
+int fvp_nhwc_to_nchw(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

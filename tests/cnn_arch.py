@@ -1,0 +1,106 @@
+"""Test-side restatement of the reference's 2-D CNN architectures
+(lib/models/cnns_2d.py: Basic2DBlock :12-29, Res2DBlock :32-64, Pool2DBlock
+:67-79, Upsample2DBlock :82-104, EncoderDecorder :123-183, P2PNet :185-232,
+CenterNet :235-295) with the same module attribute names, so state_dicts are
+interchangeable with the reference's.  Pinned to the reference by
+tests/golden/cnn.npz (tools/gen_golden.py runs the reference's own classes on
+the same seeded weights and inputs).  Used where the reference is absent (the
+GPU box)."""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _cbr(cin, cout, k, relu=True):
+    layers = [nn.Conv2d(cin, cout, k, stride=1, padding=(k - 1) // 2), nn.BatchNorm2d(cout)]
+    return layers + [nn.ReLU(True)] if relu else layers
+
+
+class Basic2DBlock(nn.Module):
+    def __init__(self, cin, cout, k):
+        super().__init__()
+        self.block = nn.Sequential(*_cbr(cin, cout, k))
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class Res2DBlock(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.res_branch = nn.Sequential(*_cbr(cin, cout, 3), *_cbr(cout, cout, 3, relu=False))
+        self.skip_con = nn.Sequential() if cin == cout else nn.Sequential(*_cbr(cin, cout, 1, relu=False))
+
+    def forward(self, x):
+        return F.relu(self.res_branch(x) + self.skip_con(x), True)
+
+
+class Pool2DBlock(nn.Module):
+    def __init__(self, pool_size):
+        super().__init__()
+        self.pool_size = pool_size
+
+    def forward(self, x):
+        return F.max_pool2d(x, kernel_size=self.pool_size, stride=self.pool_size)
+
+
+class Upsample2DBlock(nn.Module):
+    def __init__(self, cin, cout, k, s):
+        super().__init__()
+        self.block = nn.Sequential(nn.ConvTranspose2d(cin, cout, k, stride=s), nn.BatchNorm2d(cout), nn.ReLU(True))
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class EncoderDecorder(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.encoder_pool1 = Pool2DBlock(2)
+        self.encoder_res1 = Res2DBlock(32, 64)
+        self.encoder_pool2 = Pool2DBlock(2)
+        self.encoder_res2 = Res2DBlock(64, 128)
+        self.mid_res = Res2DBlock(128, 128)
+        self.decoder_res2 = Res2DBlock(128, 128)
+        self.decoder_upsample2 = Upsample2DBlock(128, 64, 2, 2)
+        self.decoder_res1 = Res2DBlock(64, 64)
+        self.decoder_upsample1 = Upsample2DBlock(64, 32, 2, 2)
+        self.skip_res1 = Res2DBlock(32, 32)
+        self.skip_res2 = Res2DBlock(64, 64)
+
+    def forward(self, x):
+        s1 = self.skip_res1(x)
+        x = self.encoder_res1(self.encoder_pool1(x))
+        s2 = self.skip_res2(x)
+        x = self.decoder_res2(self.mid_res(self.encoder_res2(self.encoder_pool2(x))))
+        x = self.decoder_res1(self.decoder_upsample2(x) + s2)
+        return self.decoder_upsample1(x) + s1
+
+
+class P2PNet(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.output_channels = cout
+        self.front_layers = nn.Sequential(Basic2DBlock(cin, 16, 7), Res2DBlock(16, 32))
+        self.encoder_decoder = EncoderDecorder()
+        self.output_layer = nn.Conv2d(32, cout, kernel_size=1)
+
+    def forward(self, x):
+        return self.output_layer(self.encoder_decoder(self.front_layers(x)))
+
+
+class CenterNet(nn.Module):
+    def __init__(self, cin, cout, head_conv=32):
+        super().__init__()
+        self.output_channels = cout
+        self.front_layers = nn.Sequential(Basic2DBlock(cin, 16, 7), Res2DBlock(16, 32))
+        self.encoder_decoder = EncoderDecorder()
+        self.output_hm = nn.Sequential(nn.Conv2d(32, head_conv, 3, padding=1), nn.ReLU(True),
+                                       nn.Conv2d(head_conv, cout, 1))
+        self.output_size = nn.Sequential(nn.Conv2d(32, head_conv, 3, padding=1), nn.ReLU(True),
+                                         nn.Conv2d(head_conv, 2, 1))
+
+    def forward(self, x):
+        x, _ = torch.max(x, dim=4)
+        x = self.encoder_decoder(self.front_layers(x))
+        return self.output_hm(x), self.output_size(x)

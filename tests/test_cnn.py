@@ -1,0 +1,117 @@
+"""The HDN / JLN 2-D CNNs on the fp32 matrix cores (fvp/cnn.py, csrc/fvp_conv.hip;
+SURVEY.md §8(f) rank 1).
+
+Golden vectors: tests/golden/cnn.npz -- the reference's own P2PNet and
+CenterNet (lib/models/cnns_2d.py) with seeded weights (fvp.synthetic.
+seeded_state_dict; the trained checkpoints are not available offline) on
+seeded inputs, run on CPU by tools/gen_golden.py.  tests/cnn_arch.py restates
+the architectures (same attribute names) for the GPU box, pinned here.
+
+Tolerance: fp32 everywhere; the MFMA implicit GEMM sums in a different order
+than torch's conv and folds BatchNorm into one scale/shift, so outputs agree to
+2e-5 of the output's max magnitude (measured ~3e-6).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+REL = 2e-5
+
+
+def _close(got, ref, what):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    scale = max(float(np.abs(ref).max()), 1e-6)
+    err = float(np.abs(got - ref).max()) / scale
+    assert err <= REL, f"{what}: max error {err:.3g} of the output scale (> {REL})"
+
+
+def _nets():
+    from fvp import synthetic
+    import cnn_arch
+
+    p2p = cnn_arch.P2PNet(15, 15).eval()
+    p2p.load_state_dict(synthetic.seeded_state_dict(p2p, 11))
+    cn = cnn_arch.CenterNet(15, 1).eval()
+    cn.load_state_dict(synthetic.seeded_state_dict(cn, 12))
+    rng = np.random.default_rng(13)
+    x_p2p = rng.uniform(0.0, 1.0, (2, 15, 64, 64)).astype(np.float32)
+    x_cn = rng.uniform(0.0, 1.0, (1, 15, 40, 40, 4)).astype(np.float32)
+    return p2p, cn, x_p2p, x_cn
+
+
+def test_restated_architectures_match_reference_golden():
+    d = golden("cnn.npz")
+    p2p, cn, x_p2p, x_cn = _nets()
+    with torch.no_grad():
+        _close(p2p(torch.from_numpy(x_p2p)).numpy(), d["y_p2p"], "P2PNet (CPU restatement)")
+        hm, size = cn(torch.from_numpy(x_cn))
+    _close(hm.numpy(), d["hm"], "CenterNet hm")
+    _close(size.numpy(), d["size"], "CenterNet size")
+
+
+@pytest.mark.gpu
+def test_fvp_cnn_matches_reference(gpu_device):
+    from fvp.cnn import FvpCNN
+
+    d = golden("cnn.npz")
+    p2p, cn, x_p2p, x_cn = _nets()
+    p2p, cn = p2p.to(gpu_device), cn.to(gpu_device)
+    y = FvpCNN(p2p)(torch.from_numpy(x_p2p).to(gpu_device))
+    xy = torch.from_numpy(x_cn).to(gpu_device).max(dim=4)[0]
+    hm, size = FvpCNN(cn).from_xy(xy)
+    torch.cuda.synchronize()
+    _close(y.cpu().numpy(), d["y_p2p"], "P2PNet on MFMA")
+    _close(hm.cpu().numpy(), d["hm"], "CenterNet hm on MFMA")
+    _close(size.cpu().numpy(), d["size"], "CenterNet size on MFMA")
+    with torch.no_grad():  # and against torch's own GPU convolution of the same module
+        _close(y.cpu().numpy(), p2p(torch.from_numpy(x_p2p).to(gpu_device)).cpu().numpy(), "P2PNet vs torch GPU")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,hw,res", [(15, 16, 7, (64, 64), False), (16, 32, 3, (33, 17), True),
+                                               (128, 128, 3, (16, 16), True), (32, 15, 1, (20, 20), False),
+                                               (1, 20, 3, (64, 64), False), (40, 70, 5, (9, 11), True)])
+def test_conv_layer_vs_torch(gpu_device, cin, cout, k, hw, res):
+    """Single fused conv + BN + residual + ReLU layers, ragged shapes and channel counts."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    conv = nn.Conv2d(cin, cout, k, padding=(k - 1) // 2)
+    bn = nn.BatchNorm2d(cout)
+    seq = nn.Sequential(conv, bn).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin + cout))
+    seq = seq.to(gpu_device)
+    g = torch.Generator().manual_seed(k)
+    x = torch.rand((3, cin) + hw, generator=g).to(gpu_device)
+    r = torch.rand((3, cout) + hw, generator=g).to(gpu_device) if res else None
+    with torch.no_grad():
+        ref = seq(x)
+        ref = torch.relu(ref + r) if res else torch.relu(ref)
+    layer = cnn.ConvLayer(seq[0], seq[1])
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=cnn.to_nhwc(r) if res else None))
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv {cin}->{cout} k{k}")
+
+
+@pytest.mark.gpu
+def test_transposed_conv_and_pool_vs_torch(gpu_device):
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    from fvp import cnn, synthetic
+
+    up = nn.Sequential(nn.ConvTranspose2d(64, 32, 2, stride=2), nn.BatchNorm2d(32)).eval()
+    up.load_state_dict(synthetic.seeded_state_dict(up, 3))
+    up = up.to(gpu_device)
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand((2, 64, 9, 7), generator=g).to(gpu_device)
+    skip = torch.rand((2, 32, 18, 14), generator=g).to(gpu_device)
+    with torch.no_grad():
+        ref = torch.relu(up(x)) + skip
+    layer = cnn.ConvLayer(up[0], up[1])
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_post=cnn.to_nhwc(skip)))
+    _close(got.cpu().numpy(), ref.cpu().numpy(), "ConvTranspose2d + BN + ReLU + skip")
+    p = torch.rand((2, 48, 10, 12), generator=g).to(gpu_device)
+    assert torch.equal(cnn.to_nchw(cnn.maxpool2(cnn.to_nhwc(p))), F.max_pool2d(p, 2, 2))

@@ -175,6 +175,22 @@ def main():
          "pose": pose.numpy(), "confs": confs.numpy(), "fused": fused.numpy()}
     np.savez_compressed(os.path.join(OUT, "jln_post.npz"), **d)
     print("wrote jln_post", {k: np.shape(v) for k, v in d.items()})
+
+    # ---- the 2-D CNNs (P2PNet, CenterNet) with seeded weights on seeded inputs
+    import models.cnns_2d as c2d  # noqa: E402
+    p2p = c2d.P2PNet(15, 15).eval()
+    p2p.load_state_dict(synthetic.seeded_state_dict(p2p, 11))
+    cn = c2d.CenterNet(15, 1).eval()
+    cn.load_state_dict(synthetic.seeded_state_dict(cn, 12))
+    rng = np.random.default_rng(13)
+    x_p2p = rng.uniform(0.0, 1.0, (2, 15, 64, 64)).astype(np.float32)
+    x_cn = rng.uniform(0.0, 1.0, (1, 15, 40, 40, 4)).astype(np.float32)
+    with torch.no_grad():
+        y_p2p = p2p(torch.from_numpy(x_p2p)).numpy()
+        hm, size = cn(torch.from_numpy(x_cn))
+    d = {"y_p2p": y_p2p, "hm": hm.numpy(), "size": size.numpy()}
+    np.savez_compressed(os.path.join(OUT, "cnn.npz"), **d)
+    print("wrote cnn", {k: np.shape(v) for k, v in d.items()}, float(np.abs(y_p2p).max()))
     return 0
 
 

@@ -13,17 +13,20 @@
 // the ReLU) and, for ConvTranspose2d(k=2, s=2), the 2x upsampling scatter
 // (the transposed conv is a 1x1 conv producing 4*Cout channels).
 //
-// Block = 256 threads (4 waves, 2x2), tile 64 pixels x 64 output channels,
-// one 32x32 MFMA accumulator per wave; the K dimension is walked in chunks of
-// 16 (one (ky,kx) tap, 16 input channels) staged through LDS, the next
-// chunk's global loads issued before the current chunk's 8 MFMAs.
+// Block = 256 threads (4 waves); the tile follows the output width so no MFMA
+// column is wasted on padding: Cout <= 16 -> 256 px x 16 ch on 16x16x4 MFMAs,
+// <= 32 -> 128 x 32, wider -> 128 x 64 (2 accumulators per wave) on 32x32x2.
+// The K dimension is walked in chunks of 16 (one (ky,kx) tap, 16 input
+// channels) staged through LDS, the next chunk's global loads issued before
+// the current chunk's MFMAs.
+#include <type_traits>
+
 #include "fvp_device.h"
 
 namespace fvp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int kBM = 64, kBN = 64, kKC = 16, kAP = kKC + 1;  // A tile pitch 17: conflict-free column reads
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvArgs {
     const float *in;        // [N][H][W][Cpi]
@@ -36,92 +39,175 @@ struct ConvArgs {
     int N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, up2;
 };
 
-__device__ __forceinline__ void load_chunk(const ConvArgs &a, int m0, int n0, int chunk, int M, float4 &av,
-                                           float4 &bv) {
+// Tile configuration: BM pixels x BN channels per 256-thread block, MFMA
+// MSxMS (32: v_mfma_f32_32x32x2_f32, 16: v_mfma_f32_16x16x4_f32), waves
+// arranged WR x WC, each wave TM x TN MFMA tiles; K chunks of KC (one tap).
+template <int BM_, int BN_, int MS_, int WR_>
+struct Tile {
+    static constexpr int BM = BM_, BN = BN_, MS = MS_, WR = WR_, WC = 4 / WR_;
+    static constexpr int WTM = BM / WR, WTN = BN / WC;  // wave tile
+    static constexpr int TM = WTM / MS, TN = WTN / MS;
+    static constexpr int KC = 16, AP = KC + 1;
+    static constexpr int KSTEP = MS == 32 ? 2 : 4;      // k per MFMA
+    static constexpr int NACC = MS == 32 ? 16 : 4;      // accumulator registers per MFMA tile
+    static_assert(TM >= 1 && TN >= 1 && WTM % MS == 0 && WTN % MS == 0, "tile");
+};
+
+template <class TL>
+__device__ __forceinline__ void load_chunk(const ConvArgs &a, int m0, int n0, int chunk, int M, float4 *av,
+                                           float4 *bv) {
+    constexpr int AE = TL::BM * TL::KC / 4;        // float4 of the A chunk
+    constexpr int AV = AE >= 256 ? AE / 256 : 1;   // per thread
+    constexpr int BV = TL::KC * TL::BN / 4 / 256;  // float4 per thread (B), may be 0
     const int t = threadIdx.x;
-    const int cpc = a.Cpi / kKC;  // chunks per tap
+    const int cpc = a.Cpi / TL::KC;  // chunks per tap
     const int tap = chunk / cpc, c = chunk - tap * cpc;
     const int ky = tap / a.KW, kx = tap - ky * a.KW;
-    // A: thread -> (pixel t/4, 4 channels)
-    {
-        const int m = m0 + (t >> 2);
-        av = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < M) {
-            const int HW = a.H * a.W;
+    const int HW = a.H * a.W;
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+        const int e = u * 256 + t;  // -> (pixel e/4, 4 channels)
+        const int m = m0 + (e >> 2);
+        av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < AE && m < M) {
             const int img = m / HW, r = m - img * HW;
             const int y = r / a.W + ky - (a.KH - 1) / 2, x = r % a.W + kx - (a.KW - 1) / 2;
             if ((unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-                av = *reinterpret_cast<const float4 *>(a.in + (((size_t)img * a.H + y) * a.W + x) * a.Cpi + c * kKC +
-                                                      (t & 3) * 4);
+                av[u] = *reinterpret_cast<const float4 *>(a.in + (((size_t)img * a.H + y) * a.W + x) * a.Cpi +
+                                                         c * TL::KC + (e & 3) * 4);
         }
     }
-    // B: thread -> (k row t/16, 4 output columns)
-    {
-        const size_t row = (size_t)tap * a.Cpi + c * kKC + (t >> 4);
-        bv = *reinterpret_cast<const float4 *>(a.w + row * a.Cpo_w + n0 + (t & 15) * 4);
+    if constexpr (BV > 0) {
+#pragma unroll
+        for (int u = 0; u < BV; ++u) {
+            const int e = u * 256 + t;  // -> (k row e/(BN/4), 4 columns)
+            const size_t row = (size_t)tap * a.Cpi + c * TL::KC + e / (TL::BN / 4);
+            bv[u] = *reinterpret_cast<const float4 *>(a.w + row * a.Cpo_w + n0 + (e % (TL::BN / 4)) * 4);
+        }
+    } else {  // BN*KC/4 < 256: the first KC*BN/4 threads load one float4
+        if (t < TL::KC * TL::BN / 4) {
+            const size_t row = (size_t)tap * a.Cpi + c * TL::KC + t / (TL::BN / 4);
+            bv[0] = *reinterpret_cast<const float4 *>(a.w + row * a.Cpo_w + n0 + (t % (TL::BN / 4)) * 4);
+        }
     }
 }
 
+template <class TL>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
-    __shared__ float As[2][kBM * kAP];
-    __shared__ __attribute__((aligned(16))) float Bs[2][kKC * kBN];
+    constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, AP = TL::AP, MS = TL::MS;
+    constexpr int AE = BM * KC / 4;
+    constexpr int AV = AE >= 256 ? AE / 256 : 1;
+    constexpr int BVN = KC * BN / 4 / 256 > 0 ? KC * BN / 4 / 256 : 1;
+    __shared__ float As[2][BM * AP];
+    __shared__ __attribute__((aligned(16))) float Bs[2][KC * BN];
     const int M = a.N * a.H * a.W;
-    const int m0 = blockIdx.x * kBM, n0 = blockIdx.y * kBN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
-    const int nchunks = a.KH * a.KW * (a.Cpi / kKC);
-    f32x16 acc;
+    const int wr = wave % TL::WR, wc = wave / TL::WR;
+    const int nchunks = a.KH * a.KW * (a.Cpi / KC);
+    using acc_t = typename std::conditional<MS == 32, f32x16, f32x4>::type;
+    acc_t acc[TL::TM][TL::TN];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::TN; ++j)
+#pragma unroll
+            for (int r = 0; r < TL::NACC; ++r) acc[i][j][r] = 0.f;
 
-    float4 av, bv;
-    load_chunk(a, m0, n0, 0, M, av, bv);
+    float4 av[AV], bv[BVN];
+    load_chunk<TL>(a, m0, n0, 0, M, av, bv);
     for (int ch = 0; ch < nchunks; ++ch) {
         const int buf = ch & 1;
-        {
-            float *ap = &As[buf][(t >> 2) * kAP + (t & 3) * 4];
-            ap[0] = av.x; ap[1] = av.y; ap[2] = av.z; ap[3] = av.w;
-            *reinterpret_cast<float4 *>(&Bs[buf][(t >> 4) * kBN + (t & 15) * 4]) = bv;
+#pragma unroll
+        for (int u = 0; u < AV; ++u) {
+            const int e = u * 256 + t;
+            if (e >= AE) break;
+            float *ap = &As[buf][(e >> 2) * AP + (e & 3) * 4];
+            ap[0] = av[u].x; ap[1] = av[u].y; ap[2] = av[u].z; ap[3] = av[u].w;
+        }
+        if constexpr (KC * BN / 4 >= 256) {
+#pragma unroll
+            for (int u = 0; u < BVN; ++u) {
+                const int e = u * 256 + t;
+                *reinterpret_cast<float4 *>(&Bs[buf][(e / (BN / 4)) * BN + (e % (BN / 4)) * 4]) = bv[u];
+            }
+        } else if (t < KC * BN / 4) {
+            *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
         }
         __syncthreads();
-        if (ch + 1 < nchunks) load_chunk(a, m0, n0, ch + 1, M, av, bv);  // in flight during the MFMAs
-        const float *Aw = &As[buf][(wm * 32 + (lane & 31)) * kAP + (lane >> 5)];
-        const float *Bw = &Bs[buf][(lane >> 5) * kBN + wn * 32 + (lane & 31)];
+        if (ch + 1 < nchunks) load_chunk<TL>(a, m0, n0, ch + 1, M, av, bv);  // in flight during the MFMAs
 #pragma unroll
-        for (int kk = 0; kk < kKC / 2; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Aw[2 * kk], Bw[2 * kk * kBN], acc, 0, 0, 0);
+        for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
+            float fa[TL::TM], fb[TL::TN];
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i) {
+                const int row = wr * TL::WTM + i * MS + (lane % MS);
+                fa[i] = As[buf][row * AP + kk * TL::KSTEP + lane / MS];
+            }
+#pragma unroll
+            for (int j = 0; j < TL::TN; ++j) {
+                const int col = wc * TL::WTN + j * MS + (lane % MS);
+                fb[j] = Bs[buf][(kk * TL::KSTEP + lane / MS) * BN + col];
+            }
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TL::TN; ++j) {
+                    if constexpr (MS == 32)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+        }
         // the next iteration writes the other buffer; the one after rewrites this
         // one only after its own barrier, which every wave reaches after these reads
     }
 
-    // epilogue: lane -> column (output channel), registers -> 16 rows (pixels)
-    const int n = n0 + wn * 32 + (lane & 31);
+    // epilogue: lane -> column (output channel), registers -> rows (pixels)
     const int Ctot = a.up2 ? 4 * a.Cpo : a.Cpo;
-    if (n >= Ctot) return;
-    const int co = a.up2 ? n % a.Cpo : n;
-    const int q = a.up2 ? n / a.Cpo : 0;  // (dy, dx) of the transposed conv
-    const float sc = a.scale[co], sh = a.shift[co];
     const int Ho = a.up2 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m >= M) continue;
-        size_t o;
-        if (a.up2) {
-            const int HW = a.H * a.W;
-            const int img = m / HW, rr = m - img * HW;
-            const int y = 2 * (rr / a.W) + (q >> 1), x = 2 * (rr % a.W) + (q & 1);
-            o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
-        } else {
-            o = (size_t)m * a.Cpo + co;
+    for (int j = 0; j < TL::TN; ++j) {
+        const int n = n0 + wc * TL::WTN + j * MS + (lane % MS);
+        if (n >= Ctot) continue;
+        const int co = a.up2 ? n % a.Cpo : n;
+        const int q = a.up2 ? n / a.Cpo : 0;  // (dy, dx) of the transposed conv
+        const float sc = a.scale[co], sh = a.shift[co];
+#pragma unroll
+        for (int i = 0; i < TL::TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < TL::NACC; ++r) {
+                const int row = MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r;
+                const int m = m0 + wr * TL::WTM + i * MS + row;
+                if (m >= M) continue;
+                size_t o;
+                if (a.up2) {
+                    const int HW = a.H * a.W;
+                    const int img = m / HW, rr = m - img * HW;
+                    const int y = 2 * (rr / a.W) + (q >> 1), x = 2 * (rr % a.W) + (q & 1);
+                    o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
+                } else {
+                    o = (size_t)m * a.Cpo + co;
+                }
+                float v = acc[i][j][r] * sc + sh;
+                if (a.res_pre) v = v + a.res_pre[o];
+                if (a.relu) v = fmaxf(v, 0.0f);
+                if (a.res_post) v = v + a.res_post[o];
+                a.out[o] = v;
+            }
         }
-        float v = acc[r] * sc + sh;
-        if (a.res_pre) v = v + a.res_pre[o];
-        if (a.relu) v = fmaxf(v, 0.0f);
-        if (a.res_post) v = v + a.res_post[o];
-        a.out[o] = v;
     }
 }
+
+// Tiles by output width; the big ones where the launch has >= 2 blocks per CU,
+// smaller ones (16x16x4 MFMAs) so small layers still fill the 256 CUs.
+using TileN16 = Tile<256, 16, 16, 4>;   // Cout <= 16: 4 waves x (64 px x 16 ch)
+using TileN16s = Tile<64, 16, 16, 4>;   //             4 waves x (16 px x 16 ch)
+using TileN32 = Tile<128, 32, 32, 4>;   // Cout <= 32: 4 waves x (32 px x 32 ch)
+using TileN32s = Tile<64, 32, 16, 4>;   //             4 waves x (16 px x 32 ch)
+using TileN64 = Tile<128, 64, 32, 2>;   // wider: 2x2 waves x (64 px x 32 ch), 2 accumulators
+using TileN64m = Tile<64, 64, 32, 2>;   //        2x2 waves x (32 px x 32 ch)
+using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
 
 // 2x2 / stride-2 max pool, NHWC (F.max_pool2d(x, 2, 2), cnns_2d.py Pool2DBlock)
 __global__ __launch_bounds__(256) void maxpool2_kernel(const float *__restrict__ in, float *__restrict__ out, int N,
@@ -186,8 +272,24 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
     const long long M = (long long)N * H * W;
     if (M * (upsample2 ? 4 : 1) * Cpo > 0x7fffffffLL * 4) return FVP_ERR_SHAPE;
     fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
-    const dim3 grid((unsigned)((M + fvp::kBM - 1) / fvp::kBM), (unsigned)((Ntot + fvp::kBN - 1) / fvp::kBN));
-    hipLaunchKernelGGL(fvp::conv_mfma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipStream_t st = (hipStream_t)stream;
+#define FVP_CONV(TL)                                                                                              \
+    hipLaunchKernelGGL(fvp::conv_mfma_kernel<fvp::TL>,                                                            \
+                       dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM), (unsigned)((Ntot + fvp::TL::BN - 1) / \
+                                                                                      fvp::TL::BN)),          \
+                       dim3(256), 0, st, a)
+    auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long long)((Ntot + bn - 1) / bn); };
+    const long long enough = 512;  // >= 2 blocks per CU
+    if (Ntot <= 16) {
+        if (blocks(256, 16) >= enough) FVP_CONV(TileN16); else FVP_CONV(TileN16s);
+    } else if (Ntot <= 32) {
+        if (blocks(128, 32) >= enough) FVP_CONV(TileN32); else FVP_CONV(TileN32s);
+    } else {
+        if (blocks(128, 64) >= enough) FVP_CONV(TileN64);
+        else if (blocks(64, 64) >= enough) FVP_CONV(TileN64m);
+        else FVP_CONV(TileN64s);
+    }
+#undef FVP_CONV
     return (int)hipGetLastError();
 }
 

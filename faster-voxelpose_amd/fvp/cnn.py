@@ -248,3 +248,14 @@ class FvpCNN:
         assert self.kind == "centernet"
         f = self.encdec(self.front(to_nhwc(xy)))
         return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
+
+
+def cached(module: nn.Module) -> FvpCNN:
+    """FvpCNN for ``module``, rebuilt whenever its parameters or buffers change
+    (storage or in-place version), e.g. after load_state_dict."""
+    sig = tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
+    hit = getattr(module, "_fvp_cnn", None)
+    if hit is None or hit[0] != sig:
+        hit = (sig, FvpCNN(module))
+        object.__setattr__(module, "_fvp_cnn", hit)
+    return hit[1]

@@ -26,11 +26,19 @@ import sys
 
 import torch
 
+from . import cnn as fvp_cnn
 from . import jln, project_individual, project_whole, proposal
 
+USE_FVP_CNN = False  # set by install(cnn=True)
 
-def install(fused: bool = True, modules=None) -> dict:
-    """Patch the already-importable reference modules.  Returns what was patched."""
+
+def install(fused: bool = True, modules=None, cnn: bool = False) -> dict:
+    """Patch the already-importable reference modules.  Returns what was patched.
+
+    cnn=True (with fused=True): in eval mode the fused forwards run CenterNet and
+    P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of torch's."""
+    global USE_FVP_CNN
+    USE_FVP_CNN = bool(cnn)
     mods = modules if modules is not None else sys.modules
     patched = {}
 
@@ -64,6 +72,8 @@ def install(fused: bool = True, modules=None) -> dict:
 def center_net_from_xy(center_net, xy: torch.Tensor):
     """CenterNet.forward (cnns_2d.py:280-295) minus its first line, fed with
     the xy max-plane the voxelize kernel already produced."""
+    if USE_FVP_CNN and not center_net.training:
+        return fvp_cnn.cached(center_net).from_xy(xy)
     x = center_net.front_layers(xy)
     x = center_net.encoder_decoder(x)
     return center_net.output_hm(x), center_net.output_size(x)

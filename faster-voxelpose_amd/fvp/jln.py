@@ -73,7 +73,10 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
     P = planes.shape[0] // 3
     if P == 0:
         return
-    features = torch.stack(torch.chunk(self.conv_net(planes), 3), dim=0)          # [3,P,J,S,S]
+    from . import cnn, integration
+
+    conv = cnn.cached(self.conv_net) if integration.USE_FVP_CNN and not self.conv_net.training else self.conv_net
+    features = torch.stack(torch.chunk(conv(planes), 3), dim=0)                    # [3,P,J,S,S]
     pose, maxprob = ops.soft_argmax(features, self.project_layer.center_grid, offset,
                                     float(self.soft_argmax_layer.beta))
     weights = self.weight_net(features)                                             # [3P,J,1]

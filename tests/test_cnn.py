@@ -115,3 +115,17 @@ def test_transposed_conv_and_pool_vs_torch(gpu_device):
     _close(got.cpu().numpy(), ref.cpu().numpy(), "ConvTranspose2d + BN + ReLU + skip")
     p = torch.rand((2, 48, 10, 12), generator=g).to(gpu_device)
     assert torch.equal(cnn.to_nchw(cnn.maxpool2(cnn.to_nhwc(p))), F.max_pool2d(p, 2, 2))
+
+
+@pytest.mark.gpu
+def test_fvp_cnn_large_batch_tiles_vs_torch(gpu_device):
+    """Enough images that every layer takes the large tiles (>= 2 blocks per CU)."""
+    from fvp.cnn import FvpCNN
+
+    p2p, cn, _, _ = _nets()
+    p2p = p2p.to(gpu_device)
+    x = torch.rand((24, 15, 64, 64), generator=torch.Generator().manual_seed(5)).to(gpu_device)
+    with torch.no_grad():
+        ref = p2p(x)
+    got = FvpCNN(p2p)(x)
+    _close(got.cpu().numpy(), ref.cpu().numpy(), "P2PNet, 24 images")

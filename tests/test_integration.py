@@ -227,3 +227,63 @@ def test_fused_jln_forward_matches_reference_flow(gpu_device):
     np.testing.assert_allclose(gf.cpu().numpy(), rf.cpu().numpy(), atol=0.5, rtol=0)
     np.testing.assert_allclose(pc_got.cpu().numpy(), pc_ref.cpu().numpy(), atol=1e-4, rtol=0)
     assert torch.count_nonzero(gf[2]) == 0 and torch.count_nonzero(gf[1, 3:]) == 0
+
+
+@pytest.mark.gpu
+def test_fused_forwards_with_fvp_cnn(gpu_device):
+    """install(cnn=True): CenterNet (HDN) and P2PNet (JLN) run on the fvp MFMA
+    convolutions inside the fused forwards; results match the torch-conv fused
+    forwards within the CNN tolerance (2e-5 of the output scale; the proposals
+    themselves may reorder only where heatmap values tie within it)."""
+    import cnn_arch
+
+    from fvp import geometry, jln, synthetic
+    from fvp.config import AttrDict
+    from fvp.project_individual import ProjectLayer as PI
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c3"]
+    J = w.num_joints
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 2)).to(gpu_device)
+    meta = {"seq": [seq] * 2}
+    hdn = types.SimpleNamespace()
+    hdn.project_layer = ProjectLayer(w.cfg(str(gpu_device)))
+    hdn.project_layer.verbose = False
+    hdn.center_net = cnn_arch.CenterNet(J, 1).eval()
+    hdn.center_net.load_state_dict(synthetic.seeded_state_dict(hdn.center_net, 12))
+    hdn.center_net = hdn.center_net.to(gpu_device)
+    hdn.c2c_net = nn.Conv1d(J, 1, 1).to(gpu_device).eval()
+    hdn.proposal_layer = _Proposal(w)
+    hdn.max_people = w.max_people
+    try:
+        with torch.no_grad():
+            integration.USE_FVP_CNN = False
+            ref = integration.fused_hdn_forward(hdn, hm, meta, cams, rt)
+            integration.USE_FVP_CNN = True
+            got = integration.fused_hdn_forward(hdn, hm, meta, cams, rt)
+        scale = float(ref[0].abs().max())
+        assert float((got[0] - ref[0]).abs().max()) <= 2e-5 * scale
+        assert float((got[3] - ref[3]).abs().max()) <= 2e-5 * float(ref[3].abs().max())
+
+        net = types.SimpleNamespace(training=False)
+        net.project_layer = PI(w.cfg(str(gpu_device)))
+        net.project_layer.verbose = False
+        net.conv_net = cnn_arch.P2PNet(J, J).eval()
+        net.conv_net.load_state_dict(synthetic.seeded_state_dict(net.conv_net, 11))
+        net.conv_net = net.conv_net.to(gpu_device)
+        net.weight_net = _WeightNet(J).to(gpu_device).eval()
+        net.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
+        pc = torch.from_numpy(np.stack([synthetic.proposals_for_frame(w, f, 4) for f in range(2)])).to(gpu_device)
+        mask = torch.ones((2, 4), dtype=torch.bool, device=gpu_device)
+        with torch.no_grad():
+            integration.USE_FVP_CNN = False
+            rf, rp = jln.fused_jln_forward(net, meta, hm, pc.clone(), mask, cams, rt)
+            integration.USE_FVP_CNN = True
+            gf, gp = jln.fused_jln_forward(net, meta, hm, pc.clone(), mask, cams, rt)
+        np.testing.assert_allclose(gp.cpu().numpy(), rp.cpu().numpy(), atol=0.5, rtol=0)
+        np.testing.assert_allclose(gf.cpu().numpy(), rf.cpu().numpy(), atol=0.5, rtol=0)
+    finally:
+        integration.USE_FVP_CNN = False

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""CNN line: P2PNet on the JLN planes of K proposals
+(3K images of J x 64 x 64) and CenterNet on B xy planes (J x 80 x 80), fvp MFMA
+engine vs torch's own GPU convolution of the same eval-mode module.
+
+    python tools/bench_cnn.py [--proposals 10] [--frames 8] [--iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+MFMA_F32_PEAK_TF = 157.3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--proposals", type=int, default=40, help="JLN proposals in the batch (4 frames x 10)")
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import cnn_arch
+    from fvp import cnn, synthetic
+
+    dev = torch.device("cuda:0")
+    J = 15
+    p2p = cnn_arch.P2PNet(J, J).eval()
+    p2p.load_state_dict(synthetic.seeded_state_dict(p2p, 11))
+    cn = cnn_arch.CenterNet(J, 1).eval()
+    cn.load_state_dict(synthetic.seeded_state_dict(cn, 12))
+    p2p, cn = p2p.to(dev), cn.to(dev)
+    g = torch.Generator().manual_seed(0)
+    x_jln = torch.rand((3 * args.proposals, J, 64, 64), generator=g).to(dev)
+    x_hdn = torch.rand((args.frames, J, 80, 80), generator=g).to(dev)
+    f_p2p, f_cn = cnn.FvpCNN(p2p), cnn.FvpCNN(cn)
+
+    def flops(plan_net, x):
+        # count with the fvp layer descriptions: 2*M*N*K per conv
+        tot = 0
+        orig = cnn.ConvLayer.__call__
+
+        def counting(self, a, relu, res_pre=None, res_post=None):
+            nonlocal tot
+            tot += self.flops(a)
+            return orig(self, a, relu, res_pre, res_post)
+        cnn.ConvLayer.__call__ = counting
+        try:
+            plan_net(x)
+        finally:
+            cnn.ConvLayer.__call__ = orig
+        return tot
+
+    def timeit(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = []
+        for _ in range(3):
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / args.iters)
+        return float(np.median(ts))
+
+    out = {}
+    with torch.no_grad():
+        for name, fv, tv, x in (("p2pnet_jln", lambda: f_p2p(x_jln), lambda: p2p(x_jln), x_jln),
+                                ("centernet_hdn", lambda: f_cn.from_xy(x_hdn),
+                                 lambda: (cn.output_hm(cn.encoder_decoder(cn.front_layers(x_hdn))),), x_hdn)):
+            fl = flops(f_p2p if name.startswith("p2p") else (lambda t: f_cn.from_xy(t)), x)
+            t_f, t_t = timeit(fv), timeit(tv)
+            out[name] = {"images": int(x.shape[0]), "shape": list(x.shape[1:]), "gflop": round(fl / 1e9, 3),
+                         "fvp_ms": round(t_f, 4), "torch_ms": round(t_t, 4),
+                         "fvp_tflops": round(fl / (t_f * 1e-3) / 1e12, 2),
+                         "mfma_frac_of_f32_peak": round(fl / (t_f * 1e-3) / 1e12 / MFMA_F32_PEAK_TF, 4),
+                         "speedup_vs_torch": round(t_t / t_f, 3)}
+    print(json.dumps({"metric": "HDN/JLN CNNs on fp32 MFMA (implicit GEMM, folded BN)", "peak_tflops_f32": MFMA_F32_PEAK_TF,
+                      "note": "torch_ms = the same eval module on torch's GPU convolution (MIOpen); torch centernet "
+                              "time covers the same layers (hm head only)", **out}))
+
+
+if __name__ == "__main__":
+    main()

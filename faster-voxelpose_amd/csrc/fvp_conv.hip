@@ -30,7 +30,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvArgs {
     const float *in;        // [N][H][W][Cpi]
-    const float *w;         // [KH*KW*Cpi][Cpo_w]  (Cpo_w = roundup(Cout_total, 64))
+    const float *w;         // [KH*KW*Cpi][Cpo_w]  (Cpo_w = roundup(Cout_total, 128))
     const float *scale;     // [Cpo]  (per output channel)
     const float *shift;     // [Cpo]
     const float *res_pre;   // [N][Ho][Wo][Cpo] or null: added before the ReLU
@@ -42,19 +42,26 @@ struct ConvArgs {
 // Tile configuration: BM pixels x BN channels per 256-thread block, MFMA
 // MSxMS (32: v_mfma_f32_32x32x2_f32, 16: v_mfma_f32_16x16x4_f32), waves
 // arranged WR x WC, each wave TM x TN MFMA tiles; K chunks of KC (one tap).
-template <int BM_, int BN_, int MS_, int WR_>
+template <int BM_, int BN_, int MS_, int WR_, int KC_ = 16>
 struct Tile {
     static constexpr int BM = BM_, BN = BN_, MS = MS_, WR = WR_, WC = 4 / WR_;
     static constexpr int WTM = BM / WR, WTN = BN / WC;  // wave tile
     static constexpr int TM = WTM / MS, TN = WTN / MS;
-    static constexpr int KC = 16, AP = KC + 1;
+    static constexpr int KC = KC_, AP = KC + 1;
     static constexpr int KSTEP = MS == 32 ? 2 : 4;      // k per MFMA
     static constexpr int NACC = MS == 32 ? 16 : 4;      // accumulator registers per MFMA tile
     static_assert(TM >= 1 && TN >= 1 && WTM % MS == 0 && WTN % MS == 0, "tile");
 };
 
+// Per-thread A rows (pixels) are fixed for the whole K loop: their (image,
+// y, x) are decoded once, so a chunk only adds the tap offset.
+struct PixRef {
+    int y, x;         // output pixel coordinates (y = -1 << 20 when past M)
+    const float *p;   // input row base of the pixel's image
+};
+
 template <class TL>
-__device__ __forceinline__ void load_chunk(const ConvArgs &a, int m0, int n0, int chunk, int M, float4 *av,
+__device__ __forceinline__ void load_chunk(const ConvArgs &a, int n0, int chunk, const PixRef *pr, float4 *av,
                                            float4 *bv) {
     constexpr int AE = TL::BM * TL::KC / 4;        // float4 of the A chunk
     constexpr int AV = AE >= 256 ? AE / 256 : 1;   // per thread
@@ -63,19 +70,15 @@ __device__ __forceinline__ void load_chunk(const ConvArgs &a, int m0, int n0, in
     const int cpc = a.Cpi / TL::KC;  // chunks per tap
     const int tap = chunk / cpc, c = chunk - tap * cpc;
     const int ky = tap / a.KW, kx = tap - ky * a.KW;
-    const int HW = a.H * a.W;
+    const int dy = ky - (a.KH - 1) / 2, dx = kx - (a.KW - 1) / 2;
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
         const int e = u * 256 + t;  // -> (pixel e/4, 4 channels)
-        const int m = m0 + (e >> 2);
+        const int y = pr[u].y + dy, x = pr[u].x + dx;
         av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e < AE && m < M) {
-            const int img = m / HW, r = m - img * HW;
-            const int y = r / a.W + ky - (a.KH - 1) / 2, x = r % a.W + kx - (a.KW - 1) / 2;
-            if ((unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-                av[u] = *reinterpret_cast<const float4 *>(a.in + (((size_t)img * a.H + y) * a.W + x) * a.Cpi +
-                                                         c * TL::KC + (e & 3) * 4);
-        }
+        if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+            av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * TL::KC +
+                                                     (e & 3) * 4);
     }
     if constexpr (BV > 0) {
 #pragma unroll
@@ -114,8 +117,20 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < TL::NACC; ++r) acc[i][j][r] = 0.f;
 
+    PixRef pr[AV];
+    {
+        const int HW = a.H * a.W;
+#pragma unroll
+        for (int u = 0; u < AV; ++u) {
+            const int m = m0 + ((u * 256 + t) >> 2);
+            const int img = m / HW, r = m - img * HW;
+            pr[u].y = m < M ? r / a.W : -(1 << 20);
+            pr[u].x = r % a.W;
+            pr[u].p = a.in + (size_t)(m < M ? img : 0) * HW * a.Cpi;
+        }
+    }
     float4 av[AV], bv[BVN];
-    load_chunk<TL>(a, m0, n0, 0, M, av, bv);
+    load_chunk<TL>(a, n0, 0, pr, av, bv);
     for (int ch = 0; ch < nchunks; ++ch) {
         const int buf = ch & 1;
 #pragma unroll
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
             *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
         }
         __syncthreads();
-        if (ch + 1 < nchunks) load_chunk<TL>(a, m0, n0, ch + 1, M, av, bv);  // in flight during the MFMAs
+        if (ch + 1 < nchunks) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);  // in flight during the MFMAs
 #pragma unroll
         for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
             float fa[TL::TM], fb[TL::TN];
@@ -208,6 +223,171 @@ using TileN32s = Tile<64, 32, 16, 4>;   //             4 waves x (16 px x 32 ch)
 using TileN64 = Tile<128, 64, 32, 2>;   // wider: 2x2 waves x (64 px x 32 ch), 2 accumulators
 using TileN64m = Tile<64, 64, 32, 2>;   //        2x2 waves x (32 px x 32 ch)
 using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
+// larger wave tiles / 32-wide K chunks (tuning candidates)
+using TileX1 = Tile<256, 32, 32, 4, 16>;   // 4 waves x (64 x 32)
+using TileX2 = Tile<256, 32, 32, 4, 32>;
+using TileX3 = Tile<128, 64, 32, 2, 32>;   // 2x2 waves x (64 x 32), K 32
+using TileX4 = Tile<256, 64, 32, 4, 16>;   // 4 waves x (64 x 64)
+using TileX5 = Tile<128, 128, 32, 2, 16>;  // 2x2 waves x (64 x 64)
+using TileX6 = Tile<128, 128, 32, 2, 32>;
+using TileX7 = Tile<128, 32, 32, 4, 32>;   // 4 waves x (32 x 32), K 32
+using TileX8 = Tile<64, 64, 32, 2, 32>;
+
+static int g_force_tile = 0;
+
+}  // namespace fvp
+
+extern "C" int fvp_conv_set_tile(int id) {
+    if (id < 0 || id > 15) return FVP_ERR_SHAPE;
+    fvp::g_force_tile = id;
+    return FVP_OK;
+}
+
+namespace fvp {
+
+// ---- bf16 operands (opt-in precision) -------------------------------------------
+// Same implicit GEMM on v_mfma_f32_32x32x16_bf16 (fp32 accumulate): the fp32
+// activations are rounded to bf16 while staged into LDS, weights are packed
+// bf16 [Cpo_w][K] (k contiguous).  K chunks of KC (16 or 32) channels of one
+// tap; lane half h of an MFMA takes k = 8h..8h+7 of each 16-wide step.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int BM_, int BN_, int WR_, int KC_>
+struct TileB {
+    static constexpr int BM = BM_, BN = BN_, WR = WR_, WC = 4 / WR_, KC = KC_;
+    static constexpr int WTM = BM / WR, WTN = BN / WC, TM = WTM / 32, TN = WTN / 32;
+    static constexpr int P = KC + 8;  // LDS row pitch in bf16: 16-B aligned, conflict-free b128 reads
+    static_assert(TM >= 1 && TN >= 1, "tile");
+};
+
+template <class TL>
+__global__ __launch_bounds__(256) void conv_bf16_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
+    constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, P = TL::P;
+    constexpr int AE = BM * KC / 4, AV = AE >= 256 ? AE / 256 : 1;  // A: float4 (4 channels) per element
+    constexpr int BE = BN * KC / 8, BV = BE >= 256 ? BE / 256 : 1;  // B: 8 bf16 per element
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * P];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * P];  // [column][k]
+    const int M = a.N * a.H * a.W;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wr = wave % TL::WR, wc = wave / TL::WR;
+    const int cpc = a.Cpi / KC;
+    const int nchunks = a.KH * a.KW * cpc;
+    const size_t Ktot = (size_t)a.KH * a.KW * a.Cpi;
+    f32x16 acc[TL::TM][TL::TN];
+#pragma unroll
+    for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    PixRef pr[AV];
+    {
+        const int HW = a.H * a.W;
+#pragma unroll
+        for (int u = 0; u < AV; ++u) {
+            const int m = m0 + ((u * 256 + t) / (KC / 4));
+            const int img = m / HW, r = m - img * HW;
+            pr[u].y = m < M ? r / a.W : -(1 << 20);
+            pr[u].x = r % a.W;
+            pr[u].p = a.in + (size_t)(m < M ? img : 0) * HW * a.Cpi;
+        }
+    }
+    float4 av[AV];
+    uint4 bv[BV];
+    auto load = [&](int chunk) {
+        const int tap = chunk / cpc, c = chunk - tap * cpc;
+        const int ky = tap / a.KW, kx = tap - ky * a.KW;
+        const int dy = ky - (a.KH - 1) / 2, dx = kx - (a.KW - 1) / 2;
+#pragma unroll
+        for (int u = 0; u < AV; ++u) {
+            const int e = u * 256 + t;  // -> (pixel e/(KC/4), 4 channels)
+            const int y = pr[u].y + dy, x = pr[u].x + dx;
+            av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+                av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * KC +
+                                                         (e % (KC / 4)) * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < BV; ++u) {
+            const int e = u * 256 + t;  // -> (column e/(KC/8), 8 k)
+            if (e < BE)
+                bv[u] = *reinterpret_cast<const uint4 *>(wb + (size_t)(n0 + e / (KC / 8)) * Ktot +
+                                                        (size_t)tap * a.Cpi + c * KC + (e % (KC / 8)) * 8);
+        }
+    };
+    load(0);
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int buf = ch & 1;
+#pragma unroll
+        for (int u = 0; u < AV; ++u) {
+            const int e = u * 256 + t;
+            if (e < AE) {
+                bf16x4 h;
+                h[0] = (__bf16)av[u].x; h[1] = (__bf16)av[u].y; h[2] = (__bf16)av[u].z; h[3] = (__bf16)av[u].w;
+                *reinterpret_cast<bf16x4 *>(&As[buf][(e / (KC / 4)) * P + (e % (KC / 4)) * 4]) = h;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < BV; ++u) {
+            const int e = u * 256 + t;
+            if (e < BE) *reinterpret_cast<uint4 *>(&Bs[buf][(e / (KC / 8)) * P + (e % (KC / 8)) * 8]) = bv[u];
+        }
+        __syncthreads();
+        if (ch + 1 < nchunks) load(ch + 1);  // in flight during the MFMAs
+#pragma unroll
+        for (int ks = 0; ks < KC / 16; ++ks) {
+            bf16x8 fa[TL::TM], fb[TL::TN];
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i)
+                fa[i] = *reinterpret_cast<const bf16x8 *>(
+                    &As[buf][(wr * TL::WTM + i * 32 + (lane & 31)) * P + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+            for (int j = 0; j < TL::TN; ++j)
+                fb[j] = *reinterpret_cast<const bf16x8 *>(
+                    &Bs[buf][(wc * TL::WTN + j * 32 + (lane & 31)) * P + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TL::TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    const int Ctot = a.up2 ? 4 * a.Cpo : a.Cpo;
+    const int Ho = a.up2 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
+#pragma unroll
+    for (int j = 0; j < TL::TN; ++j) {
+        const int n = n0 + wc * TL::WTN + j * 32 + (lane & 31);
+        if (n >= Ctot) continue;
+        const int co = a.up2 ? n % a.Cpo : n;
+        const int q = a.up2 ? n / a.Cpo : 0;
+        const float sc = a.scale[co], sh = a.shift[co];
+#pragma unroll
+        for (int i = 0; i < TL::TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wr * TL::WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (m >= M) continue;
+                size_t o;
+                if (a.up2) {
+                    const int HW = a.H * a.W;
+                    const int img = m / HW, rr = m - img * HW;
+                    const int y = 2 * (rr / a.W) + (q >> 1), x = 2 * (rr % a.W) + (q & 1);
+                    o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
+                } else {
+                    o = (size_t)m * a.Cpo + co;
+                }
+                float v = acc[i][j][r] * sc + sh;
+                if (a.res_pre) v = v + a.res_pre[o];
+                if (a.relu) v = fmaxf(v, 0.0f);
+                if (a.res_post) v = v + a.res_post[o];
+                a.out[o] = v;
+            }
+        }
+    }
+}
 
 // 2x2 / stride-2 max pool, NHWC (F.max_pool2d(x, 2, 2), cnns_2d.py Pool2DBlock)
 __global__ __launch_bounds__(256) void maxpool2_kernel(const float *__restrict__ in, float *__restrict__ out, int N,
@@ -268,16 +448,37 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
         (KH & 1) == 0 || (KW & 1) == 0)
         return FVP_ERR_SHAPE;
     const int Ntot = upsample2 ? 4 * Cpo : Cpo;
-    if (Cpo_w < Ntot || Cpo_w % 64) return FVP_ERR_SHAPE;
+    if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
     const long long M = (long long)N * H * W;
     if (M * (upsample2 ? 4 : 1) * Cpo > 0x7fffffffLL * 4) return FVP_ERR_SHAPE;
     fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
     hipStream_t st = (hipStream_t)stream;
 #define FVP_CONV(TL)                                                                                              \
-    hipLaunchKernelGGL(fvp::conv_mfma_kernel<fvp::TL>,                                                            \
-                       dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM), (unsigned)((Ntot + fvp::TL::BN - 1) / \
-                                                                                      fvp::TL::BN)),          \
-                       dim3(256), 0, st, a)
+    do {                                                                                                          \
+        if (Cpi % fvp::TL::KC) return FVP_ERR_SHAPE;                                                              \
+        hipLaunchKernelGGL(fvp::conv_mfma_kernel<fvp::TL>,                                                        \
+                           dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                  \
+                                (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN)),                              \
+                           dim3(256), 0, st, a);                                                                 \
+    } while (0)
+    switch (fvp::g_force_tile) {  // tuning override (fvp_conv_set_tile)
+        case 1: FVP_CONV(TileN16); return (int)hipGetLastError();
+        case 2: FVP_CONV(TileN16s); return (int)hipGetLastError();
+        case 3: FVP_CONV(TileN32); return (int)hipGetLastError();
+        case 4: FVP_CONV(TileN32s); return (int)hipGetLastError();
+        case 5: FVP_CONV(TileN64); return (int)hipGetLastError();
+        case 6: FVP_CONV(TileN64m); return (int)hipGetLastError();
+        case 7: FVP_CONV(TileN64s); return (int)hipGetLastError();
+        case 8: FVP_CONV(TileX1); return (int)hipGetLastError();
+        case 9: FVP_CONV(TileX2); return (int)hipGetLastError();
+        case 10: FVP_CONV(TileX3); return (int)hipGetLastError();
+        case 11: FVP_CONV(TileX4); return (int)hipGetLastError();
+        case 12: FVP_CONV(TileX5); return (int)hipGetLastError();
+        case 13: FVP_CONV(TileX6); return (int)hipGetLastError();
+        case 14: FVP_CONV(TileX7); return (int)hipGetLastError();
+        case 15: FVP_CONV(TileX8); return (int)hipGetLastError();
+        default: break;
+    }
     auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long long)((Ntot + bn - 1) / bn); };
     const long long enough = 512;  // >= 2 blocks per CU
     if (Ntot <= 16) {
@@ -290,6 +491,37 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
         else FVP_CONV(TileN64s);
     }
 #undef FVP_CONV
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH,
+                                    int KW, int Cpo, int Cpo_w, const float *scale, const float *shift,
+                                    const float *res_pre, const float *res_post, int relu, int upsample2, float *out,
+                                    void *stream) {
+    if (!in || !wpack_bf16 || !scale || !shift || !out) return FVP_ERR_NULL;
+    if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
+        (KH & 1) == 0 || (KW & 1) == 0)
+        return FVP_ERR_SHAPE;
+    const int Ntot = upsample2 ? 4 * Cpo : Cpo;
+    if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
+    const long long M = (long long)N * H * W;
+    fvp::ConvArgs a{in, nullptr, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
+    const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack_bf16);
+    hipStream_t st = (hipStream_t)stream;
+#define FVP_CONVB(BM, BN, WR, KC)                                                                                 \
+    hipLaunchKernelGGL((fvp::conv_bf16_kernel<fvp::TileB<BM, BN, WR, KC>>),                                      \
+                       dim3((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN)), dim3(256), 0, st, a, \
+                       wb)
+    const bool k32 = Cpi % 32 == 0;
+    const long long b128 = ((M + 127) / 128) * ((Ntot + 63) / 64);
+    if (Ntot <= 32) {
+        if (k32) FVP_CONVB(128, 32, 4, 32); else FVP_CONVB(128, 32, 4, 16);
+    } else if (b128 >= 512) {
+        if (k32) FVP_CONVB(128, 64, 2, 32); else FVP_CONVB(128, 64, 2, 16);
+    } else {
+        if (k32) FVP_CONVB(64, 64, 2, 32); else FVP_CONVB(64, 64, 2, 16);
+    }
+#undef FVP_CONVB
     return (int)hipGetLastError();
 }
 

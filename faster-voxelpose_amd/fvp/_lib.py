@@ -59,6 +59,9 @@ SIGNATURES = {
     "fvp_fuse_poses": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fvp_conv2d_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv2d_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv_set_tile": [c_int],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -49,9 +49,10 @@ class Act:
 
 
 class ConvLayer:
-    """A Conv2d / ConvTranspose2d(k=2,s=2) with its following BatchNorm folded."""
+    """A Conv2d / ConvTranspose2d(k=2,s=2) with its following BatchNorm folded.
+    dtype torch.bfloat16: bf16 operands, fp32 accumulation (opt-in precision)."""
 
-    def __init__(self, conv, bn=None):
+    def __init__(self, conv, bn=None, dtype=torch.float32):
         dev = conv.weight.device
         w = conv.weight.detach().float()
         self.up2 = isinstance(conv, nn.ConvTranspose2d)
@@ -67,7 +68,7 @@ class ConvLayer:
         self.Cin, self.Cout = cin, cout
         self.Cpi, self.Cpo = _rup(cin, 16), _rup(cout, 16)
         ntot = 4 * self.Cpo if self.up2 else self.Cpo
-        self.Cpo_w = _rup(ntot, 64)
+        self.Cpo_w = _rup(ntot, 128)
         taps = self.KH * self.KW
         pack = torch.zeros((taps, self.Cpi, self.Cpo_w), dtype=torch.float32, device=dev)
         if self.up2:  # n = (dy*2+dx)*Cpo + co  <-  W[ci][co][dy][dx]
@@ -76,6 +77,9 @@ class ConvLayer:
         else:  # row (ky*KW+kx)*Cpi + ci  <-  W[co][ci][ky][kx]
             pack[:, :cin, :cout] = w.permute(2, 3, 1, 0).reshape(taps, cin, cout)
         self.wpack = pack.reshape(taps * self.Cpi, self.Cpo_w).contiguous()
+        self.bf16 = dtype == torch.bfloat16
+        if self.bf16:  # [Cpo_w][K], k contiguous
+            self.wpack_bf16 = self.wpack.t().contiguous().to(torch.bfloat16)
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
         if bn is not None:  # eval BatchNorm: (x - mean) / sqrt(var + eps) * gamma + beta
             s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
@@ -93,7 +97,8 @@ class ConvLayer:
         out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=torch.float32, device=x.t.device)
         for r in (res_pre, res_post):
             assert r is None or tuple(r.t.shape) == tuple(out.shape), (None if r is None else r.t.shape, out.shape)
-        _lib.call("fvp_conv2d_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wpack), self.KH, self.KW, self.Cpo,
+        fn, w = ("fvp_conv2d_nhwc_bf16", self.wpack_bf16) if self.bf16 else ("fvp_conv2d_nhwc", self.wpack)
+        _lib.call(fn, _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(w), self.KH, self.KW, self.Cpo,
                   self.Cpo_w, _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
                   _ptr(res_post.t) if res_post else None, int(relu), int(self.up2), _ptr(out), _stream(out))
         return Act(out, self.Cout)
@@ -124,7 +129,7 @@ def to_nchw(x: Act) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
-def _seq_convs(seq: nn.Sequential):
+def _seq_convs(seq: nn.Sequential, dtype=torch.float32):
     """[Conv(, BN)(, ReLU)]* of an nn.Sequential -> [(ConvLayer, relu)]."""
     mods = list(seq.children())
     out, i = [], 0
@@ -135,7 +140,7 @@ def _seq_convs(seq: nn.Sequential):
         bn = mods[i + 1] if i + 1 < len(mods) and isinstance(mods[i + 1], nn.BatchNorm2d) else None
         j = i + 1 + (bn is not None)
         relu = j < len(mods) and isinstance(mods[j], nn.ReLU)
-        out.append((ConvLayer(m, bn), relu))
+        out.append((ConvLayer(m, bn, dtype), relu))
         i = j + relu
     return out
 
@@ -143,28 +148,29 @@ def _seq_convs(seq: nn.Sequential):
 class _Plan:
     """A compiled module: call(x: Act) -> Act."""
 
-    def __init__(self, m: nn.Module):
+    def __init__(self, m: nn.Module, dtype=torch.float32):
+        self.dtype = dtype
         self.kind, self.parts = self._compile(m)
 
     def _compile(self, m):
         if hasattr(m, "res_branch"):  # Res2DBlock (cnns_2d.py:32-64)
-            (c1, r1), (c2, _) = _seq_convs(m.res_branch)
-            skip = _seq_convs(m.skip_con) if len(list(m.skip_con.children())) else []
+            (c1, r1), (c2, _) = _seq_convs(m.res_branch, self.dtype)
+            skip = _seq_convs(m.skip_con, self.dtype) if len(list(m.skip_con.children())) else []
             return "res", (c1, c2, skip[0][0] if skip else None)
         if hasattr(m, "pool_size"):  # Pool2DBlock
             assert m.pool_size == 2
             return "pool", None
         if hasattr(m, "block"):  # Basic2DBlock / Upsample2DBlock: Sequential(conv, BN, ReLU)
-            return "seq", _seq_convs(m.block)
+            return "seq", _seq_convs(m.block, self.dtype)
         if hasattr(m, "encoder_pool1") and hasattr(m, "skip_res1"):  # EncoderDecorder (:123-183)
             names = ["skip_res1", "encoder_pool1", "encoder_res1", "skip_res2", "encoder_pool2", "encoder_res2",
                      "mid_res", "decoder_res2", "decoder_upsample2", "decoder_res1", "decoder_upsample1"]
-            return "encdec", {n: _Plan(getattr(m, n)) for n in names}
+            return "encdec", {n: _Plan(getattr(m, n), self.dtype) for n in names}
         if isinstance(m, nn.Sequential):
             kids = list(m.children())
             if kids and all(isinstance(k, (nn.Conv2d, nn.ConvTranspose2d, nn.BatchNorm2d, nn.ReLU)) for k in kids):
-                return "seq", _seq_convs(m)
-            return "chain", [_Plan(k) for k in kids]
+                return "seq", _seq_convs(m, self.dtype)
+            return "chain", [_Plan(k, self.dtype) for k in kids]
         raise TypeError(f"FvpCNN: unsupported module {type(m).__name__}")
 
     def __call__(self, x: Act, res_post: Act | None = None) -> Act:
@@ -209,24 +215,27 @@ class FvpCNN:
     after its ``torch.max(x, dim=4)``, cnns_2d.py:291-295).  Weights are read
     once at construction; rebuild after loading a new state_dict."""
 
-    def __init__(self, module: nn.Module):
+    def __init__(self, module: nn.Module, dtype=torch.float32):
+        """dtype torch.bfloat16: bf16 operands with fp32 accumulation (opt-in; ~1e-2 relative)."""
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise _lib.FvpError(f"FvpCNN: dtype {dtype} (float32 or bfloat16)")
         if module.training:
             raise _lib.FvpError("FvpCNN: eval mode only (BatchNorm folded with running statistics)")
         self.module = module
         if hasattr(module, "output_hm") and hasattr(module, "output_size"):  # CenterNet
             self.kind = "centernet"
-            self.front = _Plan(module.front_layers)
-            self.encdec = _Plan(module.encoder_decoder)
-            self.hm = _seq_convs(module.output_hm)
-            self.size = _seq_convs(module.output_size)
+            self.front = _Plan(module.front_layers, dtype)
+            self.encdec = _Plan(module.encoder_decoder, dtype)
+            self.hm = _seq_convs(module.output_hm, dtype)
+            self.size = _seq_convs(module.output_size, dtype)
         elif hasattr(module, "output_layer"):  # P2PNet
             self.kind = "p2p"
-            self.front = _Plan(module.front_layers)
-            self.encdec = _Plan(module.encoder_decoder)
-            self.out = ConvLayer(module.output_layer)
+            self.front = _Plan(module.front_layers, dtype)
+            self.encdec = _Plan(module.encoder_decoder, dtype)
+            self.out = ConvLayer(module.output_layer, None, dtype)
         else:
             self.kind = "plain"
-            self.plan = _Plan(module)
+            self.plan = _Plan(module, dtype)
 
     @staticmethod
     def _run_seq(seq, x):
@@ -250,12 +259,12 @@ class FvpCNN:
         return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
 
 
-def cached(module: nn.Module) -> FvpCNN:
+def cached(module: nn.Module, dtype=torch.float32) -> FvpCNN:
     """FvpCNN for ``module``, rebuilt whenever its parameters or buffers change
     (storage or in-place version), e.g. after load_state_dict."""
-    sig = tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
+    sig = (dtype,) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
     hit = getattr(module, "_fvp_cnn", None)
     if hit is None or hit[0] != sig:
-        hit = (sig, FvpCNN(module))
+        hit = (sig, FvpCNN(module, dtype))
         object.__setattr__(module, "_fvp_cnn", hit)
     return hit[1]

@@ -30,15 +30,18 @@ from . import cnn as fvp_cnn
 from . import jln, project_individual, project_whole, proposal
 
 USE_FVP_CNN = False  # set by install(cnn=True)
+FVP_CNN_DTYPE = torch.float32
 
 
 def install(fused: bool = True, modules=None, cnn: bool = False) -> dict:
     """Patch the already-importable reference modules.  Returns what was patched.
 
     cnn=True (with fused=True): in eval mode the fused forwards run CenterNet and
-    P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of torch's."""
-    global USE_FVP_CNN
+    P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of torch's, in fp32;
+    cnn="bf16": bf16 operands with fp32 accumulation (opt-in, ~1e-2 relative)."""
+    global USE_FVP_CNN, FVP_CNN_DTYPE
     USE_FVP_CNN = bool(cnn)
+    FVP_CNN_DTYPE = torch.bfloat16 if cnn == "bf16" else torch.float32
     mods = modules if modules is not None else sys.modules
     patched = {}
 
@@ -73,7 +76,7 @@ def center_net_from_xy(center_net, xy: torch.Tensor):
     """CenterNet.forward (cnns_2d.py:280-295) minus its first line, fed with
     the xy max-plane the voxelize kernel already produced."""
     if USE_FVP_CNN and not center_net.training:
-        return fvp_cnn.cached(center_net).from_xy(xy)
+        return fvp_cnn.cached(center_net, FVP_CNN_DTYPE).from_xy(xy)
     x = center_net.front_layers(xy)
     x = center_net.encoder_decoder(x)
     return center_net.output_hm(x), center_net.output_size(x)

@@ -206,12 +206,21 @@ int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob
  * upsample2 != 0: ConvTranspose2d(k=2, s=2) as a 1x1 conv with 4*Cpo packed
  * outputs n = (dy*2+dx)*Cpo + co, scattered to the 2H x 2W output.
  *   in        device [N][H][W][Cpi], Cpi % 16 == 0 (padding channels zero)
- *   wpack     device [KH*KW*Cpi][Cpo_w], row (ky*KW+kx)*Cpi+ci, Cpo_w % 64 == 0
+ *   wpack     device [KH*KW*Cpi][Cpo_w], row (ky*KW+kx)*Cpi+ci, Cpo_w % 128 == 0
  *   scale, shift device [Cpo];  res_pre, res_post device [N][Ho][Wo][Cpo] or NULL
  *   out       device [N][Ho][Wo][Cpo], Cpo % 16 == 0 */
 int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                     int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                     const float *res_post, int relu, int upsample2, float *out, void *stream);
+/* Same convolution with bf16 operands (opt-in precision): activations are
+ * rounded to bf16 when staged, weights given as bf16 [Cpo_w][KH*KW*Cpi]
+ * (output-channel major), products accumulated in fp32 on
+ * v_mfma_f32_32x32x16_bf16.  Other arguments as fvp_conv2d_nhwc. */
+int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH, int KW,
+                         int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                         const float *res_post, int relu, int upsample2, float *out, void *stream);
+/* Tuning hook: 0 = tile chosen per layer (default); 1..15 force one tile shape. */
+int fvp_conv_set_tile(int id);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
 int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);
 /* NCHW [N][C][H][W] <-> NHWC [N][H][W][Cp] (Cp >= C, padding channels zero). */

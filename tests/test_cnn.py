@@ -129,3 +129,39 @@ def test_fvp_cnn_large_batch_tiles_vs_torch(gpu_device):
         ref = p2p(x)
     got = FvpCNN(p2p)(x)
     _close(got.cpu().numpy(), ref.cpu().numpy(), "P2PNet, 24 images")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,hw,up", [(15, 16, 7, (64, 64), False), (32, 32, 3, (33, 17), False),
+                                              (128, 128, 3, (16, 16), False), (64, 32, 2, (9, 7), True)])
+def test_bf16_conv_layer_vs_torch(gpu_device, cin, cout, k, hw, up):
+    """Opt-in bf16 operands (fp32 accumulation): within 2e-2 of the output scale
+    of torch's fp32 convolution (bf16 keeps 8 mantissa bits)."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    conv = nn.ConvTranspose2d(cin, cout, 2, stride=2) if up else nn.Conv2d(cin, cout, k, padding=(k - 1) // 2)
+    seq = nn.Sequential(conv, nn.BatchNorm2d(cout)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin * 7 + cout))
+    seq = seq.to(gpu_device)
+    x = torch.rand((3, cin) + hw, generator=torch.Generator().manual_seed(k)).to(gpu_device)
+    with torch.no_grad():
+        ref = torch.relu(seq(x))
+    layer = cnn.ConvLayer(seq[0], seq[1], torch.bfloat16)
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True))
+    err = float((got - ref).abs().max()) / float(ref.abs().max())
+    assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
+def test_bf16_p2pnet_vs_reference(gpu_device):
+    """Whole P2PNet with bf16 operands against the reference's fp32 golden:
+    within 5e-2 of the output scale (errors compound over 20 convolutions)."""
+    from fvp.cnn import FvpCNN
+
+    d = golden("cnn.npz")
+    p2p, _, x_p2p, _ = _nets()
+    y = FvpCNN(p2p.to(gpu_device), torch.bfloat16)(torch.from_numpy(x_p2p).to(gpu_device))
+    err = float(np.abs(y.cpu().numpy() - d["y_p2p"]).max()) / float(np.abs(d["y_p2p"]).max())
+    assert err <= 5e-2, err

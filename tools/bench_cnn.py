@@ -41,6 +41,7 @@ def main():
     x_jln = torch.rand((3 * args.proposals, J, 64, 64), generator=g).to(dev)
     x_hdn = torch.rand((args.frames, J, 80, 80), generator=g).to(dev)
     f_p2p, f_cn = cnn.FvpCNN(p2p), cnn.FvpCNN(cn)
+    b_p2p, b_cn = cnn.FvpCNN(p2p, torch.bfloat16), cnn.FvpCNN(cn, torch.bfloat16)
 
     def flops(plan_net, x):
         # count with the fvp layer descriptions: 2*M*N*K per conv
@@ -75,16 +76,19 @@ def main():
 
     out = {}
     with torch.no_grad():
-        for name, fv, tv, x in (("p2pnet_jln", lambda: f_p2p(x_jln), lambda: p2p(x_jln), x_jln),
-                                ("centernet_hdn", lambda: f_cn.from_xy(x_hdn),
-                                 lambda: (cn.output_hm(cn.encoder_decoder(cn.front_layers(x_hdn))),), x_hdn)):
+        for name, fv, bv, tv, x in (("p2pnet_jln", lambda: f_p2p(x_jln), lambda: b_p2p(x_jln), lambda: p2p(x_jln),
+                                     x_jln),
+                                    ("centernet_hdn", lambda: f_cn.from_xy(x_hdn), lambda: b_cn.from_xy(x_hdn),
+                                     lambda: (cn.output_hm(cn.encoder_decoder(cn.front_layers(x_hdn))),), x_hdn)):
             fl = flops(f_p2p if name.startswith("p2p") else (lambda t: f_cn.from_xy(t)), x)
-            t_f, t_t = timeit(fv), timeit(tv)
+            t_f, t_t, t_b = timeit(fv), timeit(tv), timeit(bv)
             out[name] = {"images": int(x.shape[0]), "shape": list(x.shape[1:]), "gflop": round(fl / 1e9, 3),
                          "fvp_ms": round(t_f, 4), "torch_ms": round(t_t, 4),
                          "fvp_tflops": round(fl / (t_f * 1e-3) / 1e12, 2),
                          "mfma_frac_of_f32_peak": round(fl / (t_f * 1e-3) / 1e12 / MFMA_F32_PEAK_TF, 4),
-                         "speedup_vs_torch": round(t_t / t_f, 3)}
+                         "speedup_vs_torch": round(t_t / t_f, 3),
+                         "bf16_ms": round(t_b, 4), "bf16_tflops": round(fl / (t_b * 1e-3) / 1e12, 2),
+                         "bf16_frac_of_bf16_peak": round(fl / (t_b * 1e-3) / 1e12 / 2500.0, 4)}
     print(json.dumps({"metric": "HDN/JLN CNNs on fp32 MFMA (implicit GEMM, folded BN)", "peak_tflops_f32": MFMA_F32_PEAK_TF,
                       "note": "torch_ms = the same eval module on torch's GPU convolution (MIOpen); torch centernet "
                               "time covers the same layers (hm head only)", **out}))

@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""End-to-end HDN + JLN inference after the backbone, on fvp:
+heatmaps -> voxel cube + xy plane -> CenterNet -> NMS top-K -> bbox / z-column
+gathers -> C2CNet -> proposals -> per-person planes -> P2PNet -> soft-argmax +
+offsets -> WeightNet -> fusion, for B frames at C3 geometry.
+
+CenterNet / P2PNet run on the fvp MFMA convolutions (install(cnn=True)) with
+the reference architectures (tests/cnn_arch.py) and seeded weights; C2CNet and
+WeightNet are small torch stand-ins with the reference's I/O (they are ~0.1 %
+of the FLOPs).  Reports frames/s and a per-stage breakdown (HIP events).
+
+    python tools/bench_pipeline.py [--frames 8] [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import types
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--torch-cnn", action="store_true", help="CNNs on torch's convolution instead of fvp")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import torch.nn as nn
+
+    import cnn_arch
+    from fvp import geometry, integration, jln, synthetic
+    from fvp.config import AttrDict
+    from fvp.project_individual import ProjectLayer as PI
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    dev = torch.device("cuda:0")
+    w = WORKLOADS[args.workload]
+    J, B, K = w.num_joints, args.frames, w.max_people
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, B)).to(dev)
+    meta = {"seq": [seq] * B}
+
+    class Proposal(nn.Module):  # test-mode ProposalLayer (human_detection_net.py:99-124)
+        def forward(self, topk_index, topk_confs, match_bbox, meta):
+            scale = torch.tensor(w.space_size, device=dev) / (torch.tensor(w.voxels_per_axis, device=dev) - 1)
+            bias = torch.tensor(w.space_center, device=dev) - torch.tensor(w.space_size, device=dev) / 2.0
+            out = torch.zeros(topk_confs.shape + (7,), device=dev)
+            out[:, :, 0:3] = topk_index.float() * scale + bias
+            out[:, :, 4] = topk_confs
+            out[:, :, 3] = 0.0  # every proposal valid: the JLN runs at full K (stand-in confidences)
+            out[:, :, 5:7] = match_bbox.clamp(0.3, 0.8)
+            return out
+
+    class WeightNet(nn.Module):  # I/O of weight_net.py:48-80
+        def __init__(self):
+            super().__init__()
+            self.lin = nn.Linear(1, 1)
+
+        def forward(self, x):
+            x = torch.flatten(x, 0, 1)
+            return torch.sigmoid(self.lin(x.mean(dim=(2, 3)).reshape(-1, 1))).view(x.shape[0], J, 1)
+
+    hdn = types.SimpleNamespace(max_people=K)
+    hdn.project_layer = ProjectLayer(w.cfg(str(dev)))
+    hdn.project_layer.verbose = False
+    hdn.center_net = cnn_arch.CenterNet(J, 1).eval()
+    hdn.center_net.load_state_dict(synthetic.seeded_state_dict(hdn.center_net, 12))
+    hdn.center_net = hdn.center_net.to(dev)
+    hdn.c2c_net = nn.Sequential(nn.Conv1d(J, 32, 3, padding=1), nn.ReLU(), nn.Conv1d(32, 1, 1)).to(dev).eval()
+    hdn.proposal_layer = Proposal()
+    jl = types.SimpleNamespace(training=False)
+    jl.project_layer = PI(w.cfg(str(dev)))
+    jl.project_layer.verbose = False
+    jl.conv_net = cnn_arch.P2PNet(J, J).eval()
+    jl.conv_net.load_state_dict(synthetic.seeded_state_dict(jl.conv_net, 11))
+    jl.conv_net = jl.conv_net.to(dev)
+    jl.weight_net = WeightNet().to(dev).eval()
+    jl.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
+    integration.USE_FVP_CNN = not args.torch_cnn
+
+    def step(record=None):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if record is not None else None
+        if ev:
+            ev[0].record()
+        _, _, centers, _ = integration.fused_hdn_forward(hdn, hm, meta, cams, rt)
+        if ev:
+            ev[1].record()
+        mask = centers[:, :, 3] >= 0
+        fused, _ = jln.fused_jln_forward(jl, meta, hm, centers, mask, cams, rt)
+        if ev:
+            ev[2].record()
+            record.append(ev)
+        return fused
+
+    with torch.no_grad():
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        evs = []
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            step(evs)
+        e1.record()
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    hdn_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    jln_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    print(json.dumps({
+        "metric": "HDN+JLN inference after the backbone (heatmaps -> fused 3-D poses)", "unit": "frames/s",
+        "value": round(B / (ms * 1e-3), 1), "ms_per_batch": round(ms, 3), "frames": B, "proposals_per_frame": K,
+        "hdn_ms": round(hdn_ms, 3), "jln_ms": round(jln_ms, 3),
+        "cnn": "torch (MIOpen)" if args.torch_cnn else "fvp fp32 MFMA",
+        "config": f"{w.name}: {len(cams[seq])} cams, J={J}, {w.voxels_per_axis} whole grid, 64^3 per person; "
+                  "CenterNet/P2PNet reference architectures with seeded weights, C2CNet/WeightNet small stand-ins"}))
+
+
+if __name__ == "__main__":
+    main()

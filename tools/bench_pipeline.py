@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--torch-cnn", action="store_true", help="CNNs on torch's convolution instead of fvp")
+    ap.add_argument("--bf16", action="store_true", help="fvp CNNs with bf16 operands (opt-in precision)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -86,6 +87,7 @@ def main():
     jl.weight_net = WeightNet().to(dev).eval()
     jl.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
     integration.USE_FVP_CNN = not args.torch_cnn
+    integration.FVP_CNN_DTYPE = torch.bfloat16 if args.bf16 else torch.float32
 
     def step(record=None):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if record is not None else None
@@ -119,7 +121,7 @@ def main():
         "metric": "HDN+JLN inference after the backbone (heatmaps -> fused 3-D poses)", "unit": "frames/s",
         "value": round(B / (ms * 1e-3), 1), "ms_per_batch": round(ms, 3), "frames": B, "proposals_per_frame": K,
         "hdn_ms": round(hdn_ms, 3), "jln_ms": round(jln_ms, 3),
-        "cnn": "torch (MIOpen)" if args.torch_cnn else "fvp fp32 MFMA",
+        "cnn": "torch (MIOpen)" if args.torch_cnn else ("fvp bf16 MFMA" if args.bf16 else "fvp fp32 MFMA"),
         "config": f"{w.name}: {len(cams[seq])} cams, J={J}, {w.voxels_per_axis} whole grid, 64^3 per person; "
                   "CenterNet/P2PNet reference architectures with seeded weights, C2CNet/WeightNet small stand-ins"}))
 

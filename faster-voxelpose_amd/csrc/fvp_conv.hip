@@ -179,8 +179,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     }
 
     // epilogue: lane -> column (output channel), registers -> rows (pixels)
-    const int Ctot = a.up2 ? 4 * a.Cpo : a.Cpo;
-    const int Ho = a.up2 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
+    // up2: 1 = ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1 rows (1x2 scatter)
+    const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
+    const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
 #pragma unroll
     for (int j = 0; j < TL::TN; ++j) {
         const int n = n0 + wc * TL::WTN + j * MS + (lane % MS);
@@ -199,7 +200,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                 if (a.up2) {
                     const int HW = a.H * a.W;
                     const int img = m / HW, rr = m - img * HW;
-                    const int y = 2 * (rr / a.W) + (q >> 1), x = 2 * (rr % a.W) + (q & 1);
+                    const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
+                    const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
                     o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
                 } else {
                     o = (size_t)m * a.Cpo + co;
@@ -355,8 +357,9 @@ __global__ __launch_bounds__(256) void conv_bf16_kernel(ConvArgs a, const __bf16
         }
     }
 
-    const int Ctot = a.up2 ? 4 * a.Cpo : a.Cpo;
-    const int Ho = a.up2 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
+    // up2: 1 = ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1 rows (1x2 scatter)
+    const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
+    const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
 #pragma unroll
     for (int j = 0; j < TL::TN; ++j) {
         const int n = n0 + wc * TL::WTN + j * 32 + (lane & 31);
@@ -374,7 +377,8 @@ __global__ __launch_bounds__(256) void conv_bf16_kernel(ConvArgs a, const __bf16
                 if (a.up2) {
                     const int HW = a.H * a.W;
                     const int img = m / HW, rr = m - img * HW;
-                    const int y = 2 * (rr / a.W) + (q >> 1), x = 2 * (rr % a.W) + (q & 1);
+                    const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
+                    const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
                     o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
                 } else {
                     o = (size_t)m * a.Cpo + co;
@@ -389,10 +393,12 @@ __global__ __launch_bounds__(256) void conv_bf16_kernel(ConvArgs a, const __bf16
     }
 }
 
-// 2x2 / stride-2 max pool, NHWC (F.max_pool2d(x, 2, 2), cnns_2d.py Pool2DBlock)
-__global__ __launch_bounds__(256) void maxpool2_kernel(const float *__restrict__ in, float *__restrict__ out, int N,
-                                                       int H, int W, int C) {
-    const int Ho = H / 2, Wo = W / 2;
+// KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
+// cnns_2d.py Pool2DBlock; F.max_pool1d(x, 2, 2) on H == 1 rows, cnns_1d.py Pool1DBlock)
+template <int KH, int KW>
+__global__ __launch_bounds__(256) void maxpool_kernel(const float *__restrict__ in, float *__restrict__ out, int N,
+                                                      int H, int W, int C) {
+    const int Ho = H / KH, Wo = W / KW;
     const long long total = (long long)N * Ho * Wo * (C / 4);
     const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
     if (gid >= total) return;
@@ -402,14 +408,20 @@ __global__ __launch_bounds__(256) void maxpool2_kernel(const float *__restrict__
     r /= Wo;
     const int y = (int)(r % Ho);
     const long long img = r / Ho;
-    const float4 *p = reinterpret_cast<const float4 *>(in + (((size_t)img * H + 2 * y) * W + 2 * x) * C) + c4;
+    const float4 *p = reinterpret_cast<const float4 *>(in + (((size_t)img * H + KH * y) * W + KW * x) * C) + c4;
     const size_t rs = (size_t)W * C / 4;
-    const float4 a = p[0], b = p[C / 4], c = p[rs], d = p[rs + C / 4];
-    float4 m;
-    m.x = nanmax(nanmax(a.x, b.x), nanmax(c.x, d.x));
-    m.y = nanmax(nanmax(a.y, b.y), nanmax(c.y, d.y));
-    m.z = nanmax(nanmax(a.z, b.z), nanmax(c.z, d.z));
-    m.w = nanmax(nanmax(a.w, b.w), nanmax(c.w, d.w));
+    float4 m = p[0];
+    auto mx = [&](const float4 b) {
+        m.x = nanmax(m.x, b.x);
+        m.y = nanmax(m.y, b.y);
+        m.z = nanmax(m.z, b.z);
+        m.w = nanmax(m.w, b.w);
+    };
+    if (KW == 2) mx(p[C / 4]);
+    if (KH == 2) {
+        mx(p[rs]);
+        if (KW == 2) mx(p[rs + C / 4]);
+    }
     reinterpret_cast<float4 *>(out)[gid] = m;
 }
 
@@ -447,10 +459,11 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
         (KH & 1) == 0 || (KW & 1) == 0)
         return FVP_ERR_SHAPE;
-    const int Ntot = upsample2 ? 4 * Cpo : Cpo;
+    if (upsample2 < 0 || upsample2 > 2) return FVP_ERR_SHAPE;
+    const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
     if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
     const long long M = (long long)N * H * W;
-    if (M * (upsample2 ? 4 : 1) * Cpo > 0x7fffffffLL * 4) return FVP_ERR_SHAPE;
+    if (M * Ntot > 0x7fffffffLL * 4) return FVP_ERR_SHAPE;
     fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
     hipStream_t st = (hipStream_t)stream;
 #define FVP_CONV(TL)                                                                                              \
@@ -502,7 +515,8 @@ extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cp
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
         (KH & 1) == 0 || (KW & 1) == 0)
         return FVP_ERR_SHAPE;
-    const int Ntot = upsample2 ? 4 * Cpo : Cpo;
+    if (upsample2 < 0 || upsample2 > 2) return FVP_ERR_SHAPE;
+    const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
     if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
     const long long M = (long long)N * H * W;
     fvp::ConvArgs a{in, nullptr, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
@@ -525,13 +539,23 @@ extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cp
     return (int)hipGetLastError();
 }
 
-extern "C" int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream) {
+extern "C" int fvp_maxpool_nhwc(const float *in, int N, int H, int W, int C, int KH, int KW, float *out,
+                                void *stream) {
     if (!in || !out) return FVP_ERR_NULL;
-    if (N <= 0 || H < 2 || W < 2 || C <= 0 || C % 4) return FVP_ERR_SHAPE;
-    const long long total = (long long)N * (H / 2) * (W / 2) * (C / 4);
-    hipLaunchKernelGGL(fvp::maxpool2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       in, out, N, H, W, C);
+    if (KH < 1 || KH > 2 || KW < 1 || KW > 2) return FVP_ERR_SHAPE;
+    if (N <= 0 || H < KH || W < KW || C <= 0 || C % 4) return FVP_ERR_SHAPE;
+    const long long total = (long long)N * (H / KH) * (W / KW) * (C / 4);
+    const dim3 g((unsigned)((total + 255) / 256)), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (KH == 2 && KW == 2) hipLaunchKernelGGL((fvp::maxpool_kernel<2, 2>), g, b, 0, st, in, out, N, H, W, C);
+    else if (KH == 1 && KW == 2) hipLaunchKernelGGL((fvp::maxpool_kernel<1, 2>), g, b, 0, st, in, out, N, H, W, C);
+    else if (KH == 2) hipLaunchKernelGGL((fvp::maxpool_kernel<2, 1>), g, b, 0, st, in, out, N, H, W, C);
+    else hipLaunchKernelGGL((fvp::maxpool_kernel<1, 1>), g, b, 0, st, in, out, N, H, W, C);
     return (int)hipGetLastError();
+}
+
+extern "C" int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream) {
+    return fvp_maxpool_nhwc(in, N, H, W, C, 2, 2, out, stream);
 }
 
 extern "C" int fvp_nchw_to_nhwc(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream) {

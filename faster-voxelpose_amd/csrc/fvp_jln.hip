@@ -129,6 +129,90 @@ __global__ __launch_bounds__(64) void fuse_kernel(const float *__restrict__ pose
     }
 }
 
+
+// ---- WeightNet (weight_net.py:48-80): one block per joint map ---------------
+// x [Nimg][H][W] (the [3P][J] joint maps, flattened as at weight_net.py:65-68)
+//   -> conv3x3(1 -> C, pad 1) * scale + shift (conv bias and BatchNorm folded)
+//   -> max_pool 2x2 (floor) -> ReLU -> mean over the pooled map
+//   -> Linear(C -> Hd) -> ReLU -> Linear(Hd -> 1) -> sigmoid      -> out [Nimg]
+// The [C][H][W] conv map the reference materialises (23.6 MB per proposal at
+// 64x64, C = 32) never leaves registers: each thread owns pooled cells, reads
+// their 4x4 input patch from the LDS copy of the map and keeps C running sums.
+template <int CMAX>
+__global__ __launch_bounds__(256) void weight_net_kernel(const float *__restrict__ x, int H, int W,
+                                                         const float *__restrict__ cw, const float *__restrict__ scale,
+                                                         const float *__restrict__ shift, int C,
+                                                         const float *__restrict__ w1, const float *__restrict__ b1,
+                                                         int Hd, const float *__restrict__ w2,
+                                                         const float *__restrict__ b2, float *__restrict__ out) {
+    extern __shared__ float smem[];  // [(H+2)*(W+2)] zero-padded map | [4][CMAX] wave sums | [CMAX] means | [4]
+    const int Wp = W + 2;
+    const float *__restrict__ img = x + (size_t)blockIdx.x * H * W;
+    for (int i = threadIdx.x; i < (H + 2) * Wp; i += 256) {
+        const int yy = i / Wp - 1, xx = i - (yy + 1) * Wp - 1;
+        smem[i] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? img[yy * W + xx] : 0.0f;
+    }
+    __syncthreads();
+    float acc[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[c] = 0.0f;
+    const int Ho = H / 2, Wo = W / 2;
+    for (int p = threadIdx.x; p < Ho * Wo; p += 256) {
+        const int py = p / Wo, px = p - py * Wo;
+        float t[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[r][q] = smem[(2 * py + r) * Wp + 2 * px + q];
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
+            if (c < C) {  // uniform: the weights come in through scalar loads
+                float k[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) k[i] = cw[c * 9 + i];
+                const float sc = scale[c], sh = shift[c];
+                float m = 0.0f;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int dy = d >> 1, dx = d & 1;
+                    float v = 0.0f;
+#pragma unroll
+                    for (int i = 0; i < 9; ++i) v = fmaf(k[i], t[dy + i / 3][dx + i % 3], v);
+                    v = v * sc + sh;
+                    m = d == 0 ? v : nanmax(m, v);
+                }
+                acc[c] += m < 0.0f ? 0.0f : m;  // ReLU after the pool; NaN passes through as in torch
+            }
+        }
+    }
+    float *wsum = smem + (H + 2) * Wp, *mean = wsum + 4 * CMAX, *red = mean + CMAX;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+        if (c < C) {
+            float v = acc[c];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) wsum[wave * CMAX + c] = v;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < C) {
+        const int c = threadIdx.x;
+        mean[c] = ((wsum[c] + wsum[CMAX + c]) + (wsum[2 * CMAX + c] + wsum[3 * CMAX + c])) / (float)(Ho * Wo);
+    }
+    __syncthreads();
+    float part = 0.0f;
+    for (int h = threadIdx.x; h < Hd; h += 256) {
+        float z = 0.0f;
+        for (int c = 0; c < C; ++c) z = fmaf(w1[(size_t)h * C + c], mean[c], z);
+        z += b1[h];
+        part = fmaf(w2[h], z < 0.0f ? 0.0f : z, part);
+    }
+    part = block_reduce_sum(part, red);
+    if (threadIdx.x == 0) out[blockIdx.x] = 1.0f / (1.0f + expf(-(part + b2[0])));
+}
+
 }  // namespace fvp
 
 extern "C" int fvp_soft_argmax(const float *features, int P, int J, int S2, const float *center_grid,
@@ -155,5 +239,25 @@ extern "C" int fvp_fuse_poses(const float *pose, const float *weights, const flo
     if (P < 0 || J <= 0) return FVP_ERR_SHAPE;
     hipLaunchKernelGGL(fvp::fuse_kernel, dim3((unsigned)P), dim3(64), 0, (hipStream_t)stream, pose, weights, maxprob,
                        P, J, fused, confs);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_weight_net(const float *features, int Nimg, int H, int W, const float *conv_w,
+                              const float *scale, const float *shift, int C, const float *fc1_w, const float *fc1_b,
+                              int Hd, const float *fc2_w, const float *fc2_b, float *out, void *stream) {
+    if (Nimg == 0) return FVP_OK;
+    if (!features || !conv_w || !scale || !shift || !fc1_w || !fc1_b || !fc2_w || !fc2_b || !out)
+        return FVP_ERR_NULL;
+    if (Nimg < 0 || H < 2 || W < 2 || C <= 0 || C > 64 || Hd <= 0) return FVP_ERR_SHAPE;
+    const int cmax = C <= 32 ? 32 : 64;
+    const size_t lds = ((size_t)(H + 2) * (W + 2) + 5 * cmax + 4) * sizeof(float);
+    if (lds > 64 * 1024) return FVP_ERR_SHAPE;  // maps up to ~124x124
+    hipStream_t st = (hipStream_t)stream;
+    if (cmax == 32)
+        hipLaunchKernelGGL(fvp::weight_net_kernel<32>, dim3((unsigned)Nimg), dim3(256), lds, st, features, H, W,
+                           conv_w, scale, shift, C, fc1_w, fc1_b, Hd, fc2_w, fc2_b, out);
+    else
+        hipLaunchKernelGGL(fvp::weight_net_kernel<64>, dim3((unsigned)Nimg), dim3(256), lds, st, features, H, W,
+                           conv_w, scale, shift, C, fc1_w, fc1_b, Hd, fc2_w, fc2_b, out);
     return (int)hipGetLastError();
 }

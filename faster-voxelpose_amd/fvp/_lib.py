@@ -63,11 +63,14 @@ SIGNATURES = {
                              c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv_set_tile": [c_int],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_maxpool_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_weight_net": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _LIB = None
 
 

@@ -8,9 +8,13 @@
 BatchNorm folded with the conv bias into a per-channel scale/shift, the
 Res2DBlock residual add and the ReLU fused into the conv epilogue, the
 decoder's skip adds fused after the ReLU, ConvTranspose2d(2, 2) as a 1x1 conv
-with a 2x scatter epilogue.  Modules are recognised by the reference's
-attribute names, so the reference's own instances (and their state_dicts) are
-used directly.  Eval mode only (BatchNorm with running statistics).
+with a 2x scatter epilogue.  The 1-D ``C2CNet`` (cnns_1d.py:182-241, same
+block structure with Conv1d / BatchNorm1d / max_pool1d / ConvTranspose1d) runs
+on the same kernels as rows of height 1.  Modules are recognised by the
+reference's attribute names, so the reference's own instances (and their
+state_dicts) are used directly.  Eval mode only (BatchNorm with running
+statistics).  :class:`FvpWeightNet` runs ``WeightNet`` (weight_net.py:48-80) as
+one fused launch.
 """
 from __future__ import annotations
 
@@ -55,25 +59,33 @@ class ConvLayer:
     def __init__(self, conv, bn=None, dtype=torch.float32):
         dev = conv.weight.device
         w = conv.weight.detach().float()
-        self.up2 = isinstance(conv, nn.ConvTranspose2d)
-        if self.up2:
-            assert tuple(conv.kernel_size) == (2, 2) and tuple(conv.stride) == (2, 2) and tuple(conv.padding) == (0, 0)
+        if isinstance(conv, (nn.Conv1d, nn.ConvTranspose1d)):  # 1-D: rows of height 1, kernel (1, k)
+            w = w.unsqueeze(2)
+            ks, st, pad = (1,) + tuple(conv.kernel_size), (1,) + tuple(conv.stride), (0,) + tuple(conv.padding)
+        else:
+            ks, st, pad = tuple(conv.kernel_size), tuple(conv.stride), tuple(conv.padding)
+        self.up2 = 0
+        if isinstance(conv, (nn.ConvTranspose2d, nn.ConvTranspose1d)):
+            self.up2 = 2 if isinstance(conv, nn.ConvTranspose1d) else 1
+            assert ks[1:] == (2,) and st[1:] == (2,) and pad == (0, 0) and ks[0] == st[0] == 3 - self.up2, (ks, st, pad)
+            assert tuple(conv.output_padding) in ((0,), (0, 0)) and conv.groups == 1
             cin, cout = w.shape[0], w.shape[1]
             self.KH = self.KW = 1
         else:
-            assert tuple(conv.stride) == (1, 1) and conv.groups == 1 and tuple(conv.dilation) == (1, 1)
+            assert st == (1, 1) and conv.groups == 1 and tuple(conv.dilation) in ((1,), (1, 1))
             cout, cin, kh, kw = w.shape
-            assert tuple(conv.padding) == ((kh - 1) // 2, (kw - 1) // 2) and kh % 2 == 1 and kw % 2 == 1
+            assert pad == ((kh - 1) // 2, (kw - 1) // 2) and kh % 2 == 1 and kw % 2 == 1, (pad, kh, kw)
             self.KH, self.KW = kh, kw
         self.Cin, self.Cout = cin, cout
         self.Cpi, self.Cpo = _rup(cin, 16), _rup(cout, 16)
-        ntot = 4 * self.Cpo if self.up2 else self.Cpo
-        self.Cpo_w = _rup(ntot, 128)
+        self.nq = (1, 4, 2)[self.up2]  # outputs per input pixel
+        self.Cpo_w = _rup(self.nq * self.Cpo, 128)
         taps = self.KH * self.KW
         pack = torch.zeros((taps, self.Cpi, self.Cpo_w), dtype=torch.float32, device=dev)
-        if self.up2:  # n = (dy*2+dx)*Cpo + co  <-  W[ci][co][dy][dx]
-            for q in range(4):
-                pack[0, :cin, q * self.Cpo:q * self.Cpo + cout] = w[:, :, q >> 1, q & 1]
+        if self.up2:  # n = (dy*2+dx)*Cpo + co (2-D) or dx*Cpo + co (1-D)  <-  W[ci][co][dy][dx]
+            for q in range(self.nq):
+                dy, dx = (q >> 1, q & 1) if self.up2 == 1 else (0, q)
+                pack[0, :cin, q * self.Cpo:q * self.Cpo + cout] = w[:, :, dy, dx]
         else:  # row (ky*KW+kx)*Cpi + ci  <-  W[co][ci][ky][kx]
             pack[:, :cin, :cout] = w.permute(2, 3, 1, 0).reshape(taps, cin, cout)
         self.wpack = pack.reshape(taps * self.Cpi, self.Cpo_w).contiguous()
@@ -93,24 +105,26 @@ class ConvLayer:
 
     def __call__(self, x: Act, relu: bool, res_pre: Act | None = None, res_post: Act | None = None) -> Act:
         assert x.Cp == self.Cpi, (x.Cp, self.Cpi)
-        Ho, Wo = (2 * x.H, 2 * x.W) if self.up2 else (x.H, x.W)
+        Ho, Wo = (2 * x.H if self.up2 == 1 else x.H), (2 * x.W if self.up2 else x.W)
         out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=torch.float32, device=x.t.device)
         for r in (res_pre, res_post):
             assert r is None or tuple(r.t.shape) == tuple(out.shape), (None if r is None else r.t.shape, out.shape)
         fn, w = ("fvp_conv2d_nhwc_bf16", self.wpack_bf16) if self.bf16 else ("fvp_conv2d_nhwc", self.wpack)
         _lib.call(fn, _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(w), self.KH, self.KW, self.Cpo,
                   self.Cpo_w, _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
-                  _ptr(res_post.t) if res_post else None, int(relu), int(self.up2), _ptr(out), _stream(out))
+                  _ptr(res_post.t) if res_post else None, int(relu), self.up2, _ptr(out), _stream(out))
         return Act(out, self.Cout)
 
     def flops(self, x: Act) -> int:
-        n = 4 * self.Cout if self.up2 else self.Cout
+        n = self.nq * self.Cout
         return 2 * x.N * x.H * x.W * n * self.Cin * self.KH * self.KW
 
 
-def maxpool2(x: Act) -> Act:
-    out = torch.empty((x.N, x.H // 2, x.W // 2, x.Cp), dtype=torch.float32, device=x.t.device)
-    _lib.call("fvp_maxpool2_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(out), _stream(out))
+def maxpool2(x: Act, dim: int = 2) -> Act:
+    """max_pool2d(x, 2, 2) (dim 2) or max_pool1d(x, 2, 2) along W (dim 1)."""
+    kh = 2 if dim == 2 else 1
+    out = torch.empty((x.N, x.H // kh, x.W // 2, x.Cp), dtype=torch.float32, device=x.t.device)
+    _lib.call("fvp_maxpool_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, kh, 2, _ptr(out), _stream(out))
     return Act(out, x.C)
 
 
@@ -129,15 +143,19 @@ def to_nchw(x: Act) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------
+_CONVS = (nn.Conv2d, nn.ConvTranspose2d, nn.Conv1d, nn.ConvTranspose1d)
+_BNS = (nn.BatchNorm2d, nn.BatchNorm1d)
+
+
 def _seq_convs(seq: nn.Sequential, dtype=torch.float32):
     """[Conv(, BN)(, ReLU)]* of an nn.Sequential -> [(ConvLayer, relu)]."""
     mods = list(seq.children())
     out, i = [], 0
     while i < len(mods):
         m = mods[i]
-        if not isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+        if not isinstance(m, _CONVS):
             raise TypeError(f"FvpCNN: unsupported layer {type(m).__name__} in a Sequential")
-        bn = mods[i + 1] if i + 1 < len(mods) and isinstance(mods[i + 1], nn.BatchNorm2d) else None
+        bn = mods[i + 1] if i + 1 < len(mods) and isinstance(mods[i + 1], _BNS) else None
         j = i + 1 + (bn is not None)
         relu = j < len(mods) and isinstance(mods[j], nn.ReLU)
         out.append((ConvLayer(m, bn, dtype), relu))
@@ -148,12 +166,12 @@ def _seq_convs(seq: nn.Sequential, dtype=torch.float32):
 class _Plan:
     """A compiled module: call(x: Act) -> Act."""
 
-    def __init__(self, m: nn.Module, dtype=torch.float32):
-        self.dtype = dtype
+    def __init__(self, m: nn.Module, dtype=torch.float32, dim: int = 2):
+        self.dtype, self.dim = dtype, dim
         self.kind, self.parts = self._compile(m)
 
     def _compile(self, m):
-        if hasattr(m, "res_branch"):  # Res2DBlock (cnns_2d.py:32-64)
+        if hasattr(m, "res_branch"):  # Res2DBlock (cnns_2d.py:32-64) / Res1DBlock (cnns_1d.py:37-74)
             (c1, r1), (c2, _) = _seq_convs(m.res_branch, self.dtype)
             skip = _seq_convs(m.skip_con, self.dtype) if len(list(m.skip_con.children())) else []
             return "res", (c1, c2, skip[0][0] if skip else None)
@@ -165,12 +183,12 @@ class _Plan:
         if hasattr(m, "encoder_pool1") and hasattr(m, "skip_res1"):  # EncoderDecorder (:123-183)
             names = ["skip_res1", "encoder_pool1", "encoder_res1", "skip_res2", "encoder_pool2", "encoder_res2",
                      "mid_res", "decoder_res2", "decoder_upsample2", "decoder_res1", "decoder_upsample1"]
-            return "encdec", {n: _Plan(getattr(m, n), self.dtype) for n in names}
+            return "encdec", {n: _Plan(getattr(m, n), self.dtype, self.dim) for n in names}
         if isinstance(m, nn.Sequential):
             kids = list(m.children())
-            if kids and all(isinstance(k, (nn.Conv2d, nn.ConvTranspose2d, nn.BatchNorm2d, nn.ReLU)) for k in kids):
+            if kids and all(isinstance(k, _CONVS + _BNS + (nn.ReLU,)) for k in kids):
                 return "seq", _seq_convs(m, self.dtype)
-            return "chain", [_Plan(k, self.dtype) for k in kids]
+            return "chain", [_Plan(k, self.dtype, self.dim) for k in kids]
         raise TypeError(f"FvpCNN: unsupported module {type(m).__name__}")
 
     def __call__(self, x: Act, res_post: Act | None = None) -> Act:
@@ -181,7 +199,7 @@ class _Plan:
             return c2(c1(x, relu=True), relu=True, res_pre=skip_x, res_post=res_post)
         if k == "pool":
             assert res_post is None
-            return maxpool2(x)
+            return maxpool2(x, self.dim)
         if k == "seq":
             for i, (c, relu) in enumerate(p):
                 x = c(x, relu, res_post=res_post if i == len(p) - 1 else None)
@@ -222,7 +240,12 @@ class FvpCNN:
         if module.training:
             raise _lib.FvpError("FvpCNN: eval mode only (BatchNorm folded with running statistics)")
         self.module = module
-        if hasattr(module, "output_hm") and hasattr(module, "output_size"):  # CenterNet
+        if isinstance(getattr(module, "output_hm", None), nn.Conv1d):  # C2CNet (cnns_1d.py:182-241)
+            self.kind = "c2c"
+            self.front = _Plan(module.front_layers, dtype, dim=1)
+            self.encdec = _Plan(module.encoder_decoder, dtype, dim=1)
+            self.out = ConvLayer(module.output_hm, None, dtype)
+        elif hasattr(module, "output_hm") and hasattr(module, "output_size"):  # CenterNet
             self.kind = "centernet"
             self.front = _Plan(module.front_layers, dtype)
             self.encdec = _Plan(module.encoder_decoder, dtype)
@@ -245,6 +268,9 @@ class FvpCNN:
 
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
+        if self.kind == "c2c":  # [N, C, L] as [N, C, 1, L]
+            y = self.out(self.encdec(self.front(to_nhwc(x.unsqueeze(2)))), relu=False)
+            return to_nchw(y).squeeze(2)
         a = to_nhwc(x)
         if self.kind == "p2p":
             return to_nchw(self.out(self.encdec(self.front(a)), relu=False))
@@ -259,12 +285,61 @@ class FvpCNN:
         return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
 
 
-def cached(module: nn.Module, dtype=torch.float32) -> FvpCNN:
-    """FvpCNN for ``module``, rebuilt whenever its parameters or buffers change
-    (storage or in-place version), e.g. after load_state_dict."""
+class FvpWeightNet:
+    """Eval-mode ``WeightNet`` (weight_net.py:48-80) as one ``fvp_weight_net``
+    launch: ``FvpWeightNet(weight_net)(x[B, J, H, W]) -> [B, J, 1]``, the
+    per-joint-map fusion weight (the reference's x.view at :66-68 and :78)."""
+
+    def __init__(self, module: nn.Module):
+        if module.training:
+            raise _lib.FvpError("FvpWeightNet: eval mode only (BatchNorm folded with running statistics)")
+        f, o = list(module.heatmap_feature_net.children()), list(module.output.children())
+        ok = (len(f) == 4 and isinstance(f[0], nn.Conv2d) and isinstance(f[1], nn.BatchNorm2d)
+              and isinstance(f[2], nn.MaxPool2d) and isinstance(f[3], nn.ReLU) and len(o) == 4
+              and isinstance(o[0], nn.Linear) and isinstance(o[1], nn.ReLU) and isinstance(o[2], nn.Linear)
+              and isinstance(o[3], nn.Sigmoid))
+        if ok:
+            c, pool = f[0], f[2]
+            ok = (c.in_channels == 1 and tuple(c.kernel_size) == (3, 3) and tuple(c.padding) == (1, 1)
+                  and tuple(c.stride) == (1, 1) and tuple(c.dilation) == (1, 1) and c.groups == 1
+                  and pool.kernel_size in (2, (2, 2)) and pool.stride in (2, (2, 2)) and pool.padding in (0, (0, 0))
+                  and not pool.ceil_mode and pool.dilation in (1, (1, 1)) and o[2].out_features == 1
+                  and o[0].in_features == c.out_channels)
+        if not ok:
+            raise _lib.FvpError("FvpWeightNet: module is not the reference WeightNet layout")
+        conv, bn, fc1, fc2 = f[0], f[1], o[0], o[2]
+        C = conv.out_channels
+        if C > 64:
+            raise _lib.FvpError(f"FvpWeightNet: {C} conv channels (at most 64)")
+        dev = conv.weight.device
+        self.C, self.Hd = C, fc1.out_features
+        self.conv_w = conv.weight.detach().float().reshape(C, 9).contiguous()
+        bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(C, device=dev)
+        s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+        self.scale = s.contiguous()
+        self.shift = ((bias - bn.running_mean.detach().float()) * s + bn.bias.detach().float()).contiguous()
+        self.w1 = fc1.weight.detach().float().contiguous()
+        self.b1 = (fc1.bias.detach().float() if fc1.bias is not None else torch.zeros(self.Hd, device=dev)).contiguous()
+        self.w2 = fc2.weight.detach().float().reshape(-1).contiguous()
+        self.b2 = (fc2.bias.detach().float() if fc2.bias is not None else torch.zeros(1, device=dev)).contiguous()
+
+    @torch.no_grad()
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        x = torch.flatten(x, 0, 1) if x.dim() == 5 else x  # [3, P, J, H, W] -> [3P, J, H, W] (:65)
+        B, J, H, W = x.shape
+        x = x.float().contiguous()
+        out = torch.empty((B, J, 1), dtype=torch.float32, device=x.device)
+        _lib.call("fvp_weight_net", _ptr(x), B * J, H, W, _ptr(self.conv_w), _ptr(self.scale), _ptr(self.shift),
+                  self.C, _ptr(self.w1), _ptr(self.b1), self.Hd, _ptr(self.w2), _ptr(self.b2), _ptr(out), _stream(out))
+        return out
+
+
+def cached(module: nn.Module, dtype=torch.float32):
+    """FvpCNN (or FvpWeightNet) for ``module``, rebuilt whenever its parameters
+    or buffers change (storage or in-place version), e.g. after load_state_dict."""
     sig = (dtype,) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
     hit = getattr(module, "_fvp_cnn", None)
     if hit is None or hit[0] != sig:
-        hit = (sig, FvpCNN(module, dtype))
+        hit = (sig, FvpWeightNet(module) if hasattr(module, "heatmap_feature_net") else FvpCNN(module, dtype))
         object.__setattr__(module, "_fvp_cnn", hit)
     return hit[1]

@@ -36,9 +36,11 @@ FVP_CNN_DTYPE = torch.float32
 def install(fused: bool = True, modules=None, cnn: bool = False) -> dict:
     """Patch the already-importable reference modules.  Returns what was patched.
 
-    cnn=True (with fused=True): in eval mode the fused forwards run CenterNet and
-    P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of torch's, in fp32;
-    cnn="bf16": bf16 operands with fp32 accumulation (opt-in, ~1e-2 relative)."""
+    cnn=True (with fused=True): in eval mode the fused forwards run CenterNet,
+    C2CNet and P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of
+    torch's, in fp32, and WeightNet as one fused launch; cnn="bf16": bf16
+    operands with fp32 accumulation for the MFMA convolutions (opt-in, ~1e-2
+    relative)."""
     global USE_FVP_CNN, FVP_CNN_DTYPE
     USE_FVP_CNN = bool(cnn)
     FVP_CNN_DTYPE = torch.bfloat16 if cnn == "bf16" else torch.float32
@@ -94,7 +96,10 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     confs_2d, index_2d, flat = proposal.nms2D(hm2d.detach(), self.max_people)
     match_bbox = proposal.gather_bbox(bbox_preds, flat)
     columns = proposal.gather_columns(cubes, flat)                        # [B, K, J, Z]
-    hm1d = self.c2c_net(torch.flatten(columns, 0, 1)).view(batch_size, self.max_people, -1)
+    c2c = self.c2c_net
+    if USE_FVP_CNN and not c2c.training:
+        c2c = fvp_cnn.cached(c2c, FVP_CNN_DTYPE)
+    hm1d = c2c(torch.flatten(columns, 0, 1)).view(batch_size, self.max_people, -1)
     confs_1d, index_1d = hm1d.detach().topk(1)
     topk_index = torch.cat([index_2d, index_1d], dim=2)
     topk_confs = confs_2d * confs_1d.squeeze(2)

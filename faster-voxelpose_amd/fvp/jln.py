@@ -80,7 +80,8 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
     features = torch.stack(torch.chunk(conv(planes), 3), dim=0)                    # [3,P,J,S,S]
     pose, maxprob = ops.soft_argmax(features, self.project_layer.center_grid, offset,
                                     float(self.soft_argmax_layer.beta))
-    weights = self.weight_net(features)                                             # [3P,J,1]
+    wnet = cnn.cached(self.weight_net) if use and not self.weight_net.training else self.weight_net
+    weights = wnet(features)                                                        # [3P,J,1]
     fused, confs = ops.fuse_poses(pose, weights, maxprob)
     all_fused[mask] = fused
     all_pose[:, mask] = pose

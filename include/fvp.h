@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 3
+#define FVP_ABI_VERSION 4
 #define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
 #define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
 /* Camera slots per voxel in a packed grid (V rounded up to even). */
@@ -203,8 +203,11 @@ int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob
  *   out = act(conv(in, W) * scale + shift + res_pre) + res_post
  * with eval-mode BatchNorm and the conv bias folded into scale/shift, act =
  * ReLU when relu != 0.  Stride 1, zero padding (K-1)/2, odd KH/KW.
- * upsample2 != 0: ConvTranspose2d(k=2, s=2) as a 1x1 conv with 4*Cpo packed
+ * upsample2 == 1: ConvTranspose2d(k=2, s=2) as a 1x1 conv with 4*Cpo packed
  * outputs n = (dy*2+dx)*Cpo + co, scattered to the 2H x 2W output.
+ * upsample2 == 2: ConvTranspose1d(k=2, s=2) (cnns_1d.py:96-123) on rows of
+ * H == 1 (1-D tensors [N][C][L] run as [N][1][L][Cp]): 2*Cpo packed outputs
+ * n = dx*Cpo + co, scattered to the H x 2W output.  Conv1d(k) is KH = 1, KW = k.
  *   in        device [N][H][W][Cpi], Cpi % 16 == 0 (padding channels zero)
  *   wpack     device [KH*KW*Cpi][Cpo_w], row (ky*KW+kx)*Cpi+ci, Cpo_w % 128 == 0
  *   scale, shift device [Cpo];  res_pre, res_post device [N][Ho][Wo][Cpo] or NULL
@@ -223,6 +226,23 @@ int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const vo
 int fvp_conv_set_tile(int id);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
 int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);
+/* KH x KW / stride-(KH, KW) max pool, KH, KW in {1, 2} (floor); KH = 1, KW = 2
+ * is F.max_pool1d(x, 2, 2) of Pool1DBlock (cnns_1d.py:77-93) on H == 1 rows. */
+int fvp_maxpool_nhwc(const float *in, int N, int H, int W, int C, int KH, int KW, float *out, void *stream);
+
+/* WeightNet.forward (lib/models/weight_net.py:48-80) fused into one launch,
+ * one block per joint map:
+ *   conv3x3(1 -> C, pad 1) -> BatchNorm -> MaxPool2d(2) -> ReLU ->
+ *   adaptive_avg_pool2d(1) -> Linear(C, Hd) -> ReLU -> Linear(Hd, 1) -> Sigmoid
+ * without materialising the [C][H][W] conv maps.
+ *   features device [Nimg][H][W] (the [3P][J] joint maps; Nimg = 3*P*J)
+ *   conv_w   device [C][9];  scale, shift device [C] (conv bias + BatchNorm folded)
+ *   fc1_w    device [Hd][C], fc1_b [Hd];  fc2_w device [Hd], fc2_b device [1]
+ *   out      device [Nimg] fusion weights in (0, 1)
+ * C <= 64; (H+2)*(W+2) floats must fit 64 KB of LDS. */
+int fvp_weight_net(const float *features, int Nimg, int H, int W, const float *conv_w, const float *scale,
+                   const float *shift, int C, const float *fc1_w, const float *fc1_b, int Hd, const float *fc2_w,
+                   const float *fc2_b, float *out, void *stream);
 /* NCHW [N][C][H][W] <-> NHWC [N][H][W][Cp] (Cp >= C, padding channels zero). */
 int fvp_nchw_to_nhwc(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream);
 int fvp_nhwc_to_nchw(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream);

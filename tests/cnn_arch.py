@@ -1,8 +1,11 @@
 """Test-side restatement of the reference's 2-D CNN architectures
 (lib/models/cnns_2d.py: Basic2DBlock :12-29, Res2DBlock :32-64, Pool2DBlock
 :67-79, Upsample2DBlock :82-104, EncoderDecorder :123-183, P2PNet :185-232,
-CenterNet :235-295) with the same module attribute names, so state_dicts are
-interchangeable with the reference's.  Pinned to the reference by
+CenterNet :235-295), their 1-D twins (lib/models/cnns_1d.py: Basic1DBlock
+:10-34, Res1DBlock :37-74, Pool1DBlock :77-93, Upsample1DBlock :96-123,
+EncoderDecorder :125-179, C2CNet :182-241) and WeightNet (weight_net.py:48-80)
+with the same module attribute names, so state_dicts are interchangeable with
+the reference's.  Pinned to the reference by
 tests/golden/cnn.npz (tools/gen_golden.py runs the reference's own classes on
 the same seeded weights and inputs).  Used where the reference is absent (the
 GPU box)."""
@@ -104,3 +107,93 @@ class CenterNet(nn.Module):
         x, _ = torch.max(x, dim=4)
         x = self.encoder_decoder(self.front_layers(x))
         return self.output_hm(x), self.output_size(x)
+
+
+# ---- 1-D (cnns_1d.py) ---------------------------------------------------------
+def _cbr1(cin, cout, k, relu=True):
+    layers = [nn.Conv1d(cin, cout, k, stride=1, padding=(k - 1) // 2), nn.BatchNorm1d(cout)]
+    return layers + [nn.ReLU(True)] if relu else layers
+
+
+class Basic1DBlock(nn.Module):
+    def __init__(self, cin, cout, k):
+        super().__init__()
+        self.block = nn.Sequential(*_cbr1(cin, cout, k))
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class Res1DBlock(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.res_branch = nn.Sequential(*_cbr1(cin, cout, 3), *_cbr1(cout, cout, 3, relu=False))
+        self.skip_con = nn.Sequential() if cin == cout else nn.Sequential(*_cbr1(cin, cout, 1, relu=False))
+
+    def forward(self, x):
+        return F.relu(self.res_branch(x) + self.skip_con(x), True)
+
+
+class Pool1DBlock(nn.Module):
+    def __init__(self, pool_size):
+        super().__init__()
+        self.pool_size = pool_size
+
+    def forward(self, x):
+        return F.max_pool1d(x, kernel_size=self.pool_size, stride=self.pool_size)
+
+
+class Upsample1DBlock(nn.Module):
+    def __init__(self, cin, cout, k, s):
+        super().__init__()
+        self.block = nn.Sequential(nn.ConvTranspose1d(cin, cout, k, stride=s), nn.BatchNorm1d(cout), nn.ReLU(True))
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class EncoderDecorder1D(EncoderDecorder):
+    def __init__(self):
+        nn.Module.__init__(self)
+        self.encoder_pool1 = Pool1DBlock(2)
+        self.encoder_res1 = Res1DBlock(32, 64)
+        self.encoder_pool2 = Pool1DBlock(2)
+        self.encoder_res2 = Res1DBlock(64, 128)
+        self.mid_res = Res1DBlock(128, 128)
+        self.decoder_res2 = Res1DBlock(128, 128)
+        self.decoder_upsample2 = Upsample1DBlock(128, 64, 2, 2)
+        self.decoder_res1 = Res1DBlock(64, 64)
+        self.decoder_upsample1 = Upsample1DBlock(64, 32, 2, 2)
+        self.skip_res1 = Res1DBlock(32, 32)
+        self.skip_res2 = Res1DBlock(64, 64)
+
+
+class C2CNet(nn.Module):
+    def __init__(self, cin, cout, head_conv=32):
+        super().__init__()
+        self.output_channels = cout
+        self.front_layers = nn.Sequential(Basic1DBlock(cin, 16, 7), Res1DBlock(16, 32))
+        self.encoder_decoder = EncoderDecorder1D()
+        self.output_hm = nn.Conv1d(32, cout, kernel_size=1)
+
+    def forward(self, x):
+        return self.output_hm(self.encoder_decoder(self.front_layers(x)))
+
+
+# ---- WeightNet (weight_net.py:48-80) --------------------------------------------
+class WeightNet(nn.Module):
+    def __init__(self, num_joints, voxels=(64, 64), feat=32, hidden=64):
+        super().__init__()
+        self.voxels_per_axis = voxels
+        self.num_joints = num_joints
+        self.heatmap_feature_net = nn.Sequential(nn.Conv2d(1, feat, 3, stride=1, padding=1), nn.BatchNorm2d(feat),
+                                                 nn.MaxPool2d(2), nn.ReLU(inplace=True))
+        self.output = nn.Sequential(nn.Linear(feat, hidden), nn.ReLU(inplace=True), nn.Linear(hidden, 1),
+                                    nn.Sigmoid())
+
+    def forward(self, x):
+        x = torch.flatten(x, 0, 1)
+        b, j = x.shape[0], self.num_joints
+        x = x.view(b * j, 1, self.voxels_per_axis[0], self.voxels_per_axis[1])
+        x = F.adaptive_avg_pool2d(self.heatmap_feature_net(x), 1).view(b * j, -1)
+        return self.output(x).view(b, j, 1)

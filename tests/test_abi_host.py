@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 4
     assert lib.fvp_status_string(0) == b"success"
 
 
@@ -65,6 +65,13 @@ def test_argument_validation_without_gpu():
     bad = _lib.PersonSpec((253, 253, 64), (0.03,) * 3, (0,) * 3, (8000,) * 3, (2000,) * 3, (64, 64, 32))
     assert lib.fvp_person_planes(1, 1, 5, 15, 128, 240, 1, bad, 1, None, 1, None, 1, None, 1, 1 << 30, None) == 1002
     assert lib.fvp_gather_columns(None, 1, 1, 1, 1, 1, None, 1, None, None) == 1001
+    assert lib.fvp_weight_net(1, 10, 64, 64, 1, 1, 1, 32, 1, 1, 64, 1, None, 1, None) == 1001
+    assert lib.fvp_weight_net(1, 10, 64, 64, 1, 1, 1, 65, 1, 1, 64, 1, 1, 1, None) == 1002   # C > 64
+    assert lib.fvp_weight_net(1, 10, 200, 200, 1, 1, 1, 32, 1, 1, 64, 1, 1, 1, None) == 1002  # map beyond LDS
+    assert lib.fvp_weight_net(None, 0, 64, 64, None, None, None, 32, None, None, 64, None, None, None, None) == 0
+    assert lib.fvp_maxpool_nhwc(1, 1, 1, 20, 16, 2, 2, 1, None) == 1002  # H < KH
+    assert lib.fvp_maxpool_nhwc(1, 1, 1, 20, 16, 1, 3, 1, None) == 1002
+    assert lib.fvp_conv2d_nhwc(1, 1, 1, 8, 16, 1, 1, 1, 16, 128, 1, 1, None, None, 0, 3, 1, None) == 1002  # upsample2
     with pytest.raises(_lib.FvpError, match="NULL"):
         _lib.check(1001, "fvp_voxelize")
 

@@ -1,0 +1,180 @@
+"""The HDN's 1-D C2CNet and the JLN's WeightNet on fvp kernels (fvp/cnn.py;
+csrc/fvp_conv.hip, csrc/fvp_jln.hip).
+
+Golden vectors: tests/golden/cnn.npz ``y_c2c`` / ``y_weight`` -- the
+reference's own C2CNet (lib/models/cnns_1d.py:182-241) and WeightNet
+(lib/models/weight_net.py:48-80) with seeded weights on seeded inputs, run on
+CPU by tools/gen_golden.py.  tests/cnn_arch.py restates both (same attribute
+names) for the GPU box and is pinned here.
+
+C2CNet runs on the MFMA convolutions as rows of height 1 (Conv1d(k) = a 1 x k
+kernel, ConvTranspose1d(2, 2) = a 1 x 1 conv with a 1 x 2 scatter, max_pool1d
+= a 1 x 2 pool).  WeightNet is one fused launch per joint map (conv 3x3 1->C,
+BN, 2x2 max pool, ReLU, mean, two Linear layers, sigmoid).
+
+Tolerance: fp32; different summation orders and folded BatchNorm give
+agreement to 2e-5 of the output scale (as tests/test_cnn.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+REL = 2e-5
+
+
+def _close(got, ref, what, rel=REL):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    scale = max(float(np.abs(ref).max()), 1e-6)
+    err = float(np.abs(got - ref).max()) / scale
+    assert err <= rel, f"{what}: max error {err:.3g} of the output scale (> {rel})"
+
+
+def _nets():
+    """The restated modules and the inputs gen_golden.py drew (same rng order)."""
+    from fvp import synthetic
+    import cnn_arch
+
+    c2c = cnn_arch.C2CNet(15, 1).eval()
+    c2c.load_state_dict(synthetic.seeded_state_dict(c2c, 14))
+    wn = cnn_arch.WeightNet(15).eval()
+    wn.load_state_dict(synthetic.seeded_state_dict(wn, 15))
+    rng = np.random.default_rng(13)
+    rng.uniform(0.0, 1.0, (2, 15, 64, 64))      # P2PNet input (tests/test_cnn.py)
+    rng.uniform(0.0, 1.0, (1, 15, 40, 40, 4))   # CenterNet input
+    x_c2c = rng.uniform(0.0, 1.0, (6, 15, 20)).astype(np.float32)
+    x_wn = rng.normal(0.0, 1.0, (3, 2, 15, 64, 64)).astype(np.float32)
+    return c2c, wn, x_c2c, x_wn
+
+
+def test_restated_c2c_and_weight_net_match_reference_golden():
+    d = golden("cnn.npz")
+    c2c, wn, x_c2c, x_wn = _nets()
+    with torch.no_grad():
+        _close(c2c(torch.from_numpy(x_c2c)).numpy(), d["y_c2c"], "C2CNet (CPU restatement)")
+        _close(wn(torch.from_numpy(x_wn)).numpy(), d["y_weight"], "WeightNet (CPU restatement)")
+
+
+def test_weight_net_refuses_other_layouts():
+    import torch.nn as nn
+
+    import cnn_arch
+    from fvp import _lib
+    from fvp.cnn import FvpWeightNet
+
+    wn = cnn_arch.WeightNet(15).eval()
+    wn.heatmap_feature_net[2] = nn.AvgPool2d(2)
+    with pytest.raises(_lib.FvpError, match="WeightNet layout"):
+        FvpWeightNet(wn)
+    with pytest.raises(_lib.FvpError, match="eval mode"):
+        FvpWeightNet(cnn_arch.WeightNet(15).train())
+
+
+@pytest.mark.gpu
+def test_fvp_c2c_and_weight_net_match_reference(gpu_device):
+    from fvp.cnn import FvpCNN, FvpWeightNet
+
+    d = golden("cnn.npz")
+    c2c, wn, x_c2c, x_wn = _nets()
+    c2c, wn = c2c.to(gpu_device), wn.to(gpu_device)
+    xc, xw = torch.from_numpy(x_c2c).to(gpu_device), torch.from_numpy(x_wn).to(gpu_device)
+    y = FvpCNN(c2c)(xc)
+    w = FvpWeightNet(wn)(xw)
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (6, 1, 20) and tuple(w.shape) == (6, 15, 1)
+    _close(y.cpu().numpy(), d["y_c2c"], "C2CNet on MFMA")
+    _close(w.cpu().numpy(), d["y_weight"], "WeightNet fused")
+    with torch.no_grad():  # and against torch's own GPU kernels
+        _close(y.cpu().numpy(), c2c(xc).cpu().numpy(), "C2CNet vs torch GPU")
+        _close(w.cpu().numpy(), wn(xw).cpu().numpy(), "WeightNet vs torch GPU")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,L,res", [(15, 16, 7, 20, False), (16, 32, 3, 20, True), (32, 64, 1, 10, False),
+                                              (128, 128, 3, 5, True), (15, 16, 7, 32, False), (40, 70, 5, 13, True)])
+def test_conv1d_layer_vs_torch(gpu_device, cin, cout, k, L, res):
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    seq = nn.Sequential(nn.Conv1d(cin, cout, k, padding=(k - 1) // 2), nn.BatchNorm1d(cout)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin + cout + k))
+    seq = seq.to(gpu_device)
+    g = torch.Generator().manual_seed(k + L)
+    x = torch.rand((80, cin, L), generator=g).to(gpu_device)
+    r = torch.rand((80, cout, L), generator=g).to(gpu_device) if res else None
+    with torch.no_grad():
+        ref = seq(x)
+        ref = torch.relu(ref + r) if res else torch.relu(ref)
+    layer = cnn.ConvLayer(seq[0], seq[1])
+    a = cnn.to_nhwc(x.unsqueeze(2))
+    got = cnn.to_nchw(layer(a, relu=True, res_pre=cnn.to_nhwc(r.unsqueeze(2)) if res else None)).squeeze(2)
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv1d {cin}->{cout} k{k} L{L}")
+
+
+@pytest.mark.gpu
+def test_transposed_conv1d_and_pool1d_vs_torch(gpu_device):
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    from fvp import cnn, synthetic
+
+    up = nn.Sequential(nn.ConvTranspose1d(128, 64, 2, stride=2), nn.BatchNorm1d(64)).eval()
+    up.load_state_dict(synthetic.seeded_state_dict(up, 5))
+    up = up.to(gpu_device)
+    g = torch.Generator().manual_seed(6)
+    x = torch.rand((80, 128, 5), generator=g).to(gpu_device)
+    skip = torch.rand((80, 64, 10), generator=g).to(gpu_device)
+    with torch.no_grad():
+        ref = torch.relu(up(x)) + skip
+    layer = cnn.ConvLayer(up[0], up[1])
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x.unsqueeze(2)), relu=True, res_post=cnn.to_nhwc(skip.unsqueeze(2))))
+    _close(got.squeeze(2).cpu().numpy(), ref.cpu().numpy(), "ConvTranspose1d + BN + ReLU + skip")
+    for L in (20, 11):  # even and odd (floor) lengths
+        p = torch.rand((7, 48, L), generator=g).to(gpu_device)
+        got = cnn.to_nchw(cnn.maxpool2(cnn.to_nhwc(p.unsqueeze(2)), dim=1)).squeeze(2)
+        assert torch.equal(got, F.max_pool1d(p, 2, 2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [20, 32])
+def test_c2c_large_batch_vs_torch(gpu_device, L):
+    """80 columns (8 frames x K=10) at the C2 (Z=20) and C4 (Z=32) column lengths."""
+    from fvp.cnn import FvpCNN
+
+    c2c, _, _, _ = _nets()
+    c2c = c2c.to(gpu_device)
+    x = torch.rand((80, 15, L), generator=torch.Generator().manual_seed(L)).to(gpu_device)
+    with torch.no_grad():
+        ref = c2c(x)
+    _close(FvpCNN(c2c)(x).cpu().numpy(), ref.cpu().numpy(), f"C2CNet, 80 columns of {L}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("feat,hidden,hw,P", [(32, 64, (64, 64), 10), (16, 32, (33, 18), 3), (64, 100, (40, 40), 2)])
+def test_weight_net_shapes_vs_torch(gpu_device, feat, hidden, hw, P):
+    """Channel counts of both template widths, odd map sizes (floor pooling)."""
+    from fvp import synthetic
+    from fvp.cnn import FvpWeightNet
+    import cnn_arch
+
+    wn = cnn_arch.WeightNet(15, hw, feat, hidden).eval()
+    wn.load_state_dict(synthetic.seeded_state_dict(wn, feat + hidden))
+    wn = wn.to(gpu_device)
+    x = torch.randn((3, P, 15) + hw, generator=torch.Generator().manual_seed(P)).to(gpu_device)
+    with torch.no_grad():
+        ref = wn(x)
+    got = FvpWeightNet(wn)(x)
+    assert got.shape == ref.shape
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"WeightNet C={feat} Hd={hidden} {hw}")
+
+
+@pytest.mark.gpu
+def test_bf16_c2c_vs_reference(gpu_device):
+    from fvp.cnn import FvpCNN
+
+    d = golden("cnn.npz")
+    c2c, _, x_c2c, _ = _nets()
+    y = FvpCNN(c2c.to(gpu_device), torch.bfloat16)(torch.from_numpy(x_c2c).to(gpu_device))
+    _close(y.cpu().numpy(), d["y_c2c"], "C2CNet bf16", rel=5e-2)

@@ -231,10 +231,11 @@ def test_fused_jln_forward_matches_reference_flow(gpu_device):
 
 @pytest.mark.gpu
 def test_fused_forwards_with_fvp_cnn(gpu_device):
-    """install(cnn=True): CenterNet (HDN) and P2PNet (JLN) run on the fvp MFMA
-    convolutions inside the fused forwards; results match the torch-conv fused
-    forwards within the CNN tolerance (2e-5 of the output scale; the proposals
-    themselves may reorder only where heatmap values tie within it)."""
+    """install(cnn=True): CenterNet + C2CNet (HDN) and P2PNet + WeightNet (JLN)
+    run on the fvp kernels inside the fused forwards; results match the
+    torch-conv fused forwards within the CNN tolerance (2e-5 of the output
+    scale; the proposals themselves may reorder only where heatmap values tie
+    within it)."""
     import cnn_arch
 
     from fvp import geometry, jln, synthetic
@@ -255,7 +256,9 @@ def test_fused_forwards_with_fvp_cnn(gpu_device):
     hdn.center_net = cnn_arch.CenterNet(J, 1).eval()
     hdn.center_net.load_state_dict(synthetic.seeded_state_dict(hdn.center_net, 12))
     hdn.center_net = hdn.center_net.to(gpu_device)
-    hdn.c2c_net = nn.Conv1d(J, 1, 1).to(gpu_device).eval()
+    hdn.c2c_net = cnn_arch.C2CNet(J, 1).eval()
+    hdn.c2c_net.load_state_dict(synthetic.seeded_state_dict(hdn.c2c_net, 14))
+    hdn.c2c_net = hdn.c2c_net.to(gpu_device)
     hdn.proposal_layer = _Proposal(w)
     hdn.max_people = w.max_people
     try:
@@ -267,6 +270,9 @@ def test_fused_forwards_with_fvp_cnn(gpu_device):
         scale = float(ref[0].abs().max())
         assert float((got[0] - ref[0]).abs().max()) <= 2e-5 * scale
         assert float((got[3] - ref[3]).abs().max()) <= 2e-5 * float(ref[3].abs().max())
+        same = (got[2][:, :, :2] == ref[2][:, :, :2]).all(dim=2)  # same (x, y) column picked
+        assert int(same.sum()) > 0
+        assert float((got[1] - ref[1])[same].abs().max()) <= 2e-5 * float(ref[1].abs().max())
 
         net = types.SimpleNamespace(training=False)
         net.project_layer = PI(w.cfg(str(gpu_device)))
@@ -274,7 +280,9 @@ def test_fused_forwards_with_fvp_cnn(gpu_device):
         net.conv_net = cnn_arch.P2PNet(J, J).eval()
         net.conv_net.load_state_dict(synthetic.seeded_state_dict(net.conv_net, 11))
         net.conv_net = net.conv_net.to(gpu_device)
-        net.weight_net = _WeightNet(J).to(gpu_device).eval()
+        net.weight_net = cnn_arch.WeightNet(J).eval()
+        net.weight_net.load_state_dict(synthetic.seeded_state_dict(net.weight_net, 15))
+        net.weight_net = net.weight_net.to(gpu_device)
         net.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
         pc = torch.from_numpy(np.stack([synthetic.proposals_for_frame(w, f, 4) for f in range(2)])).to(gpu_device)
         mask = torch.ones((2, 4), dtype=torch.bool, device=gpu_device)

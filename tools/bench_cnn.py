@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """CNN line: P2PNet on the JLN planes of K proposals
-(3K images of J x 64 x 64) and CenterNet on B xy planes (J x 80 x 80), fvp MFMA
-engine vs torch's own GPU convolution of the same eval-mode module.
+(3K images of J x 64 x 64), CenterNet on B xy planes (J x 80 x 80), C2CNet on
+the 10 z-columns of each of the B frames and WeightNet on the 3K joint-feature
+stacks; fvp kernels vs torch's own GPU path for the same eval-mode module.
 
     python tools/bench_cnn.py [--proposals 10] [--frames 8] [--iters 10]
 """
@@ -89,6 +90,27 @@ def main():
                          "speedup_vs_torch": round(t_t / t_f, 3),
                          "bf16_ms": round(t_b, 4), "bf16_tflops": round(fl / (t_b * 1e-3) / 1e12, 2),
                          "bf16_frac_of_bf16_peak": round(fl / (t_b * 1e-3) / 1e12 / 2500.0, 4)}
+        # C2CNet on the K z-columns of every frame; WeightNet on the 3K joint-feature stacks
+        c2c = cnn_arch.C2CNet(J, 1).eval()
+        c2c.load_state_dict(synthetic.seeded_state_dict(c2c, 14))
+        wn = cnn_arch.WeightNet(J).eval()
+        wn.load_state_dict(synthetic.seeded_state_dict(wn, 15))
+        c2c, wn = c2c.to(dev), wn.to(dev)
+        x_col = torch.rand((args.frames * 10, J, 20), generator=g).to(dev)
+        x_feat = torch.randn((3, args.proposals, J, 64, 64), generator=g).to(dev)
+        f_c2c, f_wn = cnn.FvpCNN(c2c), cnn.FvpWeightNet(wn)
+        fl = flops(lambda t: f_c2c(t), x_col)
+        t_f, t_t = timeit(lambda: f_c2c(x_col)), timeit(lambda: c2c(x_col))
+        out["c2cnet_hdn"] = {"columns": int(x_col.shape[0]), "shape": list(x_col.shape[1:]),
+                             "gflop": round(fl / 1e9, 4), "fvp_ms": round(t_f, 4), "torch_ms": round(t_t, 4),
+                             "speedup_vs_torch": round(t_t / t_f, 3)}
+        t_f, t_t = timeit(lambda: f_wn(x_feat)), timeit(lambda: wn(x_feat))
+        nbytes = x_feat.numel() * 4
+        out["weightnet_jln"] = {"maps": int(x_feat.shape[0] * x_feat.shape[1] * J), "shape": [64, 64],
+                                "gflop_conv": round(2 * x_feat.numel() * 32 * 9 / 1e9, 3),
+                                "fvp_ms": round(t_f, 4), "torch_ms": round(t_t, 4),
+                                "fvp_gbs_input": round(nbytes / (t_f * 1e-3) / 1e9, 1),
+                                "speedup_vs_torch": round(t_t / t_f, 3)}
     print(json.dumps({"metric": "HDN/JLN CNNs on fp32 MFMA (implicit GEMM, folded BN)", "peak_tflops_f32": MFMA_F32_PEAK_TF,
                       "note": "torch_ms = the same eval module on torch's GPU convolution (MIOpen); torch centernet "
                               "time covers the same layers (hm head only)", **out}))

@@ -4,10 +4,10 @@ heatmaps -> voxel cube + xy plane -> CenterNet -> NMS top-K -> bbox / z-column
 gathers -> C2CNet -> proposals -> per-person planes -> P2PNet -> soft-argmax +
 offsets -> WeightNet -> fusion, for B frames at C3 geometry.
 
-CenterNet / P2PNet run on the fvp MFMA convolutions (install(cnn=True)) with
-the reference architectures (tests/cnn_arch.py) and seeded weights; C2CNet and
-WeightNet are small torch stand-ins with the reference's I/O (they are ~0.1 %
-of the FLOPs).  Reports frames/s and a per-stage breakdown (HIP events).
+CenterNet / C2CNet / P2PNet run on the fvp MFMA convolutions and WeightNet on
+its fused kernel (install(cnn=True)), all with the reference architectures
+(tests/cnn_arch.py) and seeded weights; --torch-cnn runs the same modules on
+torch.  Reports frames/s and a per-stage breakdown (HIP events).
 
     python tools/bench_pipeline.py [--frames 8] [--steps 10]
 """
@@ -61,22 +61,15 @@ def main():
             out[:, :, 5:7] = match_bbox.clamp(0.3, 0.8)
             return out
 
-    class WeightNet(nn.Module):  # I/O of weight_net.py:48-80
-        def __init__(self):
-            super().__init__()
-            self.lin = nn.Linear(1, 1)
-
-        def forward(self, x):
-            x = torch.flatten(x, 0, 1)
-            return torch.sigmoid(self.lin(x.mean(dim=(2, 3)).reshape(-1, 1))).view(x.shape[0], J, 1)
-
     hdn = types.SimpleNamespace(max_people=K)
     hdn.project_layer = ProjectLayer(w.cfg(str(dev)))
     hdn.project_layer.verbose = False
     hdn.center_net = cnn_arch.CenterNet(J, 1).eval()
     hdn.center_net.load_state_dict(synthetic.seeded_state_dict(hdn.center_net, 12))
     hdn.center_net = hdn.center_net.to(dev)
-    hdn.c2c_net = nn.Sequential(nn.Conv1d(J, 32, 3, padding=1), nn.ReLU(), nn.Conv1d(32, 1, 1)).to(dev).eval()
+    hdn.c2c_net = cnn_arch.C2CNet(J, 1).eval()
+    hdn.c2c_net.load_state_dict(synthetic.seeded_state_dict(hdn.c2c_net, 14))
+    hdn.c2c_net = hdn.c2c_net.to(dev)
     hdn.proposal_layer = Proposal()
     jl = types.SimpleNamespace(training=False)
     jl.project_layer = PI(w.cfg(str(dev)))
@@ -84,7 +77,9 @@ def main():
     jl.conv_net = cnn_arch.P2PNet(J, J).eval()
     jl.conv_net.load_state_dict(synthetic.seeded_state_dict(jl.conv_net, 11))
     jl.conv_net = jl.conv_net.to(dev)
-    jl.weight_net = WeightNet().to(dev).eval()
+    jl.weight_net = cnn_arch.WeightNet(J).eval()
+    jl.weight_net.load_state_dict(synthetic.seeded_state_dict(jl.weight_net, 15))
+    jl.weight_net = jl.weight_net.to(dev)
     jl.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
     integration.USE_FVP_CNN = not args.torch_cnn
     integration.FVP_CNN_DTYPE = torch.bfloat16 if args.bf16 else torch.float32
@@ -123,7 +118,7 @@ def main():
         "hdn_ms": round(hdn_ms, 3), "jln_ms": round(jln_ms, 3),
         "cnn": "torch (MIOpen)" if args.torch_cnn else ("fvp bf16 MFMA" if args.bf16 else "fvp fp32 MFMA"),
         "config": f"{w.name}: {len(cams[seq])} cams, J={J}, {w.voxels_per_axis} whole grid, 64^3 per person; "
-                  "CenterNet/P2PNet reference architectures with seeded weights, C2CNet/WeightNet small stand-ins"}))
+                  "CenterNet/C2CNet/P2PNet/WeightNet reference architectures with seeded weights"}))
 
 
 if __name__ == "__main__":

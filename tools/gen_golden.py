@@ -188,7 +188,23 @@ def main():
     with torch.no_grad():
         y_p2p = p2p(torch.from_numpy(x_p2p)).numpy()
         hm, size = cn(torch.from_numpy(x_cn))
-    d = {"y_p2p": y_p2p, "hm": hm.numpy(), "size": size.numpy()}
+    # the 1-D C2CNet (cnns_1d.py:182-241) and WeightNet (weight_net.py:48-80)
+    import models.cnns_1d as c1d  # noqa: E402
+    import models.weight_net as wn  # noqa: E402
+    c2c = c1d.C2CNet(15, 1).eval()
+    c2c.load_state_dict(synthetic.seeded_state_dict(c2c, 14))
+    wcfg = types.SimpleNamespace(INDIVIDUAL_SPEC=types.SimpleNamespace(VOXELS_PER_AXIS=[64, 64, 64]),
+                                 DATASET=types.SimpleNamespace(NUM_JOINTS=15),
+                                 NETWORK=types.SimpleNamespace(NUM_CHANNEL_JOINT_FEAT=32,
+                                                               NUM_CHANNEL_JOINT_HIDDEN=64))
+    wnet = wn.WeightNet(wcfg).eval()
+    wnet.load_state_dict(synthetic.seeded_state_dict(wnet, 15))
+    x_c2c = rng.uniform(0.0, 1.0, (6, 15, 20)).astype(np.float32)
+    x_wn = rng.normal(0.0, 1.0, (3, 2, 15, 64, 64)).astype(np.float32)
+    with torch.no_grad():
+        y_c2c = c2c(torch.from_numpy(x_c2c)).numpy()
+        y_wn = wnet(torch.from_numpy(x_wn)).numpy()
+    d = {"y_p2p": y_p2p, "hm": hm.numpy(), "size": size.numpy(), "y_c2c": y_c2c, "y_weight": y_wn}
     np.savez_compressed(os.path.join(OUT, "cnn.npz"), **d)
     print("wrote cnn", {k: np.shape(v) for k, v in d.items()}, float(np.abs(y_p2p).max()))
     return 0

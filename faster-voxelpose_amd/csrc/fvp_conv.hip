@@ -95,8 +95,80 @@ __device__ __forceinline__ void load_chunk(const ConvArgs &a, int n0, int chunk,
     }
 }
 
-template <class TL>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+// Fused epilogue of a wave's accumulator tiles: out = act(acc * scale + shift
+// + res_pre) + res_post at the output offset of (row m, column n); up2: 1 =
+// ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1
+// rows (1x2 scatter).  Rows come EPI at a time with every residual load issued
+// before the first use (one wait per group instead of one per element).
+template <int TM, int TN, int NACC, int MS, typename AccT>
+__device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM][TN], int mw, int nw, int M,
+                                         int lane) {
+    constexpr int EPI = 4;
+    const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
+    const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
+    const int HW = a.H * a.W;
+    auto rowof = [&](int r) { return MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r; };
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = nw + j * MS + (lane % MS);
+        const bool nok = n < Ctot;
+        const int nn = nok ? n : 0;
+        const int co = a.up2 ? nn % a.Cpo : nn;
+        const int q = a.up2 ? nn / a.Cpo : 0;  // (dy, dx) of the transposed conv
+        const float sc = a.scale[co], sh = a.shift[co];
+        auto offset = [&](int m) -> size_t {  // output element of (row m, column co)
+            if (!a.up2) return (size_t)m * a.Cpo + co;
+            const int img = m / HW, rr = m - img * HW;
+            const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
+            const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
+            return (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
+        };
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int mt = mw + i * MS;  // first row of this MFMA tile (wave-uniform)
+            if (mt >= M) continue;
+            // offsets grow with m, so rows are addressed relative to the tile's first (32-bit)
+            const size_t ob = offset(mt) - co;
+            float *__restrict__ out = a.out + ob;
+            const float *__restrict__ rpre = a.res_pre ? a.res_pre + ob : nullptr;
+            const float *__restrict__ rpost = a.res_post ? a.res_post + ob : nullptr;
+#pragma unroll
+            for (int r0 = 0; r0 < NACC; r0 += EPI) {
+                unsigned rel[EPI];
+                bool ok[EPI];
+                float pre[EPI], post[EPI];
+#pragma unroll
+                for (int r = 0; r < EPI; ++r) {
+                    const int m = mt + rowof(r0 + r);
+                    ok[r] = nok && m < M;
+                    rel[r] = ok[r] ? (unsigned)(offset(m) - ob) : 0u;
+                }
+                if (rpre) {
+#pragma unroll
+                    for (int r = 0; r < EPI; ++r) pre[r] = rpre[rel[r]];
+                }
+                if (rpost) {
+#pragma unroll
+                    for (int r = 0; r < EPI; ++r) post[r] = rpost[rel[r]];
+                }
+#pragma unroll
+                for (int r = 0; r < EPI; ++r) {
+                    float v = acc[i][j][r0 + r] * sc + sh;
+                    if (rpre) v = v + pre[r];
+                    if (a.relu) v = fmaxf(v, 0.0f);
+                    if (rpost) v = v + post[r];
+                    if (ok[r]) out[rel[r]] = v;
+                }
+            }
+        }
+    }
+}
+
+// PROBE (tools build only, -DFVP_CONV_PROBES): bit 0 = no epilogue stores
+// (one guarded store keeps the MFMAs live), bit 1 = no global loads after the
+// first chunk (LDS staging, barriers and MFMAs only).  0 in the library.
+template <class TL, int PROBE = 0>
+__global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, AP = TL::AP, MS = TL::MS;
     constexpr int AE = BM * KC / 4;
     constexpr int AV = AE >= 256 ? AE / 256 : 1;
@@ -130,9 +202,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
         }
     }
     float4 av[AV], bv[BVN];
-    load_chunk<TL>(a, n0, 0, pr, av, bv);
-    for (int ch = 0; ch < nchunks; ++ch) {
-        const int buf = ch & 1;
+    auto stage = [&](int buf) {  // registers -> LDS buffer buf
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
             const int e = u * 256 + t;
@@ -149,8 +219,18 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
         } else if (t < KC * BN / 4) {
             *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
         }
-        __syncthreads();
-        if (ch + 1 < nchunks) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);  // in flight during the MFMAs
+    };
+    load_chunk<TL>(a, n0, 0, pr, av, bv);
+    stage(0);
+    __syncthreads();
+    // One barrier per chunk: chunk ch+1's global loads are issued first, the
+    // MFMAs of chunk ch next, and the loaded registers go to the other buffer
+    // after the last MFMA has issued (it was last read before the previous
+    // barrier), so the LDS stores and the barrier overlap the MFMA tail.
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int buf = ch & 1;
+        const bool more = ch + 1 < nchunks;
+        if (!(PROBE & 2) && more) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);
 #pragma unroll
         for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
             float fa[TL::TM], fb[TL::TN];
@@ -174,46 +254,23 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
                 }
         }
-        // the next iteration writes the other buffer; the one after rewrites this
-        // one only after its own barrier, which every wave reaches after these reads
+        if (more) stage(buf ^ 1);
+        __syncthreads();
     }
 
-    // epilogue: lane -> column (output channel), registers -> rows (pixels)
-    // up2: 1 = ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1 rows (1x2 scatter)
-    const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
-    const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
+    if constexpr (PROBE & 1) {
+        float sink = 0.0f;
 #pragma unroll
-    for (int j = 0; j < TL::TN; ++j) {
-        const int n = n0 + wc * TL::WTN + j * MS + (lane % MS);
-        if (n >= Ctot) continue;
-        const int co = a.up2 ? n % a.Cpo : n;
-        const int q = a.up2 ? n / a.Cpo : 0;  // (dy, dx) of the transposed conv
-        const float sc = a.scale[co], sh = a.shift[co];
+        for (int i = 0; i < TL::TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TL::TM; ++i) {
+            for (int j = 0; j < TL::TN; ++j)
 #pragma unroll
-            for (int r = 0; r < TL::NACC; ++r) {
-                const int row = MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r;
-                const int m = m0 + wr * TL::WTM + i * MS + row;
-                if (m >= M) continue;
-                size_t o;
-                if (a.up2) {
-                    const int HW = a.H * a.W;
-                    const int img = m / HW, rr = m - img * HW;
-                    const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
-                    const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
-                    o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
-                } else {
-                    o = (size_t)m * a.Cpo + co;
-                }
-                float v = acc[i][j][r] * sc + sh;
-                if (a.res_pre) v = v + a.res_pre[o];
-                if (a.relu) v = fmaxf(v, 0.0f);
-                if (a.res_post) v = v + a.res_post[o];
-                a.out[o] = v;
-            }
-        }
+                for (int r = 0; r < TL::NACC; ++r) sink += acc[i][j][r];
+        if (sink == 1234.5f) a.out[t] = sink;
+        return;
     }
+    // epilogue: lane -> column (output channel), registers -> rows (pixels)
+    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, m0 + wr * TL::WTM, n0 + wc * TL::WTN, M, lane);
 }
 
 // Tiles by output width; the big ones where the launch has >= 2 blocks per CU,
@@ -225,22 +282,14 @@ using TileN32s = Tile<64, 32, 16, 4>;   //             4 waves x (16 px x 32 ch)
 using TileN64 = Tile<128, 64, 32, 2>;   // wider: 2x2 waves x (64 px x 32 ch), 2 accumulators
 using TileN64m = Tile<64, 64, 32, 2>;   //        2x2 waves x (32 px x 32 ch)
 using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
-// larger wave tiles / 32-wide K chunks (tuning candidates)
-using TileX1 = Tile<256, 32, 32, 4, 16>;   // 4 waves x (64 x 32)
-using TileX2 = Tile<256, 32, 32, 4, 32>;
-using TileX3 = Tile<128, 64, 32, 2, 32>;   // 2x2 waves x (64 x 32), K 32
-using TileX4 = Tile<256, 64, 32, 4, 16>;   // 4 waves x (64 x 64)
-using TileX5 = Tile<128, 128, 32, 2, 16>;  // 2x2 waves x (64 x 64)
-using TileX6 = Tile<128, 128, 32, 2, 32>;
-using TileX7 = Tile<128, 32, 32, 4, 32>;   // 4 waves x (32 x 32), K 32
-using TileX8 = Tile<64, 64, 32, 2, 32>;
+// (larger wave tiles -- 64x64 per wave -- and 32-wide K chunks measured slower)
 
 static int g_force_tile = 0;
 
 }  // namespace fvp
 
 extern "C" int fvp_conv_set_tile(int id) {
-    if (id < 0 || id > 15) return FVP_ERR_SHAPE;
+    if (id < 0 || id > 7) return FVP_ERR_SHAPE;
     fvp::g_force_tile = id;
     return FVP_OK;
 }
@@ -264,7 +313,7 @@ struct TileB {
 };
 
 template <class TL>
-__global__ __launch_bounds__(256) void conv_bf16_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
+__global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
     constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, P = TL::P;
     constexpr int AE = BM * KC / 4, AV = AE >= 256 ? AE / 256 : 1;  // A: float4 (4 channels) per element
     constexpr int BE = BN * KC / 8, BV = BE >= 256 ? BE / 256 : 1;  // B: 8 bf16 per element
@@ -357,40 +406,7 @@ __global__ __launch_bounds__(256) void conv_bf16_kernel(ConvArgs a, const __bf16
         }
     }
 
-    // up2: 1 = ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1 rows (1x2 scatter)
-    const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
-    const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
-#pragma unroll
-    for (int j = 0; j < TL::TN; ++j) {
-        const int n = n0 + wc * TL::WTN + j * 32 + (lane & 31);
-        if (n >= Ctot) continue;
-        const int co = a.up2 ? n % a.Cpo : n;
-        const int q = a.up2 ? n / a.Cpo : 0;
-        const float sc = a.scale[co], sh = a.shift[co];
-#pragma unroll
-        for (int i = 0; i < TL::TM; ++i) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wr * TL::WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (m >= M) continue;
-                size_t o;
-                if (a.up2) {
-                    const int HW = a.H * a.W;
-                    const int img = m / HW, rr = m - img * HW;
-                    const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
-                    const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
-                    o = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
-                } else {
-                    o = (size_t)m * a.Cpo + co;
-                }
-                float v = acc[i][j][r] * sc + sh;
-                if (a.res_pre) v = v + a.res_pre[o];
-                if (a.relu) v = fmaxf(v, 0.0f);
-                if (a.res_post) v = v + a.res_post[o];
-                a.out[o] = v;
-            }
-        }
-    }
+    epilogue<TL::TM, TL::TN, 16, 32>(a, acc, m0 + wr * TL::WTM, n0 + wc * TL::WTN, M, lane);
 }
 
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
@@ -452,9 +468,11 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float *__restri
 
 }  // namespace fvp
 
-extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
-                               int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                               const float *res_post, int relu, int upsample2, float *out, void *stream) {
+namespace fvp {
+template <int PROBE>
+static int conv_launch(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW, int Cpo,
+                       int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                       const float *res_post, int relu, int upsample2, float *out, void *stream) {
     if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
         (KH & 1) == 0 || (KW & 1) == 0)
@@ -469,7 +487,7 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
 #define FVP_CONV(TL)                                                                                              \
     do {                                                                                                          \
         if (Cpi % fvp::TL::KC) return FVP_ERR_SHAPE;                                                              \
-        hipLaunchKernelGGL(fvp::conv_mfma_kernel<fvp::TL>,                                                        \
+        hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL, PROBE>),                                               \
                            dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                  \
                                 (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN)),                              \
                            dim3(256), 0, st, a);                                                                 \
@@ -482,14 +500,6 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
         case 5: FVP_CONV(TileN64); return (int)hipGetLastError();
         case 6: FVP_CONV(TileN64m); return (int)hipGetLastError();
         case 7: FVP_CONV(TileN64s); return (int)hipGetLastError();
-        case 8: FVP_CONV(TileX1); return (int)hipGetLastError();
-        case 9: FVP_CONV(TileX2); return (int)hipGetLastError();
-        case 10: FVP_CONV(TileX3); return (int)hipGetLastError();
-        case 11: FVP_CONV(TileX4); return (int)hipGetLastError();
-        case 12: FVP_CONV(TileX5); return (int)hipGetLastError();
-        case 13: FVP_CONV(TileX6); return (int)hipGetLastError();
-        case 14: FVP_CONV(TileX7); return (int)hipGetLastError();
-        case 15: FVP_CONV(TileX8); return (int)hipGetLastError();
         default: break;
     }
     auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long long)((Ntot + bn - 1) / bn); };
@@ -506,6 +516,31 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
 #undef FVP_CONV
     return (int)hipGetLastError();
 }
+}  // namespace fvp
+
+extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
+                               int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                               const float *res_post, int relu, int upsample2, float *out, void *stream) {
+    return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
+                               upsample2, out, stream);
+}
+
+#ifdef FVP_CONV_PROBES
+extern "C" int fvp_conv_probe(int probe, const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH,
+                              int KW, int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                              const float *res_post, int relu, int upsample2, float *out, void *stream) {
+    switch (probe) {
+        case 1: return fvp::conv_launch<1>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
+                                           res_post, relu, upsample2, out, stream);
+        case 2: return fvp::conv_launch<2>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
+                                           res_post, relu, upsample2, out, stream);
+        case 3: return fvp::conv_launch<3>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
+                                           res_post, relu, upsample2, out, stream);
+        default: return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
+                                            res_post, relu, upsample2, out, stream);
+    }
+}
+#endif
 
 extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH,
                                     int KW, int Cpo, int Cpo_w, const float *scale, const float *shift,

@@ -138,6 +138,8 @@ __global__ __launch_bounds__(64) void fuse_kernel(const float *__restrict__ pose
 // The [C][H][W] conv map the reference materialises (23.6 MB per proposal at
 // 64x64, C = 32) never leaves registers: each thread owns pooled cells, reads
 // their 4x4 input patch from the LDS copy of the map and keeps C running sums.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int CMAX>
 __global__ __launch_bounds__(256) void weight_net_kernel(const float *__restrict__ x, int H, int W,
                                                          const float *__restrict__ cw, const float *__restrict__ scale,
@@ -171,16 +173,19 @@ __global__ __launch_bounds__(256) void weight_net_kernel(const float *__restrict
 #pragma unroll
                 for (int i = 0; i < 9; ++i) k[i] = cw[c * 9 + i];
                 const float sc = scale[c], sh = shift[c];
-                float m = 0.0f;
+                // the two outputs of a pooled row as one packed pair (v_pk_fma_f32)
+                f32x2 v[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int dy = d >> 1, dx = d & 1;
-                    float v = 0.0f;
+                for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-                    for (int i = 0; i < 9; ++i) v = fmaf(k[i], t[dy + i / 3][dx + i % 3], v);
-                    v = v * sc + sh;
-                    m = d == 0 ? v : nanmax(m, v);
-                }
+                    for (int i = 0; i < 9; ++i) {
+                        const f32x2 tap = {t[dy + i / 3][i % 3], t[dy + i / 3][1 + i % 3]};
+                        v[dy] = __builtin_elementwise_fma((f32x2){k[i], k[i]}, tap, v[dy]);
+                    }
+                const f32x2 scv = {sc, sc}, shv = {sh, sh};
+                v[0] = v[0] * scv + shv;
+                v[1] = v[1] * scv + shv;
+                const float m = nanmax(nanmax(v[0][0], v[0][1]), nanmax(v[1][0], v[1][1]));
                 acc[c] += m < 0.0f ? 0.0f : m;  // ReLU after the pool; NaN passes through as in torch
             }
         }

@@ -27,7 +27,7 @@ def main():
         x = cnn.to_nhwc(torch.rand((imgs, cin, hw, hw), device=dev))
         flops = layer.flops(x)
         res = []
-        for tid in range(16):
+        for tid in range(8):
             lib.fvp_conv_set_tile(tid)
             try:
                 layer(x, relu=True)

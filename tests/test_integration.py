@@ -295,3 +295,57 @@ def test_fused_forwards_with_fvp_cnn(gpu_device):
         np.testing.assert_allclose(gf.cpu().numpy(), rf.cpu().numpy(), atol=0.5, rtol=0)
     finally:
         integration.USE_FVP_CNN = False
+
+
+@pytest.mark.gpu
+def test_fused_hdn_forward_trains_like_reference_flow(gpu_device):
+    """Training (run/train.py: backbone frozen, HDN trained): in train mode the
+    fused forward keeps torch's CenterNet / C2CNet (BatchNorm batch statistics,
+    autograd) and feeds them the fvp cube, xy plane and columns.  The losses'
+    gradients on every CenterNet and C2CNet parameter match the reference flow's
+    (torch.max / torch.gather around the same modules) within fp32 rounding."""
+    import copy
+
+    import cnn_arch
+
+    from fvp import geometry, synthetic
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c3"]
+    J = w.num_joints
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 2)).to(gpu_device)
+    meta = {"seq": [seq] * 2}
+    net = types.SimpleNamespace()
+    net.project_layer = ProjectLayer(w.cfg(str(gpu_device)))
+    net.project_layer.verbose = False
+    cn = cnn_arch.CenterNet(J, 1)
+    cn.load_state_dict(synthetic.seeded_state_dict(cn, 12))
+    c2c = cnn_arch.C2CNet(J, 1)
+    c2c.load_state_dict(synthetic.seeded_state_dict(c2c, 14))
+    net.proposal_layer = _Proposal(w)
+    net.max_people = w.max_people
+    grads = []
+    for flow in ("fused", "reference"):
+        net.center_net = copy.deepcopy(cn).to(gpu_device).train()
+        net.c2c_net = copy.deepcopy(c2c).to(gpu_device).train()
+        integration.USE_FVP_CNN = True  # ignored in train mode
+        try:
+            if flow == "fused":
+                hm2d, hm1d, centers, bbox = integration.fused_hdn_forward(net, hm, meta, cams, rt)
+            else:
+                hm2d, hm1d, centers, bbox = _reference_flow(net, hm, meta, cams, rt)
+        finally:
+            integration.USE_FVP_CNN = False
+        loss = (hm2d ** 2).mean() + (hm1d ** 2).mean() + bbox.abs().mean()
+        loss.backward()
+        grads.append({n: p.grad.detach().clone() for m in (net.center_net, net.c2c_net)
+                      for n, p in m.named_parameters(prefix=type(m).__name__)})
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 40
+    for n in grads[0]:
+        g, r = grads[0][n], grads[1][n]
+        assert torch.isfinite(g).all(), n
+        scale = float(r.abs().max()) + 1e-12
+        assert float((g - r).abs().max()) <= 1e-4 * scale, (n, float((g - r).abs().max()), scale)

@@ -344,8 +344,16 @@ def test_fused_hdn_forward_trains_like_reference_flow(gpu_device):
         grads.append({n: p.grad.detach().clone() for m in (net.center_net, net.c2c_net)
                       for n, p in m.named_parameters(prefix=type(m).__name__)})
     assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 40
+    # A conv bias followed by train-mode BatchNorm has a gradient that is zero
+    # in exact arithmetic (the batch mean absorbs it); both flows leave only
+    # summation noise there (~1e-7 on GPU, differing run to run), so such
+    # parameters are checked to be ~0 in both flows rather than equal.
+    gmax = max(float(r.abs().max()) for r in grads[1].values())
     for n in grads[0]:
         g, r = grads[0][n], grads[1][n]
         assert torch.isfinite(g).all(), n
         scale = float(r.abs().max()) + 1e-12
+        if scale < 1e-4 * gmax:
+            assert float(g.abs().max()) < 1e-4 * gmax, (n, float(g.abs().max()), gmax)
+            continue
         assert float((g - r).abs().max()) <= 1e-4 * scale, (n, float((g - r).abs().max()), scale)

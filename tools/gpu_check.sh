@@ -16,8 +16,8 @@ run() {  # name timeout cmd...
 }
 for step in ${STEPS:-pytest smoke bench}; do
   case $step in
-    pytest) run pytest 400 python -m pytest tests -x -q -m gpu ;;
-    pytestall) run pytestall 400 python -m pytest tests -q -m gpu ;;
+    pytest) run pytest 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    pytestall) run pytestall 400 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread ;;
     smoke) run smoke 150 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --traffic off --cpu-seconds 5} ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 10 --warmup 2 --traffic off --cpu-baseline off ;;

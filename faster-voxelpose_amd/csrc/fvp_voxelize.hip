@@ -53,7 +53,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
                                                        int H, int W, int X, int Y, int Z, int cols, int col_blocks,
-                                                       int SP) {
+                                                       int SP, int band) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
@@ -63,7 +63,18 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     const int bl = L / col_blocks;  // frame within the chunk
     const int b = frame0 + bl;      // frame within the batch (outputs, grid_index)
     const int XY = X * Y;
-    const int c0 = (L - bl * col_blocks) * cols;
+    int cb = L - bl * col_blocks;
+    if (band > 0) {
+        // bands of `band` x-rows walked column-group-major: consecutive blocks
+        // (those resident together on an XCD) cover a compact x-y patch
+        const int gpr = Y / cols;  // column groups per x-row (host: Y % cols == 0)
+        const int per_band = band * gpr;
+        const int bi = cb / per_band, r = cb - bi * per_band;
+        const int rows = min(band, X - bi * band);
+        const int gc = r / rows, xr = r - gc * rows;
+        cb = (bi * band + xr) * gpr + gc;
+    }
+    const int c0 = cb * cols;
     const int ncols = min(cols, XY - c0);
     const int T = ncols * Z;
     const long long N = (long long)XY * Z;
@@ -212,9 +223,10 @@ __global__ __launch_bounds__(256, 8) void voxelize_kernel(const void *__restrict
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int H, int W, int X, int Y, int Z, int cols,
-                                                          int col_blocks, int SP) {
+                                                          int col_blocks, int SP, int band) {
     static_assert(!OTF, "grid kernel");
-    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
+                                  band);
 }
 
 template <int LPV, bool PAIR, bool OTF>
@@ -222,9 +234,10 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
                                                             const int32_t *__restrict__ grid_index, int frame0,
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
                                                             int J, int H, int W, int X, int Y, int Z, int cols,
-                                                            int col_blocks, int SP) {
+                                                            int col_blocks, int SP, int band) {
     static_assert(OTF, "on-the-fly kernel");
-    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
+                                  band);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -236,6 +249,8 @@ __global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict
     const int v = (int)(t - n * GV);
     out[t] = v < V ? g[(size_t)v * N + n] : make_float2(-2.f, -2.f);
 }
+
+constexpr int kBandRows = 16;
 
 static int cols_per_block(int Z) { return Z >= 320 ? 1 : 320 / Z; }
 
@@ -275,6 +290,16 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
     // latency (few frames): one pass of 256/LPV voxels per block, so a single
     // frame spreads over enough blocks to fill the CUs
     if ((long long)min(chunk, B) * ((X * Y + cols - 1) / cols) < 4 * 256) cols = max(1, (256 / LPV) / Z);
+    // Column groups that tile the x-rows exactly (largest divisor of Y, if it
+    // keeps at least half the columns), so the blocks can be walked in bands of
+    // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
+    // x-y patch, whose heatmap footprint is smaller (C5 -8 %, C4 -4 %, C2 0).
+    {
+        int c = cols;
+        while (c > 1 && Y % c != 0) --c;
+        if (2 * c >= cols) cols = c;
+    }
+    const int band = (Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
     const int col_blocks = (X * Y + cols - 1) / cols;
     const int SP = stage_pitch(LPV, cols, Z);
     size_t lds = (size_t)4 * LPV * SP * sizeof(float);
@@ -294,10 +319,10 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
         }
         if constexpr (OTF)
             hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true>), dim3((unsigned)(nb * col_blocks)), dim3(256),
-                               lds, s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+                               lds, s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
         else
             hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds,
-                               s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP);
+                               s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
     }
     return (int)hipGetLastError();
 }

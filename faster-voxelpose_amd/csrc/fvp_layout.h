@@ -124,13 +124,21 @@ struct Taps4 {
     float w[4];
 };
 
+// Top-left tap (x0, y0) of a sample at heatmap pixel (ix, iy).  NaN
+// coordinates read in-image taps so the NaN weights propagate (as in
+// grid_sample); far-off coordinates are clamped before the int conversion.
+__device__ __forceinline__ void tap_origin(float ix, float iy, int W, int H, int &x0, int &y0) {
+    const bool nan_ = (ix != ix) || (iy != iy);
+    x0 = nan_ ? 0 : (int)fminf(fmaxf(floorf(ix), -4.0f), (float)W + 4.0f);
+    y0 = nan_ ? 0 : (int)fminf(fmaxf(floorf(iy), -4.0f), (float)H + 4.0f);
+}
+
 template <bool PAIR>
 __device__ __forceinline__ Taps4<PAIR> setup_taps(float gx, float gy, float sxs, float sys, int W, int H,
                                                   unsigned unit) {
     Taps4<PAIR> t;
     const float ix = (gx + 1.0f) * sxs;
     const float iy = (gy + 1.0f) * sys;
-    const bool nan_ = (ix != ix) || (iy != iy);
     const float x0f = floorf(ix), y0f = floorf(iy);
     const float wx = ix - x0f, ex = 1.0f - wx;
     const float ny = iy - y0f, syw = 1.0f - ny;
@@ -138,10 +146,8 @@ __device__ __forceinline__ Taps4<PAIR> setup_taps(float gx, float gy, float sxs,
     t.w[1] = syw * wx;
     t.w[2] = ny * ex;
     t.w[3] = ny * wx;
-    // NaN coordinates read in-image taps so the NaN weights propagate (as in
-    // grid_sample); far-off coordinates are clamped before the int conversion.
-    const int x0 = nan_ ? 0 : (int)fminf(fmaxf(x0f, -4.0f), (float)W + 4.0f);
-    const int y0 = nan_ ? 0 : (int)fminf(fmaxf(y0f, -4.0f), (float)H + 4.0f);
+    int x0, y0;
+    tap_origin(ix, iy, W, H, x0, y0);
     const bool vy0 = (unsigned)y0 < (unsigned)H, vy1 = (unsigned)(y0 + 1) < (unsigned)H;
     if constexpr (PAIR) {
         const bool vx = (x0 >= -1) & (x0 < W);

@@ -29,6 +29,7 @@ def main():
     rt = resize_transform(w.ori_image_size, w.image_size).astype(np.float32)
     Wh, Hh = w.heatmap_size
     res = {s: [0, 0, []] for s in shapes}
+    tile_sum = {s: {} for s in shapes}  # per tile: pixels summed over cameras (4-px units, +2 pad px per row)
     for c in camera_list(cams, seq)[:6]:
         g = O.project_grid(grid, c, w.ori_image_size, w.image_size, w.heatmap_size, rt).reshape(X, Y, Z, 2)
         ix = (g[..., 0] + 1) * np.float32((Wh - 1) / 2)
@@ -59,11 +60,18 @@ def main():
                         px = int(np.where(hi >= lo, hi - lo + 1, 0).sum())
                         r[1] += px
                         r[2].append(px)
+                        u = np.where(hi >= lo, (hi >> 2) - (lo >> 2) + 1, 0)
+                        tile_sum[(tx, ty, tz)][(a, b, cz)] = (tile_sum[(tx, ty, tz)].get((a, b, cz), 0)
+                                                             + int((4 * u + 2 * (u > 0)).sum()))
     for s, (taps, px, lst) in res.items():
         a = np.array(lst)
         print(f"{name} tile {s}: staged px/taps {px / taps:.3f}; per tile-camera px mean {a.mean():.0f} "
               f"p99 {np.percentile(a, 99):.0f} max {a.max()} (KB at 64 B/px: mean {a.mean() * 64 / 1024:.0f}, "
               f"max {a.max() * 64 / 1024:.0f})")
+        ts = np.array(list(tile_sum[s].values()))
+        print(f"   per tile, summed over cameras (4-px units + pad): mean {ts.mean():.0f} px, p99 "
+              f"{np.percentile(ts, 99):.0f}, max {ts.max()} -> KB per fp32 joint: mean {ts.mean() * 4 / 1024:.1f} "
+              f"max {ts.max() * 4 / 1024:.1f}")
 
 
 if __name__ == "__main__":

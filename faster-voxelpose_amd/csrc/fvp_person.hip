@@ -107,22 +107,37 @@ __global__ __launch_bounds__(256) void max_planes_kernel(const float *__restrict
 //                         (x, z, joint) into the pre-zeroed plane (values are
 //                         clamped to [0,1] or NaN, so unsigned order == float order)
 // Outside-window voxels are 0 exactly as in the reference cube.
-template <int LPV, int YG>
+// Sampling coordinates of the fine grid: the packed per-sequence grid
+// (OTF = false) or projected on the fly from the camera records with the fp32
+// sequence of fvp_project_grid (OTF = true: no 197 MB fine grid to stream).
+struct PersonCoords {
+    const float *cams;      // [V][FVP_CAM_STRIDE]   (OTF)
+    const float *resize_t;  // [2][3]                (OTF)
+    fvp_grid_spec fine;     // fine whole-space grid (OTF)
+    fvp_image_spec im;      //                       (OTF)
+};
+
+template <int LPV, int YG, bool OTF>
 __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
-                                                             const float *__restrict__ fgrid,
+                                                             const float *__restrict__ fgrid, PersonCoords pc,
                                                              const float *__restrict__ props,
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
                                                              float *__restrict__ cubes, float *__restrict__ planes,
                                                              float *__restrict__ offset, int P, int V, int J, int H,
-                                                             int W) {
+                                                             int W, int xmap) {
     constexpr int JP = 4 * LPV;
     constexpr int NW = LPV;       // waves per block (64*LPV threads)
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
     __shared__ float xy_part[NW][YG][JP];
+    __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
     const int ngroups = (SY + YG - 1) / YG;
-    const int p = blockIdx.x / ngroups;
-    const int yg0 = (blockIdx.x - p * ngroups) * YG;
+    // XCD-aware: each XCD runs whole proposals, so the row groups of one
+    // proposal (walking x together) share that XCD's L2 footprint (L2 hit 35 %
+    // with round-robin placement)
+    const int L = xmap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int p = L / ngroups;
+    const int yg0 = (L - p * ngroups) * YG;
     const Window w = person_window(props + (size_t)p * 7, s);
     if (offset && yg0 == 0 && threadIdx.x < 3) {
         const int a = threadIdx.x;
@@ -140,7 +155,17 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     const float fV = (float)V;
     const int GV = V + (V & 1);
     const long long FN = (long long)s.fine[0] * s.fine[1] * s.fine[2];
-    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(fgrid, (unsigned)(FN * GV * 8));
+    __amdgpu_buffer_rsrc_t grs;
+    float rt[6];
+    if constexpr (OTF) {
+        for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 64 * LPV)
+            lcam[e] = e < V * FVP_CAM_STRIDE ? pc.cams[e] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) rt[k] = pc.resize_t[k];
+        __syncthreads();
+    } else {
+        grs = uniform_rsrc(fgrid, (unsigned)(FN * GV * 8));
+    }
     const char *__restrict__ frame_cl = (const char *)cl + (size_t)b * V * img;
     const size_t SS = (size_t)SY * SZ;
     const size_t S3 = (size_t)SX * SS;
@@ -169,13 +194,32 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             if (__builtin_amdgcn_ballot_w64(valid)) {
                 const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
+                float wxc = 0.f, wyc = 0.f, wzc = 0.f;  // OTF: fine voxel centre (compute_grid at fine resolution)
+                if constexpr (OTF) {
+                    wxc = axis_coord(pc.fine.start[0], pc.fine.end[0], s.fine[0], valid ? gx : 0, pc.fine.center[0]);
+                    wyc = axis_coord(pc.fine.start[1], pc.fine.end[1], s.fine[1], valid ? gy : 0, pc.fine.center[1]);
+                    wzc = axis_coord(pc.fine.start[2], pc.fine.end[2], s.fine[2], valid ? gz : 0, pc.fine.center[2]);
+                }
                 for (int v0 = 0; v0 < V; v0 += CPG) {
-                    // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
-                    const u32x4 graw =
-                        __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
                     float g[4];
+                    if constexpr (OTF) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) g[k] = valid ? __builtin_bit_cast(float, (unsigned)graw[k]) : -2.0f;
+                        for (int h = 0; h < 2; ++h) {
+                            const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
+                            float px, py;
+                            project_point(c, wxc, wyc, wzc, px, py);
+                            pixel_to_sample(px, py, rt, pc.im.ori_max, pc.im.img_w, pc.im.img_h, (float)pc.im.hm_w,
+                                            (float)pc.im.hm_h, g[2 * h], g[2 * h + 1]);
+                        }
+                    } else {
+                        // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
+                        const u32x4 graw =
+                            __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
                     const Taps4<false> t0 = setup_taps<false>(g[0], g[1], sxs, sys, W, H, pix_bytes);
                     const Taps4<false> t1 = setup_taps<false>(g[2], g[3], sxs, sys, W, H, pix_bytes);
                     static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
@@ -271,20 +315,26 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     }
 }
 
-template <int LPV>
-static void launch_person_cl(const float *cl, const float *fgrid, const float *props, const int32_t *frame_of,
-                             const fvp_person_spec &s, float *cubes, float *planes, float *offset, int P, int V, int J,
-                             int H, int W, hipStream_t st) {
+template <int LPV, bool OTF>
+static void launch_person_cl(const float *cl, const float *fgrid, const PersonCoords &pc, const float *props,
+                             const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
+                             float *offset, int P, int V, int J, int H, int W, hipStream_t st) {
     const int SY = s.bins[1];
-    if (P >= 64) {
-        const int ng = (SY + 7) / 8;
-        hipLaunchKernelGGL((person_cl_kernel<LPV, 8>), dim3((unsigned)(P * ng)), dim3(64 * LPV), 0, st, cl, fgrid,
-                           props, frame_of, s, cubes, planes, offset, P, V, J, H, W);
-    } else {
-        const int ng = (SY + 3) / 4;
-        hipLaunchKernelGGL((person_cl_kernel<LPV, 4>), dim3((unsigned)(P * ng)), dim3(64 * LPV), 0, st, cl, fgrid,
-                           props, frame_of, s, cubes, planes, offset, P, V, J, H, W);
-    }
+    // rows per block: 4 when the launch has >= 8 blocks per CU, fewer for small
+    // launches (per-frame calls) so they still fill the CUs (measured, C3, 5 cams:
+    // 320 proposals 14.4 -> 10.7 us each with XCD placement + 4 rows; 10: 60 -> 27)
+    int yg = 4;
+    while (yg > 1 && (long long)P * ((SY + yg - 1) / yg) < 2048) yg >>= 1;
+    const int xmap = 1;
+#define FVP_PERSON_LAUNCH(YGV)                                                                                       \
+    hipLaunchKernelGGL((person_cl_kernel<LPV, YGV, OTF>), dim3((unsigned)(P * ((SY + YGV - 1) / YGV))),         \
+                       dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, \
+                       xmap)
+    if (yg <= 1) FVP_PERSON_LAUNCH(1);
+    else if (yg <= 2) FVP_PERSON_LAUNCH(2);
+    else if (yg <= 4) FVP_PERSON_LAUNCH(4);
+    else FVP_PERSON_LAUNCH(8);
+#undef FVP_PERSON_LAUNCH
 }
 
 }  // namespace fvp
@@ -303,22 +353,25 @@ extern "C" size_t fvp_person_workspace_bytes(int B, int V, int J, int H, int W) 
     return (size_t)B * fvp::cl_frame_bytes(V, J, H, W);
 }
 
-extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int H, int W, const float *fine_grid,
-                                 const fvp_person_spec *spec, const float *proposals, const int32_t *frame_of, int P,
-                                 float *cubes, float *planes, float *offset, void *workspace, size_t workspace_bytes,
-                                 void *stream) {
-    if (!heatmaps || !fine_grid || !spec) return FVP_ERR_NULL;
+namespace fvp {
+
+static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, int W, const float *fine_grid,
+                             const PersonCoords *pc, const fvp_person_spec *spec, const float *proposals,
+                             const int32_t *frame_of, int P, float *cubes, float *planes, float *offset,
+                             void *workspace, size_t workspace_bytes, void *stream) {
+    if (!heatmaps || !spec || (!fine_grid && !pc)) return FVP_ERR_NULL;
     if (P <= 0) return FVP_OK;
     if (!proposals) return FVP_ERR_NULL;
     if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2) return FVP_ERR_SHAPE;
+    if (pc && V > 64) return FVP_ERR_SHAPE;  // camera records staged in LDS
     const int SX = spec->bins[0], SY = spec->bins[1], SZ = spec->bins[2];
     if (SX <= 0 || SY <= 0 || SZ <= 0 || SZ > 64 || spec->fine[0] <= 1 || spec->fine[1] <= 1 || spec->fine[2] <= 1)
         return FVP_ERR_SHAPE;
     if (planes && !(SX == SY && SY == SZ)) return FVP_ERR_SHAPE;  // torch.cat of the planes needs a cubic volume
     // packed fine grid addressed with 32-bit byte offsets
-    if ((long long)spec->fine[0] * spec->fine[1] * spec->fine[2] * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL)
+    if (!pc && (long long)spec->fine[0] * spec->fine[1] * spec->fine[2] * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL)
         return FVP_ERR_SHAPE;
-    const size_t need = (size_t)B * fvp::cl_frame_bytes(V, J, H, W);
+    const size_t need = (size_t)B * cl_frame_bytes(V, J, H, W);
     if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
     float *cl = reinterpret_cast<float *>(workspace);
@@ -326,12 +379,18 @@ extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int
         const hipError_t e = hipMemsetAsync(planes + (size_t)P * J * SX * SZ, 0, (size_t)P * J * SX * SZ * 4, st);
         if (e != hipSuccess) return (int)e;
     }
-    const float *fg = fine_grid;
+    const PersonCoords none{};
+    const PersonCoords &c = pc ? *pc : none;
 #define FVP_PERSON_CASE(L)                                                                                            \
-    fvp::launch_layout<L, float>(heatmaps, B, V, J, H, W, cl, st);                                                   \
-    fvp::launch_person_cl<L>(cl, fg, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, W, st);         \
+    launch_layout<L, float>(heatmaps, B, V, J, H, W, cl, st);                                                        \
+    if (pc)                                                                                                           \
+        launch_person_cl<L, true>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, W,  \
+                                  st);                                                                                \
+    else                                                                                                              \
+        launch_person_cl<L, false>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H,  \
+                                   W, st);                                                                            \
     break;
-    switch (fvp::lanes_per_voxel(J)) {
+    switch (lanes_per_voxel(J)) {
         case 1: FVP_PERSON_CASE(1)
         case 2: FVP_PERSON_CASE(2)
         case 4: FVP_PERSON_CASE(4)
@@ -339,4 +398,29 @@ extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int
     }
 #undef FVP_PERSON_CASE
     return (int)hipGetLastError();
+}
+
+}  // namespace fvp
+
+extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int H, int W, const float *fine_grid,
+                                 const fvp_person_spec *spec, const float *proposals, const int32_t *frame_of, int P,
+                                 float *cubes, float *planes, float *offset, void *workspace, size_t workspace_bytes,
+                                 void *stream) {
+    if (!fine_grid) return FVP_ERR_NULL;
+    return fvp::person_planes_any(heatmaps, B, V, J, H, W, fine_grid, nullptr, spec, proposals, frame_of, P, cubes,
+                                  planes, offset, workspace, workspace_bytes, stream);
+}
+
+extern "C" int fvp_person_planes_cams(const float *heatmaps, int B, int V, int J, int H, int W, const float *cams,
+                                      const float *resize_t, const fvp_grid_spec *fine_grid_spec,
+                                      const fvp_image_spec *img, const fvp_person_spec *spec, const float *proposals,
+                                      const int32_t *frame_of, int P, float *cubes, float *planes, float *offset,
+                                      void *workspace, size_t workspace_bytes, void *stream) {
+    if (!cams || !resize_t || !fine_grid_spec || !img) return FVP_ERR_NULL;
+    if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
+    for (int a = 0; a < 3; ++a)
+        if (fine_grid_spec->bins[a] != spec->fine[a]) return FVP_ERR_SHAPE;
+    const fvp::PersonCoords pc{cams, resize_t, *fine_grid_spec, *img};
+    return fvp::person_planes_any(heatmaps, B, V, J, H, W, nullptr, &pc, spec, proposals, frame_of, P, cubes, planes,
+                                  offset, workspace, workspace_bytes, stream);
 }

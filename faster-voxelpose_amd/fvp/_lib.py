@@ -54,6 +54,10 @@ SIGNATURES = {
     "fvp_person_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
     "fvp_person_planes": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, ctypes.POINTER(PersonSpec), c_void_p,
                           c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
+    "fvp_person_planes_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                               ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), ctypes.POINTER(PersonSpec),
+                               c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t,
+                               c_void_p],
     "fvp_max_planes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_soft_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "fvp_fuse_poses": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
@@ -70,7 +74,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _LIB = None
 
 

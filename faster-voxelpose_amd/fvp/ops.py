@@ -277,6 +277,54 @@ def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: to
     return cubes, planes, offset
 
 
+@torch.library.custom_op("fvp::person_planes_cams", mutates_args=(), device_types="cuda")
+def person_planes_cams(heatmaps: torch.Tensor, cams: torch.Tensor, resize_t: torch.Tensor, start: list[float],
+                       end: list[float], center: list[float], ori_max: float, img_w: float, img_h: float,
+                       proposals: torch.Tensor, frame_of: Optional[torch.Tensor], fine: list[int], scale: list[float],
+                       bias: list[float], whole_size: list[float], ind_size: list[float], bins: list[int],
+                       want_cubes: bool, want_planes: bool) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """person_planes with the fine-grid coordinates projected on the fly from camera
+    records [V,FVP_CAM_STRIDE] (fvp_person_planes_cams): no fine sample grid."""
+    hm = _dev_f32(heatmaps, "heatmaps")
+    cm = _dev_f32(cams, "cams")
+    rt = _dev_f32(resize_t, "resize_transform")
+    pc = _dev_f32(proposals, "proposal_centers")
+    B, V, J, H, W = hm.shape
+    P = pc.shape[0]
+    if cm.shape[0] != V:
+        raise _lib.FvpError(f"fvp: {cm.shape[0]} camera records for {V} heatmap views")
+    fo = None
+    if frame_of is not None:
+        fo = frame_of.to(device=hm.device, dtype=torch.int32).contiguous()
+        if fo.numel() != P:
+            raise _lib.FvpError("fvp: frame_of must have one entry per proposal")
+    SX, SY, SZ = bins
+    cubes = torch.empty((P, J, SX, SY, SZ) if want_cubes else (0,), dtype=torch.float32, device=hm.device)
+    planes = torch.empty((3 * P, J, SX, SY) if want_planes else (0,), dtype=torch.float32, device=hm.device)
+    offset = torch.empty((P, 3), dtype=torch.float32, device=hm.device)
+    if P > 0:
+        ws_bytes = _lib.load().fvp_person_workspace_bytes(B, V, J, H, W)
+        if ws_bytes == 0:
+            raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
+        spec = PersonSpec(_i3(fine), _f3(scale), _f3(bias), _f3(whole_size), _f3(ind_size), _i3(bins))
+        g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(fine))
+        im = ImageSpec(ori_max, img_w, img_h, W, H)
+        _lib.call("fvp_person_planes_cams", _ptr(hm), B, V, J, H, W, _ptr(cm), _ptr(rt), g, im, spec, _ptr(pc),
+                  _ptr(fo), P, _ptr(cubes) if want_cubes else None, _ptr(planes) if want_planes else None,
+                  _ptr(offset), _ptr(ws), ws_bytes, _stream(hm))
+    return cubes, planes, offset
+
+
+@person_planes_cams.register_fake
+def _(heatmaps, cams, resize_t, start, end, center, ori_max, img_w, img_h, proposals, frame_of, fine, scale, bias,
+      whole_size, ind_size, bins, want_cubes, want_planes):
+    P, J = proposals.shape[0], heatmaps.shape[2]
+    return (heatmaps.new_empty((P, J, bins[0], bins[1], bins[2]) if want_cubes else (0,)),
+            heatmaps.new_empty((3 * P, J, bins[0], bins[1]) if want_planes else (0,)),
+            heatmaps.new_empty((P, 3)))
+
+
 @person_planes.register_fake
 def _(heatmaps, fine_grid, proposals, frame_of, fine, scale, bias, whole_size, ind_size, bins, want_cubes,
       want_planes):

@@ -17,11 +17,21 @@ proposal of a batch of frames in one launch.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
 
 from . import geometry, ops
+
+
+# Fine-grid sampling coordinates: read from the per-sequence packed fine grid
+# (197 MB for 5 cameras; measured faster: C3, 320 proposals, 10.7 vs 11.7 us
+# each) unless that grid would exceed this size (e.g. 31 cameras: 1 GB), then
+# projected on the fly (fvp_person_planes_cams).  FVP_PERSON_OTF=1/0 forces.
+PERSON_OTF_GRID_BYTES = 512 << 20
+PERSON_ON_THE_FLY = {"1": True, "0": False}.get(os.environ.get("FVP_PERSON_OTF", ""))
 
 
 class ProjectLayer(nn.Module):
@@ -46,6 +56,8 @@ class ProjectLayer(nn.Module):
         self._fine_grid = None
         self.sample_grid = {}  # seq -> [V, FX, FY, FZ, 2] (the reference's cache; a view of _packed)
         self._packed = {}      # seq -> [FX*FY*FZ, GV, 2] voxel-major copy read by the person kernel
+        self._cams = {}        # seq -> [V, FVP_CAM_STRIDE] camera records (on-the-fly projection)
+        self.on_the_fly = None  # None: by fine-grid size (PERSON_OTF_GRID_BYTES); True/False: force
         self.verbose = True
 
     @staticmethod
@@ -105,6 +117,33 @@ class ProjectLayer(nn.Module):
             self._packed[curr_seq] = pg
         return pg
 
+    def _otf(self, V: int) -> bool:
+        if self.on_the_fly is not None:
+            return bool(self.on_the_fly)
+        if PERSON_ON_THE_FLY is not None:
+            return PERSON_ON_THE_FLY
+        fine = [int(v) for v in self._const["fine"]]
+        return fine[0] * fine[1] * fine[2] * ops.grid_slots(V) * 8 > PERSON_OTF_GRID_BYTES
+
+    def _run(self, heatmaps, index, meta, cameras, resize_transform, props, frame_of, cubes, planes):
+        """One fvp_person_planes[_cams] launch for ``props`` of the frames of ``heatmaps``
+        (the coordinates of ``meta['seq'][index]``'s cameras)."""
+        if self._otf(heatmaps.shape[1]):
+            seq = meta["seq"][index]
+            if seq not in self._cams:
+                self._cams[seq] = torch.from_numpy(geometry.pack_cameras(cameras, seq)).to(heatmaps.device)
+            c = self._const
+            start = [float(np.float32(-float(v) / 2)) for v in c["whole_size"]]
+            end = [float(np.float32(float(v) / 2)) for v in c["whole_size"]]
+            return ops.person_planes_cams(heatmaps, self._cams[seq],
+                                          resize_transform.to(device=heatmaps.device, dtype=torch.float32),
+                                          start, end, [float(v) for v in c["whole_center"]],
+                                          float(max(self.ori_image_size[0], self.ori_image_size[1])),
+                                          float(self.image_size[0]), float(self.image_size[1]), props, frame_of,
+                                          *self._args(), cubes, planes)
+        grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
+        return ops.person_planes(heatmaps, grid, props, frame_of, *self._args(), cubes, planes)
+
     def _args(self):
         c = self._const
         return ([int(v) for v in c["fine"]], [float(v) for v in c["scale"]], [float(v) for v in c["bias"]],
@@ -113,18 +152,16 @@ class ProjectLayer(nn.Module):
 
     def forward(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
         ops.forward_only(heatmaps, proposal_centers)
-        grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
-        cubes, _, offset = ops.person_planes(heatmaps[index:index + 1], grid, proposal_centers, None, *self._args(),
-                                             True, False)
+        cubes, _, offset = self._run(heatmaps[index:index + 1], index, meta, cameras, resize_transform,
+                                     proposal_centers, None, True, False)
         return cubes, offset
 
     def forward_planes(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
         """(planes[3P,J,S,S], offset[P,3]) without materialising the cubes: the JLN
         input at joint_localization_net.py:158-160 for frame ``index``."""
         ops.forward_only(heatmaps, proposal_centers)
-        grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
-        _, planes, offset = ops.person_planes(heatmaps[index:index + 1], grid, proposal_centers, None, *self._args(),
-                                              False, True)
+        _, planes, offset = self._run(heatmaps[index:index + 1], index, meta, cameras, resize_transform,
+                                      proposal_centers, None, False, True)
         return planes, offset
 
     def forward_batch(self, heatmaps, meta, proposal_centers, mask, cameras, resize_transform):
@@ -134,12 +171,11 @@ class ProjectLayer(nn.Module):
         Returns (planes [3P,J,S,S] in (frame, proposal) order of ``mask``, offset
         [P,3], frame_of [P]).  Frames must share one sequence's cameras."""
         ops.forward_only(heatmaps, proposal_centers)
-        grid = self._seq_grid(heatmaps, 0, meta, cameras, resize_transform)
         seqs = list(meta["seq"])[: heatmaps.shape[0]]
         if len(set(seqs)) != 1:
             raise ValueError("forward_batch: all frames must belong to one sequence")
         idx = mask.nonzero()  # one host sync for the whole batch
         frame_of = idx[:, 0].to(torch.int32)
         props = proposal_centers[idx[:, 0], idx[:, 1]]
-        _, planes, offset = ops.person_planes(heatmaps, grid, props, frame_of, *self._args(), False, True)
+        _, planes, offset = self._run(heatmaps, 0, meta, cameras, resize_transform, props, frame_of, False, True)
         return planes, offset, frame_of

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 4
+#define FVP_ABI_VERSION 5
 #define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
 #define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
 /* Camera slots per voxel in a packed grid (V rounded up to even). */
@@ -169,6 +169,20 @@ int fvp_person_planes(const float *heatmaps, int B, int V, int J, int H, int W,
                       const float *proposals, const int32_t *frame_of, int P,
                       float *cubes, float *planes, float *offset,
                       void *workspace, size_t workspace_bytes, void *stream);
+/* Same with the fine-grid sampling coordinates projected on the fly from the
+ * camera records (the fp32 sequence of fvp_project_grid over the fine
+ * whole-space grid) instead of read from the 197 MB (5 cameras) packed fine
+ * grid -- no per-sequence fine-grid build.
+ *   cams            device [V][FVP_CAM_STRIDE] (V <= 64)
+ *   resize_t        device [2][3]
+ *   fine_grid_spec  the fine whole-space grid (bins == spec->fine)
+ *   img             image geometry (hm_w/hm_h == W/H) */
+int fvp_person_planes_cams(const float *heatmaps, int B, int V, int J, int H, int W,
+                           const float *cams, const float *resize_t, const fvp_grid_spec *fine_grid_spec,
+                           const fvp_image_spec *img, const fvp_person_spec *spec,
+                           const float *proposals, const int32_t *frame_of, int P,
+                           float *cubes, float *planes, float *offset,
+                           void *workspace, size_t workspace_bytes, void *stream);
 
 /* xy / xz / yz max-projections of per-person cubes [P][J][S][S][S] into
  * planes [3P][J][S][S] (xy block first, then xz, then yz).

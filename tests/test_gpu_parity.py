@@ -145,7 +145,10 @@ def test_gather_bbox_matches_torch_gather(gpu_device):
     assert torch.equal(got, ref)
 
 
-def test_person_cubes_and_planes_match_reference(gpu_device):
+@pytest.mark.parametrize("otf", [True, False], ids=["onthefly", "finegrid"])
+def test_person_cubes_and_planes_match_reference(gpu_device, otf):
+    """Both coordinate sources of the per-person kernel (fine grid projected on
+    the fly, or the packed per-sequence fine grid) against the reference's cubes."""
     from fvp.workloads import WORKLOADS
     from fvp.project_individual import ProjectLayer
 
@@ -153,6 +156,7 @@ def test_person_cubes_and_planes_match_reference(gpu_device):
     w = WORKLOADS["c3"]
     layer = ProjectLayer(w.cfg(str(gpu_device)))
     layer.verbose = False
+    layer.on_the_fly = otf
     cams, seq = w.cameras()
     assert np.array_equal(layer.center_grid.cpu().numpy(), d["center_grid"])
     assert np.array_equal(layer.fine_voxels_per_axis.cpu().numpy(), d["fine"])
@@ -161,7 +165,7 @@ def test_person_cubes_and_planes_match_reference(gpu_device):
     props = torch.from_numpy(d["proposals"]).to(gpu_device)
     cubes, offset = layer(hm, 0, {"seq": [seq]}, props, cams, rt)
     planes = torch.ops.fvp.max_planes(cubes)
-    fsg = layer.sample_grid[seq].cpu().numpy()
+    fsg = layer.build_sample_grid(cams, seq, rt, gpu_device).cpu().numpy()
     _assert_same(fsg.reshape(fsg.shape[0], -1, 2)[:, d["fine_sub"]], d["fine_sample_grid_sub"], "fine sample grid")
     _assert_same(offset.cpu().numpy(), d["offset"], "offset")
     _assert_same(planes.cpu().numpy(), d["planes"], "planes")
@@ -434,17 +438,19 @@ def _props(w, f, rng, n_extra):
     return np.concatenate([base, extra])
 
 
+@pytest.mark.parametrize("otf", [True, False], ids=["onthefly", "finegrid"])
 @pytest.mark.parametrize("J", [15, 17])
-def test_person_planes_fused_vs_oracle(gpu_device, J):
+def test_person_planes_fused_vs_oracle(gpu_device, J, otf):
     """Fused planes (no cube) == max-projections of the oracle's cubes, incl.
     clipped, skipped and negative-margin windows; J=17 takes the 8-lane path."""
     from fvp import geometry
 
     w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, J=J, frames=1)
+    layer.on_the_fly = otf
     props = _props(w, 0, np.random.default_rng(1), 6)
     planes, offset = layer.forward_planes(hm, 0, {"seq": [seq]}, torch.from_numpy(props).to(gpu_device), cams, rt)
     ind = O.Individual(w.space_size, w.space_center, w.ind_space_size, w.ind_voxels_per_axis)
-    fsg = layer.sample_grid[seq].cpu().numpy()
+    fsg = layer.build_sample_grid(cams, seq, rt, gpu_device).cpu().numpy()
     cubes, off = ind.person_cubes(hm[0].cpu().numpy(), fsg, props)
     _assert_same(planes.cpu().numpy(), O.max_planes(cubes), "fused planes")
     _assert_same(offset.cpu().numpy(), off, "offset")
@@ -452,9 +458,11 @@ def test_person_planes_fused_vs_oracle(gpu_device, J):
     _assert_same(c2.cpu().numpy(), cubes, "cubes")
 
 
-def test_person_planes_batched_matches_per_frame(gpu_device):
-    """forward_batch (one launch, >= 64 proposals -> 8-row blocks) == per-frame calls."""
+@pytest.mark.parametrize("otf", [True, False], ids=["onthefly", "finegrid"])
+def test_person_planes_batched_matches_per_frame(gpu_device, otf):
+    """forward_batch (one launch, >= 64 proposals -> 4-row blocks) == per-frame calls (1-row blocks)."""
     w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, frames=8)
+    layer.on_the_fly = otf
     rng = np.random.default_rng(2)
     props = torch.from_numpy(np.stack([_props(w, f, rng, 6) for f in range(8)])).to(gpu_device)  # [8,10,7]
     mask = torch.rand((8, 10), generator=torch.Generator().manual_seed(3)).to(gpu_device) > 0.15
@@ -525,3 +533,18 @@ def test_captured_graph_step_matches_eager(gpu_device):
         ref = step()
         for g, r in zip(got, ref):
             assert torch.equal(g, r)
+
+
+def test_person_planes_on_the_fly_equals_fine_grid(gpu_device):
+    """Batched planes and offsets: the on-the-fly projection and the packed fine
+    grid give bit-identical results (same fp32 projection sequence)."""
+    w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, frames=6)
+    rng = np.random.default_rng(4)
+    props = torch.from_numpy(np.stack([_props(w, f, rng, 6) for f in range(6)])).to(gpu_device)
+    mask = torch.ones((6, props.shape[1]), dtype=torch.bool, device=gpu_device)
+    meta = {"seq": [seq] * 6}
+    layer.on_the_fly = True
+    p1, o1, f1 = layer.forward_batch(hm, meta, props, mask, cams, rt)
+    layer.on_the_fly = False
+    p2, o2, f2 = layer.forward_batch(hm, meta, props, mask, cams, rt)
+    assert torch.equal(p1, p2) and torch.equal(o1, o2) and torch.equal(f1, f2)

@@ -294,12 +294,14 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
     // keeps at least half the columns), so the blocks can be walked in bands of
     // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
     // x-y patch, whose heatmap footprint is smaller (C5 -8 %, C4 -4 %, C2 0).
-    {
+    // Small grids (C1: 400 columns) keep their column groups (measured -6 % with bands).
+    const bool big = (long long)X * Y >= 4096;
+    if (big) {
         int c = cols;
         while (c > 1 && Y % c != 0) --c;
         if (2 * c >= cols) cols = c;
     }
-    const int band = (Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
+    const int band = (big && Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
     const int col_blocks = (X * Y + cols - 1) / cols;
     const int SP = stage_pitch(LPV, cols, Z);
     size_t lds = (size_t)4 * LPV * SP * sizeof(float);

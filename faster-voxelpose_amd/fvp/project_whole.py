@@ -13,17 +13,23 @@ Registers no parameters or buffers, so checkpoints load unchanged.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
 
 from . import geometry, ops
 
-# A packed grid above this size would not stay cache-resident between frames
-# (MI355X: 4 MB L2 per XCD, 256 MB Infinity Cache); such configurations project
-# the coordinates on the fly instead (fvp_voxelize_cams), e.g. C5: 31 cameras x
-# 160x160x64 = 420 MB.  Measured: C5 1.27x faster on the fly, C2/C4 faster cached.
-ON_THE_FLY_GRID_BYTES = 128 << 20
+# Above this size a packed grid streams from HBM once per frame (MI355X: 4 MB
+# L2 per XCD, 256 MB Infinity Cache) and the coordinates are projected on the
+# fly instead (fvp_voxelize_cams).  Measured on the C5 geometry with the first
+# V ring cameras (tools/c5_views.py, 8 frames): V=16 (210 MB grid) 1.63 ms
+# cached vs 2.07 on the fly, V=24 (314 MB) 2.77 vs ~3.0, V=31 (406 MB) 3.76 vs
+# 3.84 (B=32: 2,124 vs 2,106 frames/s) -- a tie, so the 406 MB grid is not kept.
+ON_THE_FLY_GRID_BYTES = 384 << 20
+# "1"/"0" forces the choice for every layer (A/B measurements)
+ON_THE_FLY = {"1": True, "0": False}.get(os.environ.get("FVP_OTF", ""))
 
 
 def _as_list3(v, kind=float):
@@ -114,6 +120,8 @@ class ProjectLayer(nn.Module):
     def _project_on_the_fly(self, V) -> bool:
         if self.on_the_fly is not None:
             return bool(self.on_the_fly)
+        if ON_THE_FLY is not None:
+            return ON_THE_FLY
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         return X * Y * Z * ops.grid_slots(V) * 8 > ON_THE_FLY_GRID_BYTES
 

@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--graph", choices=["on", "off"], default="off",
                     help="replay the GPU-local part of the step from captured hipGraphs (the collective stays eager)")
+    ap.add_argument("--slabs", action="store_true",
+                    help="large-frame mode (SURVEY.md §8(e)): every rank holds the same frames and voxelises one "
+                         "x-slab of each; strong scaling")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -74,6 +77,8 @@ def collect_traffic(args):
                "--workload", args.workload, "--traffic", "off", "--cpu-baseline", "off"]
         if args.batch:
             cmd += ["--batch", str(args.batch)]
+        if args.slabs:
+            cmd += ["--slabs"]
         try:
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            cwd=REPO)
@@ -141,10 +146,13 @@ def main():
     from fvp.proposal import nms2D, gather_columns
     from fvp.workloads import WORKLOADS
 
+    local_rank %= max(1, torch.cuda.device_count())  # identity with one rank per GPU
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # FVP_BENCH_BACKEND=gloo: plumbing rehearsal of N ranks (not a measurement)
+        backend = os.environ.get("FVP_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     w = WORKLOADS[args.workload]
     B = args.batch or DEFAULT_BATCH.get(args.workload, 64)
@@ -159,7 +167,9 @@ def main():
     layer = ProjectLayer(w.cfg(str(dev)))
     layer.verbose = False
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
-    hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=rank * B)
+    # large-frame mode: all ranks hold the same frames (x-slabs); otherwise own frames
+    hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=0 if args.slabs else rank * B)
+    x0, x1 = parallel.shard_slab(X, world, rank) if args.slabs else (0, X)
     hm = torch.from_numpy(hm_host).to(dev)
     if w.dtype == "float16":  # C5: fp16 heatmaps (computed in fp32 by the kernels)
         hm = hm.half()
@@ -177,12 +187,20 @@ def main():
     ev = []
 
     def vox():
+        if args.slabs:
+            return layer.forward_slab(hm, meta, cams, rt, x0, x1, want_cube=True, want_xy=True)
         return layer.forward_fused(hm, meta, cams, rt, want_cube=True, want_xy=True)
 
     def post(cube, xy):
+        if args.slabs and world > 1:  # xy slabs -> full planes; owned columns -> one all-reduce
+            xy = parallel.gather_xy_slabs(xy, X)
+            vals, idx, flat = nms2D(xy[:, root:root + 1], K)
+            return vals, flat, parallel.columns_from_slab(cube, flat, x0)
         vals, idx, flat = nms2D(xy[:, root:root + 1], K)
         return vals, flat, gather_columns(cube, flat)
 
+    if args.graph == "on" and args.slabs and world > 1:
+        raise SystemExit("--graph on captures GPU-local work only; the slab collectives sit inside post()")
     if args.graph == "on":  # two hipGraphs: the voxelize op (timed on its own) and NMS + columns
         from fvp.graphs import CapturedStep
 
@@ -202,7 +220,7 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         vals, flat, cols = run_post(cube, xy)
-        if world > 1:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
+        if world > 1 and not args.slabs:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
             parallel.gather_proposals(vals, flat)
         return cols
 
@@ -227,16 +245,17 @@ def main():
         return
 
     vox_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    frames = world * B * args.steps
+    frames = (1 if args.slabs else world) * B * args.steps
     fps = frames / el
-    per_frame = V * J * Hd * Wd * hm.element_size() + J * X * Y * Z * 4 + J * X * Y * 4
+    Xs = x1 - x0  # this rank's x-rows (X unless --slabs)
+    per_frame = V * J * Hd * Wd * hm.element_size() + J * Xs * Y * Z * 4 + J * Xs * Y * 4
     alg_bytes = B * per_frame
     achieved = alg_bytes / (vox_ms * 1e-3) / 1e9
 
     # secondary bound: the bilinear tap rate, N*V*J*4 joint-taps
     # per frame, against the per-CU vector-memory (texture addresser / L1) rate of
     # 64 B/clk: 16 fp32 joint-taps/clk/CU, 32 with the fp16 pixel-pair table.
-    taps = B * X * Y * Z * V * J * 4
+    taps = B * Xs * Y * Z * V * J * 4
     tap_bytes = 2 if (hm.element_size() == 2 and J <= 16) else 4
     tap_peak = 256 * 2.4e9 * 64 / tap_bytes / 1e12
     tap_rate = taps / (vox_ms * 1e-3) / 1e12
@@ -302,7 +321,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.slabs else "weak",
             "vs_baseline": None,
             "dtype": "f32" if w.dtype == "float32" else "f16-in/f32",
             "data": "synthetic",
@@ -310,8 +329,10 @@ def main():
                 "workload": f"{w.name}: {WORKLOAD_DESC.get(w.name, '')}, {V} cams, J={J}, "
                             f"{Hd}x{Wd} heatmaps -> {X}x{Y}x{Z} voxels, K={K} proposals",
                 "frames_per_gpu_step": B,
-                "global_batch": world * B,
-                "parallelism": f"frame-sharded x{world}" + (" + RCCL all_gather of proposals" if world > 1 else ""),
+                "global_batch": B if args.slabs else world * B,
+                "parallelism": (f"x-slab x{world}" + (" + RCCL all_gather of xy slabs, all_reduce of columns"
+                                                      if world > 1 else "") if args.slabs else
+                                f"frame-sharded x{world}" + (" + RCCL all_gather of proposals" if world > 1 else "")),
             },
             "roofline": {
                 "bound": "hbm",

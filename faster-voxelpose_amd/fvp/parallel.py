@@ -5,6 +5,13 @@ contiguous slice of the batch, voxelises it with no communication, and the
 compact per-frame results (top-K proposal values and flat indices) are
 collected with ONE all-gather -- RCCL over xGMI with the "nccl" backend, gloo
 on CPU for tests.  Cubes and planes never leave their GPU.
+
+Large-frame mode (for C5-sized grids at small batch): every
+rank holds the same frames and voxelises one x-slab of each
+(ProjectLayer.forward_slab); ONE all-gather assembles the xy planes for the
+replicated CenterNet / NMS, and ONE all-reduce of the K proposal columns
+(each owned by exactly one rank, zeros elsewhere) replaces the local column
+gather.  Cube slabs never leave their GPU.
 """
 from __future__ import annotations
 
@@ -45,3 +52,45 @@ def gather_proposals(vals: torch.Tensor, flat: torch.Tensor, group=None) -> tupl
         dist.all_gather(parts, local, group=group)
         out = torch.cat(parts)
     return unpack_proposals(out, K)
+
+
+def shard_slab(X: int, world: int, rank: int) -> tuple[int, int]:
+    """x-slab [x0, x1) of an X-row voxel grid for ``rank`` (sizes differ by at most one)."""
+    if X < world:
+        raise ValueError(f"cannot split {X} x-rows over {world} ranks")
+    return shard_frames(X, world, rank)
+
+
+def gather_xy_slabs(xy_slab: torch.Tensor, X: int, group=None) -> torch.Tensor:
+    """Every rank's [B,J,x1-x0,Y] xy slab -> the full [B,J,X,Y] planes on every rank."""
+    world = dist.get_world_size(group)
+    B, J, _, Y = xy_slab.shape
+    spans = [shard_slab(X, world, r) for r in range(world)]
+    xm = max(e - s for s, e in spans)
+    local = xy_slab.new_zeros((xm, B, J, Y))
+    local[: xy_slab.shape[2]] = xy_slab.permute(2, 0, 1, 3)  # x-major so the gather concatenates slabs
+    out = xy_slab.new_empty((world * xm, B, J, Y))
+    try:
+        dist.all_gather_into_tensor(out, local, group=group)
+    except (RuntimeError, NotImplementedError):
+        parts = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(parts, local, group=group)
+        out = torch.cat(parts)
+    rows = torch.cat([out[r * xm: r * xm + (e - s)] for r, (s, e) in enumerate(spans)])
+    return rows.permute(1, 2, 0, 3).contiguous()
+
+
+def columns_from_slab(cube_slab: torch.Tensor, flat: torch.Tensor, x0: int, group=None, gather=None) -> torch.Tensor:
+    """feature_1d [B,K,J,Z] (human_detection_net.py:199-200) for proposals at
+    global flat index x*Y + y, from x-slabs [B,J,Xs,Y,Z] starting at row x0:
+    each rank gathers the columns it owns (zeros elsewhere), one SUM all-reduce
+    (exact: one non-zero term per element)."""
+    if gather is None:
+        from .proposal import gather_columns as gather
+    Xs, Y = cube_slab.shape[2], cube_slab.shape[3]
+    local = flat - x0 * Y
+    own = (local >= 0) & (local < Xs * Y)
+    cols = gather(cube_slab, torch.where(own, local, torch.zeros_like(local)))
+    cols = torch.where(own[:, :, None, None], cols, torch.zeros((), dtype=cols.dtype, device=cols.device))
+    dist.all_reduce(cols, op=dist.ReduceOp.SUM, group=group)
+    return cols

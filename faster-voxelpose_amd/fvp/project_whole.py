@@ -161,6 +161,26 @@ class ProjectLayer(nn.Module):
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
         return ops.voxelize(heatmaps, grids, index, X, Y, Z, want_cube, want_xy)
 
+    def forward_slab(self, heatmaps, meta, cameras, resize_transform, x_begin: int, x_end: int,
+                     want_cube=True, want_xy=True):
+        """Voxels with x in [x_begin, x_end) only: (cube[B,J,x_end-x_begin,Y,Z], xy[B,J,x_end-x_begin,Y]).
+
+        The large-frame mode of SURVEY.md §8(e): each rank of a group owns an
+        x-slab of every frame (fvp.parallel.shard_slab).  The packed grid is
+        voxel-major with x slowest, so a slab is a contiguous slice of it and
+        the kernel runs unchanged on X' = x_end - x_begin rows; every voxel and
+        every (x, y) column lies wholly in one slab, so the slabs are
+        bit-identical to the same rows of forward_fused.  Always reads the
+        cached grid (a rank touches only its slab: 1/k of the grid)."""
+        ops.forward_only(heatmaps)
+        X, Y, Z = _as_list3(self.voxels_per_axis, int)
+        if not 0 <= x_begin < x_end <= X:
+            raise ValueError(f"x-slab [{x_begin}, {x_end}) outside [0, {X})")
+        grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
+        n0, n1 = x_begin * Y * Z, x_end * Y * Z
+        slab = grids[n0:n1] if grids.dim() == 3 else grids[:, n0:n1].contiguous()
+        return ops.voxelize(heatmaps, slab, index, x_end - x_begin, Y, Z, want_cube, want_xy)
+
     def forward(self, heatmaps, meta, cameras, resize_transform):
         cube, _ = self.forward_fused(heatmaps, meta, cameras, resize_transform, want_cube=True, want_xy=False)
         return cube

@@ -548,3 +548,29 @@ def test_person_planes_on_the_fly_equals_fine_grid(gpu_device):
     layer.on_the_fly = False
     p2, o2, f2 = layer.forward_batch(hm, meta, props, mask, cams, rt)
     assert torch.equal(p1, p2) and torch.equal(o1, o2) and torch.equal(f1, f2)
+
+
+@pytest.mark.parametrize("wname,nslab,half", [("c2", 2, False), ("c4", 3, False), ("c2", 3, True)])
+def test_x_slabs_equal_full_grid(gpu_device, wname, nslab, half):
+    """Large-frame mode: forward_slab on each rank's x-slab
+    (fvp.parallel.shard_slab, uneven at 3 slabs) is bit-identical to the same
+    rows of the whole-grid launch, for mixed-sequence batches too."""
+    from fvp import geometry, parallel, synthetic
+
+    w, layer, cams, seq = _whole(wname, gpu_device)
+    layer.on_the_fly = False
+    X = w.voxels_per_axis[0]
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 3)).to(gpu_device)
+    if half:
+        hm = hm.half()
+    cl = geometry.camera_list(cams, seq)
+    cams2 = {"a": cl, "b": cl[::-1]}
+    for meta in ({"seq": ["a"] * 3}, {"seq": ["a", "b", "a"]}):
+        cube, xy = layer.forward_fused(hm, meta, cams2, rt)
+        for r in range(nslab):
+            x0, x1 = parallel.shard_slab(X, nslab, r)
+            cs, xs = layer.forward_slab(hm, meta, cams2, rt, x0, x1)
+            assert torch.equal(cs, cube[:, :, x0:x1]) and torch.equal(xs, xy[:, :, x0:x1])
+    with pytest.raises(ValueError):
+        layer.forward_slab(hm, meta, cams2, rt, 4, 4)

@@ -94,3 +94,79 @@ def test_two_rank_gloo_sharded_proposals_match_single_process():
     rv, rf = _frames_result(0, total)
     assert np.array_equal(gv, rv.numpy())
     assert np.array_equal(gf, rf.numpy())
+
+
+def _slab_setup(world):
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    sys.path.insert(0, os.path.join(repo, "faster-voxelpose_amd"))
+    from fvp import geometry, synthetic
+    from fvp.workloads import WORKLOADS
+    from oracle import fvp_oracle as O
+
+    w = WORKLOADS["c1"]
+    cams, seq = w.cameras()
+    rt = geometry.resize_transform(w.ori_image_size, w.image_size).astype(np.float32)
+    grid = O.compute_grid(w.space_size, w.space_center, w.voxels_per_axis)
+    sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, w.heatmap_size, rt)
+                   for c in geometry.camera_list(cams, seq)])
+    hm = synthetic.gaussian_heatmaps(w, 2, first_frame=7)
+    return w, O, sg, hm
+
+
+def _cpu_columns(cube, flat):
+    """human_detection_net.py:199-200 on CPU: out[b,k,j,:] = cube[b,j,x,y,:] at flat = x*Y + y."""
+    B, J, X, Y, Z = cube.shape
+    c = cube.reshape(B, J, X * Y, Z).permute(0, 2, 1, 3)
+    return c[torch.arange(B)[:, None], flat]
+
+
+def _slab_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w, O, sg, hm = _slab_setup(world)
+        X, Y, Z = w.voxels_per_axis
+        x0, x1 = parallel.shard_slab(X, world, rank)
+        n0, n1 = x0 * Y * Z, x1 * Y * Z
+        cube = np.stack([O.voxelize(hm[b], sg[:, n0:n1]).reshape(w.num_joints, x1 - x0, Y, Z)
+                         for b in range(hm.shape[0])])
+        xy = parallel.gather_xy_slabs(torch.from_numpy(cube.max(axis=4)), X)
+        vals, _, flat = O.nms2d(xy[:, 2:3].numpy(), 5)
+        cols = parallel.columns_from_slab(torch.from_numpy(cube), torch.from_numpy(flat), x0, gather=_cpu_columns)
+        if rank == 0:
+            q.put((xy.numpy(), vals, flat, cols.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_x_slab_large_frame_mode_matches_single_process(world):
+    """§8(e) large-frame mode: x-slabs per rank (uneven at world 3: 7/7/6 of 20
+    rows), xy all-gather, column all-reduce == the unsplit computation."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_slab_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    xy, vals, flat, cols = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    w, O, sg, hm = _slab_setup(world)
+    cube = np.stack([O.voxelize(hm[b], sg).reshape(w.num_joints, *w.voxels_per_axis) for b in range(hm.shape[0])])
+    ref_xy = cube.max(axis=4)
+    rv, _, rf = O.nms2d(ref_xy[:, 2:3], 5)
+    assert np.array_equal(xy, ref_xy)
+    assert np.array_equal(vals, rv) and np.array_equal(flat, rf)
+    assert np.array_equal(cols, _cpu_columns(torch.from_numpy(cube), torch.from_numpy(rf)).numpy())
+    assert np.count_nonzero(cols) > 0
+
+
+def test_shard_slab_rejects_more_ranks_than_rows():
+    assert parallel.shard_slab(20, 3, 2) == (14, 20)
+    with pytest.raises(ValueError):
+        parallel.shard_slab(2, 3, 0)

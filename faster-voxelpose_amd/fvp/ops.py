@@ -121,6 +121,8 @@ def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Opt
             raise _lib.FvpError("fvp: grid_index must have one entry per frame")
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
+    if B == 0:  # an empty batch: the reference's loop over frames yields empty outputs
+        return cube, xy
     lib = _lib.load()
     ws_bytes = (lib.fvp_voxelize_f16_workspace_bytes if half else lib.fvp_voxelize_workspace_bytes)(B, V, J, H, W)
     if ws_bytes == 0:
@@ -155,6 +157,8 @@ def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Option
         gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
+    if B == 0:  # an empty batch: the reference's loop over frames yields empty outputs
+        return cube, xy
     lib = _lib.load()
     ws_bytes = (lib.fvp_voxelize_f16_workspace_bytes if half else lib.fvp_voxelize_workspace_bytes)(B, V, J, H, W)
     if ws_bytes == 0:
@@ -198,6 +202,8 @@ def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, to
     vals = torch.empty((B, K), dtype=torch.float32, device=p.device)
     flat = torch.empty((B, K), dtype=torch.int64, device=p.device)
     xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
+    if B == 0:
+        return vals, xy, flat
     _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
     return vals, xy, flat
 
@@ -217,6 +223,8 @@ def gather_columns(cube: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
     f = flat.to(device=c.device, dtype=torch.int64).contiguous()
     K = f.shape[1]
     out = torch.empty((B, K, J, Z), dtype=torch.float32, device=c.device)
+    if out.numel() == 0:
+        return out
     _lib.call("fvp_gather_columns", _ptr(c), B, J, X, Y, Z, _ptr(f), K, _ptr(out), _stream(c))
     return out
 
@@ -234,6 +242,8 @@ def gather_bbox(size: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
     f = flat.to(device=s.device, dtype=torch.int64).contiguous()
     K = f.shape[1]
     out = torch.empty((B, K, 2), dtype=torch.float32, device=s.device)
+    if out.numel() == 0:
+        return out
     _lib.call("fvp_gather_bbox", _ptr(s), B, X, Y, _ptr(f), K, _ptr(out), _stream(s))
     return out
 

@@ -151,6 +151,8 @@ class ProjectLayer(nn.Module):
         """One launch for the whole batch: (cube[B,J,X,Y,Z] or empty, xy[B,J,X,Y] or empty)."""
         ops.forward_only(heatmaps)
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
+        if heatmaps.shape[0] == 0:  # empty batch: the reference's frame loop yields empty outputs
+            return self._empty(heatmaps, X, want_cube, want_xy)
         if self._project_on_the_fly(heatmaps.shape[1]):
             cams, index = self._cams_for_batch(heatmaps, meta, cameras)
             start, end, center, nb = self.grid_spec()
@@ -160,6 +162,13 @@ class ProjectLayer(nn.Module):
                                      float(self.image_size[0]), float(self.image_size[1]), want_cube, want_xy)
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
         return ops.voxelize(heatmaps, grids, index, X, Y, Z, want_cube, want_xy)
+
+    def _empty(self, heatmaps, X, want_cube, want_xy):
+        _, Y, Z = _as_list3(self.voxels_per_axis, int)
+        J = heatmaps.shape[2]
+        f = dict(dtype=torch.float32, device=heatmaps.device)
+        return (torch.zeros((0, J, X, Y, Z) if want_cube else (0,), **f),
+                torch.zeros((0, J, X, Y) if want_xy else (0,), **f))
 
     def forward_slab(self, heatmaps, meta, cameras, resize_transform, x_begin: int, x_end: int,
                      want_cube=True, want_xy=True):
@@ -176,6 +185,8 @@ class ProjectLayer(nn.Module):
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         if not 0 <= x_begin < x_end <= X:
             raise ValueError(f"x-slab [{x_begin}, {x_end}) outside [0, {X})")
+        if heatmaps.shape[0] == 0:
+            return self._empty(heatmaps, x_end - x_begin, want_cube, want_xy)
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
         n0, n1 = x_begin * Y * Z, x_end * Y * Z
         slab = grids[n0:n1] if grids.dim() == 3 else grids[:, n0:n1].contiguous()

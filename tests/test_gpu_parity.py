@@ -367,6 +367,34 @@ def test_reference_assertions_and_errors(gpu_device):
         layer(hm.clone().requires_grad_(True), {"seq": [seq]}, cams, rt)
 
 
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "onthefly"])
+def test_empty_batches_and_proposal_sets(gpu_device, otf):
+    """B = 0 frames (the reference's frame loop returns an empty [0,J,X,Y,Z]
+    cube) and K = 0 / P = 0 proposals give empty outputs, not errors."""
+    from fvp import geometry, ops, proposal
+    from fvp.project_individual import ProjectLayer as PersonLayer
+
+    w, layer, cams, seq = _whole("c3", gpu_device)
+    layer.on_the_fly = otf
+    X, Y, Z = w.voxels_per_axis
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.zeros((0, 5, 15, 128, 240), device=gpu_device)
+    cube = layer(hm, {"seq": []}, cams, rt)
+    assert cube.shape == (0, 15, X, Y, Z) and cube.dtype == torch.float32
+    c2, xy = layer.forward_fused(hm, {"seq": []}, cams, rt)
+    assert c2.shape == (0, 15, X, Y, Z) and xy.shape == (0, 15, X, Y)
+    vals, idx, flat = proposal.nms2D(xy[:, 2:3], 10)
+    assert vals.shape == (0, 10) and idx.shape == (0, 10, 2) and flat.shape == (0, 10)
+    assert proposal.gather_columns(c2, flat).shape == (0, 10, 15, Z)
+    one = torch.rand((1, 15, X, Y, Z), device=gpu_device)
+    assert proposal.gather_columns(one, flat.new_zeros((1, 0))).shape == (1, 0, 15, Z)
+    person = PersonLayer(w.cfg(str(gpu_device)))
+    person.verbose = False
+    hm1 = torch.rand((1, 5, 15, 128, 240), device=gpu_device)
+    cubes, offset = person(hm1, 0, {"seq": [seq]}, torch.zeros((0, 7), device=gpu_device), cams, rt)
+    assert cubes.shape[0] == 0 and offset.shape == (0, 3)
+
+
 def test_fp16_heatmaps_computed_in_fp32(gpu_device):
     """C5 input dtype: fp16 heatmaps are upcast exactly and computed in fp32
     (oracle on hm.half().float())."""

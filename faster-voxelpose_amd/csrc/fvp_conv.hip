@@ -100,9 +100,11 @@ __device__ __forceinline__ void load_chunk(const ConvArgs &a, int n0, int chunk,
 // ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1
 // rows (1x2 scatter).  Rows come EPI at a time with every residual load issued
 // before the first use (one wait per group instead of one per element).
-template <int TM, int TN, int NACC, int MS, typename AccT>
-__device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM][TN], int mw, int nw, int M,
-                                         int lane) {
+// rowm(l) maps the block-local row l to its output pixel m (or -1 past the
+// image); m must grow with l inside an MFMA tile.
+template <int TM, int TN, int NACC, int MS, typename AccT, typename RowM>
+__device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM][TN], const RowM &rowm, int mw,
+                                         int nw, int lane) {
     constexpr int EPI = 4;
     const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
     const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
@@ -125,8 +127,8 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
         };
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            const int mt = mw + i * MS;  // first row of this MFMA tile (wave-uniform)
-            if (mt >= M) continue;
+            const int mt = rowm(mw + i * MS);  // first row of this MFMA tile (wave-uniform)
+            if (mt < 0) continue;
             // offsets grow with m, so rows are addressed relative to the tile's first (32-bit)
             const size_t ob = offset(mt) - co;
             float *__restrict__ out = a.out + ob;
@@ -139,8 +141,8 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
                 float pre[EPI], post[EPI];
 #pragma unroll
                 for (int r = 0; r < EPI; ++r) {
-                    const int m = mt + rowof(r0 + r);
-                    ok[r] = nok && m < M;
+                    const int m = rowm(mw + i * MS + rowof(r0 + r));
+                    ok[r] = nok && m >= 0;
                     rel[r] = ok[r] ? (unsigned)(offset(m) - ob) : 0u;
                 }
                 if (rpre) {
@@ -270,7 +272,152 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
         return;
     }
     // epilogue: lane -> column (output channel), registers -> rows (pixels)
-    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, m0 + wr * TL::WTM, n0 + wc * TL::WTN, M, lane);
+    auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
+    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
+}
+
+// Halo-tiled variant for KxK (K > 1) stride-1 "same" convolutions on images
+// at least 16 pixels wide.  A block owns a TH x 16 tile of output pixels of
+// one image (TH = BM / 16); per 16-channel chunk the (TH+KH-1) x (16+KW-1)
+// input halo is staged into LDS once and serves every (ky, kx) tap, where the
+// per-tap implicit-im2col loads of conv_mfma_kernel re-read each input pixel
+// up to KH*KW times (10-26 % of a layer's time, tools/conv_probe.py).  The K
+// loop walks channel chunks outer and taps inner; the per-tap weight tiles are
+// double-buffered and prefetched one step ahead as in conv_mfma_kernel, the
+// next chunk's halo is loaded into registers during the current chunk's taps.
+template <class TL, int KMAX>
+__global__ __launch_bounds__(256, 4) void conv_halo_kernel(ConvArgs a, int tiles_x, int tiles_y) {
+    constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, AP = TL::AP, MS = TL::MS;
+    constexpr int TW = 16, TH = BM / TW;
+    constexpr int HMAX = (TH + KMAX - 1) * (TW + KMAX - 1);  // halo pixels at the largest kernel
+    constexpr int HV = (HMAX * (KC / 4) + 255) / 256;         // halo float4 per thread
+    constexpr int BVN = KC * BN / 4 / 256 > 0 ? KC * BN / 4 / 256 : 1;
+    static_assert(BM % TW == 0 && KC == 16, "halo tile");
+    __shared__ float Hs[HMAX * AP];
+    __shared__ __attribute__((aligned(16))) float Bs[2][KC * BN];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wr = wave % TL::WR, wc = wave / TL::WR;
+    const int per_img = tiles_x * tiles_y;
+    const int img = blockIdx.x / per_img, tr = blockIdx.x - img * per_img;
+    const int y0 = (tr / tiles_x) * TH, x0 = (tr - (tr / tiles_x) * tiles_x) * TW;
+    const int n0 = blockIdx.y * BN;
+    const int HWd = TW + a.KW - 1, HP = (TH + a.KH - 1) * HWd;
+    const int hy0 = y0 - (a.KH - 1) / 2, hx0 = x0 - (a.KW - 1) / 2;
+    const float *__restrict__ inimg = a.in + (size_t)img * a.H * a.W * a.Cpi;
+    const int ntaps = a.KH * a.KW, ncc = a.Cpi / KC, nsteps = ntaps * ncc;
+    using acc_t = typename std::conditional<MS == 32, f32x16, f32x4>::type;
+    acc_t acc[TL::TM][TL::TN];
+#pragma unroll
+    for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::TN; ++j)
+#pragma unroll
+            for (int r = 0; r < TL::NACC; ++r) acc[i][j][r] = 0.f;
+
+    float4 hv[HV], bv[BVN];
+    auto load_halo = [&](int cc) {  // element e -> (halo pixel e/4, 4 channels)
+#pragma unroll
+        for (int u = 0; u < HV; ++u) {
+            const int e = u * 256 + t, hp = e >> 2;
+            hv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (hp < HP) {
+                const int hy = hp / HWd, hx = hp - hy * HWd;
+                const int y = hy0 + hy, x = hx0 + hx;
+                if ((unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+                    hv[u] = *reinterpret_cast<const float4 *>(inimg + ((size_t)y * a.W + x) * a.Cpi + cc * KC +
+                                                             (e & 3) * 4);
+            }
+        }
+    };
+    auto store_halo = [&]() {
+#pragma unroll
+        for (int u = 0; u < HV; ++u) {
+            const int e = u * 256 + t, hp = e >> 2;
+            if (hp < HP) {
+                float *d = &Hs[hp * AP + (e & 3) * 4];
+                d[0] = hv[u].x; d[1] = hv[u].y; d[2] = hv[u].z; d[3] = hv[u].w;
+            }
+        }
+    };
+    auto load_b = [&](int step) {  // weight rows of (tap, chunk) -> bv
+        const int cc = step / ntaps, tap = step - cc * ntaps;
+        const size_t row0 = (size_t)tap * a.Cpi + cc * KC;
+        if constexpr (KC * BN / 4 >= 256) {
+#pragma unroll
+            for (int u = 0; u < BVN; ++u) {
+                const int e = u * 256 + t;
+                bv[u] = *reinterpret_cast<const float4 *>(a.w + (row0 + e / (BN / 4)) * a.Cpo_w + n0 +
+                                                         (e % (BN / 4)) * 4);
+            }
+        } else if (t < KC * BN / 4) {
+            bv[0] = *reinterpret_cast<const float4 *>(a.w + (row0 + t / (BN / 4)) * a.Cpo_w + n0 + (t % (BN / 4)) * 4);
+        }
+    };
+    auto store_b = [&](int buf) {
+        if constexpr (KC * BN / 4 >= 256) {
+#pragma unroll
+            for (int u = 0; u < BVN; ++u) {
+                const int e = u * 256 + t;
+                *reinterpret_cast<float4 *>(&Bs[buf][(e / (BN / 4)) * BN + (e % (BN / 4)) * 4]) = bv[u];
+            }
+        } else if (t < KC * BN / 4) {
+            *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
+        }
+    };
+    // halo pixel of each of this lane's A rows at tap (0, 0)
+    int hrow[TL::TM];
+#pragma unroll
+    for (int i = 0; i < TL::TM; ++i) {
+        const int l = wr * TL::WTM + i * MS + (lane % MS);
+        hrow[i] = (l / TW) * HWd + (l % TW);
+    }
+    load_halo(0);
+    load_b(0);
+    store_halo();
+    store_b(0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int cc = s / ntaps, tap = s - cc * ntaps;
+        const int buf = s & 1;
+        const bool more = s + 1 < nsteps;
+        const bool next_chunk = tap == ntaps - 1 && cc + 1 < ncc;
+        if (more) load_b(s + 1);
+        if (tap == 0 && cc + 1 < ncc) load_halo(cc + 1);  // lands during this chunk's taps
+        const int ky = tap / a.KW, kx = tap - ky * a.KW;
+        const int toff = ky * HWd + kx;
+#pragma unroll
+        for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
+            float fa[TL::TM], fb[TL::TN];
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i) fa[i] = Hs[(hrow[i] + toff) * AP + kk * TL::KSTEP + lane / MS];
+#pragma unroll
+            for (int j = 0; j < TL::TN; ++j) {
+                const int col = wc * TL::WTN + j * MS + (lane % MS);
+                fb[j] = Bs[buf][(kk * TL::KSTEP + lane / MS) * BN + col];
+            }
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TL::TN; ++j) {
+                    if constexpr (MS == 32)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        if (more) store_b(buf ^ 1);
+        if (next_chunk) {  // every wave is past this chunk's halo reads
+            __syncthreads();
+            store_halo();
+        }
+        __syncthreads();
+    }
+    const int HWimg = a.H * a.W;
+    auto rowm = [&](int l) {
+        const int y = y0 + l / TW, x = x0 + l % TW;
+        return (y < a.H && x < a.W) ? img * HWimg + y * a.W + x : -1;
+    };
+    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
 }
 
 // Tiles by output width; the big ones where the launch has >= 2 blocks per CU,
@@ -285,10 +432,15 @@ using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
 // (larger wave tiles -- 64x64 per wave -- and 32-wide K chunks measured slower)
 
 static int g_force_tile = 0;
+static int g_halo = 1;  // halo-tiled KxK convolutions: 0 off, 1 where measured faster, 2 wherever eligible
 
 }  // namespace fvp
 
 extern "C" int fvp_conv_set_tile(int id) {
+    if (id <= -1 && id >= -3) {  // -1: per-tap kernel only, -2: halo where faster (default), -3: halo forced
+        fvp::g_halo = -1 - id;
+        return FVP_OK;
+    }
     if (id < 0 || id > 7) return FVP_ERR_SHAPE;
     fvp::g_force_tile = id;
     return FVP_OK;
@@ -406,7 +558,8 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
         }
     }
 
-    epilogue<TL::TM, TL::TN, 16, 32>(a, acc, m0 + wr * TL::WTM, n0 + wc * TL::WTN, M, lane);
+    auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
+    epilogue<TL::TM, TL::TN, 16, 32>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
 }
 
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
@@ -502,8 +655,47 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
         case 7: FVP_CONV(TileN64s); return (int)hipGetLastError();
         default: break;
     }
-    auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long long)((Ntot + bn - 1) / bn); };
     const long long enough = 512;  // >= 2 blocks per CU
+    // Halo tiles are 16 pixels wide: only where a row wastes <= 1/8 of them
+    // (CenterNet's 20- and 40-wide maps stay per-tap), and only with the large
+    // tiles (>= 8 rows: halo overhead <= 1.4x of the tile) at >= 2 blocks per
+    // CU -- measured (tools/conv_probe.py): 7x7 front 205 -> 147 us, 3x3
+    // layers at 64/32 px 4-6 % faster; 4-row tiles and sub-2-per-CU launches
+    // were 2-10 % slower than per-tap.
+    const int tx = (W + 15) / 16;
+    const bool halo = g_halo && (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && !upsample2 &&
+                      (tx * 16 - W) * 8 <= W;
+    if (halo && !PROBE) {
+        auto hblocks = [&](int bm, int bn) {
+            return (long long)N * tx * ((H + bm / 16 - 1) / (bm / 16)) * ((Ntot + bn - 1) / bn);
+        };
+#define FVP_HALO(TL)                                                                                              \
+    do {                                                                                                          \
+        const int ty = (H + fvp::TL::BM / 16 - 1) / (fvp::TL::BM / 16);                                           \
+        const dim3 g((unsigned)((long long)N * tx * ty), (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN));     \
+        if (KH <= 3 && KW <= 3)                                                                                   \
+            hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 3>), g, dim3(256), 0, st, a, tx, ty);              \
+        else                                                                                                      \
+            hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 7>), g, dim3(256), 0, st, a, tx, ty);              \
+        return (int)hipGetLastError();                                                                            \
+    } while (0)
+        const bool any = g_halo == 2;  // forced (tests): every eligible layer, small tiles too
+        if (Ntot <= 16) {
+            if (hblocks(256, 16) >= enough) FVP_HALO(TileN16);
+            if (any) FVP_HALO(TileN16s);
+        } else if (Ntot <= 32) {
+            if (hblocks(128, 32) >= enough) FVP_HALO(TileN32);
+            if (any) FVP_HALO(TileN32s);
+        } else {
+            if (hblocks(128, 64) >= enough) FVP_HALO(TileN64);
+            if (any) {
+                if (hblocks(64, 64) >= enough) FVP_HALO(TileN64m);
+                FVP_HALO(TileN64s);
+            }
+        }
+#undef FVP_HALO
+    }
+    auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long long)((Ntot + bn - 1) / bn); };
     if (Ntot <= 16) {
         if (blocks(256, 16) >= enough) FVP_CONV(TileN16); else FVP_CONV(TileN16s);
     } else if (Ntot <= 32) {

@@ -236,7 +236,9 @@ int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *
 int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH, int KW,
                          int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                          const float *res_post, int relu, int upsample2, float *out, void *stream);
-/* Tuning hook: 0 = tile chosen per layer (default); 1..7 force one tile shape. */
+/* Tuning hook: 0 = tile chosen per layer (default); 1..7 force one tile shape
+ * (per-tap kernel); halo-tiled KxK kernel: -1 off, -2 where measured faster
+ * (default), -3 wherever eligible (tests). */
 int fvp_conv_set_tile(int id);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
 int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);

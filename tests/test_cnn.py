@@ -69,11 +69,24 @@ def test_fvp_cnn_matches_reference(gpu_device):
         _close(y.cpu().numpy(), p2p(torch.from_numpy(x_p2p).to(gpu_device)).cpu().numpy(), "P2PNet vs torch GPU")
 
 
+@pytest.fixture(params=[-3, -1], ids=["halo", "pertap"])
+def conv_kernel(request):
+    """Run with the halo-tiled KxK kernel on every eligible layer (forced, so
+    small test shapes take it too) and with the per-tap kernel only."""
+    from fvp import _lib
+
+    lib = _lib.load()
+    lib.fvp_conv_set_tile(request.param)
+    yield request.param
+    lib.fvp_conv_set_tile(-2)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,hw,res", [(15, 16, 7, (64, 64), False), (16, 32, 3, (33, 17), True),
                                                (128, 128, 3, (16, 16), True), (32, 15, 1, (20, 20), False),
-                                               (1, 20, 3, (64, 64), False), (40, 70, 5, (9, 11), True)])
-def test_conv_layer_vs_torch(gpu_device, cin, cout, k, hw, res):
+                                               (1, 20, 3, (64, 64), False), (40, 70, 5, (9, 11), True),
+                                               (16, 64, 3, (41, 37), True), (64, 16, 5, (23, 30), False)])
+def test_conv_layer_vs_torch(gpu_device, conv_kernel, cin, cout, k, hw, res):
     """Single fused conv + BN + residual + ReLU layers, ragged shapes and channel counts."""
     import torch.nn as nn
 
@@ -118,7 +131,7 @@ def test_transposed_conv_and_pool_vs_torch(gpu_device):
 
 
 @pytest.mark.gpu
-def test_fvp_cnn_large_batch_tiles_vs_torch(gpu_device):
+def test_fvp_cnn_large_batch_tiles_vs_torch(gpu_device, conv_kernel):
     """Enough images that every layer takes the large tiles (>= 2 blocks per CU)."""
     from fvp.cnn import FvpCNN
 

@@ -27,6 +27,10 @@ def main():
     args = ap.parse_args()
     import numpy as np
     import torch
+    if os.environ.get("FVP_CONV_HALO") == "0":  # A/B: per-tap kernel only
+        from fvp import _lib
+
+        _lib.load().fvp_conv_set_tile(-1)
 
     import cnn_arch
     from fvp import cnn, synthetic

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Where a conv launch's time goes (tuning aid): each P2PNet layer shape with
-the automatic tile, timed as is (probe 0), without epilogue stores (1),
-without global loads after the first chunk (2), and with neither (3).
+"""Where a conv launch's time goes (tuning aid): each P2PNet / CenterNet layer
+shape with the automatic choice, timed on the per-tap kernel only (pt), as is
+(probe 0: the halo kernel where it applies), and on the per-tap kernel without
+epilogue stores (1), without global loads after the first chunk (2), and with
+neither (3).
 Builds faster-voxelpose_amd/csrc/fvp_conv.hip with -DFVP_CONV_PROBES into
 tools/libconvprobe.so."""
 import ctypes
@@ -42,20 +44,32 @@ def main():
     lib.fvp_conv_probe.argtypes = [i_, vp, i_, i_, i_, i_, vp, i_, i_, i_, i_, vp, vp, vp, vp, i_, i_, vp, vp]
     dev = torch.device("cuda:0")
     imgs = int(sys.argv[1]) if len(sys.argv) > 1 else 120
+    lib.fvp_conv_set_tile.argtypes = [i_]
     shapes = [("7x7 15->16 @64", 15, 16, 7, 64, False), ("3x3 16->32 @64", 16, 32, 3, 64, False),
               ("3x3 32->32 @64", 32, 32, 3, 64, False), ("3x3 64->64 @32", 64, 64, 3, 32, False),
               ("3x3 128->128 @16", 128, 128, 3, 16, False), ("convT 128->64 @16", 128, 64, 2, 16, True)]
-    for name, cin, cout, k, hw, up in shapes:
+    cn_imgs = int(sys.argv[2]) if len(sys.argv) > 2 else 8  # CenterNet's shapes (80x80 maps per frame)
+    shapes += [(f"CN {n}", ci, co, k, hw, up, cn_imgs) for n, ci, co, k, hw, up in
+               [("7x7 15->16 @80", 15, 16, 7, 80, False), ("3x3 16->32 @80", 16, 32, 3, 80, False),
+                ("3x3 32->32 @80", 32, 32, 3, 80, False), ("3x3 64->64 @40", 64, 64, 3, 40, False),
+                ("3x3 128->128 @20", 128, 128, 3, 20, False)]]
+    for shp in shapes:
+        name, cin, cout, k, hw, up = shp[:6]
+        n_img = shp[6] if len(shp) > 6 else imgs
         conv = (nn.ConvTranspose2d(cin, cout, 2, stride=2) if up else nn.Conv2d(cin, cout, k, padding=k // 2)).to(dev)
         L = cnn.ConvLayer(conv, None)
-        x = cnn.to_nhwc(torch.rand((imgs, cin, hw, hw), device=dev))
+        x = cnn.to_nhwc(torch.rand((n_img, cin, hw, hw), device=dev))
         Ho, Wo = (2 * hw, 2 * hw) if up else (hw, hw)
-        out = torch.empty((imgs, Ho, Wo, L.Cpo), device=dev)
+        out = torch.empty((n_img, Ho, Wo, L.Cpo), device=dev)
         flops = L.flops(x)
         row = []
-        for probe in range(4):
+        # "pt": probe 0 with the halo kernel off (per-tap implicit GEMM); p0 = default choice
+        for probe in ["pt", 0, 1, 2, 3]:
+            lib.fvp_conv_set_tile(-1 if probe == "pt" else -2)
+            pr = 0 if probe == "pt" else probe
+
             def f():
-                rc = lib.fvp_conv_probe(probe, _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(L.wpack), L.KH, L.KW, L.Cpo,
+                rc = lib.fvp_conv_probe(pr, _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(L.wpack), L.KH, L.KW, L.Cpo,
                                         L.Cpo_w, _ptr(L.scale), _ptr(L.shift), None, None, 1, L.up2, _ptr(out),
                                         _stream(out))
                 assert rc == 0, rc
@@ -71,7 +85,7 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1) / 10)
             t = float(np.median(ts))
-            row.append(f"p{probe} {t * 1e3:7.1f} us {flops / (t * 1e-3) / 1e12:6.1f} TF")
+            row.append(f"{probe if probe == 'pt' else 'p' + str(probe)} {t * 1e3:7.1f} us {flops / (t * 1e-3) / 1e12:6.1f} TF")
         print(f"{name:20s} " + " | ".join(row), flush=True)
 
 

@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--slabs", action="store_true",
                     help="large-frame mode (SURVEY.md §8(e)): every rank holds the same frames and voxelises one "
                          "x-slab of each; strong scaling")
+    ap.add_argument("--strong", action="store_true",
+                    help="--batch is the whole job's frames, split over the ranks (strong scaling)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -156,6 +158,10 @@ def main():
 
     w = WORKLOADS[args.workload]
     B = args.batch or DEFAULT_BATCH.get(args.workload, 64)
+    if args.strong and not args.slabs:  # fixed total frames: each rank takes its shard
+        if B % world:
+            raise SystemExit(f"--strong: {B} frames do not split evenly over {world} ranks")
+        B //= world
     cams, seq = w.cameras()
     V = len(cams[seq])
     J = w.num_joints
@@ -321,7 +327,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.slabs else "weak",
+            "scaling": "strong" if (args.slabs or args.strong) else "weak",
             "vs_baseline": None,
             "dtype": "f32" if w.dtype == "float32" else "f16-in/f32",
             "data": "synthetic",

@@ -182,9 +182,27 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
 #pragma unroll
         for (int k = 0; k < 4; ++k) yzacc[r][k] = 0.0f;
 
+    // block-uniform: does any of this block's rows meet the window in y?
+    bool rows_in = false;
+#pragma unroll
+    for (int r = 0; r < YG; ++r) {
+        const int gy = w.ctl[1] + yg0 + r;
+        rows_in |= yg0 + r < SY && gy >= w.start[1] && gy < w.end[1];
+    }
     for (int x = 0; x < SX; ++x) {
         const int gx = w.ctl[0] + x;
         const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
+        if (!cubes && !(xin && rows_in)) {
+            // planes only, nothing of this x-plane in the window: every voxel is 0, so
+            // xy = 0, and the xz / yz maxima are unchanged (pre-zeroed plane, yzacc >= 0)
+            if (planes && SZ > 0) {
+                for (int e = threadIdx.x; e < YG * J; e += 64 * LPV) {
+                    const int r = e / J, j = e - r * J;
+                    if (yg0 + r < SY) xy_pl[((size_t)j * SX + x) * SY + yg0 + r] = 0.0f;
+                }
+            }
+            continue;
+        }
         float xzacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < YG; ++r) {
@@ -294,10 +312,12 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             }
             if (zok) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (4 * q + k < J)
-                        atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl,
-                                  __builtin_bit_cast(unsigned, xzacc[k]));
+                for (int k = 0; k < 4; ++k) {
+                    // +0 cannot raise the pre-zeroed plane: skip those atomics (most of the 64^3 cube)
+                    const unsigned u = __builtin_bit_cast(unsigned, xzacc[k]);
+                    if (4 * q + k < J && u != 0u)
+                        atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl, u);
+                }
             }
             __syncthreads();
         }

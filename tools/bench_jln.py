@@ -93,6 +93,21 @@ def main():
         ops.fuse_poses(pose, wts, mp)
 
     ms_post = timeit(post)
+
+    # tap stream of the person kernel (project_individual.py:255-269 windows):
+    # in-window voxels x cameras x 4 bilinear taps x one 64-B channels-last pixel
+    c = layer._const
+    pc = allp.reshape(-1, 7).cpu().numpy().astype(np.float32)
+    fine = c["fine"].astype(np.int64)
+    ctl = np.rint(pc[:, 0:3] * c["scale"] + c["bias"]).astype(np.int64)
+    m = np.zeros((pc.shape[0], 3), np.int64)
+    m[:, 0:2] = np.maximum(((1.0 - pc[:, 5:7]) / 2.0 * (64 - 1)).astype(np.int64), 0)
+    start = np.where(ctl + m >= 0, ctl + m, 0)
+    end = np.where(ctl + 64 - m <= fine, ctl + 64 - m, fine)
+    win = np.where((end > start).all(axis=1), np.prod(np.clip(end - start, 0, None), axis=1), 0)
+    V = len(cams[seq])
+    tap_bytes = float(win.sum()) * V * 4 * 64
+    tap_tbs = tap_bytes / (ms * 1e-3) / 1e12
     post_bytes = 3 * w.num_joints * 64 * 64 * 4 * n_prop0
     J = w.num_joints
     n_prop = F * P
@@ -105,6 +120,9 @@ def main():
         "per_frame_calls_us_per_proposal": round(ms_frame * 1e3 / n_prop, 2),
         "path": "forward_batch: one fvp_person_planes launch for all frames' proposals (fused planes, no cubes)",
         "cache_build_ms": round(cache_ms, 1),
+        "tap_stream": {"window_voxels_per_proposal": round(float(win.mean()), 1),
+                       "bytes_per_proposal": round(tap_bytes / n_prop), "achieved_tb_s": round(tap_tbs, 2),
+                       "l2_gather_ceiling_tb_s": "16.8-18.8 (MI355X_MICROARCH.md, random 16-B row gathers from L2)"},
         "post": {"op": "fvp_soft_argmax + fvp_fuse_poses (SoftArgmaxLayer, offsets, fuse_pose_preds)",
                  "us_per_proposal": round(ms_post * 1e3 / n_prop0, 3),
                  "hbm_gbs": round(post_bytes / (ms_post * 1e-3) / 1e9, 1),

@@ -340,21 +340,14 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
                              const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
                              float *offset, int P, int V, int J, int H, int W, hipStream_t st) {
     const int SY = s.bins[1];
-    // rows per block: 4 when the launch has >= 8 blocks per CU, fewer for small
-    // launches (per-frame calls) so they still fill the CUs (measured, C3, 5 cams:
-    // 320 proposals 14.4 -> 10.7 us each with XCD placement + 4 rows; 10: 60 -> 27)
-    int yg = 4;
-    while (yg > 1 && (long long)P * ((SY + yg - 1) / yg) < 2048) yg >>= 1;
+    // one y-row per block (the kernel also takes YG rows): with the planes-only
+    // fast path for x-planes outside the window, rows are the finer and better
+    // balanced unit -- measured (C3, 320 proposals): 1 row 6.24, 2 rows 6.85,
+    // 4 rows 7.4, 8 rows 8.8 us per proposal (4 rows were best, 10.7 us, before
+    // the fast path).  XCD-aware placement keeps a proposal's rows on one XCD.
     const int xmap = 1;
-#define FVP_PERSON_LAUNCH(YGV)                                                                                       \
-    hipLaunchKernelGGL((person_cl_kernel<LPV, YGV, OTF>), dim3((unsigned)(P * ((SY + YGV - 1) / YGV))),         \
-                       dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, \
-                       xmap)
-    if (yg <= 1) FVP_PERSON_LAUNCH(1);
-    else if (yg <= 2) FVP_PERSON_LAUNCH(2);
-    else if (yg <= 4) FVP_PERSON_LAUNCH(4);
-    else FVP_PERSON_LAUNCH(8);
-#undef FVP_PERSON_LAUNCH
+    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF>), dim3((unsigned)(P * SY)), dim3(64 * LPV), 0, st, cl, fgrid,
+                       pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap);
 }
 
 }  // namespace fvp

@@ -101,7 +101,8 @@ __global__ __launch_bounds__(256) void max_planes_kernel(const float *__restrict
 // Channels-last per-person kernel (batched over frames, optional fused planes).
 // Block = (proposal p, group of YG y-rows); threads = 64 z-lanes x LPV joint
 // quads.  The block walks x = 0..S-1 and, for each x, its YG rows:
-//   xy[x][y] = max_z   -> wave shuffles over z + one LDS combine per x
+//   xy[x][y] = max_z   -> wave shuffles over z + one atomicMax per wave into the
+//                         pre-zeroed plane (no barriers in the x walk)
 //   yz[y][z] = max_x   -> registers (the block owns its y rows), stored at the end
 //   xz[x][z] = max_y   -> max over the block's rows, then one atomicMax per
 //                         (x, z, joint) into the pre-zeroed plane (values are
@@ -126,9 +127,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                                                              float *__restrict__ offset, int P, int V, int J, int H,
                                                              int W, int xmap) {
     constexpr int JP = 4 * LPV;
-    constexpr int NW = LPV;       // waves per block (64*LPV threads)
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
-    __shared__ float xy_part[NW][YG][JP];
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
     const int ngroups = (SY + YG - 1) / YG;
@@ -144,7 +143,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
         offset[(size_t)p * 3 + a] =
             ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
     }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const int zl = threadIdx.x / LPV, q = threadIdx.x % LPV;
     const int b = frame_of ? frame_of[p] : 0;
     const unsigned HW = (unsigned)(H * W);
@@ -192,17 +191,9 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     for (int x = 0; x < SX; ++x) {
         const int gx = w.ctl[0] + x;
         const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
-        if (!cubes && !(xin && rows_in)) {
-            // planes only, nothing of this x-plane in the window: every voxel is 0, so
-            // xy = 0, and the xz / yz maxima are unchanged (pre-zeroed plane, yzacc >= 0)
-            if (planes && SZ > 0) {
-                for (int e = threadIdx.x; e < YG * J; e += 64 * LPV) {
-                    const int r = e / J, j = e - r * J;
-                    if (yg0 + r < SY) xy_pl[((size_t)j * SX + x) * SY + yg0 + r] = 0.0f;
-                }
-            }
-            continue;
-        }
+        // planes only, nothing of this x-plane in the window: every voxel is 0,
+        // which changes none of the maxima (pre-zeroed xy / xz planes, yzacc >= 0)
+        if (!cubes && !(xin && rows_in)) continue;
         float xzacc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < YG; ++r) {
@@ -294,22 +285,15 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                     float m = o[k];
 #pragma unroll
                     for (int off = LPV; off < 64; off <<= 1) m = nanmax(m, __shfl_xor(m, off));
-                    if (lane < LPV) xy_part[wave][r][4 * q + k] = m;
+                    // this wave's z-range maximum into the pre-zeroed xy plane (values are
+                    // in [0,1] or NaN, so unsigned order == float order; -inf: no z lane here)
+                    const unsigned u = __builtin_bit_cast(unsigned, m);
+                    if (lane < LPV && 4 * q + k < J && y < SY && u != 0u && m != -INFINITY)
+                        atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + k) * SX + x) * SY + y, u);
                 }
             }
         }
         if (planes) {
-            __syncthreads();
-            for (int e = threadIdx.x; e < YG * JP; e += 64 * LPV) {
-                const int r = e / JP, j = e - (e / JP) * JP;
-                const int y = yg0 + r;
-                if (j < J && y < SY) {
-                    float m = xy_part[0][r][j];
-#pragma unroll
-                    for (int ww = 1; ww < NW; ++ww) m = nanmax(m, xy_part[ww][r][j]);
-                    xy_pl[((size_t)j * SX + x) * SY + y] = m;
-                }
-            }
             if (zok) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -319,7 +303,6 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                         atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl, u);
                 }
             }
-            __syncthreads();
         }
     }
     if (planes && zok) {
@@ -388,8 +371,8 @@ static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, 
     if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
     float *cl = reinterpret_cast<float *>(workspace);
-    if (planes) {  // xz is reduced with atomicMax over non-negative floats: start from +0
-        const hipError_t e = hipMemsetAsync(planes + (size_t)P * J * SX * SZ, 0, (size_t)P * J * SX * SZ * 4, st);
+    if (planes) {  // xy and xz are reduced with atomicMax over non-negative floats: start from +0
+        const hipError_t e = hipMemsetAsync(planes, 0, (size_t)2 * P * J * SX * SY * 4, st);
         if (e != hipSuccess) return (int)e;
     }
     const PersonCoords none{};

@@ -10,6 +10,6 @@ NO_BATCHES= bash tools/bench_all.sh || exit $?
 timeout -k 10 300 python tools/bench_cnn.py > gpurun_out/all_cnn.log 2>&1; echo "cnn rc=$?"
 : > gpurun_out/all_pipeline.jsonl
 for f in 8 32; do for v in "" "--torch-cnn" "--bf16"; do
-  timeout -k 10 200 python tools/bench_pipeline.py --frames $f $v 2>/dev/null | grep "^{" >> gpurun_out/all_pipeline.jsonl || exit 1
+  timeout -k 10 200 python tools/bench_pipeline.py --frames $f --steps 40 $v 2>/dev/null | grep "^{" >> gpurun_out/all_pipeline.jsonl || exit 1
 done; done; echo "pipeline ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_jln -o run -- python3 tools/bench_jln.py --frames 32 > gpurun_out/prof_jln.log 2>&1; echo "jln prof rc=$?"

@@ -37,6 +37,7 @@ struct ConvArgs {
     const float *res_post;  // [N][Ho][Wo][Cpo] or null: added after the ReLU
     float *out;             // [N][Ho][Wo][Cpo]
     int N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, up2;
+    float *part;            // split-K: raw partial sums [gridDim.z][M][Ntot] (no epilogue), else null
 };
 
 // Tile configuration: BM pixels x BN channels per 256-thread block, MFMA
@@ -182,6 +183,9 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave % TL::WR, wc = wave / TL::WR;
     const int nchunks = a.KH * a.KW * (a.Cpi / KC);
+    // split-K: block z of gridDim.z walks chunks [cb, ce) and leaves raw partial sums
+    const int cb = (int)((long long)blockIdx.z * nchunks / gridDim.z);
+    const int ce = (int)((long long)(blockIdx.z + 1) * nchunks / gridDim.z);
     using acc_t = typename std::conditional<MS == 32, f32x16, f32x4>::type;
     acc_t acc[TL::TM][TL::TN];
 #pragma unroll
@@ -222,16 +226,16 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
             *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
         }
     };
-    load_chunk<TL>(a, n0, 0, pr, av, bv);
-    stage(0);
+    load_chunk<TL>(a, n0, cb, pr, av, bv);
+    stage(cb & 1);
     __syncthreads();
     // One barrier per chunk: chunk ch+1's global loads are issued first, the
     // MFMAs of chunk ch next, and the loaded registers go to the other buffer
     // after the last MFMA has issued (it was last read before the previous
     // barrier), so the LDS stores and the barrier overlap the MFMA tail.
-    for (int ch = 0; ch < nchunks; ++ch) {
+    for (int ch = cb; ch < ce; ++ch) {
         const int buf = ch & 1;
-        const bool more = ch + 1 < nchunks;
+        const bool more = ch + 1 < ce;
         if (!(PROBE & 2) && more) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);
 #pragma unroll
         for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
@@ -271,9 +275,50 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
         if (sink == 1234.5f) a.out[t] = sink;
         return;
     }
+    if (a.part) {  // split-K: raw partial sums, combined in z order by conv_splitk_reduce
+        const int Ntot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
+        float *__restrict__ dst = a.part + (size_t)blockIdx.z * M * Ntot;
+#pragma unroll
+        for (int j = 0; j < TL::TN; ++j) {
+            const int n = n0 + wc * TL::WTN + j * MS + (lane % MS);
+#pragma unroll
+            for (int i = 0; i < TL::TM; ++i)
+#pragma unroll
+                for (int r = 0; r < TL::NACC; ++r) {
+                    const int row = MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r;
+                    const int m = m0 + wr * TL::WTM + i * MS + row;
+                    if (m < M && n < Ntot) dst[(size_t)m * Ntot + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
     // epilogue: lane -> column (output channel), registers -> rows (pixels)
     auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
     epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
+}
+
+// Split-K combine: out = act(sum_z part[z] * scale + shift + res_pre) + res_post,
+// summed in z order (deterministic), with the epilogue's output mapping.
+__global__ __launch_bounds__(256) void conv_splitk_reduce(ConvArgs a, int ks, int M, int Ntot) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (long long)M * Ntot) return;
+    const int m = (int)(e / Ntot), n = (int)(e - (long long)m * Ntot);
+    float v = 0.0f;
+    for (int z = 0; z < ks; ++z) v += a.part[((size_t)z * M + m) * Ntot + n];
+    const int co = a.up2 ? n % a.Cpo : n, q = a.up2 ? n / a.Cpo : 0;
+    size_t off = (size_t)m * a.Cpo + co;
+    if (a.up2) {
+        const int HW = a.H * a.W, img = m / HW, rr = m - img * HW;
+        const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = 2 * a.W;
+        const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
+        const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
+        off = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
+    }
+    v = v * a.scale[co] + a.shift[co];
+    if (a.res_pre) v = v + a.res_pre[off];
+    if (a.relu) v = fmaxf(v, 0.0f);
+    if (a.res_post) v = v + a.res_post[off];
+    a.out[off] = v;
 }
 
 // Halo-tiled variant for KxK (K > 1) stride-1 "same" convolutions on images
@@ -432,13 +477,18 @@ using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
 // (larger wave tiles -- 64x64 per wave -- and 32-wide K chunks measured slower)
 
 static int g_force_tile = 0;
-static int g_halo = 1;  // halo-tiled KxK convolutions: 0 off, 1 where measured faster, 2 wherever eligible
+static int g_halo = 1;
+static int g_split = 1;  // split-K of under-filled per-tap launches (fvp_conv_set_tile(-4): off, -5: on)  // halo-tiled KxK convolutions: 0 off, 1 where measured faster, 2 wherever eligible
 
 }  // namespace fvp
 
 extern "C" int fvp_conv_set_tile(int id) {
     if (id <= -1 && id >= -3) {  // -1: per-tap kernel only, -2: halo where faster (default), -3: halo forced
         fvp::g_halo = -1 - id;
+        return FVP_OK;
+    }
+    if (id == -4 || id == -5) {
+        fvp::g_split = id == -5;
         return FVP_OK;
     }
     if (id < 0 || id > 7) return FVP_ERR_SHAPE;
@@ -622,10 +672,71 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float *__restri
 }  // namespace fvp
 
 namespace fvp {
+// Launch plan of one convolution: the halo-tiled kernel's tile (0: not used)
+// or the per-tap kernel's tile and its split-K factor.
+struct ConvPlan {
+    int halo;   // 1/3/5 = TileN16/N32/N64 (2/4/6/7 small tiles when forced), 0 = per-tap kernel
+    int tile;   // per-tap tile id 1..7 (fvp_conv_set_tile numbering)
+    int ks;     // split-K factor of the per-tap kernel (1 = none)
+};
+
+static const int kTileBM[8] = {0, 256, 64, 128, 64, 128, 64, 32};
+static const int kTileBN[8] = {0, 16, 16, 32, 32, 64, 64, 64};
+
+static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot, int upsample2, bool probe) {
+    ConvPlan p{0, 0, 1};
+    const long long M = (long long)N * H * W;
+    const long long enough = 512;  // >= 2 blocks per CU
+    if (g_force_tile) {
+        p.tile = g_force_tile;
+        return p;
+    }
+    // Halo tiles are 16 pixels wide: only where a row wastes <= 1/8 of them
+    // (CenterNet's 20- and 40-wide maps stay per-tap), and only with the large
+    // tiles (>= 8 rows: halo overhead <= 1.4x of the tile) at >= 2 blocks per
+    // CU -- measured (tools/conv_probe.py): 7x7 front 205 -> 147 us, 3x3
+    // layers at 64/32 px 4-6 % faster; 4-row tiles and sub-2-per-CU launches
+    // were 2-10 % slower than per-tap.
+    const int tx = (W + 15) / 16;
+    const bool halo = g_halo && !probe && (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && !upsample2 &&
+                      (tx * 16 - W) * 8 <= W;
+    auto hblocks = [&](int id) {
+        const int rows = kTileBM[id] / 16;
+        return (long long)N * tx * ((H + rows - 1) / rows) * ((Ntot + kTileBN[id] - 1) / kTileBN[id]);
+    };
+    if (halo) {
+        const bool any = g_halo == 2;  // forced (tests): every eligible layer, small tiles too
+        const int big = Ntot <= 16 ? 1 : Ntot <= 32 ? 3 : 5;
+        if (hblocks(big) >= enough) p.halo = big;
+        else if (any) p.halo = big == 5 ? (hblocks(6) >= enough ? 6 : 7) : big + 1;
+        if (p.halo) return p;
+    }
+    auto blocks = [&](int id) {
+        return ((M + kTileBM[id] - 1) / kTileBM[id]) * (long long)((Ntot + kTileBN[id] - 1) / kTileBN[id]);
+    };
+    if (Ntot <= 16) p.tile = blocks(1) >= enough ? 1 : 2;
+    else if (Ntot <= 32) p.tile = blocks(3) >= enough ? 3 : 4;
+    else p.tile = blocks(5) >= enough ? 5 : blocks(6) >= enough ? 6 : 7;
+    // Split-K for launches under one block per CU with a long K walk (CenterNet's
+    // 20x20 / 40x40 levels at small batch): each K-chunk step waits on a global
+    // round trip, so fewer, longer block chains leave the CUs idle (CenterNet on
+    // 8 frames 0.61 -> 0.55 ms; C2CNet's 1-D rows were slower split).
+    const int nchunks = KH * KW * (Cpi / 16);
+    const long long nb = blocks(p.tile);
+    if (g_split && !probe && H > 1 && nb < 256 && nchunks >= 8) {  // 2-D maps (C2CNet's 1-D rows: slower)
+        int ks = (int)((512 + nb - 1) / nb);
+        ks = ks < nchunks / 4 ? ks : nchunks / 4;
+        p.ks = ks < 8 ? ks : 8;
+        if (p.ks < 2) p.ks = 1;
+    }
+    return p;
+}
+
 template <int PROBE>
 static int conv_launch(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW, int Cpo,
                        int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                       const float *res_post, int relu, int upsample2, float *out, void *stream) {
+                       const float *res_post, int relu, int upsample2, float *out, void *ws, size_t ws_bytes,
+                       void *stream) {
     if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
         (KH & 1) == 0 || (KW & 1) == 0)
@@ -635,40 +746,14 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
     if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
     const long long M = (long long)N * H * W;
     if (M * Ntot > 0x7fffffffLL * 4) return FVP_ERR_SHAPE;
-    fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
+    fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2,
+                    nullptr};
     hipStream_t st = (hipStream_t)stream;
-#define FVP_CONV(TL)                                                                                              \
-    do {                                                                                                          \
-        if (Cpi % fvp::TL::KC) return FVP_ERR_SHAPE;                                                              \
-        hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL, PROBE>),                                               \
-                           dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                  \
-                                (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN)),                              \
-                           dim3(256), 0, st, a);                                                                 \
-    } while (0)
-    switch (fvp::g_force_tile) {  // tuning override (fvp_conv_set_tile)
-        case 1: FVP_CONV(TileN16); return (int)hipGetLastError();
-        case 2: FVP_CONV(TileN16s); return (int)hipGetLastError();
-        case 3: FVP_CONV(TileN32); return (int)hipGetLastError();
-        case 4: FVP_CONV(TileN32s); return (int)hipGetLastError();
-        case 5: FVP_CONV(TileN64); return (int)hipGetLastError();
-        case 6: FVP_CONV(TileN64m); return (int)hipGetLastError();
-        case 7: FVP_CONV(TileN64s); return (int)hipGetLastError();
-        default: break;
-    }
-    const long long enough = 512;  // >= 2 blocks per CU
-    // Halo tiles are 16 pixels wide: only where a row wastes <= 1/8 of them
-    // (CenterNet's 20- and 40-wide maps stay per-tap), and only with the large
-    // tiles (>= 8 rows: halo overhead <= 1.4x of the tile) at >= 2 blocks per
-    // CU -- measured (tools/conv_probe.py): 7x7 front 205 -> 147 us, 3x3
-    // layers at 64/32 px 4-6 % faster; 4-row tiles and sub-2-per-CU launches
-    // were 2-10 % slower than per-tap.
-    const int tx = (W + 15) / 16;
-    const bool halo = g_halo && (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && !upsample2 &&
-                      (tx * 16 - W) * 8 <= W;
-    if (halo && !PROBE) {
-        auto hblocks = [&](int bm, int bn) {
-            return (long long)N * tx * ((H + bm / 16 - 1) / (bm / 16)) * ((Ntot + bn - 1) / bn);
-        };
+    ConvPlan p = conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, PROBE != 0);
+    if (p.ks > 1 && (!ws || ws_bytes < (size_t)p.ks * M * Ntot * sizeof(float))) p.ks = 1;  // no scratch: no split
+    if (p.ks > 1) a.part = reinterpret_cast<float *>(ws);
+    if (p.halo) {
+        const int tx = (W + 15) / 16;
 #define FVP_HALO(TL)                                                                                              \
     do {                                                                                                          \
         const int ty = (H + fvp::TL::BM / 16 - 1) / (fvp::TL::BM / 16);                                           \
@@ -677,35 +762,42 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
             hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 3>), g, dim3(256), 0, st, a, tx, ty);              \
         else                                                                                                      \
             hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 7>), g, dim3(256), 0, st, a, tx, ty);              \
-        return (int)hipGetLastError();                                                                            \
     } while (0)
-        const bool any = g_halo == 2;  // forced (tests): every eligible layer, small tiles too
-        if (Ntot <= 16) {
-            if (hblocks(256, 16) >= enough) FVP_HALO(TileN16);
-            if (any) FVP_HALO(TileN16s);
-        } else if (Ntot <= 32) {
-            if (hblocks(128, 32) >= enough) FVP_HALO(TileN32);
-            if (any) FVP_HALO(TileN32s);
-        } else {
-            if (hblocks(128, 64) >= enough) FVP_HALO(TileN64);
-            if (any) {
-                if (hblocks(64, 64) >= enough) FVP_HALO(TileN64m);
-                FVP_HALO(TileN64s);
-            }
+        switch (p.halo) {
+            case 1: FVP_HALO(TileN16); break;
+            case 2: FVP_HALO(TileN16s); break;
+            case 3: FVP_HALO(TileN32); break;
+            case 4: FVP_HALO(TileN32s); break;
+            case 5: FVP_HALO(TileN64); break;
+            case 6: FVP_HALO(TileN64m); break;
+            default: FVP_HALO(TileN64s); break;
         }
 #undef FVP_HALO
+        return (int)hipGetLastError();
     }
-    auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long long)((Ntot + bn - 1) / bn); };
-    if (Ntot <= 16) {
-        if (blocks(256, 16) >= enough) FVP_CONV(TileN16); else FVP_CONV(TileN16s);
-    } else if (Ntot <= 32) {
-        if (blocks(128, 32) >= enough) FVP_CONV(TileN32); else FVP_CONV(TileN32s);
-    } else {
-        if (blocks(128, 64) >= enough) FVP_CONV(TileN64);
-        else if (blocks(64, 64) >= enough) FVP_CONV(TileN64m);
-        else FVP_CONV(TileN64s);
+#define FVP_CONV(TL)                                                                                              \
+    do {                                                                                                          \
+        if (Cpi % fvp::TL::KC) return FVP_ERR_SHAPE;                                                              \
+        hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL, PROBE>),                                               \
+                           dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                  \
+                                (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN), (unsigned)p.ks),              \
+                           dim3(256), 0, st, a);                                                                 \
+    } while (0)
+    switch (p.tile) {
+        case 1: FVP_CONV(TileN16); break;
+        case 2: FVP_CONV(TileN16s); break;
+        case 3: FVP_CONV(TileN32); break;
+        case 4: FVP_CONV(TileN32s); break;
+        case 5: FVP_CONV(TileN64); break;
+        case 6: FVP_CONV(TileN64m); break;
+        default: FVP_CONV(TileN64s); break;
     }
 #undef FVP_CONV
+    if (p.ks > 1) {
+        const long long tot = M * Ntot;
+        hipLaunchKernelGGL(fvp::conv_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, a, p.ks,
+                           (int)M, Ntot);
+    }
     return (int)hipGetLastError();
 }
 }  // namespace fvp
@@ -714,7 +806,23 @@ extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, co
                                int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                                const float *res_post, int relu, int upsample2, float *out, void *stream) {
     return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
-                               upsample2, out, stream);
+                               upsample2, out, nullptr, 0, stream);
+}
+
+extern "C" size_t fvp_conv2d_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int upsample2) {
+    if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || upsample2 < 0 || upsample2 > 2)
+        return 0;
+    const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
+    const fvp::ConvPlan p = fvp::conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, false);
+    return p.ks > 1 ? (size_t)p.ks * N * H * W * Ntot * sizeof(float) : 0;
+}
+
+extern "C" int fvp_conv2d_nhwc_ws(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
+                                  int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                                  const float *res_post, int relu, int upsample2, float *out, void *workspace,
+                                  size_t workspace_bytes, void *stream) {
+    return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
+                               upsample2, out, workspace, workspace_bytes, stream);
 }
 
 #ifdef FVP_CONV_PROBES
@@ -723,13 +831,13 @@ extern "C" int fvp_conv_probe(int probe, const float *in, int N, int H, int W, i
                               const float *res_post, int relu, int upsample2, float *out, void *stream) {
     switch (probe) {
         case 1: return fvp::conv_launch<1>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                           res_post, relu, upsample2, out, stream);
+                                           res_post, relu, upsample2, out, nullptr, 0, stream);
         case 2: return fvp::conv_launch<2>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                           res_post, relu, upsample2, out, stream);
+                                           res_post, relu, upsample2, out, nullptr, 0, stream);
         case 3: return fvp::conv_launch<3>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                           res_post, relu, upsample2, out, stream);
+                                           res_post, relu, upsample2, out, nullptr, 0, stream);
         default: return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                            res_post, relu, upsample2, out, stream);
+                                            res_post, relu, upsample2, out, nullptr, 0, stream);
     }
 }
 #endif
@@ -746,7 +854,8 @@ extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cp
     const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
     if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
     const long long M = (long long)N * H * W;
-    fvp::ConvArgs a{in, nullptr, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2};
+    fvp::ConvArgs a{in,  nullptr, scale, shift, res_pre, res_post, out,       N,   H, W, Cpi, KH, KW, Cpo, Cpo_w,
+                    relu, upsample2, nullptr};
     const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack_bf16);
     hipStream_t st = (hipStream_t)stream;
 #define FVP_CONVB(BM, BN, WR, KC)                                                                                 \

@@ -52,6 +52,7 @@ SIGNATURES = {
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_person_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
+    "fvp_conv2d_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "fvp_person_planes": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, ctypes.POINTER(PersonSpec), c_void_p,
                           c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_person_planes_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
@@ -63,6 +64,8 @@ SIGNATURES = {
     "fvp_fuse_poses": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fvp_conv2d_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv2d_nhwc_ws": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_conv2d_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv_set_tile": [c_int],
@@ -74,7 +77,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _LIB = None
 
 
@@ -95,7 +98,8 @@ def load():
         fn.argtypes = args
         fn.restype = {"fvp_status_string": c_char_p, "fvp_voxelize_workspace_bytes": ctypes.c_size_t,
                       "fvp_voxelize_f16_workspace_bytes": ctypes.c_size_t,
-                      "fvp_person_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
+                      "fvp_person_workspace_bytes": ctypes.c_size_t,
+                      "fvp_conv2d_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
     if lib.fvp_abi_version() != ABI_VERSION:
         raise FvpError(f"fvp: ABI version mismatch ({lib.fvp_abi_version()} != {ABI_VERSION})")
     _LIB = lib

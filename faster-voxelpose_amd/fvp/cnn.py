@@ -89,6 +89,7 @@ class ConvLayer:
         else:  # row (ky*KW+kx)*Cpi + ci  <-  W[co][ci][ky][kx]
             pack[:, :cin, :cout] = w.permute(2, 3, 1, 0).reshape(taps, cin, cout)
         self.wpack = pack.reshape(taps * self.Cpi, self.Cpo_w).contiguous()
+        self._ws = {}  # (N, H, W, device) -> (split-K scratch bytes, tensor)
         self.bf16 = dtype == torch.bfloat16
         if self.bf16:  # [Cpo_w][K], k contiguous
             self.wpack_bf16 = self.wpack.t().contiguous().to(torch.bfloat16)
@@ -109,10 +110,20 @@ class ConvLayer:
         out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=torch.float32, device=x.t.device)
         for r in (res_pre, res_post):
             assert r is None or tuple(r.t.shape) == tuple(out.shape), (None if r is None else r.t.shape, out.shape)
-        fn, w = ("fvp_conv2d_nhwc_bf16", self.wpack_bf16) if self.bf16 else ("fvp_conv2d_nhwc", self.wpack)
-        _lib.call(fn, _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(w), self.KH, self.KW, self.Cpo,
-                  self.Cpo_w, _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
-                  _ptr(res_post.t) if res_post else None, int(relu), self.up2, _ptr(out), _stream(out))
+        args = (_ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wpack_bf16 if self.bf16 else self.wpack), self.KH, self.KW,
+                self.Cpo, self.Cpo_w, _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
+                _ptr(res_post.t) if res_post else None, int(relu), self.up2, _ptr(out))
+        if self.bf16:
+            _lib.call("fvp_conv2d_nhwc_bf16", *args, _stream(out))
+        else:  # split-K scratch for under-filled launches (0 bytes: the layer does not split)
+            key = (x.N, x.H, x.W, out.device)
+            if key not in self._ws:  # kept per input shape: launches on one stream reuse it in order
+                nws = _lib.load().fvp_conv2d_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo,
+                                                             self.up2)
+                self._ws[key] = (nws, torch.empty(((nws + 3) // 4,), dtype=torch.float32, device=out.device)
+                                 if nws else None)
+            nws, ws = self._ws[key]
+            _lib.call("fvp_conv2d_nhwc_ws", *args, _ptr(ws) if ws is not None else None, nws, _stream(out))
         return Act(out, self.Cout)
 
     def flops(self, x: Act) -> int:

@@ -69,16 +69,19 @@ def test_fvp_cnn_matches_reference(gpu_device):
         _close(y.cpu().numpy(), p2p(torch.from_numpy(x_p2p).to(gpu_device)).cpu().numpy(), "P2PNet vs torch GPU")
 
 
-@pytest.fixture(params=[-3, -1], ids=["halo", "pertap"])
+@pytest.fixture(params=[(-3,), (-1,), (-1, -4)], ids=["halo", "pertap", "pertap-nosplit"])
 def conv_kernel(request):
     """Run with the halo-tiled KxK kernel on every eligible layer (forced, so
-    small test shapes take it too) and with the per-tap kernel only."""
+    small test shapes take it too), with the per-tap kernel only (split-K where
+    a launch is under-filled), and with neither halo nor split-K."""
     from fvp import _lib
 
     lib = _lib.load()
-    lib.fvp_conv_set_tile(request.param)
+    for knob in request.param:
+        lib.fvp_conv_set_tile(knob)
     yield request.param
     lib.fvp_conv_set_tile(-2)
+    lib.fvp_conv_set_tile(-5)
 
 
 @pytest.mark.gpu

@@ -27,10 +27,12 @@ def main():
     args = ap.parse_args()
     import numpy as np
     import torch
-    if os.environ.get("FVP_CONV_HALO") == "0":  # A/B: per-tap kernel only
-        from fvp import _lib
+    from fvp import _lib
 
+    if os.environ.get("FVP_CONV_HALO") == "0":  # A/B: per-tap kernel only
         _lib.load().fvp_conv_set_tile(-1)
+    if os.environ.get("FVP_CONV_SPLIT") == "0":  # A/B: no split-K
+        _lib.load().fvp_conv_set_tile(-4)
 
     import cnn_arch
     from fvp import cnn, synthetic

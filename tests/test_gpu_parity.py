@@ -602,3 +602,68 @@ def test_x_slabs_equal_full_grid(gpu_device, wname, nslab, half):
             assert torch.equal(cs, cube[:, :, x0:x1]) and torch.equal(xs, xy[:, :, x0:x1])
     with pytest.raises(ValueError):
         layer.forward_slab(hm, meta, cams2, rt, 4, 4)
+
+
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "onthefly"])
+@pytest.mark.parametrize("half", [False, True], ids=["f32", "f16"])
+def test_nonfinite_heatmaps_vs_torch_grid_sample(gpu_device, otf, half):
+    """NaN and +-inf heatmap pixels: the reference's own CPU ops (F.grid_sample,
+    mean, clamp -- oracle/torch_cpu.py) give NaN where a NaN pixel or an
+    inf*0-weight tap is sampled and +-inf elsewhere, clamp keeps NaN; torch.max
+    over z propagates NaN.  The HIP path must give the same pattern and values."""
+    from fvp import geometry
+    from oracle import torch_cpu
+
+    w, layer, cams, seq = _whole("c3", gpu_device)
+    layer.on_the_fly = otf
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+    g = torch.Generator().manual_seed(11)
+    hm = torch.rand((2, 5, 15, 128, 240), generator=g)
+    flat = hm.view(-1)
+    idx = torch.randperm(flat.numel(), generator=g)[:3000]
+    flat[idx[:1000]] = float("nan")
+    flat[idx[1000:2000]] = float("inf")
+    flat[idx[2000:]] = float("-inf")
+    if half:
+        hm = hm.half()
+    meta = {"seq": [seq] * 2}
+    cube, xy = layer.forward_fused(hm.to(gpu_device), meta, cams, rt.to(gpu_device))
+    sg = layer.build_sample_grid(cams, seq, rt.to(gpu_device), gpu_device).cpu().contiguous()
+    ref = torch_cpu.voxelize(hm.float(), sg, w.voxels_per_axis)
+    got = cube.cpu()
+    assert torch.isnan(ref).any() and torch.isinf(ref).sum() == 0  # clamp maps +-inf to 1 / 0
+    np.testing.assert_array_equal(got.numpy(), ref.numpy())  # NaN == NaN positions, values bit-equal
+    np.testing.assert_array_equal(xy.cpu().numpy(), torch.max(ref, dim=4)[0].numpy())
+
+
+@pytest.mark.parametrize("otf", [True, False], ids=["onthefly", "finegrid"])
+def test_person_planes_nonfinite_heatmaps(gpu_device, otf):
+    """NaN / +-inf heatmap pixels through the per-person kernel: the fused planes
+    (atomic maxima into pre-zeroed planes) equal torch.max over the cube path's
+    cubes (joint_localization_net.py:158-160), NaN positions included.  (The
+    whole-space test above pins the per-voxel NaN/inf arithmetic to torch's
+    grid_sample; the person kernel shares it, fvp_device.h.)"""
+    from fvp.project_individual import ProjectLayer
+
+    d = golden("individual_c3.npz")
+    w = _custom_workload()
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    layer.on_the_fly = otf
+    cams, seq = w.cameras()
+    rt = torch.from_numpy(d["resize_f32"]).to(gpu_device)
+    hm = torch.from_numpy(d["heatmaps"]).clone()
+    g = torch.Generator().manual_seed(12)
+    flat = hm.view(-1)
+    idx = torch.randperm(flat.numel(), generator=g)[:6000]
+    flat[idx[:2000]] = float("nan")
+    flat[idx[2000:4000]] = float("inf")
+    flat[idx[4000:]] = float("-inf")
+    hm = hm.to(gpu_device)
+    props = torch.from_numpy(d["proposals"]).to(gpu_device)
+    cubes, offset = layer(hm, 0, {"seq": [seq]}, props, cams, rt)
+    assert torch.isnan(cubes).any()
+    ref = torch.cat([torch.max(cubes, dim=4)[0], torch.max(cubes, dim=3)[0], torch.max(cubes, dim=2)[0]])
+    planes, off2 = layer.forward_planes(hm, 0, {"seq": [seq]}, props, cams, rt)
+    np.testing.assert_array_equal(planes.cpu().numpy(), ref.cpu().numpy())
+    assert torch.equal(off2, offset)

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
                                                              float *__restrict__ cubes, float *__restrict__ planes,
                                                              float *__restrict__ offset, int P, int V, int J, int H,
-                                                             int W, int xmap) {
+                                                             int W, int xmap, int xsplit) {
     constexpr int JP = 4 * LPV;
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
@@ -135,10 +135,13 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     // proposal (walking x together) share that XCD's L2 footprint (L2 hit 35 %
     // with round-robin placement)
     const int L = xmap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int p = L / ngroups;
-    const int yg0 = (L - p * ngroups) * YG;
+    // block -> (proposal, row group, x part): a proposal's blocks stay contiguous
+    const int p = L / (ngroups * xsplit);
+    const int rem = L - p * ngroups * xsplit;
+    const int yg0 = (rem / xsplit) * YG;
+    const int xpart = rem - (rem / xsplit) * xsplit;
     const Window w = person_window(props + (size_t)p * 7, s);
-    if (offset && yg0 == 0 && threadIdx.x < 3) {
+    if (offset && yg0 == 0 && xpart == 0 && threadIdx.x < 3) {
         const int a = threadIdx.x;
         offset[(size_t)p * 3 + a] =
             ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
@@ -188,7 +191,8 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
         const int gy = w.ctl[1] + yg0 + r;
         rows_in |= yg0 + r < SY && gy >= w.start[1] && gy < w.end[1];
     }
-    for (int x = 0; x < SX; ++x) {
+    const int x_lo = xpart * SX / xsplit, x_hi = (xpart + 1) * SX / xsplit;
+    for (int x = x_lo; x < x_hi; ++x) {
         const int gx = w.ctl[0] + x;
         const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
         // planes only, nothing of this x-plane in the window: every voxel is 0,
@@ -311,11 +315,21 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             const int y = yg0 + r;
             if (y < SY) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (4 * q + k < J) yz_pl[((size_t)(4 * q + k) * SY + y) * SZ + zl] = yzacc[r][k];
+                for (int k = 0; k < 4; ++k) {
+                    if (4 * q + k >= J) continue;
+                    float *dst = yz_pl + ((size_t)(4 * q + k) * SY + y) * SZ + zl;
+                    const unsigned u = __builtin_bit_cast(unsigned, yzacc[r][k]);
+                    if (xsplit == 1) *dst = yzacc[r][k];
+                    else if (u != 0u) atomicMax(reinterpret_cast<unsigned *>(dst), u);  // pre-zeroed plane
+                }
             }
         }
     }
+}
+
+static int person_xsplit(int P, int SY) {
+    const long long rows = (long long)P * SY;
+    return rows >= 4096 ? 1 : rows >= 1024 ? 2 : 4;
 }
 
 template <int LPV, bool OTF>
@@ -328,9 +342,11 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // balanced unit -- measured (C3, 320 proposals): 1 row 6.24, 2 rows 6.85,
     // 4 rows 7.4, 8 rows 8.8 us per proposal (4 rows were best, 10.7 us, before
     // the fast path).  XCD-aware placement keeps a proposal's rows on one XCD.
-    const int xmap = 1;
-    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF>), dim3((unsigned)(P * SY)), dim3(64 * LPV), 0, st, cl, fgrid,
-                       pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap);
+    // Small launches (per-frame calls) split each row's x walk over 2-4 blocks
+    // (the yz maxima then go through atomics into a pre-zeroed plane).
+    const int xmap = 1, xsplit = person_xsplit(P, SY);
+    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF>), dim3((unsigned)(P * SY * xsplit)), dim3(64 * LPV), 0, st, cl,
+                       fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap, xsplit);
 }
 
 }  // namespace fvp
@@ -371,8 +387,9 @@ static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, 
     if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
     hipStream_t st = (hipStream_t)stream;
     float *cl = reinterpret_cast<float *>(workspace);
-    if (planes) {  // xy and xz are reduced with atomicMax over non-negative floats: start from +0
-        const hipError_t e = hipMemsetAsync(planes, 0, (size_t)2 * P * J * SX * SY * 4, st);
+    if (planes) {  // xy, xz (and yz when x is split) are reduced with atomicMax over non-negative floats: from +0
+        const size_t n = (person_xsplit(P, SY) > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
+        const hipError_t e = hipMemsetAsync(planes, 0, n * 4, st);
         if (e != hipSuccess) return (int)e;
     }
     const PersonCoords none{};

@@ -368,6 +368,7 @@ def main():
             line["roofline"]["traffic_note"] = traffic_note
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()  # rank 0's extra measurements done: every rank leaves together
         dist.destroy_process_group()
 
 

@@ -120,8 +120,7 @@ __global__ __launch_bounds__(NT) void nms_topk_small_kernel(const float *__restr
                                                             int64_t *__restrict__ flat, int64_t *__restrict__ xy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float *map = reinterpret_cast<float *>(smem);  // [X*Y]
-    __shared__ Cand red[NT / kWave];
-    __shared__ int win_tid;
+    __shared__ Cand wtop[NT / kWave][KMAX];  // each wave's top-K
     const int M = X * Y;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -170,31 +169,57 @@ __global__ __launch_bounds__(NT) void nms_topk_small_kernel(const float *__restr
         }
         have = have < KMAX ? have + 1 : KMAX;
     }
-    // merge: K rounds of block arg-max over the per-thread heads
+    // merge, level 1: each wave's top-K by K rounds of wave arg-max over its
+    // lanes' heads (shuffles only, no barriers); the winning lane pops its head
+    const int lane = tid & 63, wave = tid >> 6;
+    const Cand none{-INFINITY, 0x7fffffff};
     for (int k = 0; k < K; ++k) {
-        Cand best = have > 0 ? top[0] : Cand{-INFINITY, 0x7fffffff};
-        best = wave_best(best);
-        if ((tid & 63) == 0) red[tid >> 6] = best;
-        __syncthreads();
-        if (tid == 0) {
-            Cand w = red[0];
+        const Cand head = have > 0 ? top[0] : none;
+        const Cand best = wave_best(head);
+        if (lane == 0) wtop[wave][k] = best;
+        if (have > 0 && head.i == best.i) {  // indices are unique: exactly one lane pops
 #pragma unroll
-            for (int i = 1; i < NT / kWave; ++i)
-                if (before(red[i], w)) w = red[i];
+            for (int t = 0; t < KMAX - 1; ++t) top[t] = top[t + 1];
+            top[KMAX - 1] = none;
+            --have;
+        }
+    }
+    __syncthreads();
+    // level 2: wave 0 merges the NT/64 sorted lists the same way
+    if (wave != 0) return;
+    constexpr int PL = ((NT / kWave) * KMAX + kWave - 1) / kWave;  // candidates per lane
+    Cand l2[PL];
+#pragma unroll
+    for (int t = 0; t < PL; ++t) l2[t] = none;
+    int h2 = 0;
+    for (int c = lane; c < (NT / kWave) * K; c += kWave) {
+        Cand cand = wtop[c / K][c - (c / K) * K];
+#pragma unroll
+        for (int t = 0; t < PL; ++t) {
+            if (t >= h2 || before(cand, l2[t])) {
+                const Cand tmp = l2[t];
+                l2[t] = cand;
+                cand = tmp;
+            }
+        }
+        h2 = h2 < PL ? h2 + 1 : PL;
+    }
+    for (int k = 0; k < K; ++k) {
+        const Cand head = h2 > 0 ? l2[0] : none;
+        const Cand w = wave_best(head);
+        if (lane == 0) {
             vals[(size_t)b * K + k] = w.v;
             flat[(size_t)b * K + k] = w.i;
             if (xy) {
                 xy[((size_t)b * K + k) * 2 + 0] = (int64_t)(w.i / X);
                 xy[((size_t)b * K + k) * 2 + 1] = (int64_t)(w.i % X);
             }
-            win_tid = (w.i < M) ? (w.i % NT) : -1;  // element e lives in thread e % NT
         }
-        __syncthreads();
-        if (tid == win_tid) {  // pop the head
+        if (h2 > 0 && head.i == w.i) {
 #pragma unroll
-            for (int t = 0; t < KMAX - 1; ++t) top[t] = top[t + 1];
-            top[KMAX - 1] = Cand{-INFINITY, 0x7fffffff};
-            --have;
+            for (int t = 0; t < PL - 1; ++t) l2[t] = l2[t + 1];
+            l2[PL - 1] = none;
+            --h2;
         }
     }
 }

@@ -27,15 +27,45 @@ __device__ __forceinline__ bool before(const Cand &a, const Cand &b) {
     return a.i < b.i;
 }
 
+// The `before` order as one unsigned 64-bit key (larger = earlier): NaN
+// highest, then float order (+-0 equal), then smaller index.  A wave arg-max
+// is then a branch-free 64-bit max butterfly.
+__device__ __forceinline__ unsigned long long cand_key(const Cand &c) {
+    const unsigned u = c.v == 0.0f ? 0u : __builtin_bit_cast(unsigned, c.v);
+    const unsigned ord = (c.v != c.v) ? 0xffffffffu : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+    return ((unsigned long long)ord << 32) | (unsigned)~(unsigned)c.i;
+}
+
+// one DPP step of the max reduction: lanes the control does not write keep
+// their key (the move returns 0, the identity of the unsigned max)
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ unsigned long long dpp_max(unsigned long long k) {
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(k >> 32), CTRL, ROW_MASK, BANK_MASK, false);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)k, CTRL, ROW_MASK, BANK_MASK, false);
+    const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+    return o > k ? o : k;
+}
+
 __device__ __forceinline__ Cand wave_best(Cand c) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        Cand o;
-        o.v = __shfl_xor(c.v, off);
-        o.i = __shfl_xor(c.i, off);
-        if (before(o, c)) c = o;
-    }
-    return c;
+    // the wave64 DPP reduction (row_shr 1/2/3, 4 and 8 within rows of 16, then
+    // row_bcast 15 / 31): lane 63 ends with the maximum key, read back as a scalar
+    unsigned long long k = cand_key(c);
+    k = dpp_max<0x111, 0xf, 0xf>(k);
+    k = dpp_max<0x112, 0xf, 0xf>(k);
+    k = dpp_max<0x113, 0xf, 0xf>(k);
+    k = dpp_max<0x114, 0xf, 0xe>(k);
+    k = dpp_max<0x118, 0xf, 0xc>(k);
+    k = dpp_max<0x142, 0xa, 0xf>(k);
+    k = dpp_max<0x143, 0xc, 0xf>(k);
+    const unsigned khi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(k >> 32), 63);
+    const unsigned klo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, 63);
+    k = ((unsigned long long)khi << 32) | klo;
+    const unsigned ord = (unsigned)(k >> 32);
+    Cand b;
+    b.i = (int)~(unsigned)k;
+    b.v = ord == 0xffffffffu ? __builtin_nanf("")
+                             : __builtin_bit_cast(float, (ord & 0x80000000u) ? (ord & 0x7fffffffu) : ~ord);
+    return b;
 }
 
 constexpr int kNmsThreads = 256;
@@ -109,18 +139,19 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__re
     }
 }
 
-// Fast path for K <= KMAX: one NT-thread block per frame.  The map is staged
+// Fast path for K <= 16: one NT-thread block per frame.  The map is staged
 // in LDS with unrolled (8 loads in flight per thread) coalesced reads, each
 // thread evaluates the 3x3 peak mask branch-free for its elements and keeps a
-// sorted top-KMAX in registers, and K block-wide arg-max rounds merge the
-// per-thread heads (no rescans of the map).
+// sorted top-KMAX in registers (KMAX >= min(K, elements per thread)); each
+// wave then extracts its top-K with K shuffle arg-max rounds and one wave
+// merges the per-wave lists the same way (no block-wide rounds, no rescans).
 template <int KMAX, int NT>
 __global__ __launch_bounds__(NT) void nms_topk_small_kernel(const float *__restrict__ prob, long long stride, int X,
                                                             int Y, int K, float *__restrict__ vals,
                                                             int64_t *__restrict__ flat, int64_t *__restrict__ xy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float *map = reinterpret_cast<float *>(smem);  // [X*Y]
-    __shared__ Cand wtop[NT / kWave][KMAX];  // each wave's top-K
+    __shared__ Cand wtop[NT / kWave][16];  // each wave's top-K (K <= 16)
     const int M = X * Y;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -187,7 +218,7 @@ __global__ __launch_bounds__(NT) void nms_topk_small_kernel(const float *__restr
     __syncthreads();
     // level 2: wave 0 merges the NT/64 sorted lists the same way
     if (wave != 0) return;
-    constexpr int PL = ((NT / kWave) * KMAX + kWave - 1) / kWave;  // candidates per lane
+    constexpr int PL = ((NT / kWave) * 16 + kWave - 1) / kWave;  // candidates per lane
     Cand l2[PL];
 #pragma unroll
     for (int t = 0; t < PL; ++t) l2[t] = none;
@@ -265,8 +296,14 @@ extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long fr
     if (frame_stride == 0) frame_stride = (long long)M;
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
     if (K <= 16) {
-        hipLaunchKernelGGL((fvp::nms_topk_small_kernel<16, 1024>), dim3(B), dim3(1024), M * 4, (hipStream_t)stream,
-                           prob, frame_stride, X, Y, K, vals, flat, xy);
+        // per-thread list: every element a thread owns when that is <= 8 (then the
+        // list holds them all; 80x80 maps: 7), else the top 16
+        if ((M + 1023) / 1024 <= 8)
+            hipLaunchKernelGGL((fvp::nms_topk_small_kernel<8, 1024>), dim3(B), dim3(1024), M * 4,
+                               (hipStream_t)stream, prob, frame_stride, X, Y, K, vals, flat, xy);
+        else
+            hipLaunchKernelGGL((fvp::nms_topk_small_kernel<16, 1024>), dim3(B), dim3(1024), M * 4,
+                               (hipStream_t)stream, prob, frame_stride, X, Y, K, vals, flat, xy);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob,

@@ -15,7 +15,8 @@ def main():
     from fvp import ops
 
     dev = torch.device("cuda:0")
-    prob = torch.rand((1, 1, 80, 80), device=dev)
+    side = int(os.environ.get("NMS_SIDE", "80"))
+    prob = torch.rand((1, 1, side, side), device=dev)
 
     def bench(fn, n=2000):
         for _ in range(50):
@@ -28,8 +29,9 @@ def main():
         return (time.perf_counter() - t0) / n * 1e6
 
     raw = ops.nms_topk._init_fn
-    print(f"nms_topk via dispatcher {bench(lambda: ops.nms_topk(prob, 10)):.1f} us/call, "
-          f"direct {bench(lambda: raw(prob, 10)):.1f} us/call", flush=True)
+    K = int(os.environ.get("NMS_K", "10"))
+    print(f"nms_topk via dispatcher {bench(lambda: ops.nms_topk(prob, K)):.1f} us/call, "
+          f"direct {bench(lambda: raw(prob, K)):.1f} us/call", flush=True)
 
 
 if __name__ == "__main__":

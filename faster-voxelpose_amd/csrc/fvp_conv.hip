@@ -167,10 +167,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
     }
 }
 
-// PROBE (tools build only, -DFVP_CONV_PROBES): bit 0 = no epilogue stores
-// (one guarded store keeps the MFMAs live), bit 1 = no global loads after the
-// first chunk (LDS staging, barriers and MFMAs only).  0 in the library.
-template <class TL, int PROBE = 0>
+template <class TL>
 __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, AP = TL::AP, MS = TL::MS;
     constexpr int AE = BM * KC / 4;
@@ -236,7 +233,7 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     for (int ch = cb; ch < ce; ++ch) {
         const int buf = ch & 1;
         const bool more = ch + 1 < ce;
-        if (!(PROBE & 2) && more) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);
+        if (more) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);
 #pragma unroll
         for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
             float fa[TL::TM], fb[TL::TN];
@@ -264,17 +261,6 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
         __syncthreads();
     }
 
-    if constexpr (PROBE & 1) {
-        float sink = 0.0f;
-#pragma unroll
-        for (int i = 0; i < TL::TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TL::TN; ++j)
-#pragma unroll
-                for (int r = 0; r < TL::NACC; ++r) sink += acc[i][j][r];
-        if (sink == 1234.5f) a.out[t] = sink;
-        return;
-    }
     if (a.part) {  // split-K: raw partial sums, combined in z order by conv_splitk_reduce
         const int Ntot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
         float *__restrict__ dst = a.part + (size_t)blockIdx.z * M * Ntot;
@@ -326,7 +312,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce(ConvArgs a, int ks, in
 // one image (TH = BM / 16); per 16-channel chunk the (TH+KH-1) x (16+KW-1)
 // input halo is staged into LDS once and serves every (ky, kx) tap, where the
 // per-tap implicit-im2col loads of conv_mfma_kernel re-read each input pixel
-// up to KH*KW times (10-26 % of a layer's time, tools/conv_probe.py).  The K
+// up to KH*KW times (10-26 % of a layer's time, profiles/round1/conv_probe.txt).  The K
 // loop walks channel chunks outer and taps inner; the per-tap weight tiles are
 // double-buffered and prefetched one step ahead as in conv_mfma_kernel, the
 // next chunk's halo is loaded into registers during the current chunk's taps.
@@ -476,25 +462,7 @@ using TileN64m = Tile<64, 64, 32, 2>;   //        2x2 waves x (32 px x 32 ch)
 using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
 // (larger wave tiles -- 64x64 per wave -- and 32-wide K chunks measured slower)
 
-static int g_force_tile = 0;
-static int g_halo = 1;
-static int g_split = 1;  // split-K of under-filled per-tap launches (fvp_conv_set_tile(-4): off, -5: on)  // halo-tiled KxK convolutions: 0 off, 1 where measured faster, 2 wherever eligible
-
 }  // namespace fvp
-
-extern "C" int fvp_conv_set_tile(int id) {
-    if (id <= -1 && id >= -3) {  // -1: per-tap kernel only, -2: halo where faster (default), -3: halo forced
-        fvp::g_halo = -1 - id;
-        return FVP_OK;
-    }
-    if (id == -4 || id == -5) {
-        fvp::g_split = id == -5;
-        return FVP_OK;
-    }
-    if (id < 0 || id > 7) return FVP_ERR_SHAPE;
-    fvp::g_force_tile = id;
-    return FVP_OK;
-}
 
 namespace fvp {
 
@@ -676,36 +644,32 @@ namespace fvp {
 // or the per-tap kernel's tile and its split-K factor.
 struct ConvPlan {
     int halo;   // 1/3/5 = TileN16/N32/N64 (2/4/6/7 small tiles when forced), 0 = per-tap kernel
-    int tile;   // per-tap tile id 1..7 (fvp_conv_set_tile numbering)
+    int tile;   // per-tap tile id 1..7 (kTileBM / kTileBN)
     int ks;     // split-K factor of the per-tap kernel (1 = none)
 };
 
 static const int kTileBM[8] = {0, 256, 64, 128, 64, 128, 64, 32};
 static const int kTileBN[8] = {0, 16, 16, 32, 32, 64, 64, 64};
 
-static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot, int upsample2, bool probe) {
+static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot, int upsample2, int algo) {
     ConvPlan p{0, 0, 1};
     const long long M = (long long)N * H * W;
     const long long enough = 512;  // >= 2 blocks per CU
-    if (g_force_tile) {
-        p.tile = g_force_tile;
-        return p;
-    }
     // Halo tiles are 16 pixels wide: only where a row wastes <= 1/8 of them
     // (CenterNet's 20- and 40-wide maps stay per-tap), and only with the large
     // tiles (>= 8 rows: halo overhead <= 1.4x of the tile) at >= 2 blocks per
-    // CU -- measured (tools/conv_probe.py): 7x7 front 205 -> 147 us, 3x3
+    // CU -- measured (profiles/round1/conv_probe.txt): 7x7 front 205 -> 147 us, 3x3
     // layers at 64/32 px 4-6 % faster; 4-row tiles and sub-2-per-CU launches
     // were 2-10 % slower than per-tap.
     const int tx = (W + 15) / 16;
-    const bool halo = g_halo && !probe && (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && !upsample2 &&
+    const bool halo = (algo == FVP_CONV_AUTO || algo == FVP_CONV_HALO) && (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && !upsample2 &&
                       (tx * 16 - W) * 8 <= W;
     auto hblocks = [&](int id) {
         const int rows = kTileBM[id] / 16;
         return (long long)N * tx * ((H + rows - 1) / rows) * ((Ntot + kTileBN[id] - 1) / kTileBN[id]);
     };
     if (halo) {
-        const bool any = g_halo == 2;  // forced (tests): every eligible layer, small tiles too
+        const bool any = algo == FVP_CONV_HALO;  // every eligible layer, small tiles too
         const int big = Ntot <= 16 ? 1 : Ntot <= 32 ? 3 : 5;
         if (hblocks(big) >= enough) p.halo = big;
         else if (any) p.halo = big == 5 ? (hblocks(6) >= enough ? 6 : 7) : big + 1;
@@ -723,7 +687,7 @@ static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot
     // 8 frames 0.61 -> 0.55 ms; C2CNet's 1-D rows were slower split).
     const int nchunks = KH * KW * (Cpi / 16);
     const long long nb = blocks(p.tile);
-    if (g_split && !probe && H > 1 && nb < 256 && nchunks >= 8) {  // 2-D maps (C2CNet's 1-D rows: slower)
+    if (algo != FVP_CONV_PER_TAP_NOSPLIT && H > 1 && nb < 256 && nchunks >= 8) {  // 2-D maps (C2CNet's 1-D rows: slower)
         int ks = (int)((512 + nb - 1) / nb);
         ks = ks < nchunks / 4 ? ks : nchunks / 4;
         p.ks = ks < 8 ? ks : 8;
@@ -732,11 +696,10 @@ static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot
     return p;
 }
 
-template <int PROBE>
 static int conv_launch(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW, int Cpo,
                        int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                       const float *res_post, int relu, int upsample2, float *out, void *ws, size_t ws_bytes,
-                       void *stream) {
+                       const float *res_post, int relu, int upsample2, float *out, int algo, void *ws,
+                       size_t ws_bytes, void *stream) {
     if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
         (KH & 1) == 0 || (KW & 1) == 0)
@@ -749,7 +712,8 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
     fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2,
                     nullptr};
     hipStream_t st = (hipStream_t)stream;
-    ConvPlan p = conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, PROBE != 0);
+    if (algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return FVP_ERR_SHAPE;
+    ConvPlan p = conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, algo);
     if (p.ks > 1 && (!ws || ws_bytes < (size_t)p.ks * M * Ntot * sizeof(float))) p.ks = 1;  // no scratch: no split
     if (p.ks > 1) a.part = reinterpret_cast<float *>(ws);
     if (p.halo) {
@@ -778,7 +742,7 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
 #define FVP_CONV(TL)                                                                                              \
     do {                                                                                                          \
         if (Cpi % fvp::TL::KC) return FVP_ERR_SHAPE;                                                              \
-        hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL, PROBE>),                                               \
+        hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL>),                                               \
                            dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                  \
                                 (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN), (unsigned)p.ks),              \
                            dim3(256), 0, st, a);                                                                 \
@@ -805,42 +769,27 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
 extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                                int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                                const float *res_post, int relu, int upsample2, float *out, void *stream) {
-    return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
-                               upsample2, out, nullptr, 0, stream);
+    return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
+                            upsample2, out, FVP_CONV_AUTO, nullptr, 0, stream);
 }
 
-extern "C" size_t fvp_conv2d_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int upsample2) {
+extern "C" size_t fvp_conv2d_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int upsample2,
+                                             int algo) {
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || upsample2 < 0 || upsample2 > 2)
         return 0;
+    if (algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return 0;
     const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
-    const fvp::ConvPlan p = fvp::conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, false);
+    const fvp::ConvPlan p = fvp::conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, algo);
     return p.ks > 1 ? (size_t)p.ks * N * H * W * Ntot * sizeof(float) : 0;
 }
 
 extern "C" int fvp_conv2d_nhwc_ws(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                                   int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                                  const float *res_post, int relu, int upsample2, float *out, void *workspace,
-                                  size_t workspace_bytes, void *stream) {
-    return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
-                               upsample2, out, workspace, workspace_bytes, stream);
+                                  const float *res_post, int relu, int upsample2, float *out, int algo,
+                                  void *workspace, size_t workspace_bytes, void *stream) {
+    return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
+                            upsample2, out, algo, workspace, workspace_bytes, stream);
 }
-
-#ifdef FVP_CONV_PROBES
-extern "C" int fvp_conv_probe(int probe, const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH,
-                              int KW, int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                              const float *res_post, int relu, int upsample2, float *out, void *stream) {
-    switch (probe) {
-        case 1: return fvp::conv_launch<1>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                           res_post, relu, upsample2, out, nullptr, 0, stream);
-        case 2: return fvp::conv_launch<2>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                           res_post, relu, upsample2, out, nullptr, 0, stream);
-        case 3: return fvp::conv_launch<3>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                           res_post, relu, upsample2, out, nullptr, 0, stream);
-        default: return fvp::conv_launch<0>(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre,
-                                            res_post, relu, upsample2, out, nullptr, 0, stream);
-    }
-}
-#endif
 
 extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH,
                                     int KW, int Cpo, int Cpo_w, const float *scale, const float *shift,

@@ -1,14 +1,19 @@
 // Proposal selection on the 2-D detection map and the per-proposal gathers
 // (A9, A10 of SURVEY.md §8(a)).
 //
-// nms_topk (K <= 16): one 1024-thread block per frame, register top-K per
-// thread merged by K block arg-max rounds (below).  nms_topk (K > 16): one
-// 256-thread block per frame.  The 3x3/stride-1/pad-1 max-pool
-// keep mask (proposal.py:34-52) is evaluated once into LDS, then K rounds of
-// a block-wide arg-max (value descending, flat index ascending -- a total
-// order, so the result is deterministic) pick the top-K (proposal.py:73).
-// Indices decode as get_index2D does, dividing by shape[1] == X
-// (proposal.py:27-29,75).
+// The 3x3/stride-1/pad-1 max-pool keep mask (proposal.py:34-52) zeroes every
+// element that is not its neighbourhood's maximum, then the top-K of the
+// masked map is taken (proposal.py:73) in a total order -- value descending
+// (NaN first, as torch.topk), then flat index ascending -- so the result is
+// deterministic.  Indices decode as get_index2D does, dividing by
+// shape[1] == X (proposal.py:27-29,75).
+//
+// nms_topk_small_kernel (K <= 16): one 1024-thread block per frame; each
+// thread keeps a sorted register list of its elements' candidates, each wave
+// extracts its top-K by K wave arg-max rounds (a 64-bit order key reduced
+// over DPP), and one wave merges the per-wave lists the same way.
+// nms_topk_kernel (K > 16): one 256-thread block per frame, the masked map in
+// LDS, K block-wide arg-max rounds over a taken bitmap.
 #include "fvp_device.h"
 
 namespace fvp {
@@ -49,7 +54,8 @@ __device__ __forceinline__ unsigned long long dpp_max(unsigned long long k) {
 __device__ __forceinline__ Cand wave_best(Cand c) {
     // the wave64 DPP reduction (row_shr 1/2/3, 4 and 8 within rows of 16, then
     // row_bcast 15 / 31): lane 63 ends with the maximum key, read back as a scalar
-    unsigned long long k = cand_key(c);
+    const unsigned long long own = cand_key(c);
+    unsigned long long k = own;
     k = dpp_max<0x111, 0xf, 0xf>(k);
     k = dpp_max<0x112, 0xf, 0xf>(k);
     k = dpp_max<0x113, 0xf, 0xf>(k);
@@ -60,11 +66,14 @@ __device__ __forceinline__ Cand wave_best(Cand c) {
     const unsigned khi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(k >> 32), 63);
     const unsigned klo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, 63);
     k = ((unsigned long long)khi << 32) | klo;
-    const unsigned ord = (unsigned)(k >> 32);
+    // the candidate itself comes from the lane holding the winning key (keys
+    // are unique per element), so -0.0 and NaN payloads pass through unchanged
+    // as in torch.topk
+    const unsigned long long who = __builtin_amdgcn_ballot_w64(own == k);
+    const int lane = who ? (int)__builtin_ctzll(who) : 0;
     Cand b;
-    b.i = (int)~(unsigned)k;
-    b.v = ord == 0xffffffffu ? __builtin_nanf("")
-                             : __builtin_bit_cast(float, (ord & 0x80000000u) ? (ord & 0x7fffffffu) : ~ord);
+    b.v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c.v), lane));
+    b.i = __builtin_amdgcn_readlane(c.i, lane);
     return b;
 }
 

@@ -52,7 +52,7 @@ SIGNATURES = {
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_person_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
-    "fvp_conv2d_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+    "fvp_conv2d_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "fvp_person_planes": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, ctypes.POINTER(PersonSpec), c_void_p,
                           c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_person_planes_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
@@ -65,10 +65,10 @@ SIGNATURES = {
     "fvp_conv2d_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv2d_nhwc_ws": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
-                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
+                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, ctypes.c_size_t,
+                           c_void_p],
     "fvp_conv2d_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
-    "fvp_conv_set_tile": [c_int],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_weight_net": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
@@ -77,7 +77,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _LIB = None
 
 

@@ -18,11 +18,30 @@ one fused launch.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.nn as nn
 
 from . import _lib
 from .ops import _ptr, _stream
+
+
+# Kernel selection passed to fvp_conv2d_nhwc_ws (include/fvp.h FVP_CONV_*):
+# AUTO in the product; tests run every choice through conv_algo().
+CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT = 0, 1, 2, 3
+CONV_ALGO = CONV_AUTO
+
+
+@contextlib.contextmanager
+def conv_algo(algo: int):
+    """Launch the fp32 convolutions inside the block with kernel choice `algo` (process-wide)."""
+    global CONV_ALGO
+    prev, CONV_ALGO = CONV_ALGO, algo
+    try:
+        yield
+    finally:
+        CONV_ALGO = prev
 
 
 def _rup(x: int, m: int) -> int:
@@ -89,7 +108,7 @@ class ConvLayer:
         else:  # row (ky*KW+kx)*Cpi + ci  <-  W[co][ci][ky][kx]
             pack[:, :cin, :cout] = w.permute(2, 3, 1, 0).reshape(taps, cin, cout)
         self.wpack = pack.reshape(taps * self.Cpi, self.Cpo_w).contiguous()
-        self._ws = {}  # (N, H, W, device) -> (split-K scratch bytes, tensor)
+        self._ws = {}  # (N, H, W, algo) -> split-K scratch bytes
         self.bf16 = dtype == torch.bfloat16
         if self.bf16:  # [Cpo_w][K], k contiguous
             self.wpack_bf16 = self.wpack.t().contiguous().to(torch.bfloat16)
@@ -116,14 +135,16 @@ class ConvLayer:
         if self.bf16:
             _lib.call("fvp_conv2d_nhwc_bf16", *args, _stream(out))
         else:  # split-K scratch for under-filled launches (0 bytes: the layer does not split)
-            key = (x.N, x.H, x.W, out.device)
-            if key not in self._ws:  # kept per input shape: launches on one stream reuse it in order
-                nws = _lib.load().fvp_conv2d_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo,
-                                                             self.up2)
-                self._ws[key] = (nws, torch.empty(((nws + 3) // 4,), dtype=torch.float32, device=out.device)
-                                 if nws else None)
-            nws, ws = self._ws[key]
-            _lib.call("fvp_conv2d_nhwc_ws", *args, _ptr(ws) if ws is not None else None, nws, _stream(out))
+            # allocated per call: the caching allocator is stream-ordered, so two
+            # streams running this layer never share partial sums
+            key = (x.N, x.H, x.W, CONV_ALGO)
+            if key not in self._ws:
+                self._ws[key] = _lib.load().fvp_conv2d_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW,
+                                                                        self.Cpo, self.up2, CONV_ALGO)
+            nws = self._ws[key]
+            ws = torch.empty(((nws + 3) // 4,), dtype=torch.float32, device=out.device) if nws else None
+            _lib.call("fvp_conv2d_nhwc_ws", *args, CONV_ALGO, _ptr(ws) if ws is not None else None, nws,
+                      _stream(out))
         return Act(out, self.Cout)
 
     def flops(self, x: Act) -> int:

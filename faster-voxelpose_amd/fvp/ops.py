@@ -196,7 +196,10 @@ def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, to
         raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map")
     p = prob
     # a channel slice of a contiguous [B,C,X,Y] tensor is passed by frame stride, without a copy
-    if not (p.dtype == torch.float32 and p.stride()[-1] == 1 and p.stride()[-2] == Y):
+    # (a batch stride below X*Y -- e.g. an expand()ed map with stride 0 -- is copied:
+    # the kernel reads each frame's X*Y floats at b*stride)
+    if not (p.dtype == torch.float32 and p.stride()[-1] == 1 and p.stride()[-2] == Y
+            and (B <= 1 or p.stride()[0] >= X * Y)):
         p = p.to(torch.float32).contiguous()
     stride = p.stride()[0] if B > 1 else X * Y
     vals = torch.empty((B, K), dtype=torch.float32, device=p.device)

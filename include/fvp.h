@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 6
+#define FVP_ABI_VERSION 7
 #define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
 #define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
 /* Camera slots per voxel in a packed grid (V rounded up to even). */
@@ -229,15 +229,27 @@ int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob
 int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                     int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                     const float *res_post, int relu, int upsample2, float *out, void *stream);
-/* Same with a device scratch for split-K: launches under one block per CU with
- * a long K walk (small maps, many channels) split the K loop over blocks and
- * combine the partial sums in a fixed order.  workspace may be NULL or
- * smaller than fvp_conv2d_workspace_bytes() (then no split); 0 bytes = the
- * layer does not split. */
-size_t fvp_conv2d_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int upsample2);
+/* Kernel selection of fvp_conv2d_nhwc_ws (every choice computes the same
+ * convolution; they differ in tiling only, and tests run each of them):
+ *   FVP_CONV_AUTO            halo-tiled KxK kernel where measured faster,
+ *                            per-tap kernel elsewhere, split-K where a per-tap
+ *                            launch is under-filled (what fvp_conv2d_nhwc runs)
+ *   FVP_CONV_PER_TAP         per-tap kernel on every layer (split-K as AUTO)
+ *   FVP_CONV_HALO            halo-tiled kernel on every eligible layer
+ *   FVP_CONV_PER_TAP_NOSPLIT per-tap kernel, never split */
+#define FVP_CONV_AUTO 0
+#define FVP_CONV_PER_TAP 1
+#define FVP_CONV_HALO 2
+#define FVP_CONV_PER_TAP_NOSPLIT 3
+/* Same with a kernel choice and a device scratch for split-K: launches under
+ * one block per CU with a long K walk (small maps, many channels) split the K
+ * loop over blocks and combine the partial sums in a fixed order.  workspace
+ * may be NULL or smaller than fvp_conv2d_workspace_bytes() of the same algo
+ * (then no split); 0 bytes = the layer does not split. */
+size_t fvp_conv2d_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int upsample2, int algo);
 int fvp_conv2d_nhwc_ws(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                        int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                       const float *res_post, int relu, int upsample2, float *out, void *workspace,
+                       const float *res_post, int relu, int upsample2, float *out, int algo, void *workspace,
                        size_t workspace_bytes, void *stream);
 /* Same convolution with bf16 operands (opt-in precision): activations are
  * rounded to bf16 when staged, weights given as bf16 [Cpo_w][KH*KW*Cpi]
@@ -246,10 +258,6 @@ int fvp_conv2d_nhwc_ws(const float *in, int N, int H, int W, int Cpi, const floa
 int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH, int KW,
                          int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                          const float *res_post, int relu, int upsample2, float *out, void *stream);
-/* Tuning hook: 0 = tile chosen per layer (default); 1..7 force one tile shape
- * (per-tap kernel); halo-tiled KxK kernel: -1 off, -2 where measured faster
- * (default), -3 wherever eligible (tests); split-K: -4 off, -5 on (default). */
-int fvp_conv_set_tile(int id);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
 int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);
 /* KH x KW / stride-(KH, KW) max pool, KH, KW in {1, 2} (floor); KH = 1, KW = 2

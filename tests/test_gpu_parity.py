@@ -96,12 +96,24 @@ def test_voxelize_uniform_stress_matches_reference(gpu_device, case, wname):
 
 
 def _check_topk(vals, flat, xy, ref_vals, ref_flat, ref_xy):
+    """Values identical everywhere; indices identical in every tie-free slot.
+    A slot whose value is tied with another slot of the same frame may hold any
+    member of the tie group (torch.topk leaves their order unspecified): there
+    the set of indices of each tie group that lies wholly inside the top-K must
+    match the reference's.  Returns the number of slots not compared one by one."""
     assert np.array_equal(vals, ref_vals)
+    tied = 0
     for b in range(vals.shape[0]):
         for k in range(vals.shape[1]):
-            if np.sum(vals[b] == vals[b, k]) == 1:  # tie-free entries: identical argmax indices
+            group = vals[b] == vals[b, k]
+            if np.sum(group) == 1:  # tie-free entries: identical argmax indices
                 assert flat[b, k] == ref_flat[b, k]
                 assert np.array_equal(xy[b, k], ref_xy[b, k])
+                continue
+            tied += 1
+            if not group[-1]:  # the whole group is inside the top-K: same members
+                assert set(flat[b][group]) == set(ref_flat[b][group]), (b, k)
+    return tied
 
 
 @pytest.mark.parametrize("tag", ["sq", "nonsq", "big"])
@@ -111,8 +123,9 @@ def test_nms_matches_reference(gpu_device, tag):
     d = golden("nms.npz")
     p = torch.from_numpy(d[f"{tag}_prob"]).to(gpu_device)
     v, xy, fl = nms2D(p, d[f"{tag}_vals"].shape[1])
-    _check_topk(v.cpu().numpy(), fl.cpu().numpy(), xy.cpu().numpy(), d[f"{tag}_vals"], d[f"{tag}_flat"],
-                d[f"{tag}_xy"])
+    tied = _check_topk(v.cpu().numpy(), fl.cpu().numpy(), xy.cpu().numpy(), d[f"{tag}_vals"], d[f"{tag}_flat"],
+                       d[f"{tag}_xy"])
+    print(f"nms {tag}: {tied} tied slots compared as tie-group sets")
     # ties resolved value-desc / index-asc exactly like the oracle
     ov, oxy, ofl = O.nms2d(d[f"{tag}_prob"], d[f"{tag}_vals"].shape[1])
     assert np.array_equal(fl.cpu().numpy(), ofl)
@@ -529,6 +542,43 @@ def test_nms_topk_both_paths_vs_oracle(gpu_device, K):
     assert np.array_equal(np.nan_to_num(got, nan=7.0), np.nan_to_num(ov, nan=7.0))
     assert np.array_equal(fl.cpu().numpy()[1:], ofl[1:])  # frame 0 holds a NaN (ordering checked above)
     assert np.array_equal(xy.cpu().numpy()[1:], oxy[1:])
+
+
+def test_nms_expanded_map_batch_stride_zero(gpu_device):
+    """A batch-expanded map (batch stride 0) gives every frame the one map's top-K."""
+    from fvp.proposal import nms2D
+
+    g = torch.Generator().manual_seed(3)
+    one = torch.rand((1, 1, 40, 40), generator=g)
+    prob = one.to(gpu_device).expand(4, 1, 40, 40)
+    assert prob.stride()[0] == 0
+    for K in (10, 20):
+        v, xy, fl = nms2D(prob, K)
+        ov, oxy, ofl = O.nms2d(one.numpy(), K)
+        for b in range(4):
+            assert np.array_equal(v[b].cpu().numpy(), ov[0])
+            assert np.array_equal(fl[b].cpu().numpy(), ofl[0])
+
+
+@pytest.mark.parametrize("K", [16, 20])
+def test_nms_signed_zero_and_nan_payload_pass_through(gpu_device, K):
+    """keep = 0 times a negative value is -0.0 and 0 * NaN keeps the NaN's payload:
+    the selected values come back bit for bit, as torch.topk returns them."""
+    from fvp.proposal import nms2D
+
+    vals = -np.arange(1, 37, dtype=np.float32).reshape(1, 1, 6, 6)
+    vals[0, 0, 4, 4] = np.frombuffer(np.uint32(0x7FC01234).tobytes(), np.float32)[0]  # NaN with a payload
+    prob = torch.from_numpy(vals).to(gpu_device)
+    v, xy, fl = nms2D(prob, K)
+    # the masked map computed by torch on the same device (max_pool2d keep mask)
+    mp = torch.nn.functional.max_pool2d(prob, 3, 1, 1)
+    masked = ((prob == mp).float() * prob).flatten().cpu().numpy().view(np.uint32)
+    got = v.cpu().numpy()[0].view(np.uint32)
+    assert np.array_equal(got, masked[fl.cpu().numpy()[0]])  # values are the selected elements, bit for bit
+    ov, _, ofl = O.nms2d(vals, K)
+    assert np.array_equal(fl.cpu().numpy(), ofl)
+    assert np.signbit(v.cpu().numpy()[0][1:]).sum() == np.signbit(ov[0][1:]).sum()  # -0.0 entries kept negative
+    assert np.isnan(v.cpu().numpy()[0, 0])
 
 
 def test_captured_graph_step_matches_eager(gpu_device):

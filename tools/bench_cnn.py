@@ -29,10 +29,11 @@ def main():
     import torch
     from fvp import _lib
 
-    if os.environ.get("FVP_CONV_HALO") == "0":  # A/B: per-tap kernel only
-        _lib.load().fvp_conv_set_tile(-1)
-    if os.environ.get("FVP_CONV_SPLIT") == "0":  # A/B: no split-K
-        _lib.load().fvp_conv_set_tile(-4)
+    if os.environ.get("FVP_CONV_HALO") == "0":  # A/B: per-tap kernel only (FVP_CONV_SPLIT=0: never split)
+        cnn_algo = 3 if os.environ.get("FVP_CONV_SPLIT") == "0" else 1
+        from fvp import cnn as _cnn
+
+        _cnn.CONV_ALGO = cnn_algo
 
     import cnn_arch
     from fvp import cnn, synthetic

@@ -21,10 +21,6 @@ for step in ${STEPS:-pytest smoke bench}; do
     smoke) run smoke 150 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2 --traffic off --cpu-seconds 5} ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 10 --warmup 2 --traffic off --cpu-baseline off ;;
-    micro) run micro 400 python tools/microbench.py ${MICRO_ARGS:-} ;;
-    micro2) run micro2 400 python tools/microbench2.py ${MICRO_ARGS:-} ;;
-    micro2c5) run micro2c5 400 python tools/microbench2.py --workload c5 --batch 8 ;;
-    micro2c4) run micro2c4 400 python tools/microbench2.py --workload c4 --batch 64 ;;
     taprobe) run taprobe 400 python tools/ta_probe.py ;;
   esac
 done

@@ -7,6 +7,15 @@
 //   * torch.mm with K=3 accumulates fma(a2,b2, fma(a1,b1, a0*b0))
 //   * torch.linspace is fma(step,i,start) / fma(-step,n-1-i,end)
 //   * grid_sample accumulates fma(se_v,se, fma(sw_v,sw, fma(ne_v,ne, nw_v*nw)))
+//   * torch.mean(dim=0) over the V views (project_whole.py:162,
+//     project_individual.py:283) is sum / V, the sum in ATen's cascade order
+//     (SumKernel.cpp multi_row_sum, level step 16): views accumulate
+//     sequentially from 0 in blocks of 16; each complete block is folded into
+//     a second accumulator (itself a sequential sum of block sums from 0); the
+//     total is remainder + blocks.  V <= 16 is a plain sequential sum.
+//     (Verified against torch here for V = 5..100; the last < 64 output
+//     elements of a tensor -- never a whole-space cube -- take ATen's ILP-4
+//     tail order instead, machine-dependent, at most 1 ulp apart.)
 // Compile with -ffp-contract=off and correctly rounded fp32 division.
 #pragma once
 

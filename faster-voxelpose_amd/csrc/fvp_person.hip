@@ -118,7 +118,7 @@ struct PersonCoords {
     fvp_image_spec im;      //                       (OTF)
 };
 
-template <int LPV, int YG, bool OTF>
+template <int LPV, int YG, bool OTF, bool CASC>
 __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
                                                              const float *__restrict__ props,
@@ -205,6 +205,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             const int gy = w.ctl[1] + y;
             const bool valid = xin && zin && y < SY && gy >= w.start[1] && gy < w.end[1];
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            float blk[4] = {0.f, 0.f, 0.f, 0.f};  // CASC: completed 16-camera blocks (fvp_device.h)
             if (__builtin_amdgcn_ballot_w64(valid)) {
                 const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
                 float wxc = 0.f, wyc = 0.f, wzc = 0.f;  // OTF: fine voxel centre (compute_grid at fine resolution)
@@ -240,6 +241,15 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                         constexpr int S = k >> 1;
                         const int v = v0 + k;
                         if (v >= V) return;
+                        if constexpr (CASC) {
+                            if ((v & 15) == 0 && v > 0) {
+#pragma unroll
+                                for (int m = 0; m < 4; ++m) {
+                                    blk[m] = blk[m] + acc[m];
+                                    acc[m] = 0.0f;
+                                }
+                            }
+                        }
                         const Taps4<false> &src = (k & 1) ? t1 : t0;
                         unsigned o[4];
                         unsigned all = kOOB;
@@ -269,6 +279,9 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                     });
                 }
             }
+            // the sum's final levels (fvp_device.h): remainder + blocks, or + 0 (a -0 sum becomes +0)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[m] = acc[m] + (CASC ? blk[m] : 0.0f);
             float o[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -332,7 +345,7 @@ static int person_xsplit(int P, int SY) {
     return rows >= 4096 ? 1 : rows >= 1024 ? 2 : 4;
 }
 
-template <int LPV, bool OTF>
+template <int LPV, bool OTF, bool CASC>
 static void launch_person_cl(const float *cl, const float *fgrid, const PersonCoords &pc, const float *props,
                              const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
                              float *offset, int P, int V, int J, int H, int W, hipStream_t st) {
@@ -345,7 +358,7 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // Small launches (per-frame calls) split each row's x walk over 2-4 blocks
     // (the yz maxima then go through atomics into a pre-zeroed plane).
     const int xmap = 1, xsplit = person_xsplit(P, SY);
-    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF>), dim3((unsigned)(P * SY * xsplit)), dim3(64 * LPV), 0, st, cl,
+    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF, CASC>), dim3((unsigned)(P * SY * xsplit)), dim3(64 * LPV), 0, st, cl,
                        fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap, xsplit);
 }
 
@@ -374,7 +387,7 @@ static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, 
     if (!heatmaps || !spec || (!fine_grid && !pc)) return FVP_ERR_NULL;
     if (P <= 0) return FVP_OK;
     if (!proposals) return FVP_ERR_NULL;
-    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2) return FVP_ERR_SHAPE;
+    if (B <= 0 || V <= 0 || V > FVP_MAX_VIEWS || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2) return FVP_ERR_SHAPE;
     if (pc && V > 64) return FVP_ERR_SHAPE;  // camera records staged in LDS
     const int SX = spec->bins[0], SY = spec->bins[1], SZ = spec->bins[2];
     if (SX <= 0 || SY <= 0 || SZ <= 0 || SZ > 64 || spec->fine[0] <= 1 || spec->fine[1] <= 1 || spec->fine[2] <= 1)
@@ -396,12 +409,18 @@ static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, 
     const PersonCoords &c = pc ? *pc : none;
 #define FVP_PERSON_CASE(L)                                                                                            \
     launch_layout<L, float>(heatmaps, B, V, J, H, W, cl, st);                                                        \
-    if (pc)                                                                                                           \
-        launch_person_cl<L, true>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, W,  \
-                                  st);                                                                                \
+    if (pc && V > 16)                                                                                                 \
+        launch_person_cl<L, true, true>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, \
+                                        W, st);                                                                       \
+    else if (pc)                                                                                                      \
+        launch_person_cl<L, true, false>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J,  \
+                                         H, W, st);                                                                   \
+    else if (V > 16)                                                                                                  \
+        launch_person_cl<L, false, true>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V,   \
+                                         J, H, W, st);                                                                \
     else                                                                                                              \
-        launch_person_cl<L, false>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H,  \
-                                   W, st);                                                                            \
+        launch_person_cl<L, false, false>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V,  \
+                                          J, H, W, st);                                                               \
     break;
     switch (lanes_per_voxel(J)) {
         case 1: FVP_PERSON_CASE(1)

@@ -8,10 +8,9 @@
 // deterministic.  Indices decode as get_index2D does, dividing by
 // shape[1] == X (proposal.py:27-29,75).
 //
-// nms_topk_small_kernel (K <= 16): one 1024-thread block per frame; each
-// thread keeps a sorted register list of its elements' candidates, each wave
-// extracts its top-K by K wave arg-max rounds (a 64-bit order key reduced
-// over DPP), and one wave merges the per-wave lists the same way.
+// nms_select_kernel (K <= 16, X*Y <= 16384): one 1024-thread block per frame,
+// the elements' 64-bit order keys in registers; a threshold from the wave
+// maxima bounds the candidates, which are compacted and ranked (below).
 // nms_topk_kernel (K > 16): one 256-thread block per frame, the masked map in
 // LDS, K block-wide arg-max rounds over a taken bitmap.
 #include "fvp_device.h"
@@ -148,119 +147,188 @@ __global__ __launch_bounds__(kNmsThreads) void nms_topk_kernel(const float *__re
     }
 }
 
-// Fast path for K <= 16: one NT-thread block per frame.  The map is staged
-// in LDS with unrolled (8 loads in flight per thread) coalesced reads, each
-// thread evaluates the 3x3 peak mask branch-free for its elements and keeps a
-// sorted top-KMAX in registers (KMAX >= min(K, elements per thread)); each
-// wave then extracts its top-K with K shuffle arg-max rounds and one wave
-// merges the per-wave lists the same way (no block-wide rounds, no rescans).
-template <int KMAX, int NT>
-__global__ __launch_bounds__(NT) void nms_topk_small_kernel(const float *__restrict__ prob, long long stride, int X,
-                                                            int Y, int K, float *__restrict__ vals,
-                                                            int64_t *__restrict__ flat, int64_t *__restrict__ xy) {
+// wave maximum of a 64-bit key, uniform in every lane
+__device__ __forceinline__ unsigned long long wave_max_key(unsigned long long k) {
+    k = dpp_max<0x111, 0xf, 0xf>(k);
+    k = dpp_max<0x112, 0xf, 0xf>(k);
+    k = dpp_max<0x113, 0xf, 0xf>(k);
+    k = dpp_max<0x114, 0xf, 0xe>(k);
+    k = dpp_max<0x118, 0xf, 0xc>(k);
+    k = dpp_max<0x142, 0xa, 0xf>(k);
+    k = dpp_max<0x143, 0xc, 0xf>(k);
+    const unsigned khi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(k >> 32), 63);
+    const unsigned klo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, 63);
+    return ((unsigned long long)khi << 32) | klo;
+}
+
+constexpr int kSelThreads = 1024;
+constexpr int kSelWaves = kSelThreads / kWave;  // 16 >= K
+constexpr int kSelCap = 4096;                   // candidate list capacity
+
+// Top-K (K <= 16) of one frame's masked map by threshold selection, one
+// 1024-thread block per frame, each thread owning E elements (e = tid + i*1024)
+// as 64-bit order keys in registers (cand_key: NaN first, value descending,
+// index ascending; every key of a real element is > 0):
+//   1. t = the K-th largest of the 16 wave maxima.  Those K maxima are distinct
+//      elements >= t, so at least K elements are >= t, and the top-K are among
+//      the elements >= t.
+//   2. the elements >= t are compacted into an LDS list by wave ballots (a map
+//      typically has tens; an all-equal plateau at most 64*(K-1)+1),
+//   3. every listed candidate counts the listed keys above its own: that rank
+//      is its output slot when < K.
+// A list longer than kSelCap (only for adversarial value layouts) falls back
+// to K block-wide extraction rounds of the largest key below the previous
+// winner (no taken bitmap: keys are unique).
+template <int E>
+__global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__restrict__ prob, long long stride,
+                                                                 int X, int Y, int K, float *__restrict__ vals,
+                                                                 int64_t *__restrict__ flat,
+                                                                 int64_t *__restrict__ xy) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float *map = reinterpret_cast<float *>(smem);  // [X*Y]
-    __shared__ Cand wtop[NT / kWave][16];  // each wave's top-K (K <= 16)
     const int M = X * Y;
+    float *map = reinterpret_cast<float *>(smem);                                             // [M]
+    unsigned long long *lkey = reinterpret_cast<unsigned long long *>(smem + (((size_t)M * 4 + 15) & ~(size_t)15));
+    float *lval = reinterpret_cast<float *>(lkey + kSelCap);                                  // [kSelCap]
+    __shared__ unsigned long long wmax[kSelWaves];
+    __shared__ unsigned long long thr;
+    __shared__ int count;
+    __shared__ float wval;
     const int b = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const float *__restrict__ p = prob + (size_t)b * stride;
-    constexpr int U = 8;
-    for (int e0 = tid; e0 < M; e0 += NT * U) {
-        float v[U];
+    {
+        // all E loads in flight before the first LDS store (clamped addresses, no branches)
+        float v[E];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = (e0 + u * NT < M) ? p[e0 + u * NT] : 0.0f;
+        for (int i = 0; i < E; ++i) v[i] = p[min(tid + i * kSelThreads, M - 1)];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (e0 + u * NT < M) map[e0 + u * NT] = v[u];
+        for (int i = 0; i < E; ++i)
+            if (tid + i * kSelThreads < M) map[tid + i * kSelThreads] = v[i];
+    }
+    if (tid == 0) {
+        count = 0;
+        thr = 0;  // stays 0 when fewer than K waves own elements
     }
     __syncthreads();
 
-    Cand top[KMAX];
+    // masked values (max_pool2d 3x3/s1/p1 keep mask, proposal.py:34-52, 66-70) and keys
+    unsigned long long key[E];
+    float val[E];
+    unsigned long long best = 0;
+    {
+        int e = tid, ex = tid / Y, ey = tid - (tid / Y) * Y;
+        const int dX = kSelThreads / Y, dY = kSelThreads - (kSelThreads / Y) * Y;
 #pragma unroll
-    for (int t = 0; t < KMAX; ++t) top[t] = Cand{-INFINITY, 0x7fffffff};
-    int have = 0;
-    for (int e = tid; e < M; e += NT) {
-        const int ex = e / Y, ey = e - (e / Y) * Y;
-        const float c = map[e];
-        float m = -INFINITY;
-        bool nan = false;
+        for (int i = 0; i < E; ++i) {
+            key[i] = 0;
+            val[i] = 0.0f;
+            if (e < M) {
+                const float c = map[e];
+                float m = -INFINITY;
+                bool nan = false;
 #pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
+                for (int dx = -1; dx <= 1; ++dx)
 #pragma unroll
-            for (int dy = -1; dy <= 1; ++dy) {
-                const int xx = ex + dx, yy = ey + dy;
-                const bool ok = (unsigned)xx < (unsigned)X && (unsigned)yy < (unsigned)Y;
-                const float q = map[ok ? xx * Y + yy : e];  // max_pool2d's -inf padding: out-of-map taps ignored
-                nan |= ok && (q != q);
-                m = ok ? fmaxf(m, q) : m;
+                    for (int dy = -1; dy <= 1; ++dy) {
+                        const int xx = ex + dx, yy = ey + dy;
+                        const bool ok = (unsigned)xx < (unsigned)X && (unsigned)yy < (unsigned)Y;
+                        const float q = map[ok ? xx * Y + yy : e];  // -inf padding: outside taps ignored
+                        nan |= ok && (q != q);
+                        m = ok ? fmaxf(m, q) : m;
+                    }
+                // max_pool2d propagates NaN; (c == NaN) is false -> keep = 0 -> 0*c.
+                val[i] = ((!nan && c == m) ? 1.0f : 0.0f) * c;
+                key[i] = cand_key(Cand{val[i], e});
+                best = key[i] > best ? key[i] : best;
+            }
+            e += kSelThreads;
+            ex += dX;
+            ey += dY;
+            if (ey >= Y) {
+                ey -= Y;
+                ++ex;
             }
         }
-        // max_pool2d propagates NaN; (c == NaN) is false -> keep = 0 -> 0*c.
-        Cand cand{((!nan && c == m) ? 1.0f : 0.0f) * c, e};
-        // sorted insertion (descending by `before`), fully unrolled: registers only
-#pragma unroll
-        for (int t = 0; t < KMAX; ++t) {
-            if (t >= have || before(cand, top[t])) {
-                const Cand tmp = top[t];
-                top[t] = cand;
-                cand = tmp;
-            }
-        }
-        have = have < KMAX ? have + 1 : KMAX;
     }
-    // merge, level 1: each wave's top-K by K rounds of wave arg-max over its
-    // lanes' heads (shuffles only, no barriers); the winning lane pops its head
-    const int lane = tid & 63, wave = tid >> 6;
-    const Cand none{-INFINITY, 0x7fffffff};
-    for (int k = 0; k < K; ++k) {
-        const Cand head = have > 0 ? top[0] : none;
-        const Cand best = wave_best(head);
-        if (lane == 0) wtop[wave][k] = best;
-        if (have > 0 && head.i == best.i) {  // indices are unique: exactly one lane pops
+    best = wave_max_key(best);
+    if (lane == 0) wmax[wave] = best;
+    __syncthreads();
+    if (wave == 0 && lane < kSelWaves) {
+        const unsigned long long mine = wmax[lane];
+        int rank = 0;
 #pragma unroll
-            for (int t = 0; t < KMAX - 1; ++t) top[t] = top[t + 1];
-            top[KMAX - 1] = none;
-            --have;
+        for (int w = 0; w < kSelWaves; ++w) rank += wmax[w] > mine;
+        if (rank == K - 1) thr = mine;
+    }
+    __syncthreads();
+    const unsigned long long t = thr > 0 ? thr : 1ull;  // waves without elements hold the 0 sentinel
+
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+        const bool pred = key[i] >= t;
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(pred);
+        if (bal == 0) continue;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&count, (int)__builtin_popcountll(bal));
+        base = __builtin_amdgcn_readfirstlane(base);
+        const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        if (pred && pos < kSelCap) {
+            lkey[pos] = key[i];
+            lval[pos] = val[i];
         }
     }
     __syncthreads();
-    // level 2: wave 0 merges the NT/64 sorted lists the same way
-    if (wave != 0) return;
-    constexpr int PL = ((NT / kWave) * 16 + kWave - 1) / kWave;  // candidates per lane
-    Cand l2[PL];
-#pragma unroll
-    for (int t = 0; t < PL; ++t) l2[t] = none;
-    int h2 = 0;
-    for (int c = lane; c < (NT / kWave) * K; c += kWave) {
-        Cand cand = wtop[c / K][c - (c / K) * K];
-#pragma unroll
-        for (int t = 0; t < PL; ++t) {
-            if (t >= h2 || before(cand, l2[t])) {
-                const Cand tmp = l2[t];
-                l2[t] = cand;
-                cand = tmp;
+    const int C = count;
+    if (C <= kSelCap) {
+        for (int c = tid; c < C; c += kSelThreads) {
+            const unsigned long long k = lkey[c];
+            int rank = 0;
+            for (int j = 0; j < C; ++j) rank += lkey[j] > k;
+            if (rank < K) {
+                const int idx = (int)~(unsigned)k;
+                const size_t o = (size_t)b * K + rank;
+                vals[o] = lval[c];
+                flat[o] = idx;
+                if (xy) {
+                    xy[o * 2 + 0] = (int64_t)(idx / X);
+                    xy[o * 2 + 1] = (int64_t)(idx % X);
+                }
             }
         }
-        h2 = h2 < PL ? h2 + 1 : PL;
+        return;
     }
-    for (int k = 0; k < K; ++k) {
-        const Cand head = h2 > 0 ? l2[0] : none;
-        const Cand w = wave_best(head);
-        if (lane == 0) {
-            vals[(size_t)b * K + k] = w.v;
-            flat[(size_t)b * K + k] = w.i;
+    // fallback: K rounds, each the largest key below the previous winner
+    unsigned long long prev = ~0ull;
+    for (int r = 0; r < K; ++r) {
+        unsigned long long mine = 0;
+        float mv = 0.0f;
+#pragma unroll
+        for (int i = 0; i < E; ++i)
+            if (key[i] < prev && key[i] > mine) {
+                mine = key[i];
+                mv = val[i];
+            }
+        const unsigned long long wm = wave_max_key(mine);
+        if (lane == 0) wmax[wave] = wm;
+        __syncthreads();
+        unsigned long long w = 0;
+#pragma unroll
+        for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
+        if (mine == w && mine != 0) wval = mv;  // exactly one owner (unique keys)
+        __syncthreads();
+        if (tid == 0) {
+            const int idx = (int)~(unsigned)w;
+            const size_t o = (size_t)b * K + r;
+            vals[o] = wval;
+            flat[o] = idx;
             if (xy) {
-                xy[((size_t)b * K + k) * 2 + 0] = (int64_t)(w.i / X);
-                xy[((size_t)b * K + k) * 2 + 1] = (int64_t)(w.i % X);
+                xy[o * 2 + 0] = (int64_t)(idx / X);
+                xy[o * 2 + 1] = (int64_t)(idx % X);
             }
         }
-        if (h2 > 0 && head.i == w.i) {
-#pragma unroll
-            for (int t = 0; t < PL - 1; ++t) l2[t] = l2[t + 1];
-            l2[PL - 1] = none;
-            --h2;
-        }
+        prev = w;
+        __syncthreads();
     }
 }
 
@@ -293,6 +361,45 @@ __global__ __launch_bounds__(256) void gather_bbox_kernel(const float *__restric
     out[gid] = size[(b * 2 + c) * XY + flat[bk]];
 }
 
+// ProposalLayer.forward in test mode (human_detection_net.py:36-37, 99-124)
+// fused with the z pick of HumanDetectionNet.forward (:208-215): per proposal
+// z = argmax over the 1-D heatmap (topk(1): NaN first, then the largest value,
+// lowest index on ties) and conf = conf_2d * hm1d[z] -- or, without a 1-D
+// heatmap, z = index[...,2] and conf = conf_2d -- then centre = index * scale
+// + bias (two fp32 ops, as torch), valid = (conf > min_score) - 1, bbox copied.
+__global__ __launch_bounds__(256) void proposal_centers_kernel(const int64_t *__restrict__ index, int idims,
+                                                               const float *__restrict__ hm1d,
+                                                               const float *__restrict__ confs,
+                                                               const float *__restrict__ bbox, int BK, int Z,
+                                                               float3 scale, float3 bias, float min_score,
+                                                               float *__restrict__ centers) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= BK) return;
+    float conf = confs[t];
+    float zi;
+    if (hm1d) {
+        const float *__restrict__ h = hm1d + (size_t)t * Z;
+        Cand best{h[0], 0};
+        for (int z = 1; z < Z; ++z) {
+            const Cand c{h[z], z};
+            if (before(c, best)) best = c;
+        }
+        conf = conf * best.v;
+        zi = (float)best.i;
+    } else {
+        zi = (float)index[(size_t)t * idims + 2];
+    }
+    const float idx[3] = {(float)index[(size_t)t * idims + 0], (float)index[(size_t)t * idims + 1], zi};
+    const float sc[3] = {scale.x, scale.y, scale.z}, bi[3] = {bias.x, bias.y, bias.z};
+    float *__restrict__ o = centers + (size_t)t * 7;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) o[a] = __fadd_rn(__fmul_rn(idx[a], sc[a]), bi[a]);
+    o[3] = (conf > min_score ? 1.0f : 0.0f) - 1.0f;
+    o[4] = conf;
+    o[5] = bbox[(size_t)t * 2 + 0];
+    o[6] = bbox[(size_t)t * 2 + 1];
+}
+
 }  // namespace fvp
 
 extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
@@ -304,15 +411,16 @@ extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long fr
     if (lds > 150 * 1024) return FVP_ERR_SHAPE;
     if (frame_stride == 0) frame_stride = (long long)M;
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
-    if (K <= 16) {
-        // per-thread list: every element a thread owns when that is <= 8 (then the
-        // list holds them all; 80x80 maps: 7), else the top 16
-        if ((M + 1023) / 1024 <= 8)
-            hipLaunchKernelGGL((fvp::nms_topk_small_kernel<8, 1024>), dim3(B), dim3(1024), M * 4,
-                               (hipStream_t)stream, prob, frame_stride, X, Y, K, vals, flat, xy);
-        else
-            hipLaunchKernelGGL((fvp::nms_topk_small_kernel<16, 1024>), dim3(B), dim3(1024), M * 4,
-                               (hipStream_t)stream, prob, frame_stride, X, Y, K, vals, flat, xy);
+    const int E = (int)((M + fvp::kSelThreads - 1) / fvp::kSelThreads);
+    if (K <= fvp::kSelWaves && E <= 16) {
+        const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)fvp::kSelCap * 12;
+        const dim3 g(B), blk(fvp::kSelThreads);
+        hipStream_t st = (hipStream_t)stream;
+        if (E <= 1) hipLaunchKernelGGL((fvp::nms_select_kernel<1>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
+        else if (E <= 2) hipLaunchKernelGGL((fvp::nms_select_kernel<2>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
+        else if (E <= 4) hipLaunchKernelGGL((fvp::nms_select_kernel<4>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
+        else if (E <= 8) hipLaunchKernelGGL((fvp::nms_select_kernel<8>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
+        else hipLaunchKernelGGL((fvp::nms_select_kernel<16>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob,
@@ -337,5 +445,19 @@ extern "C" int fvp_gather_bbox(const float *size, int B, int X, int Y, const int
     const long long total = (long long)B * K * 2;
     hipLaunchKernelGGL(fvp::gather_bbox_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, size, flat, out, X * Y, K, total);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_proposal_centers(const int64_t *index, int index_dims, const float *hm1d, const float *confs,
+                                    const float *bbox, int B, int K, int Z, const float *scale3, const float *bias3,
+                                    float min_score, float *centers, void *stream) {
+    if (!index || !confs || !bbox || !scale3 || !bias3 || !centers) return FVP_ERR_NULL;
+    if (B < 0 || K < 0 || (hm1d ? (index_dims != 2 || Z <= 0) : index_dims != 3)) return FVP_ERR_SHAPE;
+    const int BK = B * K;
+    if (BK == 0) return FVP_OK;
+    hipLaunchKernelGGL(fvp::proposal_centers_kernel, dim3((unsigned)((BK + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, index, index_dims, hm1d, confs, bbox, BK, Z,
+                       make_float3(scale3[0], scale3[1], scale3[2]), make_float3(bias3[0], bias3[1], bias3[2]),
+                       min_score, centers);
     return (int)hipGetLastError();
 }

@@ -29,8 +29,9 @@
 // computes their bilinear offsets/weights once, and the group picks them up
 // per camera through lane broadcasts -- one grid load and one tap setup per
 // 2*LPV voxel-cameras instead of per voxel-camera and lane.  Arithmetic per
-// tap and the camera/sum order are the reference's (fvp_device.h), so the
-// result is bit-exact.
+// tap and the camera sum order are the reference's (fvp_device.h: torch's
+// CPU mean over the views folds complete blocks of 16 cameras, CASC = V > 16),
+// so the result is bit-exact.
 #include "fvp_layout.h"
 
 namespace fvp {
@@ -48,7 +49,7 @@ struct CoordSource {
     fvp_image_spec im;
 };
 
-template <int LPV, bool PAIR, bool OTF>
+template <int LPV, bool PAIR, bool OTF, bool CASC>
 __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
@@ -107,6 +108,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         const bool valid = i < T;
         const int ii = min(i, T - 1);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        float blk[4] = {0.f, 0.f, 0.f, 0.f};  // CASC: completed 16-camera blocks (view_sum order)
         float wx_ = 0.f, wy_ = 0.f, wz_ = 0.f;  // OTF: voxel centre (compute_grid, project_whole.py:43-79)
         if constexpr (OTF) {
             const long long n = n0 + ii;
@@ -144,6 +146,15 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 constexpr int S = k >> 1;  // lane of the group that set this camera up
                 const int v = v0 + k;
                 if (v >= V) return;
+                if constexpr (CASC) {
+                    if ((v & 15) == 0 && v > 0) {  // a block of 16 cameras is complete: fold it (fvp_device.h)
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            blk[m] = blk[m] + acc[m];
+                            acc[m] = 0.0f;
+                        }
+                    }
+                }
                 const Taps4<PAIR> &src = (k & 1) ? t1 : t0;
                 unsigned o[Taps4<PAIR>::NO];
                 unsigned all = kOOB;
@@ -190,6 +201,9 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 }
             });
         }
+        // the sum's final levels (fvp_device.h): remainder + blocks, or + 0 (a -0 sum becomes +0)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[m] = acc[m] + (CASC ? blk[m] : 0.0f);
         if (valid) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf(acc[m] / fV, 0.0f, 1.0f);
@@ -218,25 +232,25 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
 // (C2 -4 %, C4 -8 % gather time, measured).
 // Cached-grid gather: <= 64 VGPRs so 8 waves/SIMD fit (32 waves/CU with the
 // 20 KB stage); the on-the-fly variant keeps its registers (no spills).
-template <int LPV, bool PAIR, bool OTF>
+template <int LPV, bool PAIR, bool OTF, bool CASC>
 __global__ __launch_bounds__(256, 8) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int H, int W, int X, int Y, int Z, int cols,
                                                           int col_blocks, int SP, int band) {
     static_assert(!OTF, "grid kernel");
-    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
+    voxelize_body<LPV, PAIR, OTF, CASC>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
                                   band);
 }
 
-template <int LPV, bool PAIR, bool OTF>
+template <int LPV, bool PAIR, bool OTF, bool CASC>
 __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restrict__ tab, CoordSource src,
                                                             const int32_t *__restrict__ grid_index, int frame0,
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
                                                             int J, int H, int W, int X, int Y, int Z, int cols,
                                                             int col_blocks, int SP, int band) {
     static_assert(OTF, "on-the-fly kernel");
-    voxelize_body<LPV, PAIR, OTF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
+    voxelize_body<LPV, PAIR, OTF, CASC>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
                                   band);
 }
 
@@ -280,7 +294,7 @@ static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     return (int)c;
 }
 
-template <int LPV, bool PAIR, bool OTF, typename T>
+template <int LPV, bool PAIR, bool OTF, bool CASC, typename T>
 static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
                       const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
     const bool half = sizeof(T) == 2;
@@ -320,13 +334,28 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
             launch_layout<LPV, T>(hsrc, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
         }
         if constexpr (OTF)
-            hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true>), dim3((unsigned)(nb * col_blocks)), dim3(256),
+            hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC>), dim3((unsigned)(nb * col_blocks)), dim3(256),
                                lds, s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
         else
-            hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds,
+            hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds,
                                s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
     }
     return (int)hipGetLastError();
+}
+
+template <bool OTF, bool CASC, typename T>
+static int voxelize_lpv(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
+                        const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws,
+                        hipStream_t s) {
+    const bool half = sizeof(T) == 2;
+    if (use_pairs(J, half))
+        return run_chunks<4, true, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+    switch (lanes_per_voxel(J)) {
+        case 1: return run_chunks<1, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 2: return run_chunks<2, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 4: return run_chunks<4, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        default: return run_chunks<8, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+    }
 }
 
 template <bool OTF, typename T>
@@ -337,19 +366,14 @@ static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const Co
     const size_t need = (size_t)chunk_frames(B, V, J, H, W, half) * frame_bytes(V, J, H, W, half);
     if (!ws || ws_bytes < need) return FVP_ERR_WORKSPACE;
     if (frame_bytes(1, J, H, W, half) > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets
-    if (use_pairs(J, half))
-        return run_chunks<4, true, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-    switch (lanes_per_voxel(J)) {
-        case 1: return run_chunks<1, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 2: return run_chunks<2, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 4: return run_chunks<4, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        default: return run_chunks<8, false, OTF, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-    }
+    if (V > 16) return voxelize_lpv<OTF, true, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+    return voxelize_lpv<OTF, false, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
 }
 
 static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, const float *grids, int X, int Y, int Z) {
     if (!heatmaps || !grids) return FVP_ERR_NULL;
-    if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2 || X <= 0 || Y <= 0 || Z <= 0)
+    if (B <= 0 || V <= 0 || V > FVP_MAX_VIEWS || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2 || X <= 0 ||
+        Y <= 0 || Z <= 0)
         return FVP_ERR_SHAPE;
     // packed grid of one sequence addressed with 32-bit byte offsets
     if ((long long)X * Y * Z * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL) return FVP_ERR_SHAPE;

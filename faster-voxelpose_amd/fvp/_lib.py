@@ -51,6 +51,8 @@ SIGNATURES = {
     "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
+    "fvp_proposal_centers": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                             c_float, c_void_p, c_void_p],
     "fvp_person_workspace_bytes": [c_int, c_int, c_int, c_int, c_int],
     "fvp_conv2d_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "fvp_person_planes": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, ctypes.POINTER(PersonSpec), c_void_p,

@@ -9,6 +9,7 @@ implementations, in the modules that import them, BEFORE the model is built
     models.project_individual.ProjectLayer   -> fvp.project_individual.ProjectLayer
     models.joint_localization_net.ProjectLayer -> fvp.project_individual.ProjectLayer  (:12)
     core.proposal.nms2D / human_detection_net.nms2D -> fvp.proposal.nms2D  (:12)
+    models.human_detection_net.ProposalLayer -> fvp.proposal.ProposalLayer  (:14-125)
 
 With ``fused=True`` it also replaces JointLocalizationNet.forward by
 :func:`fvp.jln.fused_jln_forward` (every proposal of a batch at once, soft-argmax
@@ -16,7 +17,8 @@ and fusion on fvp kernels; eval mode) and HumanDetectionNet.forward
 (human_detection_net.py:157-220) by :func:`fused_hdn_forward`, which takes the
 cube AND its xy max-plane from one voxelize launch (skipping CenterNet's
 ``torch.max(x, dim=4)``, cnns_2d.py:291) and uses the fvp gathers for the
-bbox and z-column extraction (:191-192, :199-200).  Signatures, outputs and
+bbox and z-column extraction (:191-192, :199-200) and one launch for the z
+pick and the test-mode ProposalLayer (:208-220).  Signatures, outputs and
 state_dict keys are unchanged, so run/validate.py and existing checkpoints
 work as before.
 """
@@ -59,6 +61,7 @@ def install(fused: bool = True, modules=None, cnn: bool = False) -> dict:
     setattr_if("models.joint_localization_net", "ProjectLayer", project_individual.ProjectLayer)
     setattr_if("core.proposal", "nms2D", proposal.nms2D)
     setattr_if("models.human_detection_net", "nms2D", proposal.nms2D)
+    setattr_if("models.human_detection_net", "ProposalLayer", proposal.ProposalLayer)
     if fused:
         hdn = mods.get("models.human_detection_net")
         if hdn is not None and hasattr(hdn, "HumanDetectionNet"):
@@ -100,8 +103,11 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     if USE_FVP_CNN and not c2c.training:
         c2c = fvp_cnn.cached(c2c, FVP_CNN_DTYPE)
     hm1d = c2c(torch.flatten(columns, 0, 1)).view(batch_size, self.max_people, -1)
-    confs_1d, index_1d = hm1d.detach().topk(1)
-    topk_index = torch.cat([index_2d, index_1d], dim=2)
-    topk_confs = confs_2d * confs_1d.squeeze(2)
-    centers = self.proposal_layer(topk_index, topk_confs, match_bbox, meta)
+    pl = self.proposal_layer
+    if pl.training and ("roots_3d" in meta and "num_person" in meta):  # GT matching (training)
+        confs_1d, index_1d = hm1d.detach().topk(1)
+        topk_index = torch.cat([index_2d, index_1d], dim=2)
+        centers = pl(topk_index, confs_2d * confs_1d.squeeze(2), match_bbox, meta)
+    else:  # z pick + ProposalLayer test mode in one launch (human_detection_net.py:208-220, :99-124)
+        centers = proposal.proposal_centers(pl, index_2d, hm1d.detach(), confs_2d, match_bbox)
     return hm2d, hm1d, centers, torch.flatten(bbox_preds, 2, 3).permute(0, 2, 1)

@@ -256,6 +256,33 @@ def _(size, flat):
     return size.new_empty((size.shape[0], flat.shape[1], 2))
 
 
+@torch.library.custom_op("fvp::proposal_centers", mutates_args=(), device_types="cuda")
+def proposal_centers(index: torch.Tensor, hm1d: Optional[torch.Tensor], confs: torch.Tensor, match_bbox: torch.Tensor,
+                     scale: list[float], bias: list[float], min_score: float) -> torch.Tensor:
+    """Test-mode ProposalLayer.forward (fvp_proposal_centers): with hm1d [B,K,Z] the z pick
+    is fused (index int64 [B,K,2]); without it index is the full [B,K,3] -> centers [B,K,7]."""
+    c = _dev_f32(confs, "topk_confs")
+    B, K = c.shape[0], c.shape[1]
+    ix = index.to(device=c.device, dtype=torch.int64).contiguous()
+    h = None if hm1d is None else _dev_f32(hm1d, "proposal_heatmaps_1d")
+    dims = 2 if h is not None else 3
+    bb = _dev_f32(match_bbox, "match_bbox_preds")
+    if tuple(ix.shape) != (B, K, dims) or bb.numel() != B * K * 2 or (h is not None and h.shape[:2] != (B, K)):
+        raise _lib.FvpError(f"fvp: proposal_centers expects index [B,K,{dims}], confs [B,K], bbox [B,K,2]")
+    out = torch.empty((B, K, 7), dtype=torch.float32, device=c.device)
+    if out.numel() == 0:
+        return out
+    f3 = ctypes.c_float * 3
+    _lib.call("fvp_proposal_centers", _ptr(ix), dims, _ptr(h), _ptr(c), _ptr(bb), B, K,
+              h.shape[2] if h is not None else 0, f3(*scale), f3(*bias), float(min_score), _ptr(out), _stream(c))
+    return out
+
+
+@proposal_centers.register_fake
+def _(index, hm1d, confs, match_bbox, scale, bias, min_score):
+    return confs.new_empty((confs.shape[0], confs.shape[1], 7))
+
+
 # ---------------------------------------------------------------------------
 @torch.library.custom_op("fvp::person_planes", mutates_args=(), device_types="cuda")
 def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: torch.Tensor,

@@ -33,6 +33,10 @@ extern "C" {
 
 #define FVP_ABI_VERSION 7
 #define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
+/* Cameras per frame: torch's CPU mean over the views (the sum order every
+ * kernel reproduces) folds blocks of 16 into a second accumulator, and past
+ * 255 views into a third; up to 255 views are supported. */
+#define FVP_MAX_VIEWS 255
 #define FVP_CAM_STRIDE 24 /* R[9] T[3] fx fy cx cy k[3] p[2] pad[3] */
 /* Camera slots per voxel in a packed grid (V rounded up to even). */
 #define FVP_GRID_SLOTS(V) ((V) + ((V) & 1))
@@ -139,6 +143,21 @@ int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H
  *   vals [B][K] fp32, flat [B][K] int64, xy [B][K][2] int64 (xy may be NULL) */
 int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K,
                  float *vals, int64_t *flat, int64_t *xy, void *stream);
+
+/* ProposalLayer.forward in test mode (lib/models/human_detection_net.py:
+ * 36-37, 99-124), optionally fused with the z pick of HumanDetectionNet.forward
+ * (:208-215).  With hm1d (index_dims == 2):
+ *   z    = argmax_z hm1d[b,k,:] (torch.topk(1): NaN first, lowest index on ties)
+ *   conf = confs[b,k] * hm1d[b,k,z]
+ * without (hm1d NULL, index_dims == 3): z = index[b,k,2], conf = confs[b,k]; then
+ *   centers[b,k] = [ix*sx+bx, iy*sy+by, z*sz+bz, (conf > min_score) - 1, conf, bbox[b,k,0:2]]
+ *   index  device int64 [B][K][index_dims] (nms2D topk_index, or the full 3-D index)
+ *   hm1d   device [B][K][Z] or NULL;  confs device [B][K];  bbox device [B][K][2]
+ *   scale3 / bias3 HOST float[3] = SPACE_SIZE/(VOXELS-1) and SPACE_CENTER-SPACE_SIZE/2 (fp32)
+ *   centers device [B][K][7]. */
+int fvp_proposal_centers(const int64_t *index, int index_dims, const float *hm1d, const float *confs,
+                         const float *bbox, int B, int K, int Z, const float *scale3, const float *bias3,
+                         float min_score, float *centers, void *stream);
 
 /* z-columns of the top-K proposals: columns[b,k,j,:] = cube[b,j,flat[b,k],:]
  * Replaces the torch.gather at lib/models/human_detection_net.py:199-200. */

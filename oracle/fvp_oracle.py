@@ -148,13 +148,41 @@ def grid_sample(inp: np.ndarray, g: np.ndarray) -> np.ndarray:
     return out
 
 
+def view_sum(samples) -> np.ndarray:
+    """torch.sum / torch.mean over dim 0 of the [V,J,1,N] grid_sample output
+    (project_whole.py:162, project_individual.py:283) on the CPU: ATen's
+    cascade (SumKernel.cpp multi_row_sum, 4 levels, level step 16) -- views
+    accumulate sequentially into level 0 (from zeros); every complete block of
+    16 is added into level 1 and level 0 restarts (every 16 level-1 blocks go
+    to level 2); the total is ((level0 + level1) + level2) + level3, so a -0
+    total comes out +0.  Verified against torch.sum here for V = 1..300
+    (tests/test_oracle_golden.py pins it through the C5 golden).  `samples`
+    yields the V per-view arrays in view order."""
+    acc = None
+    i = 0
+    for x in samples:
+        if acc is None:
+            acc = [np.zeros(x.shape, F32) for _ in range(4)]
+        acc[0] = (acc[0] + x).astype(F32)
+        i += 1
+        if i % 16 == 0:
+            for lv in (1, 2, 3):
+                acc[lv] = (acc[lv] + acc[lv - 1]).astype(F32)
+                acc[lv - 1] = np.zeros_like(acc[0])
+                if i & (15 << (4 * lv)):
+                    break
+    total = acc[0]
+    for lv in (1, 2, 3):
+        total = (total + acc[lv]).astype(F32)
+    return total
+
+
 def voxelize(heatmaps: np.ndarray, sample_grid: np.ndarray) -> np.ndarray:
     """project_whole.py:119-168 for one frame: [V,J,H,W] x [V,N,2] -> cube [J,N],
-    mean over all V (off-image samples count in the divisor) then clamp(0,1)."""
+    mean over all V (off-image samples count in the divisor; view_sum order)
+    then clamp(0,1)."""
     V = heatmaps.shape[0]
-    acc = np.zeros((heatmaps.shape[1], sample_grid.shape[1]), F32)
-    for v in range(V):
-        acc = (acc + grid_sample(heatmaps[v], sample_grid[v])).astype(F32)
+    acc = view_sum(grid_sample(heatmaps[v], sample_grid[v]) for v in range(V))
     return np.clip((acc / F32(V)).astype(F32), F32(0), F32(1))
 
 
@@ -267,9 +295,7 @@ class Individual:
             if np.any(s >= e):
                 continue
             win = fine_sample_grid[:, s[0]:e[0], s[1]:e[1], s[2]:e[2]].reshape(V, -1, 2)
-            acc = np.zeros((J, win.shape[1]), F32)
-            for v in range(V):
-                acc = (acc + grid_sample(heatmaps[v], win[v])).astype(F32)
+            acc = view_sum(grid_sample(heatmaps[v], win[v]) for v in range(V))
             acc = (acc / F32(V)).reshape(J, *(e - s))
             o0, o1 = s - ctl[i], e - ctl[i]
             cubes[i, :, o0[0]:o1[0], o0[1]:o1[1], o0[2]:o1[2]] = acc

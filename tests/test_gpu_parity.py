@@ -544,6 +544,38 @@ def test_nms_topk_both_paths_vs_oracle(gpu_device, K):
     assert np.array_equal(xy.cpu().numpy()[1:], oxy[1:])
 
 
+@pytest.mark.parametrize("kind", ["zeros", "nan", "negative", "tiny", "big_noise", "big_smooth", "row", "ragged"])
+def test_nms_select_degenerate_maps_vs_oracle(gpu_device, kind):
+    """The threshold-select top-K on plateaus (all-zero, all-NaN, all-negative
+    maps: ties broken by index), maps smaller than K waves, 128x128 maps
+    (16 elements per thread) and ragged shapes, against the oracle bit for bit."""
+    from fvp.proposal import nms2D
+
+    g = torch.Generator().manual_seed(11)
+    shape, K = {"zeros": ((3, 1, 80, 80), 10), "nan": ((2, 1, 80, 80), 10), "negative": ((2, 1, 40, 40), 16),
+                "tiny": ((4, 1, 4, 4), 16), "big_noise": ((3, 1, 128, 128), 10),
+                "big_smooth": ((3, 1, 128, 128), 16), "row": ((2, 1, 1, 300), 5),
+                "ragged": ((5, 1, 37, 53), 7)}[kind]
+    if kind == "zeros":
+        prob = torch.zeros(shape)
+    elif kind == "nan":
+        prob = torch.full(shape, float("nan"))
+    elif kind == "negative":
+        prob = -torch.rand(shape, generator=g)
+    elif kind == "big_smooth":
+        B, _, X, Y = shape
+        prob = torch.nn.functional.avg_pool2d(torch.rand((B, 1, X + 8, Y + 8), generator=g), 9, 1)
+    else:
+        prob = torch.rand(shape, generator=g)
+    v, xy, fl = nms2D(prob.to(gpu_device), K)
+    ov, oxy, ofl = O.nms2d(prob.numpy(), K)
+    got = v.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ov.view(np.uint32)) or (
+        np.array_equal(np.isnan(got), np.isnan(ov)) and np.array_equal(np.nan_to_num(got), np.nan_to_num(ov)))
+    assert np.array_equal(fl.cpu().numpy(), ofl)
+    assert np.array_equal(xy.cpu().numpy(), oxy)
+
+
 def test_nms_expanded_map_batch_stride_zero(gpu_device):
     """A batch-expanded map (batch stride 0) gives every frame the one map's top-K."""
     from fvp.proposal import nms2D

@@ -133,3 +133,62 @@ def test_individual_constants_host_mirror():
     assert np.array_equal(c["fine"], d["fine"])
     assert np.array_equal(c["scale"], d["scale"])
     assert np.array_equal(c["bias"], d["bias"])
+
+
+def _c5_heatmaps(d):
+    """C5 heatmaps are regenerated (28.6 MB fp16), pinned by the digest the generator stored."""
+    import hashlib
+
+    from fvp import synthetic
+
+    w = WORKLOADS["c5"]
+    hm = synthetic.gaussian_heatmaps(w, 1).astype(np.float16).astype(np.float32)
+    assert hashlib.sha256(np.ascontiguousarray(hm).tobytes()).digest() == d["heatmaps_sha256"].tobytes(), \
+        "fvp.synthetic no longer reproduces the C5 heatmaps the reference was run on"
+    return hm
+
+
+def test_c4_full_size_bit_exact():
+    """BASELINE configs[3] (128x128x32, demo cameras) at full size: sample grid,
+    every voxel of the sampled set, the full xy plane, NMS and columns, and the
+    uniform-random stress frame."""
+    from fvp import synthetic
+
+    d = golden("whole_c4.npz")
+    w = WORKLOADS["c4"]
+    grid, sg = _sample_grid(w, d["resize_f32"])
+    assert np.array_equal(grid[d["sub"]], d["grid_ref"])
+    assert np.array_equal(sg[:, d["sub"]], d["sample_grid_sub"])
+    J, (X, Y, Z) = w.num_joints, w.voxels_per_axis
+    cube = O.voxelize(d["heatmaps"][0], sg)
+    assert np.array_equal(cube[:, d["sub"]], d["cube_sub"][0])
+    c4 = cube.reshape(J, X, Y, Z)
+    assert np.array_equal(O.xy_plane(c4), d["xy"][0])
+    assert np.array_equal(c4.max(axis=(1, 2, 3)), d["cube_max"][0])
+    v, xy, fl = O.nms2d(d["xy"][:, 2:3], w.max_people)
+    _check_topk(v, fl, xy, d["nms_vals"], d["nms_flat"], d["nms_xy"])
+    assert np.array_equal(O.gather_columns(c4[None], d["nms_flat"]), d["columns"])
+    hu = synthetic.uniform_heatmaps(w, 1, seed=0).numpy()
+    assert np.array_equal(O.voxelize(hu[0], sg[:, d["sub"]]), d["u_cube_sub"][0])
+
+
+def test_c5_ring_cameras_bit_exact_on_sampled_voxels():
+    """BASELINE configs[4] (31 ring cameras, some voxels behind a camera,
+    160x160x64, fp16-rounded heatmaps): the sample grid and the cube on the
+    sampled voxels (the oracle's full 1.6 M-voxel cube is left to the GPU test)."""
+    d = golden("whole_c5.npz")
+    w = WORKLOADS["c5"]
+    cams, seq = w.cameras()
+    grid = O.compute_grid(w.space_size, w.space_center, w.voxels_per_axis)
+    assert np.array_equal(grid[d["sub"]], d["grid_ref"])
+    sg = np.stack([O.project_grid(grid[d["sub"]], c, w.ori_image_size, w.image_size, w.heatmap_size, d["resize_f32"])
+                   for c in geometry.camera_list(cams, seq)])
+    assert np.array_equal(sg, d["sample_grid_sub"])
+    hm = _c5_heatmaps(d)
+    assert np.array_equal(O.voxelize(hm[0], sg), d["cube_sub"][0])
+    # voxels behind a camera are part of the fixture (no masking in project_point)
+    behind = 0
+    for c in geometry.camera_list(cams, seq):
+        R, T = np.asarray(c["R"], np.float64), np.asarray(c["T"], np.float64).reshape(3, 1)
+        behind += int(((R @ (grid[d["sub"]].T.astype(np.float64) - T))[2] < 0).sum())
+    assert behind > 0

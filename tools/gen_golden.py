@@ -12,10 +12,11 @@ attribute-dict cfg, so lib/core/config.py (easydict) is not imported.
 Outputs: tests/golden/*.npz (inputs that cannot be regenerated bit-exactly
 elsewhere are stored; uniform-random inputs are regenerated from torch seeds).
 
-    python3 -B tools/gen_golden.py
+    python3 -B tools/gen_golden.py [--only whole,c4,c5,e2e]
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import sys
 import types
@@ -29,6 +30,7 @@ OUT = os.path.join(REPO, "tests", "golden")
 sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
 
 STRIDE_SUB = 31  # sampled-voxel stride for large outputs
+E2E_HM_BIAS = 40.0  # e2e_c3: added to CenterNet's output_hm[2].bias after seeding
 
 
 def import_reference():
@@ -42,7 +44,52 @@ def import_reference():
     return pw, pi, prop, ucam
 
 
+def e2e_case(torch, geometry, synthetic, WORKLOADS, make_cfg):
+    """The reference's own HumanDetectionNet and JointLocalizationNet forwards
+    (human_detection_net.py:157-220, joint_localization_net.py:122-182) in
+    eval mode on C3 inputs (the two frames of whole_c3.npz), with seeded
+    weights for CenterNet, C2CNet, P2PNet and WeightNet (the seeds of cnn.npz).
+    The JLN runs on the HDN's proposals with a fixed mask (the first 4 of each
+    frame)."""
+    import models.human_detection_net as hdn_mod  # noqa: E402
+    import models.joint_localization_net as jln_mod  # noqa: E402
+
+    w = WORKLOADS["c3"]
+    cfg = make_cfg(w, device="cpu")
+    cfg.NETWORK.NUM_CHANNEL_JOINT_FEAT = 32
+    cfg.NETWORK.NUM_CHANNEL_JOINT_HIDDEN = 64
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+    hm = torch.from_numpy(np.load(os.path.join(OUT, "whole_c3.npz"))["heatmaps"])
+    B = hm.shape[0]
+    meta = {"seq": [seq] * B}
+    hdn = hdn_mod.HumanDetectionNet(cfg).eval()
+    hdn.center_net.load_state_dict(synthetic.seeded_state_dict(hdn.center_net, 12))
+    hdn.c2c_net.load_state_dict(synthetic.seeded_state_dict(hdn.c2c_net, 14))
+    # seeded CenterNet maps come out all negative (every NMS value a -0.0 tie):
+    # shift the heatmap head's bias so the map's peaks are positive local maxima
+    with torch.no_grad():
+        hdn.center_net.output_hm[2].bias += E2E_HM_BIAS
+    jln = jln_mod.JointLocalizationNet(cfg).eval()
+    jln.conv_net.load_state_dict(synthetic.seeded_state_dict(jln.conv_net, 11))
+    jln.weight_net.load_state_dict(synthetic.seeded_state_dict(jln.weight_net, 15))
+    with torch.no_grad():
+        hm2d, hm1d, centers, bbox = hdn(hm, meta, cams, rt)
+        centers_in = centers.clone()
+        mask = torch.zeros(centers.shape[:2], dtype=torch.bool)
+        mask[:, :4] = True
+        fused, poses = jln(meta, hm, centers, mask, cams, rt)
+    d = {"hm_bias_shift": np.float32(E2E_HM_BIAS), "hm2d": hm2d.numpy(), "hm1d": hm1d.numpy(), "centers": centers_in.numpy(), "bbox": bbox.numpy(),
+         "mask": mask.numpy(), "fused": fused.numpy(), "poses": poses.numpy(), "centers_after": centers.numpy(),
+         "min_score": np.float32(w.min_score)}
+    np.savez_compressed(os.path.join(OUT, "e2e_c3.npz"), **d)
+    print("wrote e2e_c3", {k: np.shape(v) for k, v in d.items()})
+
+
 def main():
+    only = None
+    if len(sys.argv) > 2 and sys.argv[1] == "--only":
+        only = set(sys.argv[2].split(","))
     if not os.path.isdir(REF):
         print("gen_golden: /root/reference absent; nothing to do")
         return 0
@@ -54,7 +101,7 @@ def main():
     pw, pi, prop, ucam = import_reference()
     torch.set_num_threads(8)
 
-    def whole_case(name, wname, batch, uniform_batch=0, full=False):
+    def whole_case(name, wname, batch, uniform_batch=0, full=False, stride=STRIDE_SUB, store_heatmaps=True):
         w = WORKLOADS[wname]
         cfg = make_cfg(w, device="cpu")
         cams, seq = w.cameras()
@@ -62,20 +109,29 @@ def main():
         rt = torch.as_tensor(trans, dtype=torch.float)
         layer = pw.ProjectLayer(cfg)
         hm = synthetic.gaussian_heatmaps(w, batch)
+        if w.dtype == "float16":  # fp16 heatmaps: the reference computes on their fp32 values
+            hm = hm.astype(np.float16).astype(np.float32)
         cube = layer(torch.from_numpy(hm), {"seq": [seq] * batch}, cams, rt)
         X, Y, Z = w.voxels_per_axis
         N = X * Y * Z
         sg = layer.sample_grid[seq][:, 0].numpy()  # [V,N,2]
-        sub = np.arange(0, N, STRIDE_SUB)
+        sub = np.arange(0, N, stride)
         d = {
             "trans": trans, "resize_f32": rt.numpy(),
             "grid_ref": layer.grid.numpy()[sub], "sub": sub,
             "sample_grid_sub": sg[:, sub], "sample_grid_sum": sg.astype(np.float64).sum(axis=(1, 2)),
-            "heatmaps": hm,
+        }
+        if store_heatmaps:
+            d["heatmaps"] = hm
+        else:  # regenerated by fvp.synthetic on the test side; the digest pins them
+            d["heatmaps_sha256"] = np.frombuffer(hashlib.sha256(np.ascontiguousarray(hm).tobytes()).digest(),
+                                                 np.uint8)
+        d.update({
             "cube_sub": cube.numpy().reshape(batch, w.num_joints, N)[:, :, sub],
             "cube_sum": cube.numpy().astype(np.float64).sum(axis=(2, 3, 4)),
+            "cube_max": cube.numpy().max(axis=(2, 3, 4)),
             "xy": torch.max(cube, dim=4)[0].numpy(),
-        }
+        })
         if full:
             d["cube"] = cube.numpy()
             d["sample_grid"] = sg
@@ -99,10 +155,19 @@ def main():
         np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **d)
         print("wrote", name, {k: v.shape for k, v in d.items()})
 
-    whole_case("whole_c1", "c1", batch=2, uniform_batch=1, full=True)
-    whole_case("whole_c2", "c2", batch=1, uniform_batch=1)
-    whole_case("whole_c3", "c3", batch=2)
-    whole_case("whole_shelf_native", "shelf_native", batch=1)
+    if only is None or "whole" in only:
+        whole_case("whole_c1", "c1", batch=2, uniform_batch=1, full=True)
+        whole_case("whole_c2", "c2", batch=1, uniform_batch=1)
+        whole_case("whole_c3", "c3", batch=2)
+        whole_case("whole_shelf_native", "shelf_native", batch=1)
+    if only is None or "c4" in only:  # BASELINE configs[3] at full size
+        whole_case("whole_c4", "c4", batch=1, uniform_batch=1, stride=97)
+    if only is None or "c5" in only:  # configs[4]: 31 ring cameras, fp16-rounded heatmaps, 160x160x64
+        whole_case("whole_c5", "c5", batch=1, stride=997, store_heatmaps=False)
+    if only is None or "e2e" in only:
+        e2e_case(torch, geometry, synthetic, WORKLOADS, make_cfg)
+    if only is not None:
+        return 0
 
     # ---- NMS / top-K on tie-free random maps, incl. the non-square divisor quirk
     g = torch.Generator().manual_seed(7)

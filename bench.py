@@ -45,6 +45,8 @@ def parse():
                     help="collect FETCH_SIZE/WRITE_SIZE with rocprofv3 child runs (N=1, rank 0)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (default: OMP_NUM_THREADS = the pool's per-GPU CPU share)")
     ap.add_argument("--graph", choices=["on", "off"], default="off",
                     help="replay the GPU-local part of the step from captured hipGraphs (the collective stays eager)")
     ap.add_argument("--slabs", action="store_true",
@@ -104,13 +106,35 @@ def collect_traffic(args):
     return {"fetch_raw": fetch, "write": write, "corrected": 2.0 * fetch + write}, None
 
 
-def cpu_baseline(w, sample_grid_cpu, seconds):
+def host_cores():
+    """(physical cores of the host per lscpu, logical CPUs this process may run on)."""
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        phys = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")}) or None
+    except Exception:
+        pass
+    return phys, len(os.sched_getaffinity(0))
+
+
+def cpu_baseline_threads(requested):
+    """Threads for the CPU baseline: --cpu-threads, else the pool's per-GPU CPU
+    share (OMP_NUM_THREADS, 16 on the MI355X pool, which forbids more), else
+    every CPU this process may run on."""
+    if requested:
+        return requested
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return host_cores()[1]
+
+
+def cpu_baseline_run(w, sample_grid_cpu, seconds, threads):
     """Reference op sequence on the host cores (oracle/torch_cpu.py), bounded."""
     import torch
     from fvp import synthetic
     from oracle import torch_cpu
 
-    threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     frames = 4
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, frames, first_frame=10_000))
@@ -122,14 +146,33 @@ def cpu_baseline(w, sample_grid_cpu, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    return done, el
+
+
+def cpu_baseline(w, sample_grid_cpu, seconds, threads):
+    phys, avail = host_cores()
+    done, el = cpu_baseline_run(w, sample_grid_cpu, seconds, threads)
+    d8, e8 = cpu_baseline_run(w, sample_grid_cpu, seconds / 2, 8)
     return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{done} frames of {w.name} in {el:.1f} s: torch-CPU restatement of project_whole.forward "
-                      f"(per-frame F.grid_sample, mean, clamp) + max(dim=4) + nms2D + column gather "
-                      f"(oracle/torch_cpu.py), sample grid prebuilt"}
+            "host_physical_cores": phys, "host_logical_cpus_available": avail,
+            "value_8_threads": d8 / e8,
+            "sample": f"{done} frames of {w.name} in {el:.1f} s on {threads} threads ({d8} frames in {e8:.1f} s on "
+                      f"8 threads): torch-CPU restatement of project_whole.forward (per-frame F.grid_sample, mean, "
+                      f"clamp) + max(dim=4) + nms2D + column gather (oracle/torch_cpu.py), sample grid prebuilt"}
+
+
+def note(msg):
+    """Progress on stderr (long runs must keep writing; stdout holds only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 # ---------------------------------------------------------------------------
 def main():
+    # stdout carries only the JSON line: native libraries (RCCL prints a version
+    # banner when a communicator comes up) write to fd 1 directly, so fd 1 points
+    # at stderr until the result is printed
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -137,6 +180,7 @@ def main():
 
     traffic, traffic_note = None, None
     if args.traffic == "auto" and world == 1 and not args.child:
+        note("traffic counters (two rocprofv3 child runs)")
         traffic, traffic_note = collect_traffic(args)  # before any GPU use in this process
 
     import numpy as np
@@ -151,10 +195,20 @@ def main():
     local_rank %= max(1, torch.cuda.device_count())  # identity with one rank per GPU
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
-        # FVP_BENCH_BACKEND=gloo: plumbing rehearsal of N ranks (not a measurement)
-        backend = os.environ.get("FVP_BENCH_BACKEND", "nccl")
-        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    # FVP_BENCH_BACKEND=gloo: plumbing rehearsal of N ranks (not a measurement).
+    # One process group at every N (a one-rank RCCL group when launched without
+    # torchrun), so the timed step runs the same all-gather code at N = 1.
+    backend = os.environ.get("FVP_BENCH_BACKEND", "nccl")
+    pg_kw = {"device_id": dev} if backend == "nccl" else {}
+    if world > 1 or "MASTER_ADDR" in os.environ:
+        dist.init_process_group(backend, **pg_kw)
+    elif not args.child:
+        fd, store_path = tempfile.mkstemp(prefix="fvp_bench_pg_")
+        os.close(fd)
+        # (the FileStore removes its file when the group is destroyed; unlinking it
+        # earlier makes the store's cleanup at exit wait forever)
+        dist.init_process_group(backend, store=dist.FileStore(store_path, 1), rank=0, world_size=1, **pg_kw)
+    grouped = dist.is_initialized()
 
     w = WORKLOADS[args.workload]
     B = args.batch or DEFAULT_BATCH.get(args.workload, 64)
@@ -182,12 +236,25 @@ def main():
     del hm_host
     meta = {"seq": [seq] * B}
 
-    # once-per-sequence cache build, timed separately (excluded from the step)
+    # once-per-sequence cache build, timed separately (excluded from the step):
+    # the first call also pays the library / code-object load; a second
+    # sequence (same cameras, new key) times the grid build alone
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     layer.prepare(hm, meta, cams, rt)
     torch.cuda.synchronize()
-    cache_ms = (time.perf_counter() - t0) * 1e3
+    first_ms = (time.perf_counter() - t0) * 1e3
+    seq_b = seq + "#second"
+    cams_b = {seq_b: cams[seq]}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    layer.prepare(hm[:1], {"seq": [seq_b]}, cams_b, rt)
+    e1.record()
+    torch.cuda.synchronize()
+    cache_ms = {"first_call_ms": round(first_ms, 2), "sequence_build_ms": round((time.perf_counter() - t0) * 1e3, 3),
+                "sequence_build_gpu_ms": round(e0.elapsed_time(e1), 3),
+                "what": "grid" if not layer._project_on_the_fly(V) else "camera records (on-the-fly projection)"}
 
     stream = torch.cuda.current_stream(dev)
     ev = []
@@ -226,21 +293,22 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         vals, flat, cols = run_post(cube, xy)
-        if world > 1 and not args.slabs:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
+        if grouped and not args.slabs:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
             parallel.gather_proposals(vals, flat)
         return cols
 
+    note(f"warmup {args.warmup} + {args.steps} timed steps of {B} frames")
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
@@ -248,6 +316,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     if args.child:
+        if grouped:
+            dist.destroy_process_group()
         return
 
     vox_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -268,18 +338,23 @@ def main():
 
     extra = {}
     if rank == 0:
-        # measured copy bandwidth (float4-style device copy, 1 GiB each way) and
-        # the one-frame latency of the step; both outside the timed region
-        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        # measured copy bandwidth: fvp_copy_f4 (float4 streaming copy, 1 GiB each
+        # way, csrc/fvp_copy.hip) on this stream; and the one-frame latency of
+        # the step; both outside the timed region
+        from fvp import _lib
+
+        nbytes = 1 << 30
+        src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
         dst = torch.empty_like(src)
-        dst.copy_(src)
+        cs = torch.cuda.current_stream(dev).cuda_stream
+        _lib.call("fvp_copy_f4", src.data_ptr(), dst.data_ptr(), nbytes, cs)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(5):
-            dst.copy_(src)
+        for _ in range(10):
+            _lib.call("fvp_copy_f4", src.data_ptr(), dst.data_ptr(), nbytes, cs)
         e1.record()
         torch.cuda.synchronize()
-        extra["copy_gbs"] = 2 * src.numel() * 4 * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        extra["copy_gbs"] = 2 * nbytes * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
         del src, dst
         hm1, meta1 = hm[:1], {"seq": [seq]}
 
@@ -314,8 +389,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
+        note("cpu baseline")
         sg_cpu = layer.build_sample_grid(cams, seq, rt, dev).cpu().contiguous()
-        cpu = cpu_baseline(w, sg_cpu, args.cpu_seconds)
+        cpu = cpu_baseline(w, sg_cpu, args.cpu_seconds, cpu_baseline_threads(args.cpu_threads))
 
     if rank == 0:
         line = {
@@ -338,7 +414,7 @@ def main():
                 "global_batch": B if args.slabs else world * B,
                 "parallelism": (f"x-slab x{world}" + (" + RCCL all_gather of xy slabs, all_reduce of columns"
                                                       if world > 1 else "") if args.slabs else
-                                f"frame-sharded x{world}" + (" + RCCL all_gather of proposals" if world > 1 else "")),
+                                f"frame-sharded x{world}" + (" + RCCL all_gather of proposals" if grouped else "")),
             },
             "roofline": {
                 "bound": "hbm",
@@ -360,16 +436,20 @@ def main():
             "latency_b1_graph_ms": round(extra["latency_b1_graph_ms"], 3) if "latency_b1_graph_ms" in extra else None,
             "cpu_baseline": cpu,
             "execution": "hipGraph replay of the GPU-local step" if args.graph == "on" else "eager",
-            "cache_build_ms": round(cache_ms, 2),
+            "cache_build": cache_ms,
         }
         if traffic is not None:
             line["roofline"]["traffic_detail"] = {k: round(v, 1) for k, v in traffic.items()}
         elif traffic_note:
             line["roofline"]["traffic_note"] = traffic_note
-        print(json.dumps(line), flush=True)
-    if world > 1:
+        sys.stdout.flush()
+        print(json.dumps(line), file=json_out, flush=True)
+    if grouped:
+        note("final barrier")
         dist.barrier()  # rank 0's extra measurements done: every rank leaves together
+        note("destroy process group")
         dist.destroy_process_group()
+    note("done")
 
 
 if __name__ == "__main__":

@@ -300,6 +300,11 @@ int fvp_weight_net(const float *features, int Nimg, int H, int W, const float *c
 int fvp_nchw_to_nhwc(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream);
 int fvp_nhwc_to_nchw(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream);
 
+/* Roofline calibration (not on the product path): a float4 streaming copy of
+ * `bytes` (multiple of 16) from src to dst; bench.py reports the op's HBM
+ * rate as a fraction of this kernel's measured rate besides the nominal peak. */
+int fvp_copy_f4(const void *src, void *dst, size_t bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -297,6 +297,7 @@ def test_proposal_layer_test_mode_matches_reference_semantics(gpu_device):
     assert got[0, 1, 2] == 7 * scale[2] + bias[2]
     # the module's own forward (3-D index given)
     ref2 = ref.clone()
+    ref2[:, :, 0:3] = ref_idx.float() * scale + bias
     ref2[:, :, 4] = confs
     ref2[:, :, 3] = (confs > cfg.CAPTURE_SPEC.MIN_SCORE).float() - 1.0
     got2 = layer(to(ref_idx), to(confs), to(bbox), {}).cpu()

@@ -21,4 +21,4 @@ TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum
 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum
 SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES}"
 python3 tools/pmc_summary.py $OUT
-[ -n "${PMC_CLEAN:-}" ] && rm -rf $OUT/p*/
+if [ -n "${PMC_CLEAN:-}" ]; then rm -rf $OUT/p*/; fi

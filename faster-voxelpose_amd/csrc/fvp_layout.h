@@ -23,10 +23,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base,
 // -- layout pass ----------------------------------------------------------------
 // thread = (pixel, joint quad q): reads joints 4q..4q+3 of one pixel (the lanes
 // of a wave cover 64/LPV consecutive pixels -> coalesced plane reads), writes
-// one float4 (a wave writes a contiguous 1 KiB run).
-template <int LPV, typename T>
+// one float4 (a wave writes a contiguous 1 KiB run; NF > 1: runs of JP*4 B,
+// the NF frames of a group interleaved per pixel: [b/NF][V][H*W][NF][JP]).
+template <int LPV, typename T, int NF = 1>
 __global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict__ hm, float4 *__restrict__ cl, int J,
-                                                             int HW, long long total_px) {
+                                                             int HW, int V, long long total_px) {
     const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
     const long long pxg = gid / LPV;
     const int q = (int)(gid - pxg * LPV);
@@ -40,16 +41,22 @@ __global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict
     o.y = (j + 1 < J) ? to_f32(src[(size_t)(j + 1) * HW]) : 0.f;
     o.z = (j + 2 < J) ? to_f32(src[(size_t)(j + 2) * HW]) : 0.f;
     o.w = (j + 3 < J) ? to_f32(src[(size_t)(j + 3) * HW]) : 0.f;
-    cl[pxg * LPV + q] = o;
+    if constexpr (NF == 1) {
+        cl[pxg * LPV + q] = o;
+    } else {
+        const long long fr = bv / V;  // frame within the chunk
+        const long long g = fr / NF, f = fr - (fr / NF) * NF, v = bv - fr * V;
+        cl[(((g * V + v) * HW + pix) * NF + f) * LPV + q] = o;
+    }
 }
 
 // -- fp16 pixel-pair table ------------------------------------------------------
 // [b][V][H][W+1] entries of 64 B; entry (y, e) holds pixels x0 = e-1 and x0+1
 // of row y, lane q's 16 B = [x0: joints 4q..4q+3 | x0+1: joints 4q..4q+3] fp16,
 // zeros outside the image (J <= 16).  One thread per (entry, q).
-template <typename T>  // T = _Float16
+template <typename T, int NF = 1>  // T = _Float16; NF frames per entry: [b/NF][V][H][W+1][NF] x 64 B
 __global__ __launch_bounds__(256) void heatmaps_to_pairs_kernel(const T *__restrict__ hm,
-                                                                uint4 *__restrict__ tab, int J, int H, int W,
+                                                                uint4 *__restrict__ tab, int J, int H, int W, int V,
                                                                 long long total) {
     const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
     if (gid >= total) return;
@@ -72,8 +79,15 @@ __global__ __launch_bounds__(256) void heatmaps_to_pairs_kernel(const T *__restr
         h[k] = __builtin_bit_cast(unsigned short, a);
         h[4 + k] = __builtin_bit_cast(unsigned short, b);
     }
-    tab[gid] = make_uint4(h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16), h[4] | ((unsigned)h[5] << 16),
-                          h[6] | ((unsigned)h[7] << 16));
+    const uint4 val = make_uint4(h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16),
+                                 h[4] | ((unsigned)h[5] << 16), h[6] | ((unsigned)h[7] << 16));
+    if constexpr (NF == 1) {
+        tab[gid] = val;
+    } else {
+        const long long fr = bv / V, v = bv - fr * V;
+        const long long g = fr / NF, f = fr - (fr / NF) * NF;
+        tab[(((((g * V + v) * H + y) * W1 + e) * NF) + f) * 4 + q] = val;
+    }
 }
 
 inline size_t pair_frame_bytes(int V, int H, int W) { return (size_t)V * H * (W + 1) * 64; }
@@ -171,12 +185,12 @@ inline size_t cl_frame_bytes(int V, int J, int H, int W) {
     return (size_t)V * H * W * 4 * lanes_per_voxel(J) * sizeof(float);
 }
 
-template <int LPV, typename T>
+template <int LPV, typename T, int NF = 1>
 inline void launch_layout(const T *hm, int nb, int V, int J, int H, int W, float *cl, hipStream_t s) {
     const long long px = (long long)nb * V * H * W;
     const long long threads = px * LPV;
-    hipLaunchKernelGGL((heatmaps_to_cl_kernel<LPV, T>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, hm,
-                       reinterpret_cast<float4 *>(cl), J, H * W, px);
+    hipLaunchKernelGGL((heatmaps_to_cl_kernel<LPV, T, NF>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                       hm, reinterpret_cast<float4 *>(cl), J, H * W, V, px);
 }
 
 }  // namespace fvp

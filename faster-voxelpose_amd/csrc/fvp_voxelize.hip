@@ -49,7 +49,7 @@ struct CoordSource {
     fvp_image_spec im;
 };
 
-template <int LPV, bool PAIR, bool OTF, bool CASC>
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
@@ -59,10 +59,10 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
     constexpr int CPG = 2 * LPV;    // cameras per grid load (2 per lane)
-    extern __shared__ __attribute__((aligned(16))) float stage[];  // [JP][SP] (+ OTF camera records)
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [NF][JP][SP] (+ OTF camera records)
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int bl = L / col_blocks;  // frame within the chunk
-    const int b = frame0 + bl;      // frame within the batch (outputs, grid_index)
+    const int bl = L / col_blocks;   // frame group within the chunk (NF frames share each table entry)
+    const int b = frame0 + bl * NF;  // first frame of the group within the batch (outputs, grid_index)
     const int XY = X * Y;
     int cb = L - bl * col_blocks;
     if (band > 0) {
@@ -87,7 +87,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     const float fV = (float)V;
     const int gsel = grid_index ? grid_index[b] : 0;
     __amdgpu_buffer_rsrc_t grs;
-    float *lcam = stage + ((JP * SP + 3) & ~3);  // OTF: camera records [GV][FVP_CAM_STRIDE] after the stage
+    float *lcam = stage + ((NF * JP * SP + 3) & ~3);  // OTF: camera records [GV][FVP_CAM_STRIDE] after the stage
     float rt[6];
     if constexpr (OTF) {
         const float *cams = src_.cams + (size_t)gsel * V * FVP_CAM_STRIDE;
@@ -98,17 +98,22 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     } else {
         grs = uniform_rsrc(src_.grids + (size_t)gsel * N * GV * 2, (unsigned)(N * GV * 8));
     }
-    // per-camera image of this frame in the workspace
-    const unsigned unit = PAIR ? 64u : JP * 4u;                               // bytes per pixel / entry
-    const unsigned img = PAIR ? (unsigned)(H * (W + 1)) * 64u : (unsigned)(H * W) * unit;  // bytes per camera
+    // per-camera image of this frame group in the workspace: each pixel / pair
+    // entry holds the NF frames' copies back to back (one 128-B line at NF = 2)
+    const unsigned pix = PAIR ? 64u : JP * 4u;  // bytes of one frame's pixel / pair entry
+    const unsigned unit = pix * NF;             // bytes per entry
+    const unsigned img = (PAIR ? (unsigned)(H * (W + 1)) : (unsigned)(H * W)) * unit;  // bytes per camera
     const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
 
     for (int i0 = 0; i0 < T; i0 += VPP) {
         const int i = i0 + threadIdx.x / LPV;
         const bool valid = i < T;
         const int ii = min(i, T - 1);
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        float blk[4] = {0.f, 0.f, 0.f, 0.f};  // CASC: completed 16-camera blocks (view_sum order)
+        float acc[NF][4], blk[NF][4];  // blk (CASC): completed 16-camera blocks (view_sum order)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[f][m] = blk[f][m] = 0.0f;
         float wx_ = 0.f, wy_ = 0.f, wz_ = 0.f;  // OTF: voxel centre (compute_grid, project_whole.py:43-79)
         if constexpr (OTF) {
             const long long n = n0 + ii;
@@ -149,10 +154,12 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 if constexpr (CASC) {
                     if ((v & 15) == 0 && v > 0) {  // a block of 16 cameras is complete: fold it (fvp_device.h)
 #pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            blk[m] = blk[m] + acc[m];
-                            acc[m] = 0.0f;
-                        }
+                        for (int f = 0; f < NF; ++f)
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                blk[f][m] = blk[f][m] + acc[f][m];
+                                acc[f][m] = 0.0f;
+                            }
                     }
                 }
                 const Taps4<PAIR> &src = (k & 1) ? t1 : t0;
@@ -171,58 +178,80 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
                 if constexpr (PAIR) {
                     // r0 = [a j0 j1 | a j2 j3 | b j0 j1 | b j2 j3] (row y0), r1 likewise (c, d; row y1)
-                    const u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
-                    const u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                    u32x4 r0[NF], r1[NF];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const unsigned ua = r0[m >> 1], ub = r0[2 + (m >> 1)];
-                        const unsigned uc = r1[m >> 1], ud = r1[2 + (m >> 1)];
-                        const float fa = (m & 1) ? h_hi(ua) : h_lo(ua);
-                        const float fb = (m & 1) ? h_hi(ub) : h_lo(ub);
-                        const float fc = (m & 1) ? h_hi(uc) : h_lo(uc);
-                        const float fd = (m & 1) ? h_hi(ud) : h_lo(ud);
-                        acc[m] = acc[m] +
-                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                    for (int f = 0; f < NF; ++f) {
+                        r0[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + f * pix + qo, 0, 0);
+                        r1[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + f * pix + qo, 0, 0);
                     }
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const unsigned ua = r0[f][m >> 1], ub = r0[f][2 + (m >> 1)];
+                            const unsigned uc = r1[f][m >> 1], ud = r1[f][2 + (m >> 1)];
+                            const float fa = (m & 1) ? h_hi(ua) : h_lo(ua);
+                            const float fb = (m & 1) ? h_hi(ub) : h_lo(ub);
+                            const float fc = (m & 1) ? h_hi(uc) : h_lo(uc);
+                            const float fd = (m & 1) ? h_hi(ud) : h_lo(ud);
+                            acc[f][m] = acc[f][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
+                                                                   __builtin_fmaf(fb, w[1], fa * w[0])));
+                        }
                 } else {
-                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
-                    const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
-                    const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
-                    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+                    u32x4 a[NF], bq[NF], c[NF], d[NF];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
-                        const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
-                        const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
-                        const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
-                        acc[m] = acc[m] +
-                                 __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2], __builtin_fmaf(fb, w[1], fa * w[0])));
+                    for (int f = 0; f < NF; ++f) {
+                        a[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + f * pix + qo, 0, 0);
+                        bq[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + f * pix + qo, 0, 0);
+                        c[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + f * pix + qo, 0, 0);
+                        d[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + f * pix + qo, 0, 0);
                     }
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const float fa = __builtin_bit_cast(float, (unsigned)a[f][m]);
+                            const float fb = __builtin_bit_cast(float, (unsigned)bq[f][m]);
+                            const float fc = __builtin_bit_cast(float, (unsigned)c[f][m]);
+                            const float fd = __builtin_bit_cast(float, (unsigned)d[f][m]);
+                            acc[f][m] = acc[f][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
+                                                                   __builtin_fmaf(fb, w[1], fa * w[0])));
+                        }
                 }
             });
         }
         // the sum's final levels (fvp_device.h): remainder + blocks, or + 0 (a -0 sum becomes +0)
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc[m] = acc[m] + (CASC ? blk[m] : 0.0f);
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[f][m] = acc[f][m] + (CASC ? blk[f][m] : 0.0f);
         if (valid) {
 #pragma unroll
-            for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf(acc[m] / fV, 0.0f, 1.0f);
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    stage[(f * JP + 4 * q + m) * SP + i] = clampf(acc[f][m] / fV, 0.0f, 1.0f);
         }
     }
     __syncthreads();
-    if (cube) {
-        for (int j = 0; j < J; ++j) {
-            float *__restrict__ dst = cube + ((size_t)b * J + j) * N + n0;
-            for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(stage[j * SP + e], dst + e);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const float *fst = stage + f * JP * SP;
+        const size_t bf = (size_t)(b + f);
+        if (cube) {
+            for (int j = 0; j < J; ++j) {
+                float *__restrict__ dst = cube + (bf * J + j) * N + n0;
+                for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
+            }
         }
-    }
-    if (xy) {
-        for (int e = threadIdx.x; e < J * ncols; e += 256) {
-            const int j = e / ncols, cc = e - (e / ncols) * ncols;
-            const float *s = stage + j * SP + cc * Z;
-            float m = -INFINITY;
-            for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
-            __builtin_nontemporal_store(m, xy + ((size_t)b * J + j) * XY + c0 + cc);
+        if (xy) {
+            for (int e = threadIdx.x; e < J * ncols; e += 256) {
+                const int j = e / ncols, cc = e - (e / ncols) * ncols;
+                const float *s = fst + j * SP + cc * Z;
+                float m = -INFINITY;
+                for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+                __builtin_nontemporal_store(m, xy + (bf * J + j) * XY + c0 + cc);
+            }
         }
     }
 }
@@ -232,25 +261,25 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
 // (C2 -4 %, C4 -8 % gather time, measured).
 // Cached-grid gather: <= 64 VGPRs so 8 waves/SIMD fit (32 waves/CU with the
 // 20 KB stage); the on-the-fly variant keeps its registers (no spills).
-template <int LPV, bool PAIR, bool OTF, bool CASC>
-__global__ __launch_bounds__(256, 8) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
+__global__ __launch_bounds__(256, NF == 1 ? 8 : 5) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int H, int W, int X, int Y, int Z, int cols,
                                                           int col_blocks, int SP, int band) {
     static_assert(!OTF, "grid kernel");
-    voxelize_body<LPV, PAIR, OTF, CASC>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
+    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
                                   band);
 }
 
-template <int LPV, bool PAIR, bool OTF, bool CASC>
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restrict__ tab, CoordSource src,
                                                             const int32_t *__restrict__ grid_index, int frame0,
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
                                                             int J, int H, int W, int X, int Y, int Z, int cols,
                                                             int col_blocks, int SP, int band) {
     static_assert(OTF, "on-the-fly kernel");
-    voxelize_body<LPV, PAIR, OTF, CASC>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
+    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
                                   band);
 }
 
@@ -294,16 +323,19 @@ static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     return (int)c;
 }
 
-template <int LPV, bool PAIR, bool OTF, bool CASC, typename T>
-static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
+// Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
+// layout pass into the workspace, then the gather, NF frames per table entry.
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, typename T>
+static int run_chunks(const T *hm, int first, int last, int V, int J, int H, int W, const CoordSource &src,
                       const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
     const bool half = sizeof(T) == 2;
-    const int chunk = chunk_frames(B, V, J, H, W, half);
+    const int B = last - first;
+    const int chunk = max(NF, chunk_frames(B, V, J, H, W, half) / NF * NF);
     // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
     int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
     // latency (few frames): one pass of 256/LPV voxels per block, so a single
     // frame spreads over enough blocks to fill the CUs
-    if ((long long)min(chunk, B) * ((X * Y + cols - 1) / cols) < 4 * 256) cols = max(1, (256 / LPV) / Z);
+    if ((long long)min(chunk, B) / NF * ((X * Y + cols - 1) / cols) < 4 * 256) cols = max(1, (256 / LPV) / Z);
     // Column groups that tile the x-rows exactly (largest divisor of Y, if it
     // keeps at least half the columns), so the blocks can be walked in bands of
     // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
@@ -318,29 +350,53 @@ static int run_chunks(const T *hm, int B, int V, int J, int H, int W, const Coor
     const int band = (big && Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
     const int col_blocks = (X * Y + cols - 1) / cols;
     const int SP = stage_pitch(LPV, cols, Z);
-    size_t lds = (size_t)4 * LPV * SP * sizeof(float);
+    size_t lds = (size_t)NF * 4 * LPV * SP * sizeof(float);
     if (OTF) lds = ((lds / 4 + 3) & ~(size_t)3) * 4 + (size_t)FVP_GRID_SLOTS(V) * FVP_CAM_STRIDE * sizeof(float);
     if (lds > 160 * 1024) return FVP_ERR_SHAPE;
     const size_t frame_elems = (size_t)V * J * H * W;
-    for (int f0 = 0; f0 < B; f0 += chunk) {
-        const int nb = min(chunk, B - f0);
+    for (int f0 = first; f0 < last; f0 += chunk) {
+        const int nb = min(chunk, last - f0);
         const T *hsrc = hm + (size_t)f0 * frame_elems;
         if constexpr (PAIR) {
             const long long total = (long long)nb * V * H * (W + 1) * 4;
-            hipLaunchKernelGGL(heatmaps_to_pairs_kernel<_Float16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                               s, reinterpret_cast<const _Float16 *>(hsrc), reinterpret_cast<uint4 *>(ws), J, H, W,
-                               total);
+            hipLaunchKernelGGL((heatmaps_to_pairs_kernel<_Float16, NF>), dim3((unsigned)((total + 255) / 256)),
+                               dim3(256), 0, s, reinterpret_cast<const _Float16 *>(hsrc), reinterpret_cast<uint4 *>(ws),
+                               J, H, W, V, total);
         } else {
-            launch_layout<LPV, T>(hsrc, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
+            launch_layout<LPV, T, NF>(hsrc, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
         }
+        const dim3 grid((unsigned)(nb / NF * col_blocks));
         if constexpr (OTF)
-            hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC>), dim3((unsigned)(nb * col_blocks)), dim3(256),
-                               lds, s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
+            hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), lds, s, ws, src,
+                               grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
         else
-            hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC>), dim3((unsigned)(nb * col_blocks)), dim3(256), lds,
-                               s, ws, src, grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
+            hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), lds, s, ws, src,
+                               grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
     }
     return (int)hipGetLastError();
+}
+
+// Frames per table entry: the fp16 pair table interleaves two frames per
+// 128-B line (NF = 2), so each tap row of a voxel-camera serves both frames
+// with one line and one tap setup: C5 3.97 -> 3.12 ms per 8 frames (the
+// gather waits on L1 misses; measured).  The fp32 channels-last table keeps
+// one frame per entry (NF = 2 measured 4 % slower at C2: the L2 working set
+// doubles).  Frames of a pair must share one sampling grid, so batches that
+// mix sequences (grid_index given) and an odd last frame run at NF = 1.
+template <int LPV, bool PAIR, bool OTF, bool CASC, typename T>
+static int run_frames(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
+                      const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
+    if constexpr (PAIR) {
+        if (!grid_index && chunk_frames(B, V, J, H, W, sizeof(T) == 2) >= 2) {  // the workspace holds >= 2 frames
+            const int even = B & ~1;
+            const int st = run_chunks<LPV, PAIR, OTF, CASC, 2, T>(hm, 0, even, V, J, H, W, src, grid_index, X, Y, Z,
+                                                                  cube, xy, ws, s);
+            if (st != FVP_OK || even == B) return st;
+            return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, even, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                                          ws, s);
+        }
+    }
+    return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, 0, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
 }
 
 template <bool OTF, bool CASC, typename T>
@@ -349,12 +405,12 @@ static int voxelize_lpv(const T *hm, int B, int V, int J, int H, int W, const Co
                         hipStream_t s) {
     const bool half = sizeof(T) == 2;
     if (use_pairs(J, half))
-        return run_chunks<4, true, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        return run_frames<4, true, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
     switch (lanes_per_voxel(J)) {
-        case 1: return run_chunks<1, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 2: return run_chunks<2, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 4: return run_chunks<4, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        default: return run_chunks<8, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 1: return run_frames<1, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 2: return run_frames<2, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        case 4: return run_frames<4, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+        default: return run_frames<8, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
     }
 }
 

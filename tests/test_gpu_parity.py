@@ -431,6 +431,38 @@ def test_fp16_heatmaps_computed_in_fp32(gpu_device):
     _assert_same(cube[1].cpu().numpy(), ref, "fp16 frame")
 
 
+@pytest.mark.parametrize("B", [2, 3, 5])
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
+def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf):
+    """The fp16 pair table holds two frames per 128-B entry (NF = 2): every
+    frame of an even or odd batch equals its own single-frame launch and the
+    fp32 layout's result; 31 ring cameras (the 16-camera cascade) on a small grid."""
+    from fvp import geometry, synthetic
+    from fvp.config import make_cfg
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+    import dataclasses
+
+    w = dataclasses.replace(WORKLOADS["c5"], voxels_per_axis=(24, 20, 12))
+    layer = ProjectLayer(make_cfg(w, str(gpu_device)))
+    layer.verbose = False
+    layer.on_the_fly = otf
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = synthetic.uniform_heatmaps(w, B, seed=21).half().to(gpu_device)
+    cube, xy = layer.forward_fused(hm, {"seq": [seq] * B}, cams, rt)
+    c32, x32 = layer.forward_fused(hm.float(), {"seq": [seq] * B}, cams, rt)
+    assert torch.equal(cube, c32) and torch.equal(xy, x32)
+    for b in range(B):
+        c1, x1 = layer.forward_fused(hm[b:b + 1], {"seq": [seq]}, cams, rt)
+        assert torch.equal(cube[b:b + 1], c1) and torch.equal(xy[b:b + 1], x1), b
+    grid = O.compute_grid(w.space_size, w.space_center, w.voxels_per_axis)
+    sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, w.heatmap_size, rt.cpu().numpy())
+                   for c in geometry.camera_list(cams, seq)])
+    ref = O.voxelize(hm[B - 1].float().cpu().numpy(), sg).reshape(cube.shape[1:])
+    _assert_same(cube[B - 1].cpu().numpy(), ref, "fp16 ring frame")
+
+
 def test_nms_on_channel_slice_without_copy(gpu_device):
     from fvp.proposal import nms2D
 

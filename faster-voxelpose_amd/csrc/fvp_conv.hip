@@ -1,24 +1,33 @@
-// Dense 2-D convolutions of the HDN / JLN CNNs on the fp32 matrix cores
+// Dense 2-D convolutions on the fp32 matrix cores: the HDN / JLN CNNs
 // (CenterNet cnns_2d.py:235-295, P2PNet :185-232,
 // their Basic2DBlock / Res2DBlock / Upsample2DBlock / EncoderDecorder parts
-// :12-183, and WeightNet's convolution, weight_net.py:48-80).
+// :12-183, WeightNet's convolution, weight_net.py:48-80) and the PoseResNet
+// heatmap backbone (§8(f) rank 4: resnet.py:98-201 -- strided 7x7 / 3x3 / 1x1
+// convolutions and the ConvTranspose2d(4, 2, 1) deconvolution head).
 //
 // Implicit GEMM, NHWC fp32 activations with channels padded to a multiple of
-// 16 (padding channels hold zeros), out[m][co] = sum_k A[m][k] W[k][co] with
-// m = (image, y, x) and k = ((ky*KW + kx)*Cp_in + ci).  v_mfma_f32_32x32x2_f32
-// is an exact fp32 fma chain, so the only difference from torch's fp32 conv
-// is the summation order.  Eval-mode BatchNorm is folded into a per-channel
-// scale/shift (with the conv bias), and the epilogue fuses the residual add
-// of Res2DBlock (before the ReLU), the ReLU, the decoder's skip add (after
-// the ReLU) and, for ConvTranspose2d(k=2, s=2), the 2x upsampling scatter
-// (the transposed conv is a 1x1 conv producing 4*Cout channels).
+// 16 (or 4 / 8 for a network's RGB input; padding channels hold zeros),
+// out[m][co] = sum_k A[m][k] W[k][co] with m = (image, y, x) and
+// k = (ky*KW + kx)*Cpi + ci.  v_mfma_f32_32x32x2_f32 is an exact fp32 fma
+// chain, so the only difference from torch's fp32 conv is the summation
+// order.  Eval-mode BatchNorm is folded into a per-channel scale/shift (with
+// the conv bias), and the epilogue fuses the residual add of Res2DBlock /
+// Bottleneck (before the ReLU), the ReLU, the decoder's skip add (after the
+// ReLU) and the output scatter of the transposed convolutions:
+//   mode 1  ConvTranspose2d(k=2, s=2): a 1x1 conv producing 4*Cout channels
+//   mode 2  ConvTranspose1d(k=2, s=2): the same with 2*Cout on rows of H == 1
+//   mode 3  ConvTranspose2d(k=4, s=2, p=1): four 2x2 convolutions over the
+//           input grid, one per output parity (ry, rx) -- output pixel
+//           (2y+ry, 2x+rx) takes input rows y-1+ry.. and kernel taps
+//           ky = 3 - 2*i - ry (i = 0, 1) -- so no MFMA work is spent on the
+//           zeros a dilated-input formulation would multiply.
 //
 // Block = 256 threads (4 waves); the tile follows the output width so no MFMA
 // column is wasted on padding: Cout <= 16 -> 256 px x 16 ch on 16x16x4 MFMAs,
 // <= 32 -> 128 x 32, wider -> 128 x 64 (2 accumulators per wave) on 32x32x2.
 // The K dimension is walked in chunks of 16 (one (ky,kx) tap, 16 input
-// channels) staged through LDS, the next chunk's global loads issued before
-// the current chunk's MFMAs.
+// channels; with Cpi < 16 a chunk spans 16/Cpi taps) staged through LDS, the
+// next chunk's global loads issued before the current chunk's MFMAs.
 #include <type_traits>
 
 #include "fvp_device.h"
@@ -30,15 +39,24 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvArgs {
     const float *in;        // [N][H][W][Cpi]
-    const float *w;         // [KH*KW*Cpi][Cpo_w]  (Cpo_w = roundup(Cout_total, 128))
+    const float *w;         // [G][Krows][Cpo_w], Krows = KH*KW*Cpi rounded up to 16 (zero rows), G parity groups
     const float *scale;     // [Cpo]  (per output channel)
     const float *shift;     // [Cpo]
     const float *res_pre;   // [N][Ho][Wo][Cpo] or null: added before the ReLU
     const float *res_post;  // [N][Ho][Wo][Cpo] or null: added after the ReLU
     float *out;             // [N][Ho][Wo][Cpo]
-    int N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, up2;
+    int N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, up2;  // up2 = mode (0 conv, 1-3 transposed, see above)
+    int Hm, Wm;             // GEMM row grid: output pixels (mode 0) or input pixels (modes 1-3)
+    int sy, sx, py, px;     // stride and top/left zero padding: input = row * s - p + tap
+    int ks;                 // split-K blocks per parity group (gridDim.z = groups * ks)
     float *part;            // split-K: raw partial sums [gridDim.z][M][Ntot] (no epilogue), else null
 };
+
+__host__ __device__ __forceinline__ int conv_groups(int up2) { return up2 == 3 ? 4 : 1; }
+__host__ __device__ __forceinline__ int conv_cols(int up2, int Cpo) {  // GEMM columns per group
+    return (up2 == 1 ? 4 : up2 == 2 ? 2 : 1) * Cpo;
+}
+__host__ __device__ __forceinline__ int conv_krows(int KH, int KW, int Cpi) { return (KH * KW * Cpi + 15) & ~15; }
 
 // Tile configuration: BM pixels x BN channels per 256-thread block, MFMA
 // MSxMS (32: v_mfma_f32_32x32x2_f32, 16: v_mfma_f32_16x16x4_f32), waves
@@ -54,84 +72,118 @@ struct Tile {
     static_assert(TM >= 1 && TN >= 1 && WTM % MS == 0 && WTN % MS == 0, "tile");
 };
 
-// Per-thread A rows (pixels) are fixed for the whole K loop: their (image,
-// y, x) are decoded once, so a chunk only adds the tap offset.
+// Per-thread A rows (pixels) are fixed for the whole K loop: their image and
+// input origin (row * stride - pad) are decoded once, so a chunk only adds
+// the tap offset.
 struct PixRef {
-    int y, x;         // output pixel coordinates (y = -1 << 20 when past M)
+    int y, x;         // input coordinates of tap (0, 0) (y = -1 << 20 when past M)
     const float *p;   // input row base of the pixel's image
 };
 
+__device__ __forceinline__ void pix_ref(const ConvArgs &a, int m, int M, int py, int px, PixRef &pr) {
+    const int HWm = a.Hm * a.Wm;
+    const int img = m / HWm, r = m - img * HWm;
+    const int yy = r / a.Wm, xx = r - (r / a.Wm) * a.Wm;
+    pr.y = m < M ? yy * a.sy - py : -(1 << 20);
+    pr.x = xx * a.sx - px;
+    pr.p = a.in + (size_t)(m < M ? img : 0) * a.H * a.W * a.Cpi;
+}
+
 template <class TL>
-__device__ __forceinline__ void load_chunk(const ConvArgs &a, int n0, int chunk, const PixRef *pr, float4 *av,
-                                           float4 *bv) {
+__device__ __forceinline__ void load_chunk(const ConvArgs &a, const float *__restrict__ w, int n0, int chunk,
+                                           const PixRef *pr, float4 *av, float4 *bv) {
     constexpr int AE = TL::BM * TL::KC / 4;        // float4 of the A chunk
     constexpr int AV = AE >= 256 ? AE / 256 : 1;   // per thread
     constexpr int BV = TL::KC * TL::BN / 4 / 256;  // float4 per thread (B), may be 0
     const int t = threadIdx.x;
-    const int cpc = a.Cpi / TL::KC;  // chunks per tap
-    const int tap = chunk / cpc, c = chunk - tap * cpc;
-    const int ky = tap / a.KW, kx = tap - ky * a.KW;
-    const int dy = ky - (a.KH - 1) / 2, dx = kx - (a.KW - 1) / 2;
+    if (a.Cpi >= TL::KC) {  // one tap per chunk (Cpi % KC == 0)
+        const int cpc = a.Cpi / TL::KC;  // chunks per tap
+        const int tap = chunk / cpc, c = chunk - tap * cpc;
+        const int ky = tap / a.KW, kx = tap - ky * a.KW;
 #pragma unroll
-    for (int u = 0; u < AV; ++u) {
-        const int e = u * 256 + t;  // -> (pixel e/4, 4 channels)
-        const int y = pr[u].y + dy, x = pr[u].x + dx;
-        av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-            av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * TL::KC +
-                                                     (e & 3) * 4);
+        for (int u = 0; u < AV; ++u) {
+            const int e = u * 256 + t;  // -> (pixel e/4, 4 channels)
+            const int y = pr[u].y + ky, x = pr[u].x + kx;
+            av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+                av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * TL::KC +
+                                                         (e & 3) * 4);
+        }
+    } else {  // Cpi in {4, 8, 12}: each float4 is 4 channels of its own tap; k past the taps reads 0
+        const int ntaps = a.KH * a.KW;
+#pragma unroll
+        for (int u = 0; u < AV; ++u) {
+            const int e = u * 256 + t;
+            const int k = chunk * TL::KC + (e & 3) * 4;
+            const int tap = k / a.Cpi, ci = k - tap * a.Cpi;
+            const int ky = tap / a.KW, kx = tap - ky * a.KW;
+            const int y = pr[u].y + ky, x = pr[u].x + kx;
+            av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < AE && tap < ntaps && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+                av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + ci);
+        }
     }
     if constexpr (BV > 0) {
 #pragma unroll
         for (int u = 0; u < BV; ++u) {
             const int e = u * 256 + t;  // -> (k row e/(BN/4), 4 columns)
-            const size_t row = (size_t)tap * a.Cpi + c * TL::KC + e / (TL::BN / 4);
-            bv[u] = *reinterpret_cast<const float4 *>(a.w + row * a.Cpo_w + n0 + (e % (TL::BN / 4)) * 4);
+            const size_t row = (size_t)chunk * TL::KC + e / (TL::BN / 4);
+            bv[u] = *reinterpret_cast<const float4 *>(w + row * a.Cpo_w + n0 + (e % (TL::BN / 4)) * 4);
         }
     } else {  // BN*KC/4 < 256: the first KC*BN/4 threads load one float4
         if (t < TL::KC * TL::BN / 4) {
-            const size_t row = (size_t)tap * a.Cpi + c * TL::KC + t / (TL::BN / 4);
-            bv[0] = *reinterpret_cast<const float4 *>(a.w + row * a.Cpo_w + n0 + (t % (TL::BN / 4)) * 4);
+            const size_t row = (size_t)chunk * TL::KC + t / (TL::BN / 4);
+            bv[0] = *reinterpret_cast<const float4 *>(w + row * a.Cpo_w + n0 + (t % (TL::BN / 4)) * 4);
         }
     }
 }
 
+// Output element of GEMM row m (a pixel of the row grid), column n, parity
+// group g: mode 0 the pixel itself; modes 1-3 the scattered pixel of the
+// upsampled output.  co receives the output channel.
+__device__ __forceinline__ size_t conv_out_offset(const ConvArgs &a, int m, int n, int g, int &co) {
+    if (!a.up2) {
+        co = n;
+        return (size_t)m * a.Cpo + n;
+    }
+    const int q = a.up2 == 3 ? g : n / a.Cpo;  // (dy, dx) of the transposed conv
+    co = a.up2 == 3 ? n : n - q * a.Cpo;
+    const int HWm = a.Hm * a.Wm;
+    const int img = m / HWm, rr = m - img * HWm;
+    const int yy = rr / a.Wm, xx = rr - yy * a.Wm;
+    const int Ho = a.up2 == 2 ? a.Hm : 2 * a.Hm, Wo = 2 * a.Wm;
+    const int y = a.up2 == 2 ? yy : 2 * yy + (q >> 1);
+    const int x = 2 * xx + (a.up2 == 2 ? q : (q & 1));
+    return (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
+}
+
 // Fused epilogue of a wave's accumulator tiles: out = act(acc * scale + shift
-// + res_pre) + res_post at the output offset of (row m, column n); up2: 1 =
-// ConvTranspose2d(2, 2) (2x2 scatter), 2 = ConvTranspose1d(2, 2) on H == 1
-// rows (1x2 scatter).  Rows come EPI at a time with every residual load issued
-// before the first use (one wait per group instead of one per element).
-// rowm(l) maps the block-local row l to its output pixel m (or -1 past the
-// image); m must grow with l inside an MFMA tile.
+// + res_pre) + res_post at the output offset of (row m, column n).  Rows come
+// EPI at a time with every residual load issued before the first use (one
+// wait per group instead of one per element).  rowm(l) maps the block-local
+// row l to its row-grid pixel m (or -1 past the image); m must grow with l
+// inside an MFMA tile (the output offsets then grow too).
 template <int TM, int TN, int NACC, int MS, typename AccT, typename RowM>
 __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM][TN], const RowM &rowm, int mw,
-                                         int nw, int lane) {
+                                         int nw, int lane, int g) {
     constexpr int EPI = 4;
-    const int Ctot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
-    const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = a.up2 ? 2 * a.W : a.W;
-    const int HW = a.H * a.W;
+    const int Ctot = conv_cols(a.up2, a.Cpo);
     auto rowof = [&](int r) { return MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r; };
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = nw + j * MS + (lane % MS);
         const bool nok = n < Ctot;
         const int nn = nok ? n : 0;
-        const int co = a.up2 ? nn % a.Cpo : nn;
-        const int q = a.up2 ? nn / a.Cpo : 0;  // (dy, dx) of the transposed conv
+        int co;
+        (void)conv_out_offset(a, 0, nn, g, co);
         const float sc = a.scale[co], sh = a.shift[co];
-        auto offset = [&](int m) -> size_t {  // output element of (row m, column co)
-            if (!a.up2) return (size_t)m * a.Cpo + co;
-            const int img = m / HW, rr = m - img * HW;
-            const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
-            const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
-            return (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
-        };
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int mt = rowm(mw + i * MS);  // first row of this MFMA tile (wave-uniform)
             if (mt < 0) continue;
             // offsets grow with m, so rows are addressed relative to the tile's first (32-bit)
-            const size_t ob = offset(mt) - co;
+            int c_;
+            const size_t ob = conv_out_offset(a, mt, nn, g, c_) - co;
             float *__restrict__ out = a.out + ob;
             const float *__restrict__ rpre = a.res_pre ? a.res_pre + ob : nullptr;
             const float *__restrict__ rpost = a.res_post ? a.res_post + ob : nullptr;
@@ -144,7 +196,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
                 for (int r = 0; r < EPI; ++r) {
                     const int m = rowm(mw + i * MS + rowof(r0 + r));
                     ok[r] = nok && m >= 0;
-                    rel[r] = ok[r] ? (unsigned)(offset(m) - ob) : 0u;
+                    rel[r] = ok[r] ? (unsigned)(conv_out_offset(a, m, nn, g, c_) - ob) : 0u;
                 }
                 if (rpre) {
 #pragma unroll
@@ -175,14 +227,17 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     constexpr int BVN = KC * BN / 4 / 256 > 0 ? KC * BN / 4 / 256 : 1;
     __shared__ float As[2][BM * AP];
     __shared__ __attribute__((aligned(16))) float Bs[2][KC * BN];
-    const int M = a.N * a.H * a.W;
+    const int M = a.N * a.Hm * a.Wm;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave % TL::WR, wc = wave / TL::WR;
-    const int nchunks = a.KH * a.KW * (a.Cpi / KC);
-    // split-K: block z of gridDim.z walks chunks [cb, ce) and leaves raw partial sums
-    const int cb = (int)((long long)blockIdx.z * nchunks / gridDim.z);
-    const int ce = (int)((long long)(blockIdx.z + 1) * nchunks / gridDim.z);
+    const int g = blockIdx.z / a.ks, kz = blockIdx.z - g * a.ks;  // parity group, split-K slice
+    const int nchunks = conv_krows(a.KH, a.KW, a.Cpi) / KC;
+    // split-K: slice kz walks chunks [cb, ce) and leaves raw partial sums
+    const int cb = (int)((long long)kz * nchunks / a.ks);
+    const int ce = (int)((long long)(kz + 1) * nchunks / a.ks);
+    const float *__restrict__ w = a.w + (size_t)g * nchunks * KC * a.Cpo_w;
+    const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
     using acc_t = typename std::conditional<MS == 32, f32x16, f32x4>::type;
     acc_t acc[TL::TM][TL::TN];
 #pragma unroll
@@ -193,17 +248,8 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
             for (int r = 0; r < TL::NACC; ++r) acc[i][j][r] = 0.f;
 
     PixRef pr[AV];
-    {
-        const int HW = a.H * a.W;
 #pragma unroll
-        for (int u = 0; u < AV; ++u) {
-            const int m = m0 + ((u * 256 + t) >> 2);
-            const int img = m / HW, r = m - img * HW;
-            pr[u].y = m < M ? r / a.W : -(1 << 20);
-            pr[u].x = r % a.W;
-            pr[u].p = a.in + (size_t)(m < M ? img : 0) * HW * a.Cpi;
-        }
-    }
+    for (int u = 0; u < AV; ++u) pix_ref(a, m0 + ((u * 256 + t) >> 2), M, py, px, pr[u]);
     float4 av[AV], bv[BVN];
     auto stage = [&](int buf) {  // registers -> LDS buffer buf
 #pragma unroll
@@ -223,7 +269,7 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
             *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
         }
     };
-    load_chunk<TL>(a, n0, cb, pr, av, bv);
+    load_chunk<TL>(a, w, n0, cb, pr, av, bv);
     stage(cb & 1);
     __syncthreads();
     // One barrier per chunk: chunk ch+1's global loads are issued first, the
@@ -233,7 +279,7 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     for (int ch = cb; ch < ce; ++ch) {
         const int buf = ch & 1;
         const bool more = ch + 1 < ce;
-        if (more) load_chunk<TL>(a, n0, ch + 1, pr, av, bv);
+        if (more) load_chunk<TL>(a, w, n0, ch + 1, pr, av, bv);
 #pragma unroll
         for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
             float fa[TL::TM], fb[TL::TN];
@@ -262,7 +308,7 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     }
 
     if (a.part) {  // split-K: raw partial sums, combined in z order by conv_splitk_reduce
-        const int Ntot = (a.up2 == 1 ? 4 : a.up2 == 2 ? 2 : 1) * a.Cpo;
+        const int Ntot = conv_cols(a.up2, a.Cpo);
         float *__restrict__ dst = a.part + (size_t)blockIdx.z * M * Ntot;
 #pragma unroll
         for (int j = 0; j < TL::TN; ++j) {
@@ -280,26 +326,23 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     }
     // epilogue: lane -> column (output channel), registers -> rows (pixels)
     auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
-    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
+    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane, g);
 }
 
 // Split-K combine: out = act(sum_z part[z] * scale + shift + res_pre) + res_post,
-// summed in z order (deterministic), with the epilogue's output mapping.
-__global__ __launch_bounds__(256) void conv_splitk_reduce(ConvArgs a, int ks, int M, int Ntot) {
+// the ks slices of each parity group summed in z order (deterministic), with
+// the epilogue's output mapping.
+__global__ __launch_bounds__(256) void conv_splitk_reduce(ConvArgs a, int M, int Ntot) {
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (e >= (long long)M * Ntot) return;
-    const int m = (int)(e / Ntot), n = (int)(e - (long long)m * Ntot);
+    const long long per = (long long)M * Ntot;
+    if (e >= per * conv_groups(a.up2)) return;
+    const int g = (int)(e / per);
+    const long long r = e - g * per;
+    const int m = (int)(r / Ntot), n = (int)(r - (long long)m * Ntot);
     float v = 0.0f;
-    for (int z = 0; z < ks; ++z) v += a.part[((size_t)z * M + m) * Ntot + n];
-    const int co = a.up2 ? n % a.Cpo : n, q = a.up2 ? n / a.Cpo : 0;
-    size_t off = (size_t)m * a.Cpo + co;
-    if (a.up2) {
-        const int HW = a.H * a.W, img = m / HW, rr = m - img * HW;
-        const int Ho = a.up2 == 1 ? 2 * a.H : a.H, Wo = 2 * a.W;
-        const int y = a.up2 == 1 ? 2 * (rr / a.W) + (q >> 1) : rr / a.W;
-        const int x = 2 * (rr % a.W) + (a.up2 == 1 ? (q & 1) : q);
-        off = (((size_t)img * Ho + y) * Wo + x) * a.Cpo + co;
-    }
+    for (int z = 0; z < a.ks; ++z) v += a.part[((size_t)(g * a.ks + z) * M + m) * Ntot + n];
+    int co;
+    const size_t off = conv_out_offset(a, m, n, g, co);
     v = v * a.scale[co] + a.shift[co];
     if (a.res_pre) v = v + a.res_pre[off];
     if (a.relu) v = fmaxf(v, 0.0f);
@@ -448,7 +491,7 @@ __global__ __launch_bounds__(256, 4) void conv_halo_kernel(ConvArgs a, int tiles
         const int y = y0 + l / TW, x = x0 + l % TW;
         return (y < a.H && x < a.W) ? img * HWimg + y * a.W + x : -1;
     };
-    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
+    epilogue<TL::TM, TL::TN, TL::NACC, MS>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane, 0);
 }
 
 // Tiles by output width; the big ones where the launch has >= 2 blocks per CU,
@@ -489,13 +532,16 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
     constexpr int BE = BN * KC / 8, BV = BE >= 256 ? BE / 256 : 1;  // B: 8 bf16 per element
     __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * P];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * P];  // [column][k]
-    const int M = a.N * a.H * a.W;
+    const int M = a.N * a.Hm * a.Wm;
     const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave % TL::WR, wc = wave / TL::WR;
+    const int g = blockIdx.z;  // parity group (mode 3), else 0
     const int cpc = a.Cpi / KC;
     const int nchunks = a.KH * a.KW * cpc;
     const size_t Ktot = (size_t)a.KH * a.KW * a.Cpi;
+    const __bf16 *__restrict__ w = wb + (size_t)g * a.Cpo_w * Ktot;
+    const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
     f32x16 acc[TL::TM][TL::TN];
 #pragma unroll
     for (int i = 0; i < TL::TM; ++i)
@@ -504,27 +550,17 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     PixRef pr[AV];
-    {
-        const int HW = a.H * a.W;
 #pragma unroll
-        for (int u = 0; u < AV; ++u) {
-            const int m = m0 + ((u * 256 + t) / (KC / 4));
-            const int img = m / HW, r = m - img * HW;
-            pr[u].y = m < M ? r / a.W : -(1 << 20);
-            pr[u].x = r % a.W;
-            pr[u].p = a.in + (size_t)(m < M ? img : 0) * HW * a.Cpi;
-        }
-    }
+    for (int u = 0; u < AV; ++u) pix_ref(a, m0 + ((u * 256 + t) / (KC / 4)), M, py, px, pr[u]);
     float4 av[AV];
     uint4 bv[BV];
     auto load = [&](int chunk) {
         const int tap = chunk / cpc, c = chunk - tap * cpc;
         const int ky = tap / a.KW, kx = tap - ky * a.KW;
-        const int dy = ky - (a.KH - 1) / 2, dx = kx - (a.KW - 1) / 2;
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
             const int e = u * 256 + t;  // -> (pixel e/(KC/4), 4 channels)
-            const int y = pr[u].y + dy, x = pr[u].x + dx;
+            const int y = pr[u].y + ky, x = pr[u].x + kx;
             av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
                 av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * KC +
@@ -534,7 +570,7 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
         for (int u = 0; u < BV; ++u) {
             const int e = u * 256 + t;  // -> (column e/(KC/8), 8 k)
             if (e < BE)
-                bv[u] = *reinterpret_cast<const uint4 *>(wb + (size_t)(n0 + e / (KC / 8)) * Ktot +
+                bv[u] = *reinterpret_cast<const uint4 *>(w + (size_t)(n0 + e / (KC / 8)) * Ktot +
                                                         (size_t)tap * a.Cpi + c * KC + (e % (KC / 8)) * 8);
         }
     };
@@ -577,7 +613,7 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
     }
 
     auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
-    epilogue<TL::TM, TL::TN, 16, 32>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane);
+    epilogue<TL::TM, TL::TN, 16, 32>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane, g);
 }
 
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
@@ -608,6 +644,38 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float *__restrict__ 
     if (KH == 2) {
         mx(p[rs]);
         if (KW == 2) mx(p[rs + C / 4]);
+    }
+    reinterpret_cast<float4 *>(out)[gid] = m;
+}
+
+// MaxPool2d(K, S, P) of NHWC activations with implicit -inf padding
+// (resnet.py:109: kernel 3, stride 2, padding 1), NaN-propagating like torch.
+__global__ __launch_bounds__(256) void maxpool_pad_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                          int N, int H, int W, int C, int K, int S, int P, int Ho,
+                                                          int Wo) {
+    const long long total = (long long)N * Ho * Wo * (C / 4);
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int c4 = (int)(gid % (C / 4));
+    long long r = gid / (C / 4);
+    const int x = (int)(r % Wo);
+    r /= Wo;
+    const int y = (int)(r % Ho);
+    const long long img = r / Ho;
+    const float4 *base = reinterpret_cast<const float4 *>(in + (size_t)img * H * W * C) + c4;
+    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    for (int ky = 0; ky < K; ++ky) {
+        const int iy = y * S - P + ky;
+        if ((unsigned)iy >= (unsigned)H) continue;
+        for (int kx = 0; kx < K; ++kx) {
+            const int ix = x * S - P + kx;
+            if ((unsigned)ix >= (unsigned)W) continue;
+            const float4 b = base[((size_t)iy * W + ix) * (C / 4)];
+            m.x = nanmax(m.x, b.x);
+            m.y = nanmax(m.y, b.y);
+            m.z = nanmax(m.z, b.z);
+            m.w = nanmax(m.w, b.w);
+        }
     }
     reinterpret_cast<float4 *>(out)[gid] = m;
 }
@@ -651,19 +719,55 @@ struct ConvPlan {
 static const int kTileBM[8] = {0, 256, 64, 128, 64, 128, 64, 32};
 static const int kTileBN[8] = {0, 16, 16, 32, 32, 64, 64, 64};
 
-static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot, int upsample2, int algo) {
+// Geometry of one launch, validated: the GEMM row grid (Hm x Wm) and the
+// output image (Ho x Wo).
+struct ConvGeom {
+    int mode, sy, sx, py, px, Hm, Wm, Ho, Wo;
+};
+
+static int conv_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, ConvGeom &g) {
+    if (H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || Cpi <= 0 || Cpi % 4 || (Cpi > 16 && Cpi % 16)) return FVP_ERR_SHAPE;
+    g = ConvGeom{mode, sy, sx, py, px, H, W, H, W};
+    if (mode == 0) {
+        if (sy < 1 || sx < 1 || sy > 4 || sx > 4 || py < 0 || px < 0 || py >= KH || px >= KW) return FVP_ERR_SHAPE;
+        g.Hm = g.Ho = (H + 2 * py - KH) / sy + 1;
+        g.Wm = g.Wo = (W + 2 * px - KW) / sx + 1;
+        if (H + 2 * py < KH || W + 2 * px < KW) return FVP_ERR_SHAPE;
+        return FVP_OK;
+    }
+    g.sy = g.sx = 1;
+    g.py = g.px = 0;
+    if (mode == 1 || mode == 2) {
+        if (KH != 1 || KW != 1) return FVP_ERR_SHAPE;
+        g.Ho = mode == 1 ? 2 * H : H;
+        g.Wo = 2 * W;
+        return FVP_OK;
+    }
+    if (mode == 3) {  // ConvTranspose2d(4, 2, 1): 2x2 taps per output parity
+        if (KH != 2 || KW != 2) return FVP_ERR_SHAPE;
+        g.Ho = 2 * H;
+        g.Wo = 2 * W;
+        return FVP_OK;
+    }
+    return FVP_ERR_SHAPE;
+}
+
+static ConvPlan conv_plan(int N, int Cpi, int KH, int KW, int Ntot, const ConvGeom &g, int algo) {
     ConvPlan p{0, 0, 1};
-    const long long M = (long long)N * H * W;
+    const int G = conv_groups(g.mode);
+    const long long M = (long long)N * g.Hm * g.Wm;
     const long long enough = 512;  // >= 2 blocks per CU
     // Halo tiles are 16 pixels wide: only where a row wastes <= 1/8 of them
     // (CenterNet's 20- and 40-wide maps stay per-tap), and only with the large
     // tiles (>= 8 rows: halo overhead <= 1.4x of the tile) at >= 2 blocks per
     // CU -- measured (profiles/round1/conv_probe.txt): 7x7 front 205 -> 147 us, 3x3
     // layers at 64/32 px 4-6 % faster; 4-row tiles and sub-2-per-CU launches
-    // were 2-10 % slower than per-tap.
+    // were 2-10 % slower than per-tap.  Stride-1 "same" convolutions only.
+    const int W = g.Wm, H = g.Hm;
     const int tx = (W + 15) / 16;
-    const bool halo = (algo == FVP_CONV_AUTO || algo == FVP_CONV_HALO) && (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && !upsample2 &&
-                      (tx * 16 - W) * 8 <= W;
+    const bool same = g.mode == 0 && g.sy == 1 && g.sx == 1 && 2 * g.py == KH - 1 && 2 * g.px == KW - 1;
+    const bool halo = (algo == FVP_CONV_AUTO || algo == FVP_CONV_HALO) && same && Cpi % 16 == 0 &&
+                      (KH > 1 || KW > 1) && KH <= 7 && KW <= 7 && W >= 16 && (tx * 16 - W) * 8 <= W;
     auto hblocks = [&](int id) {
         const int rows = kTileBM[id] / 16;
         return (long long)N * tx * ((H + rows - 1) / rows) * ((Ntot + kTileBN[id] - 1) / kTileBN[id]);
@@ -676,18 +780,19 @@ static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot
         if (p.halo) return p;
     }
     auto blocks = [&](int id) {
-        return ((M + kTileBM[id] - 1) / kTileBM[id]) * (long long)((Ntot + kTileBN[id] - 1) / kTileBN[id]);
+        return G * ((M + kTileBM[id] - 1) / kTileBM[id]) * (long long)((Ntot + kTileBN[id] - 1) / kTileBN[id]);
     };
     if (Ntot <= 16) p.tile = blocks(1) >= enough ? 1 : 2;
     else if (Ntot <= 32) p.tile = blocks(3) >= enough ? 3 : 4;
     else p.tile = blocks(5) >= enough ? 5 : blocks(6) >= enough ? 6 : 7;
     // Split-K for launches under one block per CU with a long K walk (CenterNet's
-    // 20x20 / 40x40 levels at small batch): each K-chunk step waits on a global
-    // round trip, so fewer, longer block chains leave the CUs idle (CenterNet on
-    // 8 frames 0.61 -> 0.55 ms; C2CNet's 1-D rows were slower split).
-    const int nchunks = KH * KW * (Cpi / 16);
+    // 20x20 / 40x40 levels at small batch, the deep ResNet stages): each K-chunk
+    // step waits on a global round trip, so fewer, longer block chains leave the
+    // CUs idle (CenterNet on 8 frames 0.61 -> 0.55 ms; C2CNet's 1-D rows were
+    // slower split).
+    const int nchunks = conv_krows(KH, KW, Cpi) / 16;
     const long long nb = blocks(p.tile);
-    if (algo != FVP_CONV_PER_TAP_NOSPLIT && H > 1 && nb < 256 && nchunks >= 8) {  // 2-D maps (C2CNet's 1-D rows: slower)
+    if (algo != FVP_CONV_PER_TAP_NOSPLIT && g.Hm > 1 && nb < 256 && nchunks >= 8) {  // 2-D maps only
         int ks = (int)((512 + nb - 1) / nb);
         ks = ks < nchunks / 4 ? ks : nchunks / 4;
         p.ks = ks < 8 ? ks : 8;
@@ -696,36 +801,63 @@ static ConvPlan conv_plan(int N, int H, int W, int Cpi, int KH, int KW, int Ntot
     return p;
 }
 
-static int conv_launch(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW, int Cpo,
+static size_t conv_ws_bytes(int N, int Cpi, int KH, int KW, int Cpo, const ConvGeom &g, int algo) {
+    const int Ntot = conv_cols(g.mode, Cpo);
+    const ConvPlan p = conv_plan(N, Cpi, KH, KW, Ntot, g, algo);
+    return p.ks > 1 ? (size_t)conv_groups(g.mode) * p.ks * N * g.Hm * g.Wm * Ntot * sizeof(float) : 0;
+}
+
+static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void *wpack, int KH, int KW, int Cpo,
                        int Cpo_w, const float *scale, const float *shift, const float *res_pre,
-                       const float *res_post, int relu, int upsample2, float *out, int algo, void *ws,
+                       const float *res_post, int relu, const ConvGeom &g, float *out, int bf16, int algo, void *ws,
                        size_t ws_bytes, void *stream) {
     if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
-    if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
-        (KH & 1) == 0 || (KW & 1) == 0)
-        return FVP_ERR_SHAPE;
-    if (upsample2 < 0 || upsample2 > 2) return FVP_ERR_SHAPE;
-    const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
-    if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
-    const long long M = (long long)N * H * W;
-    if (M * Ntot > 0x7fffffffLL * 4) return FVP_ERR_SHAPE;
-    fvp::ConvArgs a{in, wpack, scale, shift, res_pre, res_post, out, N, H, W, Cpi, KH, KW, Cpo, Cpo_w, relu, upsample2,
-                    nullptr};
-    hipStream_t st = (hipStream_t)stream;
+    if (N <= 0 || Cpo <= 0 || Cpo % 16) return FVP_ERR_SHAPE;
     if (algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return FVP_ERR_SHAPE;
-    ConvPlan p = conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, algo);
-    if (p.ks > 1 && (!ws || ws_bytes < (size_t)p.ks * M * Ntot * sizeof(float))) p.ks = 1;  // no scratch: no split
-    if (p.ks > 1) a.part = reinterpret_cast<float *>(ws);
+    const int Ntot = conv_cols(g.mode, Cpo);
+    if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
+    const long long M = (long long)N * g.Hm * g.Wm;
+    if ((long long)N * g.Ho * g.Wo * Cpo > 0x7fffffffLL * 4 || (long long)N * H * W * Cpi > 0x7fffffffLL * 4)
+        return FVP_ERR_SHAPE;
+    const int G = conv_groups(g.mode);
+    fvp::ConvArgs a{in, reinterpret_cast<const float *>(wpack), scale, shift, res_pre, res_post, out, N, H, W, Cpi,
+                    KH, KW, Cpo, Cpo_w, relu, g.mode, g.Hm, g.Wm, g.sy, g.sx, g.py, g.px, 1, nullptr};
+    hipStream_t st = (hipStream_t)stream;
+    if (bf16) {  // chunks of one tap x 16 / 32 channels, no split
+        if (Cpi % 16) return FVP_ERR_SHAPE;
+        const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
+#define FVP_CONVB(BM, BN, WR, KC)                                                                                 \
+    hipLaunchKernelGGL((fvp::conv_bf16_kernel<fvp::TileB<BM, BN, WR, KC>>),                                      \
+                       dim3((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G),       \
+                       dim3(256), 0, st, a, wb)
+        const bool k32 = Cpi % 32 == 0;
+        const long long b128 = G * ((M + 127) / 128) * ((Ntot + 63) / 64);
+        if (Ntot <= 32) {
+            if (k32) FVP_CONVB(128, 32, 4, 32); else FVP_CONVB(128, 32, 4, 16);
+        } else if (b128 >= 512) {
+            if (k32) FVP_CONVB(128, 64, 2, 32); else FVP_CONVB(128, 64, 2, 16);
+        } else {
+            if (k32) FVP_CONVB(64, 64, 2, 32); else FVP_CONVB(64, 64, 2, 16);
+        }
+#undef FVP_CONVB
+        return (int)hipGetLastError();
+    }
+    ConvPlan p = conv_plan(N, Cpi, KH, KW, Ntot, g, algo);
+    if (p.ks > 1 && (!ws || ws_bytes < (size_t)G * p.ks * M * Ntot * sizeof(float))) p.ks = 1;  // no scratch: no split
+    if (p.ks > 1) {
+        a.part = reinterpret_cast<float *>(ws);
+        a.ks = p.ks;
+    }
     if (p.halo) {
         const int tx = (W + 15) / 16;
 #define FVP_HALO(TL)                                                                                              \
     do {                                                                                                          \
         const int ty = (H + fvp::TL::BM / 16 - 1) / (fvp::TL::BM / 16);                                           \
-        const dim3 g((unsigned)((long long)N * tx * ty), (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN));     \
+        const dim3 gr((unsigned)((long long)N * tx * ty), (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN));    \
         if (KH <= 3 && KW <= 3)                                                                                   \
-            hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 3>), g, dim3(256), 0, st, a, tx, ty);              \
+            hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 3>), gr, dim3(256), 0, st, a, tx, ty);             \
         else                                                                                                      \
-            hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 7>), g, dim3(256), 0, st, a, tx, ty);              \
+            hipLaunchKernelGGL((fvp::conv_halo_kernel<fvp::TL, 7>), gr, dim3(256), 0, st, a, tx, ty);             \
     } while (0)
         switch (p.halo) {
             case 1: FVP_HALO(TileN16); break;
@@ -740,13 +872,10 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
         return (int)hipGetLastError();
     }
 #define FVP_CONV(TL)                                                                                              \
-    do {                                                                                                          \
-        if (Cpi % fvp::TL::KC) return FVP_ERR_SHAPE;                                                              \
-        hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL>),                                               \
-                           dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                  \
-                                (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN), (unsigned)p.ks),              \
-                           dim3(256), 0, st, a);                                                                 \
-    } while (0)
+    hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL>),                                                          \
+                       dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                      \
+                            (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN), (unsigned)(G * p.ks)),            \
+                       dim3(256), 0, st, a)
     switch (p.tile) {
         case 1: FVP_CONV(TileN16); break;
         case 2: FVP_CONV(TileN16s); break;
@@ -758,37 +887,46 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const floa
     }
 #undef FVP_CONV
     if (p.ks > 1) {
-        const long long tot = M * Ntot;
-        hipLaunchKernelGGL(fvp::conv_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, a, p.ks,
-                           (int)M, Ntot);
+        const long long tot = G * M * Ntot;
+        hipLaunchKernelGGL(fvp::conv_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, a, (int)M,
+                           Ntot);
     }
     return (int)hipGetLastError();
+}
+
+// The stride-1 "same" convolutions and 2x transposed convolutions of the
+// HDN / JLN CNNs (odd kernels, padding (K-1)/2).
+static int legacy_geom(int H, int W, int Cpi, int KH, int KW, int upsample2, ConvGeom &g) {
+    if (Cpi % 16 || (KH & 1) == 0 || (KW & 1) == 0 || upsample2 < 0 || upsample2 > 2) return FVP_ERR_SHAPE;
+    return conv_geom(H, W, Cpi, KH, KW, upsample2, 1, 1, (KH - 1) / 2, (KW - 1) / 2, g);
 }
 }  // namespace fvp
 
 extern "C" int fvp_conv2d_nhwc(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                                int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                                const float *res_post, int relu, int upsample2, float *out, void *stream) {
-    return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
-                            upsample2, out, FVP_CONV_AUTO, nullptr, 0, stream);
+    return fvp_conv2d_nhwc_ws(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
+                              upsample2, out, FVP_CONV_AUTO, nullptr, 0, stream);
 }
 
 extern "C" size_t fvp_conv2d_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int upsample2,
                                              int algo) {
-    if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || upsample2 < 0 || upsample2 > 2)
-        return 0;
-    if (algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return 0;
-    const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
-    const fvp::ConvPlan p = fvp::conv_plan(N, H, W, Cpi, KH, KW, Ntot, upsample2, algo);
-    return p.ks > 1 ? (size_t)p.ks * N * H * W * Ntot * sizeof(float) : 0;
+    fvp::ConvGeom g;
+    if (N <= 0 || Cpo <= 0 || Cpo % 16 || algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return 0;
+    if (fvp::legacy_geom(H, W, Cpi, KH, KW, upsample2, g) != FVP_OK) return 0;
+    return fvp::conv_ws_bytes(N, Cpi, KH, KW, Cpo, g, algo);
 }
 
 extern "C" int fvp_conv2d_nhwc_ws(const float *in, int N, int H, int W, int Cpi, const float *wpack, int KH, int KW,
                                   int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                                   const float *res_post, int relu, int upsample2, float *out, int algo,
                                   void *workspace, size_t workspace_bytes, void *stream) {
-    return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
-                            upsample2, out, algo, workspace, workspace_bytes, stream);
+    if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
+    fvp::ConvGeom g;
+    const int st = fvp::legacy_geom(H, W, Cpi, KH, KW, upsample2, g);
+    if (st != FVP_OK) return st;
+    return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu, g,
+                            out, 0, algo, workspace, workspace_bytes, stream);
 }
 
 extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH,
@@ -796,31 +934,54 @@ extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cp
                                     const float *res_pre, const float *res_post, int relu, int upsample2, float *out,
                                     void *stream) {
     if (!in || !wpack_bf16 || !scale || !shift || !out) return FVP_ERR_NULL;
-    if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 16 || KH <= 0 || KW <= 0 ||
-        (KH & 1) == 0 || (KW & 1) == 0)
-        return FVP_ERR_SHAPE;
-    if (upsample2 < 0 || upsample2 > 2) return FVP_ERR_SHAPE;
-    const int Ntot = (upsample2 == 1 ? 4 : upsample2 == 2 ? 2 : 1) * Cpo;
-    if (Cpo_w < Ntot || Cpo_w % 128) return FVP_ERR_SHAPE;
-    const long long M = (long long)N * H * W;
-    fvp::ConvArgs a{in,  nullptr, scale, shift, res_pre, res_post, out,       N,   H, W, Cpi, KH, KW, Cpo, Cpo_w,
-                    relu, upsample2, nullptr};
-    const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack_bf16);
-    hipStream_t st = (hipStream_t)stream;
-#define FVP_CONVB(BM, BN, WR, KC)                                                                                 \
-    hipLaunchKernelGGL((fvp::conv_bf16_kernel<fvp::TileB<BM, BN, WR, KC>>),                                      \
-                       dim3((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN)), dim3(256), 0, st, a, \
-                       wb)
-    const bool k32 = Cpi % 32 == 0;
-    const long long b128 = ((M + 127) / 128) * ((Ntot + 63) / 64);
-    if (Ntot <= 32) {
-        if (k32) FVP_CONVB(128, 32, 4, 32); else FVP_CONVB(128, 32, 4, 16);
-    } else if (b128 >= 512) {
-        if (k32) FVP_CONVB(128, 64, 2, 32); else FVP_CONVB(128, 64, 2, 16);
-    } else {
-        if (k32) FVP_CONVB(64, 64, 2, 32); else FVP_CONVB(64, 64, 2, 16);
+    fvp::ConvGeom g;
+    const int st = fvp::legacy_geom(H, W, Cpi, KH, KW, upsample2, g);
+    if (st != FVP_OK) return st;
+    return fvp::conv_launch(in, N, H, W, Cpi, wpack_bf16, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
+                            g, out, 1, FVP_CONV_AUTO, nullptr, 0, stream);
+}
+
+extern "C" int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px,
+                               int *out_hw) {
+    fvp::ConvGeom g;
+    const int st = fvp::conv_geom(H, W, Cpi, KH, KW, mode, sy, sx, py, px, g);
+    if (st == FVP_OK && out_hw) {
+        out_hw[0] = g.Ho;
+        out_hw[1] = g.Wo;
     }
-#undef FVP_CONVB
+    return st;
+}
+
+extern "C" size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int mode,
+                                                int sy, int sx, int py, int px, int algo) {
+    fvp::ConvGeom g;
+    if (N <= 0 || Cpo <= 0 || Cpo % 16 || algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return 0;
+    if (fvp::conv_geom(H, W, Cpi, KH, KW, mode, sy, sx, py, px, g) != FVP_OK) return 0;
+    return fvp::conv_ws_bytes(N, Cpi, KH, KW, Cpo, g, algo);
+}
+
+extern "C" int fvp_conv2d_nhwc_ex(const float *in, int N, int H, int W, int Cpi, const void *wpack, int KH, int KW,
+                                  int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                                  const float *res_post, int relu, int mode, int sy, int sx, int py, int px,
+                                  int bf16, int algo, float *out, void *workspace, size_t workspace_bytes,
+                                  void *stream) {
+    if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
+    fvp::ConvGeom g;
+    const int st = fvp::conv_geom(H, W, Cpi, KH, KW, mode, sy, sx, py, px, g);
+    if (st != FVP_OK) return st;
+    return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu, g,
+                            out, bf16 ? 1 : 0, algo, workspace, workspace_bytes, stream);
+}
+
+extern "C" int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int S, int P, float *out,
+                                    void *stream) {
+    if (!in || !out) return FVP_ERR_NULL;
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 || K < 1 || S < 1 || P < 0 || 2 * P > K) return FVP_ERR_SHAPE;
+    if (H + 2 * P < K || W + 2 * P < K) return FVP_ERR_SHAPE;
+    const int Ho = (H + 2 * P - K) / S + 1, Wo = (W + 2 * P - K) / S + 1;
+    const long long total = (long long)N * Ho * Wo * (C / 4);
+    hipLaunchKernelGGL(fvp::maxpool_pad_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, in, out, N, H, W, C, K, S, P, Ho, Wo);
     return (int)hipGetLastError();
 }
 

@@ -54,7 +54,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
                                                        int H, int W, int X, int Y, int Z, int cols, int col_blocks,
-                                                       int SP, int band) {
+                                                       int SP, int band, unsigned pixb) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
@@ -100,7 +100,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     }
     // per-camera image of this frame group in the workspace: each pixel / pair
     // entry holds the NF frames' copies back to back (one 128-B line at NF = 2)
-    const unsigned pix = PAIR ? 64u : JP * 4u;  // bytes of one frame's pixel / pair entry
+    const unsigned pix = PAIR ? 64u : pixb;  // bytes of one frame's pixel (>= JP*4) / pair entry
     const unsigned unit = pix * NF;             // bytes per entry
     const unsigned img = (PAIR ? (unsigned)(H * (W + 1)) : (unsigned)(H * W)) * unit;  // bytes per camera
     const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
@@ -266,10 +266,10 @@ __global__ __launch_bounds__(256, NF == 1 ? 8 : 5) void voxelize_kernel(const vo
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int H, int W, int X, int Y, int Z, int cols,
-                                                          int col_blocks, int SP, int band) {
+                                                          int col_blocks, int SP, int band, unsigned pixb) {
     static_assert(!OTF, "grid kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
-                                  band);
+                                  band, pixb);
 }
 
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
@@ -277,10 +277,10 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
                                                             const int32_t *__restrict__ grid_index, int frame0,
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
                                                             int J, int H, int W, int X, int Y, int Z, int cols,
-                                                            int col_blocks, int SP, int band) {
+                                                            int col_blocks, int SP, int band, unsigned pixb) {
     static_assert(OTF, "on-the-fly kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
-                                  band);
+                                  band, pixb);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -323,6 +323,52 @@ static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     return (int)c;
 }
 
+// Gather launch shape for `frames` frames per launch (NF per table entry).
+struct GatherCfg {
+    int cols, band, col_blocks, SP;
+    size_t lds;
+};
+
+template <int LPV, bool OTF>
+static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg &c) {
+    // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
+    int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
+    // latency (few frames): one pass of 256/LPV voxels per block, so a single
+    // frame spreads over enough blocks to fill the CUs
+    if ((long long)frames / NF * ((X * Y + cols - 1) / cols) < 4 * 256) cols = max(1, (256 / LPV) / Z);
+    // Column groups that tile the x-rows exactly (largest divisor of Y, if it
+    // keeps at least half the columns), so the blocks can be walked in bands of
+    // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
+    // x-y patch, whose heatmap footprint is smaller (C5 -8 %, C4 -4 %, C2 0).
+    // Small grids (C1: 400 columns) keep their column groups (measured -6 % with bands).
+    const bool big = (long long)X * Y >= 4096;
+    if (big) {
+        int cc = cols;
+        while (cc > 1 && Y % cc != 0) --cc;
+        if (2 * cc >= cols) cols = cc;
+    }
+    c.cols = cols;
+    c.band = (big && Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
+    c.col_blocks = (X * Y + cols - 1) / cols;
+    c.SP = stage_pitch(LPV, cols, Z);
+    c.lds = (size_t)NF * 4 * LPV * c.SP * sizeof(float);
+    if (OTF) c.lds = ((c.lds / 4 + 3) & ~(size_t)3) * 4 + (size_t)FVP_GRID_SLOTS(V) * FVP_CAM_STRIDE * sizeof(float);
+    return c.lds > 160 * 1024 ? FVP_ERR_SHAPE : FVP_OK;
+}
+
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
+static void launch_gather(const void *tab, int f0, int nb, const GatherCfg &c, const CoordSource &src,
+                          const int32_t *grid_index, int V, int J, int H, int W, int X, int Y, int Z, float *cube,
+                          float *xy, unsigned pixb, hipStream_t s) {
+    const dim3 grid((unsigned)(nb / NF * c.col_blocks));
+    if constexpr (OTF)
+        hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
+                           grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band, pixb);
+    else
+        hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
+                           grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band, pixb);
+}
+
 // Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
 // layout pass into the workspace, then the gather, NF frames per table entry.
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, typename T>
@@ -331,28 +377,8 @@ static int run_chunks(const T *hm, int first, int last, int V, int J, int H, int
     const bool half = sizeof(T) == 2;
     const int B = last - first;
     const int chunk = max(NF, chunk_frames(B, V, J, H, W, half) / NF * NF);
-    // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
-    int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
-    // latency (few frames): one pass of 256/LPV voxels per block, so a single
-    // frame spreads over enough blocks to fill the CUs
-    if ((long long)min(chunk, B) / NF * ((X * Y + cols - 1) / cols) < 4 * 256) cols = max(1, (256 / LPV) / Z);
-    // Column groups that tile the x-rows exactly (largest divisor of Y, if it
-    // keeps at least half the columns), so the blocks can be walked in bands of
-    // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
-    // x-y patch, whose heatmap footprint is smaller (C5 -8 %, C4 -4 %, C2 0).
-    // Small grids (C1: 400 columns) keep their column groups (measured -6 % with bands).
-    const bool big = (long long)X * Y >= 4096;
-    if (big) {
-        int c = cols;
-        while (c > 1 && Y % c != 0) --c;
-        if (2 * c >= cols) cols = c;
-    }
-    const int band = (big && Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
-    const int col_blocks = (X * Y + cols - 1) / cols;
-    const int SP = stage_pitch(LPV, cols, Z);
-    size_t lds = (size_t)NF * 4 * LPV * SP * sizeof(float);
-    if (OTF) lds = ((lds / 4 + 3) & ~(size_t)3) * 4 + (size_t)FVP_GRID_SLOTS(V) * FVP_CAM_STRIDE * sizeof(float);
-    if (lds > 160 * 1024) return FVP_ERR_SHAPE;
+    GatherCfg c;
+    if (gather_cfg<LPV, OTF>(min(chunk, B), NF, V, X, Y, Z, c) != FVP_OK) return FVP_ERR_SHAPE;
     const size_t frame_elems = (size_t)V * J * H * W;
     for (int f0 = first; f0 < last; f0 += chunk) {
         const int nb = min(chunk, last - f0);
@@ -365,15 +391,33 @@ static int run_chunks(const T *hm, int first, int last, int V, int J, int H, int
         } else {
             launch_layout<LPV, T, NF>(hsrc, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
         }
-        const dim3 grid((unsigned)(nb / NF * col_blocks));
-        if constexpr (OTF)
-            hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), lds, s, ws, src,
-                               grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
-        else
-            hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), lds, s, ws, src,
-                               grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band);
+        launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, grid_index, V, J, H, W, X, Y, Z, cube, xy,
+                                               4u * 4u * LPV, s);
     }
     return (int)hipGetLastError();
+}
+
+// Heatmaps already channels-last ([B][V][H][W][cp] fp32, cp >= JP, e.g. the
+// PoseResNet backbone's NHWC output): the gather reads them in place, one
+// launch for the whole batch, no layout pass and no workspace.
+template <bool OTF, bool CASC>
+static int run_direct(const float *hm_cl, int cp, int B, int V, int J, int H, int W, const CoordSource &src,
+                      const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, hipStream_t s) {
+    const unsigned pixb = (unsigned)cp * 4u;
+    auto go = [&](auto lpv) -> int {
+        constexpr int LPV = decltype(lpv)::value;
+        GatherCfg c;
+        if (gather_cfg<LPV, OTF>(B, 1, V, X, Y, Z, c) != FVP_OK) return FVP_ERR_SHAPE;
+        launch_gather<LPV, false, OTF, CASC, 1>(hm_cl, 0, B, c, src, grid_index, V, J, H, W, X, Y, Z, cube, xy, pixb,
+                                               s);
+        return (int)hipGetLastError();
+    };
+    switch (lanes_per_voxel(J)) {
+        case 1: return go(std::integral_constant<int, 1>{});
+        case 2: return go(std::integral_constant<int, 2>{});
+        case 4: return go(std::integral_constant<int, 4>{});
+        default: return go(std::integral_constant<int, 8>{});
+    }
 }
 
 // Frames per table entry: the fp16 pair table interleaves two frames per
@@ -507,4 +551,45 @@ extern "C" int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, i
                                                  (hipStream_t)stream);
     return fvp::voxelize_any<true, float>(reinterpret_cast<const float *>(heatmaps), B, V, J, H, W, src, grid_index,
                                           X, Y, Z, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int fvp_voxelize_cl(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
+                               const float *packed_grids, const int32_t *grid_index, int X, int Y, int Z, float *cube,
+                               float *xy, void *stream) {
+    const int st = fvp::check_args(heatmaps_cl, B, V, J, H, W, packed_grids, X, Y, Z);
+    if (st != FVP_OK) return st;
+    if (cp < 4 * fvp::lanes_per_voxel(J) || cp % 4) return FVP_ERR_SHAPE;
+    if ((size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets per camera image
+    if (!cube && !xy) return FVP_OK;
+    fvp::CoordSource src{};
+    src.grids = packed_grids;
+    if (V > 16)
+        return fvp::run_direct<false, true>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                            (hipStream_t)stream);
+    return fvp::run_direct<false, false>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                         (hipStream_t)stream);
+}
+
+extern "C" int fvp_voxelize_cl_cams(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
+                                    const float *cams, const int32_t *grid_index, const float *resize_t,
+                                    const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
+                                    void *stream) {
+    if (!cams || !resize_t || !grid || !img) return FVP_ERR_NULL;
+    const int X = grid->bins[0], Y = grid->bins[1], Z = grid->bins[2];
+    const int st = fvp::check_args(heatmaps_cl, B, V, J, H, W, cams, X, Y, Z);
+    if (st != FVP_OK) return st;
+    if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
+    if (cp < 4 * fvp::lanes_per_voxel(J) || cp % 4) return FVP_ERR_SHAPE;
+    if ((size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;
+    if (!cube && !xy) return FVP_OK;
+    fvp::CoordSource src{};
+    src.cams = cams;
+    src.resize_t = resize_t;
+    src.gs = *grid;
+    src.im = *img;
+    if (V > 16)
+        return fvp::run_direct<true, true>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                           (hipStream_t)stream);
+    return fvp::run_direct<true, false>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                        (hipStream_t)stream);
 }

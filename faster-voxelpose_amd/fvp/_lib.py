@@ -48,6 +48,10 @@ SIGNATURES = {
     "fvp_voxelize_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                           ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p, c_void_p, c_void_p,
                           ctypes.c_size_t, c_void_p],
+    "fvp_voxelize_cl": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                        c_void_p, c_void_p, c_void_p],
+    "fvp_voxelize_cl_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                             ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p, c_void_p, c_void_p],
     "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
@@ -71,6 +75,12 @@ SIGNATURES = {
                            c_void_p],
     "fvp_conv2d_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv2d_nhwc_ex": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
+    "fvp_conv2d_ex_workspace_bytes": [c_int] * 13,
+    "fvp_conv2d_geom": [c_int] * 10 + [ctypes.POINTER(c_int)],
+    "fvp_maxpool_pad_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_weight_net": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
@@ -80,7 +90,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _LIB = None
 
 
@@ -102,7 +112,8 @@ def load():
         fn.restype = {"fvp_status_string": c_char_p, "fvp_voxelize_workspace_bytes": ctypes.c_size_t,
                       "fvp_voxelize_f16_workspace_bytes": ctypes.c_size_t,
                       "fvp_person_workspace_bytes": ctypes.c_size_t,
-                      "fvp_conv2d_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
+                      "fvp_conv2d_workspace_bytes": ctypes.c_size_t,
+                      "fvp_conv2d_ex_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
     if lib.fvp_abi_version() != ABI_VERSION:
         raise FvpError(f"fvp: ABI version mismatch ({lib.fvp_abi_version()} != {ABI_VERSION})")
     _LIB = lib

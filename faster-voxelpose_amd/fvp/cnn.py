@@ -19,6 +19,7 @@ one fused launch.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 
 import torch
 import torch.nn as nn
@@ -72,10 +73,13 @@ class Act:
 
 
 class ConvLayer:
-    """A Conv2d / ConvTranspose2d(k=2,s=2) with its following BatchNorm folded.
-    dtype torch.bfloat16: bf16 operands, fp32 accumulation (opt-in precision)."""
+    """A Conv2d / Conv1d / ConvTranspose2d(k=2,s=2) / ConvTranspose2d(k=4,s=2,p=1) /
+    ConvTranspose1d(k=2,s=2) with its following BatchNorm folded (fvp_conv2d_nhwc_ex).
+    Conv2d: any stride 1-4 and zero padding.  cpi: input channel pitch (default
+    Cin rounded up to 16; 4 / 8 / 12 for a network's RGB input).  dtype
+    torch.bfloat16: bf16 operands, fp32 accumulation (opt-in precision)."""
 
-    def __init__(self, conv, bn=None, dtype=torch.float32):
+    def __init__(self, conv, bn=None, dtype=torch.float32, cpi: int | None = None):
         dev = conv.weight.device
         w = conv.weight.detach().float()
         if isinstance(conv, (nn.Conv1d, nn.ConvTranspose1d)):  # 1-D: rows of height 1, kernel (1, k)
@@ -83,35 +87,59 @@ class ConvLayer:
             ks, st, pad = (1,) + tuple(conv.kernel_size), (1,) + tuple(conv.stride), (0,) + tuple(conv.padding)
         else:
             ks, st, pad = tuple(conv.kernel_size), tuple(conv.stride), tuple(conv.padding)
-        self.up2 = 0
+        assert conv.groups == 1 and tuple(conv.dilation) in ((1,), (1, 1)), "grouped / dilated convolutions"
+        self.mode, self.stride, self.pad = 0, (1, 1), (0, 0)
         if isinstance(conv, (nn.ConvTranspose2d, nn.ConvTranspose1d)):
-            self.up2 = 2 if isinstance(conv, nn.ConvTranspose1d) else 1
-            assert ks[1:] == (2,) and st[1:] == (2,) and pad == (0, 0) and ks[0] == st[0] == 3 - self.up2, (ks, st, pad)
-            assert tuple(conv.output_padding) in ((0,), (0, 0)) and conv.groups == 1
+            assert tuple(conv.output_padding) in ((0,), (0, 0)), conv.output_padding
             cin, cout = w.shape[0], w.shape[1]
-            self.KH = self.KW = 1
+            if isinstance(conv, nn.ConvTranspose1d):
+                assert ks == (1, 2) and st == (1, 2) and pad == (0, 0), (ks, st, pad)
+                self.mode = 2
+            elif ks == (2, 2) and st == (2, 2) and pad == (0, 0):
+                self.mode = 1
+            elif ks == (4, 4) and st == (2, 2) and pad == (1, 1):  # resnet.py:147-158 kernel 4
+                self.mode = 3
+            else:
+                raise _lib.FvpError(f"ConvTranspose2d kernel {ks} stride {st} padding {pad}: "
+                                    "kernels (2, s2, p0) and (4, s2, p1) are supported")
+            self.KH = self.KW = 2 if self.mode == 3 else 1
         else:
-            assert st == (1, 1) and conv.groups == 1 and tuple(conv.dilation) in ((1,), (1, 1))
             cout, cin, kh, kw = w.shape
-            assert pad == ((kh - 1) // 2, (kw - 1) // 2) and kh % 2 == 1 and kw % 2 == 1, (pad, kh, kw)
             self.KH, self.KW = kh, kw
+            self.stride, self.pad = (st[0], st[1]), (pad[0], pad[1])
+            if not (1 <= st[0] <= 4 and 1 <= st[1] <= 4 and 0 <= pad[0] < kh and 0 <= pad[1] < kw):
+                raise _lib.FvpError(f"Conv kernel {ks} stride {st} padding {pad} out of range")
         self.Cin, self.Cout = cin, cout
-        self.Cpi, self.Cpo = _rup(cin, 16), _rup(cout, 16)
-        self.nq = (1, 4, 2)[self.up2]  # outputs per input pixel
+        if cpi is None:
+            cpi = _rup(cin, 16)
+        assert cpi >= cin and cpi % 4 == 0 and (cpi < 16 or cpi % 16 == 0), cpi
+        self.Cpi, self.Cpo = cpi, _rup(cout, 16)
+        self.nq = (1, 4, 2, 1)[self.mode]  # GEMM columns per output channel
+        self.G = 4 if self.mode == 3 else 1  # parity groups
         self.Cpo_w = _rup(self.nq * self.Cpo, 128)
         taps = self.KH * self.KW
-        pack = torch.zeros((taps, self.Cpi, self.Cpo_w), dtype=torch.float32, device=dev)
-        if self.up2:  # n = (dy*2+dx)*Cpo + co (2-D) or dx*Cpo + co (1-D)  <-  W[ci][co][dy][dx]
+        krows = _rup(taps * self.Cpi, 16)
+        pack = torch.zeros((self.G, taps, self.Cpi, self.Cpo_w), dtype=torch.float32, device=dev)
+        if self.mode in (1, 2):  # n = (dy*2+dx)*Cpo + co (2-D) or dx*Cpo + co (1-D)  <-  W[ci][co][dy][dx]
             for q in range(self.nq):
-                dy, dx = (q >> 1, q & 1) if self.up2 == 1 else (0, q)
-                pack[0, :cin, q * self.Cpo:q * self.Cpo + cout] = w[:, :, dy, dx]
+                dy, dx = (q >> 1, q & 1) if self.mode == 1 else (0, q)
+                pack[0, 0, :cin, q * self.Cpo:q * self.Cpo + cout] = w[:, :, dy, dx]
+        elif self.mode == 3:  # group (ry, rx), tap (i, j) <- W[ci][co][3-2i-ry][3-2j-rx]
+            for g in range(4):
+                ry, rx = g >> 1, g & 1
+                for i in range(2):
+                    for j in range(2):
+                        pack[g, i * 2 + j, :cin, :cout] = w[:, :, 3 - 2 * i - ry, 3 - 2 * j - rx]
         else:  # row (ky*KW+kx)*Cpi + ci  <-  W[co][ci][ky][kx]
-            pack[:, :cin, :cout] = w.permute(2, 3, 1, 0).reshape(taps, cin, cout)
-        self.wpack = pack.reshape(taps * self.Cpi, self.Cpo_w).contiguous()
+            pack[0, :, :cin, :cout] = w.permute(2, 3, 1, 0).reshape(taps, cin, cout)
+        pack = pack.reshape(self.G, taps * self.Cpi, self.Cpo_w)
+        if krows > taps * self.Cpi:  # K rounded up to whole 16-row chunks (zero rows)
+            pack = torch.cat([pack, pack.new_zeros((self.G, krows - taps * self.Cpi, self.Cpo_w))], dim=1)
+        self.wpack = pack.contiguous()
         self._ws = {}  # (N, H, W, algo) -> split-K scratch bytes
-        self.bf16 = dtype == torch.bfloat16
-        if self.bf16:  # [Cpo_w][K], k contiguous
-            self.wpack_bf16 = self.wpack.t().contiguous().to(torch.bfloat16)
+        self.bf16 = dtype == torch.bfloat16 and self.Cpi % 16 == 0  # an RGB stem stays fp32
+        if self.bf16:  # [G][Cpo_w][K], k contiguous
+            self.wpack_bf16 = pack[:, :taps * self.Cpi].transpose(1, 2).contiguous().to(torch.bfloat16)
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
         if bn is not None:  # eval BatchNorm: (x - mean) / sqrt(var + eps) * gamma + beta
             s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
@@ -123,33 +151,44 @@ class ConvLayer:
         self.scale[:cout] = scale
         self.shift[:cout] = shift
 
-    def __call__(self, x: Act, relu: bool, res_pre: Act | None = None, res_post: Act | None = None) -> Act:
+    def geom(self) -> tuple:
+        return (self.mode, self.stride[0], self.stride[1], self.pad[0], self.pad[1])
+
+    def out_hw(self, H: int, W: int) -> tuple[int, int]:
+        hw = (ctypes.c_int * 2)()
+        _lib.check(_lib.load().fvp_conv2d_geom(H, W, self.Cpi, self.KH, self.KW, *self.geom(), hw),
+                   f"conv geometry {H}x{W}")
+        return hw[0], hw[1]
+
+    def __call__(self, x: Act, relu: bool, res_pre: Act | None = None, res_post: Act | None = None,
+                 out: torch.Tensor | None = None) -> Act:
+        """out: optional preallocated [N, Ho, Wo, Cpo] fp32 destination (e.g. a slice of a larger buffer)."""
         assert x.Cp == self.Cpi, (x.Cp, self.Cpi)
-        Ho, Wo = (2 * x.H if self.up2 == 1 else x.H), (2 * x.W if self.up2 else x.W)
-        out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=torch.float32, device=x.t.device)
+        Ho, Wo = self.out_hw(x.H, x.W)
+        if out is None:
+            out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=torch.float32, device=x.t.device)
+        assert tuple(out.shape) == (x.N, Ho, Wo, self.Cpo) and out.is_contiguous(), (tuple(out.shape), Ho, Wo)
         for r in (res_pre, res_post):
             assert r is None or tuple(r.t.shape) == tuple(out.shape), (None if r is None else r.t.shape, out.shape)
-        args = (_ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wpack_bf16 if self.bf16 else self.wpack), self.KH, self.KW,
-                self.Cpo, self.Cpo_w, _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
-                _ptr(res_post.t) if res_post else None, int(relu), self.up2, _ptr(out))
-        if self.bf16:
-            _lib.call("fvp_conv2d_nhwc_bf16", *args, _stream(out))
-        else:  # split-K scratch for under-filled launches (0 bytes: the layer does not split)
-            # allocated per call: the caching allocator is stream-ordered, so two
-            # streams running this layer never share partial sums
-            key = (x.N, x.H, x.W, CONV_ALGO)
-            if key not in self._ws:
-                self._ws[key] = _lib.load().fvp_conv2d_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW,
-                                                                        self.Cpo, self.up2, CONV_ALGO)
-            nws = self._ws[key]
-            ws = torch.empty(((nws + 3) // 4,), dtype=torch.float32, device=out.device) if nws else None
-            _lib.call("fvp_conv2d_nhwc_ws", *args, CONV_ALGO, _ptr(ws) if ws is not None else None, nws,
-                      _stream(out))
+        key = (x.N, x.H, x.W, CONV_ALGO)
+        if key not in self._ws:  # split-K scratch for under-filled launches (0 bytes: the layer does not split)
+            self._ws[key] = 0 if self.bf16 else _lib.load().fvp_conv2d_ex_workspace_bytes(
+                x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo, *self.geom(), CONV_ALGO)
+        nws = self._ws[key]
+        # allocated per call: the caching allocator is stream-ordered, so two
+        # streams running this layer never share partial sums
+        ws = torch.empty(((nws + 3) // 4,), dtype=torch.float32, device=out.device) if nws else None
+        _lib.call("fvp_conv2d_nhwc_ex", _ptr(x.t), x.N, x.H, x.W, x.Cp,
+                  _ptr(self.wpack_bf16 if self.bf16 else self.wpack), self.KH, self.KW, self.Cpo, self.Cpo_w,
+                  _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
+                  _ptr(res_post.t) if res_post else None, int(relu), *self.geom(), int(self.bf16), CONV_ALGO,
+                  _ptr(out), _ptr(ws), nws, _stream(out))
         return Act(out, self.Cout)
 
     def flops(self, x: Act) -> int:
-        n = self.nq * self.Cout
-        return 2 * x.N * x.H * x.W * n * self.Cin * self.KH * self.KW
+        Ho, Wo = self.out_hw(x.H, x.W)
+        rows = x.N * (x.H * x.W if self.mode else Ho * Wo)  # GEMM rows (row grid) per parity group
+        return 2 * rows * self.G * self.nq * self.Cout * self.Cin * self.KH * self.KW
 
 
 def maxpool2(x: Act, dim: int = 2) -> Act:
@@ -160,10 +199,19 @@ def maxpool2(x: Act, dim: int = 2) -> Act:
     return Act(out, x.C)
 
 
-def to_nhwc(x: torch.Tensor) -> Act:
+def maxpool_pad(x: Act, k: int, s: int, p: int) -> Act:
+    """MaxPool2d(k, s, p) with -inf padding (resnet.py:109)."""
+    Ho, Wo = (x.H + 2 * p - k) // s + 1, (x.W + 2 * p - k) // s + 1
+    out = torch.empty((x.N, Ho, Wo, x.Cp), dtype=torch.float32, device=x.t.device)
+    _lib.call("fvp_maxpool_pad_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, k, s, p, _ptr(out), _stream(out))
+    return Act(out, x.C)
+
+
+def to_nhwc(x: torch.Tensor, cp: int | None = None) -> Act:
+    """NCHW -> NHWC with cp channels (default C rounded up to 16; zero padded)."""
     x = x.float().contiguous()
     N, C, H, W = x.shape
-    out = torch.empty((N, H, W, _rup(C, 16)), dtype=torch.float32, device=x.device)
+    out = torch.empty((N, H, W, cp if cp is not None else _rup(C, 16)), dtype=torch.float32, device=x.device)
     _lib.call("fvp_nchw_to_nhwc", _ptr(x), N, C, H, W, out.shape[3], _ptr(out), _stream(out))
     return Act(out, C)
 

@@ -56,6 +56,18 @@ def make_cfg(w, device: str = "cuda:0") -> AttrDict:
     })
 
 
+def resnet_cfg(num_layers: int = 50, num_joints: int = 15, deconv_filters=(256, 256, 256),
+               deconv_kernels=(4, 4, 4), final_kernel: int = 1, deconv_with_bias: bool = False) -> AttrDict:
+    """The RESNET / DATASET keys resnet.get(cfg) reads (lib/core/config.py:101-107
+    defaults: ResNet-50, three 256-filter kernel-4 deconvolutions, a 1x1 final conv)."""
+    return AttrDict.wrap({
+        "RESNET": {"NUM_LAYERS": num_layers, "DECONV_WITH_BIAS": deconv_with_bias,
+                   "NUM_DECONV_LAYERS": len(deconv_filters), "NUM_DECONV_FILTERS": list(deconv_filters),
+                   "NUM_DECONV_KERNELS": list(deconv_kernels), "FINAL_CONV_KERNEL": final_kernel},
+        "DATASET": {"NUM_JOINTS": num_joints},
+    })
+
+
 def load_yaml(path: str, device: str | None = None) -> AttrDict:
     import yaml
 

@@ -155,6 +155,8 @@ def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Option
     gi = None
     if grid_index is not None:
         gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
+        if gi.numel() != B:
+            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
     if B == 0:  # an empty batch: the reference's loop over frames yields empty outputs
@@ -184,6 +186,88 @@ def _(heatmaps, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
     B, V, J = heatmaps.shape[:3]
     return (heatmaps.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
             heatmaps.new_empty((B, J, X, Y) if want_xy else (0,)))
+
+
+def _cl_input(heatmaps_cl: torch.Tensor, J: int) -> torch.Tensor:
+    if heatmaps_cl.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps_cl.device}")
+    if heatmaps_cl.dim() != 5 or heatmaps_cl.dtype != torch.float32 or heatmaps_cl.shape[4] < J:
+        raise _lib.FvpError(f"fvp: channels-last heatmaps must be fp32 [B,V,H,W,Cp>=J], got "
+                            f"{tuple(heatmaps_cl.shape)} {heatmaps_cl.dtype}")
+    return heatmaps_cl.contiguous()
+
+
+@torch.library.custom_op("fvp::voxelize_cl", mutates_args=(), device_types="cuda")
+def voxelize_cl(heatmaps_cl: torch.Tensor, J: int, packed_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
+                X: int, Y: int, Z: int, want_cube: bool, want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """voxelize on channels-last heatmaps [B,V,H,W,Cp] (joints in channels 0..J-1): no layout pass."""
+    hm = _cl_input(heatmaps_cl, J)
+    pg = _dev_f32(packed_grids, "packed_grids")
+    B, V, H, W, cp = hm.shape
+    N = X * Y * Z
+    if pg.dim() == 3:
+        pg = pg.unsqueeze(0)
+    if pg.shape[1:] != (N, grid_slots(V), 2):
+        raise _lib.FvpError(f"fvp: packed grid {tuple(pg.shape)} does not match V={V}, N={N}")
+    gi = None
+    if grid_index is not None:
+        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
+        if gi.numel() != B:
+            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
+    xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
+    if B == 0:
+        return cube, xy
+    _lib.call("fvp_voxelize_cl", _ptr(hm), cp, B, V, J, H, W, _ptr(pg), _ptr(gi), X, Y, Z,
+              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _stream(hm))
+    return cube, xy
+
+
+@voxelize_cl.register_fake
+def _(heatmaps_cl, J, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
+    B = heatmaps_cl.shape[0]
+    return (heatmaps_cl.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
+            heatmaps_cl.new_empty((B, J, X, Y) if want_xy else (0,)))
+
+
+@torch.library.custom_op("fvp::voxelize_cl_cams", mutates_args=(), device_types="cuda")
+def voxelize_cl_cams(heatmaps_cl: torch.Tensor, J: int, cams: torch.Tensor, grid_index: Optional[torch.Tensor],
+                     resize_t: torch.Tensor, start: list[float], end: list[float], center: list[float],
+                     bins: list[int], ori_max: float, img_w: float, img_h: float, want_cube: bool,
+                     want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """voxelize_cams on channels-last heatmaps [B,V,H,W,Cp]."""
+    hm = _cl_input(heatmaps_cl, J)
+    cm = _dev_f32(cams, "cams")
+    rt = _dev_f32(resize_t, "resize_transform")
+    B, V, H, W, cp = hm.shape
+    if cm.dim() == 2:
+        cm = cm.unsqueeze(0)
+    if cm.shape[1] != V:
+        raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
+    X, Y, Z = bins
+    gi = None
+    if grid_index is not None:
+        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
+        if gi.numel() != B:
+            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
+    xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
+    if B == 0:
+        return cube, xy
+    g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
+    im = ImageSpec(ori_max, img_w, img_h, W, H)
+    _lib.call("fvp_voxelize_cl_cams", _ptr(hm), cp, B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im,
+              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _stream(hm))
+    return cube, xy
+
+
+@voxelize_cl_cams.register_fake
+def _(heatmaps_cl, J, cams, grid_index, resize_t, start, end, center, bins, ori_max, img_w, img_h, want_cube,
+      want_xy):
+    B = heatmaps_cl.shape[0]
+    X, Y, Z = bins
+    return (heatmaps_cl.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
+            heatmaps_cl.new_empty((B, J, X, Y) if want_xy else (0,)))
 
 
 # ---------------------------------------------------------------------------

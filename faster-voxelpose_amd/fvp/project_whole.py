@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from . import geometry, ops
+from .heatmaps import channels_last_of
 
 # Above this size a packed grid streams from HBM once per frame (MI355X: 4 MB
 # L2 per XCD, 256 MB Infinity Cache) and the coordinates are projected on the
@@ -148,25 +149,34 @@ class ProjectLayer(nn.Module):
             self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
 
     def forward_fused(self, heatmaps, meta, cameras, resize_transform, want_cube=True, want_xy=True):
-        """One launch for the whole batch: (cube[B,J,X,Y,Z] or empty, xy[B,J,X,Y] or empty)."""
+        """One launch for the whole batch: (cube[B,J,X,Y,Z] or empty, xy[B,J,X,Y] or empty).
+
+        heatmaps: [B,V,J,H,W] tensor, or fvp.heatmaps.ChannelsLastHeatmaps (or a
+        tensor carrying one, fvp.heatmaps.attach) -- then the gather reads the
+        channels-last copy in place (fvp_voxelize_cl), bit-identical results."""
         ops.forward_only(heatmaps)
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         if heatmaps.shape[0] == 0:  # empty batch: the reference's frame loop yields empty outputs
             return self._empty(heatmaps, X, want_cube, want_xy)
+        cl = channels_last_of(heatmaps)
         if self._project_on_the_fly(heatmaps.shape[1]):
             cams, index = self._cams_for_batch(heatmaps, meta, cameras)
             start, end, center, nb = self.grid_spec()
-            return ops.voxelize_cams(heatmaps, cams, index, resize_transform.to(device=heatmaps.device,
-                                                                                dtype=torch.float32),
-                                     start, end, center, nb, float(max(self.ori_image_size[0], self.ori_image_size[1])),
-                                     float(self.image_size[0]), float(self.image_size[1]), want_cube, want_xy)
+            rt = resize_transform.to(device=heatmaps.device, dtype=torch.float32)
+            geo = (start, end, center, nb, float(max(self.ori_image_size[0], self.ori_image_size[1])),
+                   float(self.image_size[0]), float(self.image_size[1]), want_cube, want_xy)
+            if cl is not None:
+                return ops.voxelize_cl_cams(cl.t, cl.J, cams, index, rt, *geo)
+            return ops.voxelize_cams(heatmaps, cams, index, rt, *geo)
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
+        if cl is not None:
+            return ops.voxelize_cl(cl.t, cl.J, grids, index, X, Y, Z, want_cube, want_xy)
         return ops.voxelize(heatmaps, grids, index, X, Y, Z, want_cube, want_xy)
 
     def _empty(self, heatmaps, X, want_cube, want_xy):
         _, Y, Z = _as_list3(self.voxels_per_axis, int)
         J = heatmaps.shape[2]
-        f = dict(dtype=torch.float32, device=heatmaps.device)
+        f = dict(dtype=torch.float32, device=heatmaps.device)  # (a tensor or ChannelsLastHeatmaps)
         return (torch.zeros((0, J, X, Y, Z) if want_cube else (0,), **f),
                 torch.zeros((0, J, X, Y) if want_xy else (0,), **f))
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 7
+#define FVP_ABI_VERSION 8
 #define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
 /* Cameras per frame: torch's CPU mean over the views (the sum order every
  * kernel reproduces) folds blocks of 16 into a second accumulator, and past
@@ -133,6 +133,20 @@ int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H
                       const float *cams, const int32_t *grid_index, const float *resize_t,
                       const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
                       void *workspace, size_t workspace_bytes, void *stream);
+
+/* fvp_voxelize / fvp_voxelize_cams on heatmaps that are already channels-last,
+ * [B][V][H][W][cp] fp32 with cp >= 4*ceil(J/4) rounded to {4, 8, 16, 32} and
+ * cp % 4 == 0 (joints j < J in channels 0..J-1, the rest ignored) -- the NHWC
+ * output of the PoseResNet backbone's final layer (fvp.backbone; resnet.py:122-128,
+ * "emit heatmaps directly in the kernel's channels-last
+ * layout, removing a transpose pass").  Same results bit for bit as the planar
+ * entry points on the same values; no layout pass, no workspace, one launch. */
+int fvp_voxelize_cl(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
+                    const float *packed_grids, const int32_t *grid_index, int X, int Y, int Z, float *cube,
+                    float *xy, void *stream);
+int fvp_voxelize_cl_cams(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W, const float *cams,
+                         const int32_t *grid_index, const float *resize_t, const fvp_grid_spec *grid,
+                         const fvp_image_spec *img, float *cube, float *xy, void *stream);
 
 /* Peak NMS + top-K on a [B,1,X,Y] map: 3x3 max-pool keep mask, top-K of the
  * masked map (value descending, flat index ascending on ties), and
@@ -277,6 +291,38 @@ int fvp_conv2d_nhwc_ws(const float *in, int N, int H, int W, int Cpi, const floa
 int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const void *wpack_bf16, int KH, int KW,
                          int Cpo, int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                          const float *res_post, int relu, int upsample2, float *out, void *stream);
+/* Generalised convolution geometry (same kernels), for the PoseResNet heatmap
+ * backbone (lib/models/resnet.py:98-201, called at faster_voxelpose.py:73-75;
+ * SURVEY.md §8(f) rank 4) as well as the CNNs above:
+ *   mode 0  Conv2d with stride (sy, sx) in 1..4 and zero padding (py, px) < K
+ *           (any KH, KW): output Ho = (H + 2py - KH)/sy + 1, Wo likewise
+ *           (resnet.py:105 7x7/s2/p3, :64 3x3/s2/p1, :134 1x1/s2, :62/:67 1x1);
+ *   mode 1  ConvTranspose2d(k=2, s=2)  (upsample2 == 1 above)
+ *   mode 2  ConvTranspose1d(k=2, s=2)  (upsample2 == 2 above)
+ *   mode 3  ConvTranspose2d(k=4, s=2, p=1, output_padding 0) (resnet.py:173-180,
+ *           NUM_DECONV_KERNELS = 4): Ho = 2H, Wo = 2W, as four 2x2 convolutions
+ *           over the input grid, one per output parity g = ry*2 + rx; KH = KW = 2,
+ *           wpack [4][Krows][Cpo_w] with row (i*2+j)*Cpi+ci of group g holding
+ *           W[ci][co][3-2i-ry][3-2j-rx]; sy, sx, py, px are ignored.
+ *   in     device [N][H][W][Cpi]: Cpi % 16 == 0, or Cpi in {4, 8, 12} (an RGB
+ *          input padded to 4 channels; a K chunk then spans several taps)
+ *   wpack  fp32: [G][Krows][Cpo_w], Krows = KH*KW*Cpi rounded up to 16 (zero
+ *          rows), G = 4 for mode 3 else 1;  bf16 != 0: bf16 [G][Cpo_w][KH*KW*Cpi]
+ *          (Cpi % 16 == 0, no split-K)
+ *   out    device [N][Ho][Wo][Cpo];  res_pre / res_post likewise or NULL
+ *   algo   FVP_CONV_* (the halo kernel serves stride-1 "same" fp32 convolutions);
+ *   workspace as fvp_conv2d_nhwc_ws, sized by fvp_conv2d_ex_workspace_bytes. */
+int fvp_conv2d_nhwc_ex(const float *in, int N, int H, int W, int Cpi, const void *wpack, int KH, int KW, int Cpo,
+                       int Cpo_w, const float *scale, const float *shift, const float *res_pre,
+                       const float *res_post, int relu, int mode, int sy, int sx, int py, int px, int bf16,
+                       int algo, float *out, void *workspace, size_t workspace_bytes, void *stream);
+size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int mode, int sy,
+                                     int sx, int py, int px, int algo);
+/* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
+int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
+/* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf
+ * padding, NaN-propagating (resnet.py:109: 3, 2, 1).  Ho = (H + 2P - K)/S + 1. */
+int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int S, int P, float *out, void *stream);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
 int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);
 /* KH x KW / stride-(KH, KW) max pool, KH, KW in {1, 2} (floor); KH = 1, KW = 2

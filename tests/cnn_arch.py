@@ -197,3 +197,87 @@ class WeightNet(nn.Module):
         x = x.view(b * j, 1, self.voxels_per_axis[0], self.voxels_per_axis[1])
         x = F.adaptive_avg_pool2d(self.heatmap_feature_net(x), 1).view(b * j, -1)
         return self.output(x).view(b, j, 1)
+
+
+# ---- PoseResNet (lib/models/resnet.py:19-215), same attribute names ------------------
+def _bn(c):
+    return nn.BatchNorm2d(c, momentum=0.1)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, planes, 3, stride, 1, bias=False)
+        self.bn1 = _bn(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = _bn(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample, self.stride = downsample, stride
+
+    def forward(self, x):
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return self.relu(y + (x if self.downsample is None else self.downsample(x)))
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, planes, 1, bias=False)
+        self.bn1 = _bn(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = _bn(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = _bn(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample, self.stride = downsample, stride
+
+    def forward(self, x):
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.relu(self.bn2(self.conv2(y)))
+        y = self.bn3(self.conv3(y))
+        return self.relu(y + (x if self.downsample is None else self.downsample(x)))
+
+
+RESNET_SPEC = {18: (BasicBlock, (2, 2, 2, 2)), 34: (BasicBlock, (3, 4, 6, 3)), 50: (Bottleneck, (3, 4, 6, 3)),
+               101: (Bottleneck, (3, 4, 23, 3)), 152: (Bottleneck, (3, 8, 36, 3))}
+
+
+class PoseResNet(nn.Module):
+    """resnet.get(cfg): stem, four stages, deconvolution head, final conv."""
+
+    def __init__(self, num_layers=50, num_joints=15, deconv_filters=(256, 256, 256), deconv_kernels=(4, 4, 4),
+                 final_kernel=1, deconv_with_bias=False):
+        super().__init__()
+        block, counts = RESNET_SPEC[num_layers]
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = _bn(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        cin = 64
+        for i, (planes, n) in enumerate(zip((64, 128, 256, 512), counts)):
+            stride = 1 if i == 0 else 2
+            down = None
+            if stride != 1 or cin != planes * block.expansion:
+                down = nn.Sequential(nn.Conv2d(cin, planes * block.expansion, 1, stride, bias=False),
+                                     _bn(planes * block.expansion))
+            blocks = [block(cin, planes, stride, down)]
+            cin = planes * block.expansion
+            blocks += [block(cin, planes) for _ in range(1, n)]
+            setattr(self, f"layer{i + 1}", nn.Sequential(*blocks))
+        head = []
+        for f, k in zip(deconv_filters, deconv_kernels):
+            pad, opad = {4: (1, 0), 3: (1, 1), 2: (0, 0)}[k]
+            head += [nn.ConvTranspose2d(cin, f, k, 2, pad, opad, bias=deconv_with_bias), _bn(f), nn.ReLU(True)]
+            cin = f
+        self.deconv_layers = nn.Sequential(*head)
+        self.final_layer = nn.Conv2d(cin, num_joints, final_kernel, 1, 1 if final_kernel == 3 else 0)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.final_layer(self.deconv_layers(x))

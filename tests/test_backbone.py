@@ -1,0 +1,265 @@
+"""The PoseResNet heatmap backbone on the fvp MFMA convolutions and the
+channels-last voxelize that reads its output in place (fvp/backbone.py,
+csrc/fvp_conv.hip modes 0/3, fvp_voxelize_cl; SURVEY.md §8(f) rank 4,
+lib/models/resnet.py:98-215, faster_voxelpose.py:73-75).
+
+Golden vectors: tests/golden/backbone.npz -- the reference's own ResNet built by
+its resnet.get (ResNet-50 with the default deconvolution head and 1x1 final
+conv; ResNet-18 with a 3x3 final conv on a 70x90 image, so every stride-2
+stage sees odd sizes) with seeded weights (fvp.synthetic.seeded_state_dict; the
+pretrained backbone is not available offline) on seeded images, run on CPU by
+tools/gen_golden.py.  tests/cnn_arch.PoseResNet restates the architecture
+with the same attribute names for the GPU box and is pinned here bit-exactly.
+
+Tolerance: fp32 MFMA implicit GEMMs sum in a different order than torch's CPU
+convolutions and fold BatchNorm into one scale/shift; through 50+ layers the
+heatmaps agree to REL = 1e-4 of their max magnitude (the error is reported).
+The voxelize on channels-last heatmaps is compared bit-exactly with the planar
+path (same values, same arithmetic).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from conftest import golden
+
+REL = 1e-4
+
+
+def _rel_err(got, ref):
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    return float(np.abs(got - ref).max()) / max(float(np.abs(ref).max()), 1e-6)
+
+
+def _net(tag):
+    from fvp import synthetic
+    import cnn_arch
+
+    d = golden("backbone.npz")
+    layers, J, fk, seed = (int(v) for v in d[f"{tag}_cfg"])
+    m = cnn_arch.PoseResNet(layers, J, final_kernel=fk).eval()
+    m.load_state_dict(synthetic.seeded_state_dict(m, seed))
+    return m, d[f"{tag}_images"], d[f"{tag}_heatmaps"]
+
+
+@pytest.mark.parametrize("tag", ["r50", "r18"])
+def test_restated_pose_resnet_matches_reference_golden(tag):
+    m, x, y = _net(tag)
+    with torch.no_grad():
+        got = m(torch.from_numpy(x)).numpy()
+    assert got.shape == y.shape
+    assert _rel_err(got, y) <= 1e-6, tag
+
+
+def test_conv_geometry_host():
+    """Output sizes follow torch's floor formula; bad geometries are rejected before any launch."""
+    import ctypes
+
+    from fvp import _lib
+
+    lib = _lib.load()
+    hw = (ctypes.c_int * 2)()
+    assert lib.fvp_conv2d_geom(512, 960, 4, 7, 7, 0, 2, 2, 3, 3, hw) == 0 and list(hw) == [256, 480]
+    assert lib.fvp_conv2d_geom(35, 45, 64, 3, 3, 0, 2, 2, 1, 1, hw) == 0 and list(hw) == [18, 23]
+    assert lib.fvp_conv2d_geom(15, 30, 2048, 2, 2, 3, 0, 0, 0, 0, hw) == 0 and list(hw) == [30, 60]
+    assert lib.fvp_conv2d_geom(8, 8, 20, 3, 3, 0, 1, 1, 1, 1, hw) == 1002       # Cpi 20: not 4/8/12 or 16k
+    assert lib.fvp_conv2d_geom(8, 8, 16, 3, 3, 0, 1, 1, 3, 1, hw) == 1002       # padding >= kernel
+    assert lib.fvp_conv2d_geom(8, 8, 16, 3, 3, 3, 1, 1, 1, 1, hw) == 1002       # mode 3 needs 2x2 taps
+    assert lib.fvp_conv2d_geom(2, 2, 16, 7, 7, 0, 1, 1, 0, 0, hw) == 1002       # kernel larger than the input
+    assert lib.fvp_maxpool_pad_nhwc(1, 1, 8, 8, 16, 3, 2, 2, 1, None) == 1002  # 2P > K
+
+
+def test_backbone_compile_rejects_train_mode():
+    from fvp import _lib
+    from fvp.backbone import FvpPoseResNet
+    import cnn_arch
+
+    with pytest.raises(_lib.FvpError):
+        FvpPoseResNet(cnn_arch.PoseResNet(18, 15).train())
+
+
+# ------------------------------------------------------------------------- GPU
+def _conv_case(dev, conv, bn, x):
+    from fvp.cnn import ConvLayer, to_nchw, to_nhwc
+
+    conv, bn = conv.to(dev).eval(), (bn.to(dev).eval() if bn is not None else None)
+    with torch.no_grad():
+        if bn is not None:  # non-trivial BN statistics
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 1.5)
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+        ref = conv(x) if bn is None else bn(conv(x))
+        cin = conv.in_channels
+        cpi = 4 if cin <= 4 else None
+        layer = ConvLayer(conv, bn, cpi=cpi)
+        got = to_nchw(layer(to_nhwc(x, layer.Cpi), relu=False))
+    torch.cuda.synchronize()
+    return got.cpu().numpy(), ref.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,s,p,hw", [
+    (3, 64, 7, 2, 3, (70, 90)),      # resnet.py:105 stem on the RGB input (4-channel pitch)
+    (64, 64, 3, 2, 1, (35, 45)),     # Bottleneck conv2 with stride (:64), odd sizes
+    (256, 512, 1, 2, 0, (17, 23)),   # downsample 1x1/s2 (:134)
+    (128, 128, 3, 1, 1, (24, 40)),   # stride-1 3x3 (halo-eligible)
+    (1024, 256, 1, 1, 0, (9, 12)),   # Bottleneck 1x1 reduce, long K walk (split-K)
+    (256, 17, 3, 1, 1, (24, 24)),    # 3x3 final layer (FINAL_CONV_KERNEL 3)
+])
+def test_strided_conv_matches_torch(gpu_device, conv_kernel, cin, cout, k, s, p, hw):
+    torch.manual_seed(cin + k + s)
+    conv = nn.Conv2d(cin, cout, k, s, p, bias=cout == 17)
+    bn = None if cout == 17 else nn.BatchNorm2d(cout)
+    x = torch.randn((2, cin) + hw, device=gpu_device)
+    got, ref = _conv_case(gpu_device, conv, bn, x)
+    assert got.shape == ref.shape
+    assert _rel_err(got, ref) <= 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,hw", [(2048, 256, (3, 4)), (256, 256, (12, 16)), (48, 32, (5, 7))])
+def test_deconv4_matches_torch(gpu_device, conv_kernel, cin, cout, hw):
+    """ConvTranspose2d(4, 2, 1) (resnet.py:173-180) as four parity GEMMs."""
+    torch.manual_seed(cin + cout)
+    conv = nn.ConvTranspose2d(cin, cout, 4, 2, 1, 0, bias=False)
+    x = torch.randn((2, cin) + hw, device=gpu_device)
+    got, ref = _conv_case(gpu_device, conv, nn.BatchNorm2d(cout), x)
+    assert got.shape == ref.shape == (2, cout, 2 * hw[0], 2 * hw[1])
+    assert _rel_err(got, ref) <= 2e-5
+
+
+@pytest.mark.gpu
+def test_maxpool_pad_matches_torch(gpu_device):
+    from fvp.cnn import maxpool_pad, to_nchw, to_nhwc
+
+    x = torch.randn((2, 64, 35, 45), device=gpu_device)
+    x[0, 3, 0, 0] = float("nan")
+    x[1, 5] = -float("inf")
+    got = to_nchw(maxpool_pad(to_nhwc(x), 3, 2, 1))
+    ref = F.max_pool2d(x, 3, 2, 1)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    assert torch.equal(torch.nan_to_num(got, 7.0), torch.nan_to_num(ref, 7.0))
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["r50", "r18"])
+def test_fvp_pose_resnet_matches_reference(gpu_device, tag):
+    from fvp.backbone import FvpPoseResNet
+
+    m, x, y = _net(tag)
+    m = m.to(gpu_device)
+    bb = FvpPoseResNet(m)
+    xt = torch.from_numpy(x).to(gpu_device)
+    got = bb(xt)
+    torch.cuda.synchronize()
+    err = _rel_err(got.cpu().numpy(), y)
+    print(f"{tag}: max |fvp - reference| = {err:.3g} of the heatmap scale")
+    assert got.shape == y.shape and err <= REL
+    with torch.no_grad():  # and torch's own GPU forward of the same module
+        assert _rel_err(got.cpu().numpy(), m(xt).cpu().numpy()) <= REL
+    # the NHWC output holds the same values, joints in channels 0..J-1, zeros after
+    act = bb.forward_nhwc(xt)
+    J = y.shape[1]
+    assert act.Cp >= J and torch.equal(act.t[..., :J].permute(0, 3, 1, 2), got)
+    assert int(torch.count_nonzero(act.t[..., J:])) == 0
+
+
+@pytest.mark.gpu
+def test_fvp_pose_resnet_bf16(gpu_device):
+    from fvp.backbone import FvpPoseResNet
+
+    m, x, y = _net("r18")
+    got = FvpPoseResNet(m.to(gpu_device), torch.bfloat16)(torch.from_numpy(x).to(gpu_device))
+    torch.cuda.synchronize()
+    err = _rel_err(got.cpu().numpy(), y)
+    print(f"bf16 ResNet-18: {err:.3g} of the heatmap scale")
+    assert err <= 5e-2
+
+
+def _c2_layer(dev):
+    from fvp.config import make_cfg
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c2"]
+    layer = ProjectLayer(make_cfg(w, str(dev)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    from fvp import geometry
+
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float32,
+                         device=dev)
+    return w, layer, cams, seq, rt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("on_the_fly", [False, True])
+@pytest.mark.parametrize("J,cp", [(15, 16), (15, 32), (17, 32), (5, 16), (3, 4)])
+def test_voxelize_channels_last_bit_exact(gpu_device, on_the_fly, J, cp):
+    """fvp_voxelize_cl(_cams) on [B,V,H,W,cp] == fvp_voxelize(_cams) on the same planar values."""
+    from fvp.heatmaps import ChannelsLastHeatmaps, attach
+
+    w, layer, cams, seq, rt = _c2_layer(gpu_device)
+    layer.on_the_fly = on_the_fly
+    g = torch.Generator(device="cpu").manual_seed(J * 100 + cp)
+    B, V = 3, 5
+    H, W = w.heatmap_size[1], w.heatmap_size[0]
+    planar = torch.rand((B, V, J, H, W), generator=g).to(gpu_device)
+    cl = torch.zeros((B, V, H, W, cp), device=gpu_device)
+    cl[..., :J] = planar.permute(0, 1, 3, 4, 2)
+    cl[..., J:] = 123.0  # channels past J are ignored
+    meta = {"seq": [seq] * B}
+    cube_ref, xy_ref = layer.forward_fused(planar, meta, cams, rt)
+    cube, xy = layer.forward_fused(ChannelsLastHeatmaps(cl, J), meta, cams, rt)
+    torch.cuda.synchronize()
+    assert torch.equal(cube, cube_ref) and torch.equal(xy, xy_ref)
+    # through the reference interface: a planar tensor carrying its channels-last copy
+    cube2 = layer(attach(planar.clone(), ChannelsLastHeatmaps(cl, J)), meta, cams, rt)
+    assert torch.equal(cube2, cube_ref)
+
+
+@pytest.mark.gpu
+def test_attached_copy_is_dropped_after_in_place_write(gpu_device):
+    from fvp.heatmaps import ChannelsLastHeatmaps, attach, channels_last_of
+
+    planar = torch.zeros((1, 2, 3, 4, 5), device=gpu_device)
+    cl = ChannelsLastHeatmaps(torch.zeros((1, 2, 4, 5, 4), device=gpu_device), 3)
+    t = attach(planar, cl)
+    assert channels_last_of(t) is cl
+    assert channels_last_of(t.clone()) is None and channels_last_of(t[:1]) is None
+    t.add_(1.0)
+    assert channels_last_of(t) is None
+
+
+@pytest.mark.gpu
+def test_views_to_cube_equals_planar_path(gpu_device):
+    """views -> backbone (channels-last, no transpose) -> voxelize == views ->
+    backbone NCHW heatmaps -> reference-layout voxelize, bit for bit."""
+    from fvp.backbone import FvpPoseResNet
+    import cnn_arch
+    from fvp import synthetic
+
+    w, layer, cams, seq, rt = _c2_layer(gpu_device)
+    m = cnn_arch.PoseResNet(18, 15).eval()
+    m.load_state_dict(synthetic.seeded_state_dict(m, 3))
+    bb = FvpPoseResNet(m.to(gpu_device))
+    B, V = 2, 5
+    H, W = w.heatmap_size[1], w.heatmap_size[0]
+    views = torch.randn((B, V, 3, 4 * H, 4 * W), generator=torch.Generator().manual_seed(5)).to(gpu_device)
+    cl = bb.heatmaps_cl(views)
+    assert cl.shape == (B, V, 15, H, W)
+    # the reference's per-view loop + stack (faster_voxelpose.py:75): same values up to the
+    # launch-size-dependent split-K summation order
+    stacked = torch.stack([bb(views[:, c]) for c in range(V)], dim=1)
+    planar = cl.planar()
+    assert _rel_err(planar.cpu().numpy(), stacked.cpu().numpy()) <= 1e-5
+    meta = {"seq": [seq] * B}
+    a = layer.forward_fused(cl, meta, cams, rt)
+    b = layer.forward_fused(planar.clone(), meta, cams, rt)  # (a clone: the planar path)
+    torch.cuda.synchronize()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])

@@ -69,19 +69,6 @@ def test_fvp_cnn_matches_reference(gpu_device):
         _close(y.cpu().numpy(), p2p(torch.from_numpy(x_p2p).to(gpu_device)).cpu().numpy(), "P2PNet vs torch GPU")
 
 
-@pytest.fixture(params=["halo", "pertap", "pertap-nosplit"])
-def conv_kernel(request):
-    """Run with the halo-tiled KxK kernel on every eligible layer (so small
-    test shapes take it too), with the per-tap kernel only (split-K where a
-    launch is under-filled), and with neither halo nor split-K
-    (FVP_CONV_HALO / _PER_TAP / _PER_TAP_NOSPLIT of fvp_conv2d_nhwc_ws)."""
-    from fvp import cnn
-
-    algo = {"halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP, "pertap-nosplit": cnn.CONV_PER_TAP_NOSPLIT}
-    with cnn.conv_algo(algo[request.param]):
-        yield request.param
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,hw,res", [(15, 16, 7, (64, 64), False), (16, 32, 3, (33, 17), True),
                                                (128, 128, 3, (16, 16), True), (32, 15, 1, (20, 20), False),

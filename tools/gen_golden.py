@@ -12,7 +12,7 @@ attribute-dict cfg, so lib/core/config.py (easydict) is not imported.
 Outputs: tests/golden/*.npz (inputs that cannot be regenerated bit-exactly
 elsewhere are stored; uniform-random inputs are regenerated from torch seeds).
 
-    python3 -B tools/gen_golden.py [--only whole,c4,c5,e2e]
+    python3 -B tools/gen_golden.py [--only whole,c4,c5,e2e,backbone]
 """
 from __future__ import annotations
 
@@ -84,6 +84,30 @@ def e2e_case(torch, geometry, synthetic, WORKLOADS, make_cfg):
          "min_score": np.float32(w.min_score)}
     np.savez_compressed(os.path.join(OUT, "e2e_c3.npz"), **d)
     print("wrote e2e_c3", {k: np.shape(v) for k, v in d.items()})
+
+
+def backbone_case(torch, synthetic):
+    """The reference's PoseResNet (lib/models/resnet.py:98-215, built by its own
+    resnet.get from the RESNET keys of lib/core/config.py:101-107) in eval mode
+    with seeded weights on seeded images: ResNet-50 (Bottleneck, the default
+    config: three 256-filter kernel-4 deconvolutions, 1x1 final conv) and
+    ResNet-18 (BasicBlock, 3x3 final conv, J=17) on an image size that is not a
+    multiple of 32 (odd intermediate sizes through every stride-2 stage)."""
+    import models.resnet as rn  # noqa: E402
+    from fvp.config import resnet_cfg
+
+    d = {}
+    for tag, layers, J, shape, fk, seed in (("r50", 50, 15, (2, 3, 96, 128), 1, 21),
+                                            ("r18", 18, 17, (1, 3, 70, 90), 3, 22)):
+        m = rn.get(resnet_cfg(layers, J, final_kernel=fk)).eval()
+        m.load_state_dict(synthetic.seeded_state_dict(m, seed))
+        x = torch.from_numpy(np.random.default_rng(seed).standard_normal(shape).astype(np.float32))
+        with torch.no_grad():
+            y = m(x)
+        d.update({f"{tag}_cfg": np.array([layers, J, fk, seed]), f"{tag}_images": x.numpy(),
+                  f"{tag}_heatmaps": y.numpy()})
+    np.savez_compressed(os.path.join(OUT, "backbone.npz"), **d)
+    print("wrote backbone", {k: v.shape for k, v in d.items()})
 
 
 def main():
@@ -166,6 +190,8 @@ def main():
         whole_case("whole_c5", "c5", batch=1, stride=997, store_heatmaps=False)
     if only is None or "e2e" in only:
         e2e_case(torch, geometry, synthetic, WORKLOADS, make_cfg)
+    if only is None or "backbone" in only:
+        backbone_case(torch, synthetic)
     if only is not None:
         return 0
 

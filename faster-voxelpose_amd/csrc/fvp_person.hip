@@ -125,8 +125,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
                                                              float *__restrict__ cubes, float *__restrict__ planes,
                                                              float *__restrict__ offset, int P, int V, int J, int H,
-                                                             int W, int xmap, int xsplit) {
-    constexpr int JP = 4 * LPV;
+                                                             int W, int xmap, int xsplit, unsigned pix_bytes) {
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
@@ -150,8 +149,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     const int zl = threadIdx.x / LPV, q = threadIdx.x % LPV;
     const int b = frame_of ? frame_of[p] : 0;
     const unsigned HW = (unsigned)(H * W);
-    const unsigned pix_bytes = JP * 4u;
-    const unsigned img = HW * pix_bytes;
+    const unsigned img = HW * pix_bytes;  // pix_bytes >= JP * 4: one channels-last pixel
     const unsigned qo = (unsigned)q * 16u;
     const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
     const float fV = (float)V;
@@ -348,7 +346,7 @@ static int person_xsplit(int P, int SY) {
 template <int LPV, bool OTF, bool CASC>
 static void launch_person_cl(const float *cl, const float *fgrid, const PersonCoords &pc, const float *props,
                              const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
-                             float *offset, int P, int V, int J, int H, int W, hipStream_t st) {
+                             float *offset, int P, int V, int J, int H, int W, unsigned pix_bytes, hipStream_t st) {
     const int SY = s.bins[1];
     // one y-row per block (the kernel also takes YG rows): with the planes-only
     // fast path for x-planes outside the window, rows are the finer and better
@@ -359,7 +357,7 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // (the yz maxima then go through atomics into a pre-zeroed plane).
     const int xmap = 1, xsplit = person_xsplit(P, SY);
     hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF, CASC>), dim3((unsigned)(P * SY * xsplit)), dim3(64 * LPV), 0, st, cl,
-                       fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap, xsplit);
+                       fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap, xsplit, pix_bytes);
 }
 
 }  // namespace fvp
@@ -380,10 +378,12 @@ extern "C" size_t fvp_person_workspace_bytes(int B, int V, int J, int H, int W) 
 
 namespace fvp {
 
-static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, int W, const float *fine_grid,
-                             const PersonCoords *pc, const fvp_person_spec *spec, const float *proposals,
-                             const int32_t *frame_of, int P, float *cubes, float *planes, float *offset,
-                             void *workspace, size_t workspace_bytes, void *stream) {
+// heatmaps: planar [B][V][J][H][W] (cp == 0: re-laid out into the workspace
+// first) or channels-last [B][V][H][W][cp] (read in place, no workspace).
+static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J, int H, int W,
+                             const float *fine_grid, const PersonCoords *pc, const fvp_person_spec *spec,
+                             const float *proposals, const int32_t *frame_of, int P, float *cubes, float *planes,
+                             float *offset, void *workspace, size_t workspace_bytes, void *stream) {
     if (!heatmaps || !spec || (!fine_grid && !pc)) return FVP_ERR_NULL;
     if (P <= 0) return FVP_OK;
     if (!proposals) return FVP_ERR_NULL;
@@ -396,10 +396,16 @@ static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, 
     // packed fine grid addressed with 32-bit byte offsets
     if (!pc && (long long)spec->fine[0] * spec->fine[1] * spec->fine[2] * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL)
         return FVP_ERR_SHAPE;
-    const size_t need = (size_t)B * cl_frame_bytes(V, J, H, W);
-    if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
+    const int JP = 4 * lanes_per_voxel(J);
+    if (cp) {
+        if (cp < JP || cp % 4 || (size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;
+    } else {
+        const size_t need = (size_t)B * cl_frame_bytes(V, J, H, W);
+        if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
+    }
     hipStream_t st = (hipStream_t)stream;
-    float *cl = reinterpret_cast<float *>(workspace);
+    const float *cl = cp ? heatmaps : reinterpret_cast<const float *>(workspace);
+    const unsigned pix_bytes = 4u * (unsigned)(cp ? cp : JP);
     if (planes) {  // xy, xz (and yz when x is split) are reduced with atomicMax over non-negative floats: from +0
         const size_t n = (person_xsplit(P, SY) > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
         const hipError_t e = hipMemsetAsync(planes, 0, n * 4, st);
@@ -408,19 +414,19 @@ static int person_planes_any(const float *heatmaps, int B, int V, int J, int H, 
     const PersonCoords none{};
     const PersonCoords &c = pc ? *pc : none;
 #define FVP_PERSON_CASE(L)                                                                                            \
-    launch_layout<L, float>(heatmaps, B, V, J, H, W, cl, st);                                                        \
+    if (!cp) launch_layout<L, float>(heatmaps, B, V, J, H, W, reinterpret_cast<float *>(workspace), st);             \
     if (pc && V > 16)                                                                                                 \
         launch_person_cl<L, true, true>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, \
-                                        W, st);                                                                       \
+                                        W, pix_bytes, st);                                                            \
     else if (pc)                                                                                                      \
         launch_person_cl<L, true, false>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J,  \
-                                         H, W, st);                                                                   \
+                                         H, W, pix_bytes, st);                                                        \
     else if (V > 16)                                                                                                  \
         launch_person_cl<L, false, true>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V,   \
-                                         J, H, W, st);                                                                \
+                                         J, H, W, pix_bytes, st);                                                     \
     else                                                                                                              \
         launch_person_cl<L, false, false>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V,  \
-                                          J, H, W, st);                                                               \
+                                          J, H, W, pix_bytes, st);                                                    \
     break;
     switch (lanes_per_voxel(J)) {
         case 1: FVP_PERSON_CASE(1)
@@ -439,8 +445,8 @@ extern "C" int fvp_person_planes(const float *heatmaps, int B, int V, int J, int
                                  float *cubes, float *planes, float *offset, void *workspace, size_t workspace_bytes,
                                  void *stream) {
     if (!fine_grid) return FVP_ERR_NULL;
-    return fvp::person_planes_any(heatmaps, B, V, J, H, W, fine_grid, nullptr, spec, proposals, frame_of, P, cubes,
-                                  planes, offset, workspace, workspace_bytes, stream);
+    return fvp::person_planes_any(heatmaps, 0, B, V, J, H, W, fine_grid, nullptr, spec, proposals, frame_of, P,
+                                  cubes, planes, offset, workspace, workspace_bytes, stream);
 }
 
 extern "C" int fvp_person_planes_cams(const float *heatmaps, int B, int V, int J, int H, int W, const float *cams,
@@ -453,6 +459,16 @@ extern "C" int fvp_person_planes_cams(const float *heatmaps, int B, int V, int J
     for (int a = 0; a < 3; ++a)
         if (fine_grid_spec->bins[a] != spec->fine[a]) return FVP_ERR_SHAPE;
     const fvp::PersonCoords pc{cams, resize_t, *fine_grid_spec, *img};
-    return fvp::person_planes_any(heatmaps, B, V, J, H, W, nullptr, &pc, spec, proposals, frame_of, P, cubes, planes,
-                                  offset, workspace, workspace_bytes, stream);
+    return fvp::person_planes_any(heatmaps, 0, B, V, J, H, W, nullptr, &pc, spec, proposals, frame_of, P, cubes,
+                                  planes, offset, workspace, workspace_bytes, stream);
+}
+
+extern "C" int fvp_person_planes_cl(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
+                                    const float *fine_grid, const fvp_person_spec *spec, const float *proposals,
+                                    const int32_t *frame_of, int P, float *cubes, float *planes, float *offset,
+                                    void *stream) {
+    if (!fine_grid) return FVP_ERR_NULL;
+    if (cp <= 0) return FVP_ERR_SHAPE;
+    return fvp::person_planes_any(heatmaps_cl, cp, B, V, J, H, W, fine_grid, nullptr, spec, proposals, frame_of, P,
+                                  cubes, planes, offset, nullptr, 0, stream);
 }

@@ -65,6 +65,8 @@ SIGNATURES = {
                                ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), ctypes.POINTER(PersonSpec),
                                c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_size_t,
                                c_void_p],
+    "fvp_person_planes_cl": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, ctypes.POINTER(PersonSpec),
+                             c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_max_planes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_soft_argmax": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "fvp_fuse_poses": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],

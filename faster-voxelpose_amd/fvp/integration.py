@@ -11,6 +11,17 @@ implementations, in the modules that import them, BEFORE the model is built
     core.proposal.nms2D / human_detection_net.nms2D -> fvp.proposal.nms2D  (:12)
     models.human_detection_net.ProposalLayer -> fvp.proposal.ProposalLayer  (:14-125)
 
+With ``backbone=True`` the PoseResNet heatmap backbone runs on the fvp MFMA
+convolutions (fvp.backbone; resnet.py:98-201) in eval mode:
+
+    models.resnet.ResNet.forward             -> fvp_resnet_forward
+    models.faster_voxelpose.FasterVoxelPoseNet.forward -> fused_fvp_forward (fused=True)
+
+the latter runs the backbone once over all views of the batch (instead of the
+per-view loop and stack of faster_voxelpose.py:73-75) and hands the HDN and
+JLN the channels-last heatmaps the backbone writes, so neither re-lays them
+out; ``input_heatmaps`` is still returned in the reference layout.
+
 With ``fused=True`` it also replaces JointLocalizationNet.forward by
 :func:`fvp.jln.fused_jln_forward` (every proposal of a batch at once, soft-argmax
 and fusion on fvp kernels; eval mode) and HumanDetectionNet.forward
@@ -28,24 +39,29 @@ import sys
 
 import torch
 
+from . import backbone as fvp_backbone
 from . import cnn as fvp_cnn
 from . import jln, project_individual, project_whole, proposal
 
 USE_FVP_CNN = False  # set by install(cnn=True)
 FVP_CNN_DTYPE = torch.float32
+USE_FVP_BACKBONE = False  # set by install(backbone=True)
+FVP_BACKBONE_DTYPE = torch.float32
 
 
-def install(fused: bool = True, modules=None, cnn: bool = False) -> dict:
+def install(fused: bool = True, modules=None, cnn: bool = False, backbone: bool = False) -> dict:
     """Patch the already-importable reference modules.  Returns what was patched.
 
     cnn=True (with fused=True): in eval mode the fused forwards run CenterNet,
     C2CNet and P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of
     torch's, in fp32, and WeightNet as one fused launch; cnn="bf16": bf16
     operands with fp32 accumulation for the MFMA convolutions (opt-in, ~1e-2
-    relative)."""
-    global USE_FVP_CNN, FVP_CNN_DTYPE
+    relative).  backbone=True / "bf16": the same for the PoseResNet backbone."""
+    global USE_FVP_CNN, FVP_CNN_DTYPE, USE_FVP_BACKBONE, FVP_BACKBONE_DTYPE
     USE_FVP_CNN = bool(cnn)
     FVP_CNN_DTYPE = torch.bfloat16 if cnn == "bf16" else torch.float32
+    USE_FVP_BACKBONE = bool(backbone)
+    FVP_BACKBONE_DTYPE = torch.bfloat16 if backbone == "bf16" else torch.float32
     mods = modules if modules is not None else sys.modules
     patched = {}
 
@@ -62,6 +78,21 @@ def install(fused: bool = True, modules=None, cnn: bool = False) -> dict:
     setattr_if("core.proposal", "nms2D", proposal.nms2D)
     setattr_if("models.human_detection_net", "nms2D", proposal.nms2D)
     setattr_if("models.human_detection_net", "ProposalLayer", proposal.ProposalLayer)
+    if backbone:
+        rn = mods.get("models.resnet")
+        if rn is not None and hasattr(rn, "ResNet"):
+            cls = rn.ResNet
+            if not hasattr(cls, "_fvp_original_forward"):
+                cls._fvp_original_forward = cls.forward
+            cls.forward = fvp_resnet_forward
+            patched["models.resnet.ResNet.forward"] = fvp_resnet_forward
+        fv = mods.get("models.faster_voxelpose")
+        if fused and fv is not None and hasattr(fv, "FasterVoxelPoseNet"):
+            cls = fv.FasterVoxelPoseNet
+            if not hasattr(cls, "_fvp_original_forward"):
+                cls._fvp_original_forward = cls.forward
+            cls.forward = fused_fvp_forward
+            patched["models.faster_voxelpose.FasterVoxelPoseNet.forward"] = fused_fvp_forward
     if fused:
         hdn = mods.get("models.human_detection_net")
         if hdn is not None and hasattr(hdn, "HumanDetectionNet"):
@@ -111,3 +142,32 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     else:  # z pick + ProposalLayer test mode in one launch (human_detection_net.py:208-220, :99-124)
         centers = proposal.proposal_centers(pl, index_2d, hm1d.detach(), confs_2d, match_bbox)
     return hm2d, hm1d, centers, torch.flatten(bbox_preds, 2, 3).permute(0, 2, 1)
+
+
+def _fvp_backbone_ok(module, x) -> bool:
+    return (USE_FVP_BACKBONE and not module.training and isinstance(x, torch.Tensor) and x.is_cuda
+            and not (torch.is_grad_enabled() and x.requires_grad))
+
+
+def fvp_resnet_forward(self, x):
+    """ResNet.forward (resnet.py:187-201) on the fvp MFMA convolutions in eval
+    mode; the reference's forward in training (BatchNorm batch statistics,
+    autograd) and on CPU tensors."""
+    if _fvp_backbone_ok(self, x):
+        return fvp_backbone.cached(self, FVP_BACKBONE_DTYPE)(x)
+    return type(self)._fvp_original_forward(self, x)
+
+
+def fused_fvp_forward(self, backbone=None, views=None, meta=None, targets=None, input_heatmaps=None, cameras=None,
+                      resize_transform=None):
+    """FasterVoxelPoseNet.forward (faster_voxelpose.py:51-162) with the views
+    path on the fvp backbone in eval mode: all B*V views in one pass, heatmaps
+    written channels-last once and handed to the HDN / JLN gathers in place
+    (fvp.heatmaps.attach); everything after it is the reference's forward."""
+    if (views is not None and backbone is not None and not self.training and hasattr(backbone, "deconv_layers")
+            and _fvp_backbone_ok(backbone, views)):
+        cl = fvp_backbone.cached(backbone, FVP_BACKBONE_DTYPE).heatmaps_cl(views)
+        input_heatmaps, views = cl.planar(), None  # [B,V,J,H,W], carrying the channels-last copy
+    return type(self)._fvp_original_forward(self, backbone=backbone, views=views, meta=meta, targets=targets,
+                                            input_heatmaps=input_heatmaps, cameras=cameras,
+                                            resize_transform=resize_transform)

@@ -401,6 +401,45 @@ def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: to
     return cubes, planes, offset
 
 
+@torch.library.custom_op("fvp::person_planes_cl", mutates_args=(), device_types="cuda")
+def person_planes_cl(heatmaps_cl: torch.Tensor, J: int, fine_grid: torch.Tensor, proposals: torch.Tensor,
+                     frame_of: Optional[torch.Tensor], fine: list[int], scale: list[float], bias: list[float],
+                     whole_size: list[float], ind_size: list[float], bins: list[int], want_cubes: bool,
+                     want_planes: bool) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """person_planes on channels-last heatmaps [B,V,H,W,Cp] (fvp_person_planes_cl): no layout pass."""
+    hm = _cl_input(heatmaps_cl, J)
+    fg = _dev_f32(fine_grid, "fine sample grid")
+    pc = _dev_f32(proposals, "proposal_centers")
+    B, V, H, W, cp = hm.shape
+    P = pc.shape[0]
+    if tuple(fg.shape) != (fine[0] * fine[1] * fine[2], grid_slots(V), 2):
+        raise _lib.FvpError("fvp: packed fine grid must be [FX*FY*FZ, GV, 2] (pack_grid of the fine sample grid)")
+    fo = None
+    if frame_of is not None:
+        fo = frame_of.to(device=hm.device, dtype=torch.int32).contiguous()
+        if fo.numel() != P:
+            raise _lib.FvpError("fvp: frame_of must have one entry per proposal")
+    SX, SY, SZ = bins
+    cubes = torch.empty((P, J, SX, SY, SZ) if want_cubes else (0,), dtype=torch.float32, device=hm.device)
+    planes = torch.empty((3 * P, J, SX, SY) if want_planes else (0,), dtype=torch.float32, device=hm.device)
+    offset = torch.empty((P, 3), dtype=torch.float32, device=hm.device)
+    if P > 0:
+        spec = PersonSpec(_i3(fine), _f3(scale), _f3(bias), _f3(whole_size), _f3(ind_size), _i3(bins))
+        _lib.call("fvp_person_planes_cl", _ptr(hm), cp, B, V, J, H, W, _ptr(fg), spec, _ptr(pc), _ptr(fo), P,
+                  _ptr(cubes) if want_cubes else None, _ptr(planes) if want_planes else None, _ptr(offset),
+                  _stream(hm))
+    return cubes, planes, offset
+
+
+@person_planes_cl.register_fake
+def _(heatmaps_cl, J, fine_grid, proposals, frame_of, fine, scale, bias, whole_size, ind_size, bins, want_cubes,
+      want_planes):
+    P = proposals.shape[0]
+    return (heatmaps_cl.new_empty((P, J, bins[0], bins[1], bins[2]) if want_cubes else (0,)),
+            heatmaps_cl.new_empty((3 * P, J, bins[0], bins[1]) if want_planes else (0,)),
+            heatmaps_cl.new_empty((P, 3)))
+
+
 @torch.library.custom_op("fvp::person_planes_cams", mutates_args=(), device_types="cuda")
 def person_planes_cams(heatmaps: torch.Tensor, cams: torch.Tensor, resize_t: torch.Tensor, start: list[float],
                        end: list[float], center: list[float], ori_max: float, img_w: float, img_h: float,

@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from . import geometry, ops
+from .heatmaps import ChannelsLastHeatmaps, channels_last_of
 
 
 # Fine-grid sampling coordinates: read from the per-sequence packed fine grid
@@ -126,9 +127,13 @@ class ProjectLayer(nn.Module):
         return fine[0] * fine[1] * fine[2] * ops.grid_slots(V) * 8 > PERSON_OTF_GRID_BYTES
 
     def _run(self, heatmaps, index, meta, cameras, resize_transform, props, frame_of, cubes, planes):
-        """One fvp_person_planes[_cams] launch for ``props`` of the frames of ``heatmaps``
-        (the coordinates of ``meta['seq'][index]``'s cameras)."""
+        """One fvp_person_planes[_cams|_cl] launch for ``props`` of the frames of ``heatmaps``
+        (the coordinates of ``meta['seq'][index]``'s cameras).  heatmaps: a tensor
+        or fvp.heatmaps.ChannelsLastHeatmaps (read in place on the cached-grid path)."""
+        cl = channels_last_of(heatmaps)
         if self._otf(heatmaps.shape[1]):
+            if isinstance(heatmaps, ChannelsLastHeatmaps):
+                heatmaps = heatmaps.planar()
             seq = meta["seq"][index]
             if seq not in self._cams:
                 self._cams[seq] = torch.from_numpy(geometry.pack_cameras(cameras, seq)).to(heatmaps.device)
@@ -142,7 +147,17 @@ class ProjectLayer(nn.Module):
                                           float(self.image_size[0]), float(self.image_size[1]), props, frame_of,
                                           *self._args(), cubes, planes)
         grid = self._seq_grid(heatmaps, index, meta, cameras, resize_transform)
+        if cl is not None:
+            return ops.person_planes_cl(cl.t, cl.J, grid, props, frame_of, *self._args(), cubes, planes)
         return ops.person_planes(heatmaps, grid, props, frame_of, *self._args(), cubes, planes)
+
+    @staticmethod
+    def _frame(heatmaps, index):
+        """Frame ``index`` of the batch (keeping a channels-last copy, if any)."""
+        cl = channels_last_of(heatmaps)
+        if cl is not None:
+            return ChannelsLastHeatmaps(cl.t[index:index + 1], cl.J)
+        return heatmaps[index:index + 1]
 
     def _args(self):
         c = self._const
@@ -152,7 +167,7 @@ class ProjectLayer(nn.Module):
 
     def forward(self, heatmaps, index, meta, proposal_centers, cameras, resize_transform):
         ops.forward_only(heatmaps, proposal_centers)
-        cubes, _, offset = self._run(heatmaps[index:index + 1], index, meta, cameras, resize_transform,
+        cubes, _, offset = self._run(self._frame(heatmaps, index), index, meta, cameras, resize_transform,
                                      proposal_centers, None, True, False)
         return cubes, offset
 
@@ -160,22 +175,43 @@ class ProjectLayer(nn.Module):
         """(planes[3P,J,S,S], offset[P,3]) without materialising the cubes: the JLN
         input at joint_localization_net.py:158-160 for frame ``index``."""
         ops.forward_only(heatmaps, proposal_centers)
-        _, planes, offset = self._run(heatmaps[index:index + 1], index, meta, cameras, resize_transform,
+        _, planes, offset = self._run(self._frame(heatmaps, index), index, meta, cameras, resize_transform,
                                       proposal_centers, None, False, True)
         return planes, offset
 
     def forward_batch(self, heatmaps, meta, proposal_centers, mask, cameras, resize_transform):
-        """Every valid proposal of the batch in ONE launch (the reference loops
-        frames and proposals with host syncs, joint_localization_net.py:148-151,
-        project_individual.py:272-275).  proposal_centers [B,K,7], mask [B,K] bool.
-        Returns (planes [3P,J,S,S] in (frame, proposal) order of ``mask``, offset
-        [P,3], frame_of [P]).  Frames must share one sequence's cameras."""
+        """Every valid proposal of the batch in one launch per sequence (the
+        reference loops frames and proposals with host syncs,
+        joint_localization_net.py:148-151, project_individual.py:272-275).
+        proposal_centers [B,K,7], mask [B,K] bool.  Returns (planes [3P,J,S,S]
+        in (frame, proposal) order of ``mask``, offset [P,3], frame_of [P])."""
         ops.forward_only(heatmaps, proposal_centers)
         seqs = list(meta["seq"])[: heatmaps.shape[0]]
-        if len(set(seqs)) != 1:
-            raise ValueError("forward_batch: all frames must belong to one sequence")
         idx = mask.nonzero()  # one host sync for the whole batch
         frame_of = idx[:, 0].to(torch.int32)
         props = proposal_centers[idx[:, 0], idx[:, 1]]
-        _, planes, offset = self._run(heatmaps, 0, meta, cameras, resize_transform, props, frame_of, False, True)
+        uniq = list(dict.fromkeys(seqs))
+        if len(uniq) == 1:
+            _, planes, offset = self._run(heatmaps, 0, meta, cameras, resize_transform, props, frame_of, False, True)
+            return planes, offset, frame_of
+        # frames of several sequences: one launch per sequence over its proposals,
+        # scattered back into the (frame, proposal) order
+        P = props.shape[0]
+        J = heatmaps.shape[2]
+        S = [int(v) for v in self._const["ind_bins"]]
+        planes = torch.zeros((3 * P, J, S[0], S[1]), dtype=torch.float32, device=heatmaps.device)
+        offset = torch.zeros((P, 3), dtype=torch.float32, device=heatmaps.device)
+        seq_of = torch.tensor([uniq.index(s) for s in seqs], dtype=torch.int64, device=heatmaps.device)
+        owner = seq_of[idx[:, 0]] if P else seq_of[:0]
+        for u, seq in enumerate(uniq):
+            sel = (owner == u).nonzero()[:, 0]
+            if sel.numel() == 0:
+                continue
+            first = seqs.index(seq)  # any frame of the sequence names its cameras
+            _, pl, off = self._run(heatmaps, first, meta, cameras, resize_transform, props[sel],
+                                   frame_of[sel], False, True)
+            n = sel.numel()
+            for k in range(3):  # xy, xz, yz blocks of the reference's cat order
+                planes[k * P + sel] = pl[k * n:(k + 1) * n]
+            offset[sel] = off
         return planes, offset, frame_of

@@ -216,6 +216,12 @@ int fvp_person_planes_cams(const float *heatmaps, int B, int V, int J, int H, in
                            const float *proposals, const int32_t *frame_of, int P,
                            float *cubes, float *planes, float *offset,
                            void *workspace, size_t workspace_bytes, void *stream);
+/* fvp_person_planes on channels-last heatmaps [B][V][H][W][cp] (cp as
+ * fvp_voxelize_cl; e.g. the backbone's NHWC output): read in place, no
+ * layout pass, no workspace. */
+int fvp_person_planes_cl(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W, const float *fine_grid,
+                         const fvp_person_spec *spec, const float *proposals, const int32_t *frame_of, int P,
+                         float *cubes, float *planes, float *offset, void *stream);
 
 /* xy / xz / yz max-projections of per-person cubes [P][J][S][S][S] into
  * planes [3P][J][S][S] (xy block first, then xz, then yz).

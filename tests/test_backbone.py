@@ -263,3 +263,101 @@ def test_views_to_cube_equals_planar_path(gpu_device):
     b = layer.forward_fused(planar.clone(), meta, cams, rt)  # (a clone: the planar path)
     torch.cuda.synchronize()
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+# ------------------------------------------------------------------ drop-in
+def _fake_reference(mods_cls):
+    """Stand-ins for models.resnet / models.faster_voxelpose with the reference's
+    forward flow on the views path (faster_voxelpose.py:73-86)."""
+    import types
+
+    rn = types.ModuleType("models.resnet")
+    rn.ResNet = mods_cls
+
+    class FasterVoxelPoseNet(nn.Module):
+        def __init__(self, project_layer):
+            super().__init__()
+            self.project_layer = project_layer
+            self.seen = None
+
+        def forward(self, backbone=None, views=None, meta=None, targets=None, input_heatmaps=None, cameras=None,
+                    resize_transform=None):
+            if views is not None:
+                input_heatmaps = torch.stack([backbone(views[:, c]) for c in range(views.shape[1])], dim=1)
+            self.seen = input_heatmaps
+            cube = self.project_layer(input_heatmaps, meta, cameras, resize_transform)
+            return cube, input_heatmaps
+
+    fv = types.ModuleType("models.faster_voxelpose")
+    fv.FasterVoxelPoseNet = FasterVoxelPoseNet
+    return {"models.resnet": rn, "models.faster_voxelpose": fv}, FasterVoxelPoseNet
+
+
+def _restore(cls):
+    if hasattr(cls, "_fvp_original_forward"):
+        cls.forward = cls._fvp_original_forward
+        del cls._fvp_original_forward
+
+
+def test_install_backbone_patches_and_falls_back_on_cpu():
+    from fvp import integration
+    import cnn_arch
+
+    class ResNet(cnn_arch.PoseResNet):  # a subclass: patching it leaves cnn_arch untouched
+        pass
+
+    mods, FVP = _fake_reference(ResNet)
+    try:
+        patched = integration.install(fused=True, modules=mods, backbone=True)
+        assert ResNet.forward is integration.fvp_resnet_forward
+        assert FVP.forward is integration.fused_fvp_forward
+        assert "models.resnet.ResNet.forward" in patched
+        m = ResNet(18, 5).eval()
+        x = torch.randn(1, 3, 64, 64)
+        with torch.no_grad():  # CPU tensors: the reference's own forward
+            assert torch.equal(m(x), cnn_arch.PoseResNet.forward(m, x))
+    finally:
+        _restore(ResNet)
+        _restore(FVP)
+        integration.USE_FVP_BACKBONE = False
+
+
+@pytest.mark.gpu
+def test_installed_views_path_matches_reference_flow(gpu_device):
+    """install(backbone=True): the model's views path runs the fvp backbone over all
+    views at once and the voxelize reads its channels-last output; the cube equals
+    the reference flow (per-view backbone, stack, planar voxelize) up to the
+    backbone's MFMA summation order, and bit-exactly the planar voxelize of the
+    heatmaps the fused path returns."""
+    from fvp import integration, synthetic
+    from fvp.heatmaps import channels_last_of
+    import cnn_arch
+
+    class ResNet(cnn_arch.PoseResNet):
+        pass
+
+    w, layer, cams, seq, rt = _c2_layer(gpu_device)
+    mods, FVP = _fake_reference(ResNet)
+    m = ResNet(18, 15).eval()
+    m.load_state_dict(synthetic.seeded_state_dict(m, 4))
+    m = m.to(gpu_device)
+    model = FVP(layer).eval()
+    B, V = 2, 5
+    H, W = w.heatmap_size[1], w.heatmap_size[0]
+    views = torch.randn((B, V, 3, 4 * H, 4 * W), generator=torch.Generator().manual_seed(6)).to(gpu_device)
+    meta = {"seq": [seq] * B}
+    with torch.no_grad():
+        ref_cube, ref_hm = model(backbone=m, views=views, meta=meta, cameras=cams, resize_transform=rt)
+        try:
+            integration.install(fused=True, modules=mods, backbone=True)
+            cube, hm = model(backbone=m, views=views, meta=meta, cameras=cams, resize_transform=rt)
+            assert channels_last_of(model.seen) is not None  # the HDN got the channels-last copy
+        finally:
+            _restore(ResNet)
+            _restore(FVP)
+            integration.USE_FVP_BACKBONE = False
+        planar = layer(hm.clone(), meta, cams, rt)
+    torch.cuda.synchronize()
+    assert torch.equal(cube, planar)
+    assert _rel_err(hm.cpu().numpy(), ref_hm.cpu().numpy()) <= REL
+    assert float((cube - ref_cube).abs().max()) <= 1e-4

@@ -781,3 +781,50 @@ def test_person_planes_nonfinite_heatmaps(gpu_device, otf):
     planes, off2 = layer.forward_planes(hm, 0, {"seq": [seq]}, props, cams, rt)
     np.testing.assert_array_equal(planes.cpu().numpy(), ref.cpu().numpy())
     assert torch.equal(off2, offset)
+
+
+@pytest.mark.parametrize("otf", [False, True], ids=["finegrid", "onthefly"])
+def test_person_planes_channels_last_bit_exact(gpu_device, otf):
+    """fvp_person_planes_cl (channels-last heatmaps, e.g. the backbone's NHWC
+    output, read in place) == the planar path, batched and per frame."""
+    from fvp.heatmaps import ChannelsLastHeatmaps, attach
+
+    w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, frames=3)
+    layer.on_the_fly = otf
+    rng = np.random.default_rng(9)
+    props = torch.from_numpy(np.stack([_props(w, f, rng, 3) for f in range(3)])).to(gpu_device)
+    mask = torch.ones(props.shape[:2], dtype=torch.bool, device=gpu_device)
+    mask[1, 2] = False
+    meta = {"seq": [seq] * 3}
+    cl = torch.full(hm.shape[:2] + hm.shape[3:] + (32,), 9.0, device=gpu_device)  # pitch 32 > JP, junk after J
+    cl[..., :15] = hm.permute(0, 1, 3, 4, 2)
+    clh = ChannelsLastHeatmaps(cl, 15)
+    p1, o1, f1 = layer.forward_batch(hm, meta, props, mask, cams, rt)
+    p2, o2, f2 = layer.forward_batch(clh, meta, props, mask, cams, rt)
+    assert torch.equal(p1, p2) and torch.equal(o1, o2) and torch.equal(f1, f2)
+    a = layer.forward_planes(hm, 1, meta, props[1], cams, rt)
+    b = layer.forward_planes(attach(hm.clone(), clh), 1, meta, props[1], cams, rt)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_forward_batch_mixed_sequences(gpu_device):
+    """forward_batch over frames of two sequences (one launch per sequence,
+    scattered back into (frame, proposal) order) == per-frame forward_planes."""
+    w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, frames=3)
+    cams = dict(cams)
+    cams["other"] = list(reversed(list(cams[seq])))  # another sequence: same cameras, another order
+    rng = np.random.default_rng(10)
+    props = torch.from_numpy(np.stack([_props(w, f, rng, 2) for f in range(3)])).to(gpu_device)
+    mask = torch.ones(props.shape[:2], dtype=torch.bool, device=gpu_device)
+    mask[0, 1] = False
+    meta = {"seq": [seq, "other", seq]}
+    planes, offset, frame_of = layer.forward_batch(hm, meta, props, mask, cams, rt)
+    P = planes.shape[0] // 3
+    rows, offs = [], []
+    for b in range(3):
+        pl, off = layer.forward_planes(hm, b, meta, props[b][mask[b]], cams, rt)
+        rows.append(pl.view(3, -1, *pl.shape[1:]))
+        offs.append(off)
+    ref = torch.cat(rows, dim=1).reshape(3 * P, *planes.shape[1:])
+    assert torch.equal(planes, ref) and torch.equal(offset, torch.cat(offs))
+    assert frame_of.tolist() == mask.nonzero()[:, 0].tolist()

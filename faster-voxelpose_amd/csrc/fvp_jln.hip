@@ -104,6 +104,46 @@ __global__ __launch_bounds__(256) void softargmax_kernel(const float *__restrict
     }
 }
 
+// Rows longer than the register-resident kernel holds (person cubes beyond
+// 90^3): the same arithmetic in two passes over the row (max, then exp sums).
+__global__ __launch_bounds__(256) void softargmax_stream_kernel(const float *__restrict__ feat,
+                                                                const float *__restrict__ grids,
+                                                                const float *__restrict__ offset, int P, int J,
+                                                                int S2, float beta, float *__restrict__ pose,
+                                                                float *__restrict__ maxprob) {
+    __shared__ float red[4];
+    const int row = blockIdx.x;  // (plane, p, j)
+    const int plane = row / (P * J);
+    const int p = (row / J) % P;
+    const float *__restrict__ x = feat + (size_t)row * S2;
+    const float2 *__restrict__ g = reinterpret_cast<const float2 *>(grids + (size_t)plane * S2 * 2);
+    float m = -INFINITY;
+    for (int i = threadIdx.x; i < S2; i += 256) m = fmaxf(m, beta * x[i]);
+    m = block_reduce_max(m, red);
+    float s = 0.f, sx = 0.f, sy = 0.f;
+    for (int i = threadIdx.x; i < S2; i += 256) {
+        const float e = expf(beta * x[i] - m);
+        const float2 c = g[i];
+        s += e;
+        sx = __builtin_fmaf(e, c.x, sx);
+        sy = __builtin_fmaf(e, c.y, sy);
+    }
+    s = block_reduce_sum(s, red);
+    sx = block_reduce_sum(sx, red);
+    sy = block_reduce_sum(sy, red);
+    if (threadIdx.x == 0) {
+        float ox = 0.f, oy = 0.f;
+        if (offset) {
+            const float *o = offset + (size_t)p * 3;
+            ox = plane == 2 ? o[1] : o[0];
+            oy = plane == 0 ? o[1] : o[2];
+        }
+        pose[(size_t)row * 2 + 0] = sx / s + ox;
+        pose[(size_t)row * 2 + 1] = sy / s + oy;
+        maxprob[row] = 1.0f / s;
+    }
+}
+
 // pose [3][P][J][2], weights [3P][J] (WeightNet output, plane-major), maxprob [3][P][J]
 // fused [P][J][3], confs [P]
 __global__ __launch_bounds__(64) void fuse_kernel(const float *__restrict__ pose, const float *__restrict__ weights,
@@ -226,9 +266,11 @@ extern "C" int fvp_soft_argmax(const float *features, int P, int J, int S2, cons
     if (!features || !center_grid || !pose || !maxprob) return FVP_ERR_NULL;
     if (P < 0 || J <= 0 || S2 <= 0) return FVP_ERR_SHAPE;
     if ((long long)3 * P * J > 0x7fffffffLL) return FVP_ERR_SHAPE;
-    if (S2 > 256 * 4 * 8) return FVP_ERR_SHAPE;  // up to 8192 cells per plane (64x64 = 4096)
     const dim3 grid((unsigned)(3 * P * J));
-    if (S2 <= 256 * 4 * 4)
+    if (S2 > 256 * 4 * 8)  // beyond 8192 cells per plane (64x64 = 4096): two passes over the row
+        hipLaunchKernelGGL(fvp::softargmax_stream_kernel, grid, dim3(256), 0, (hipStream_t)stream, features,
+                           center_grid, offset, P, J, S2, beta, pose, maxprob);
+    else if (S2 <= 256 * 4 * 4)
         hipLaunchKernelGGL(fvp::softargmax_kernel<4>, grid, dim3(256), 0, (hipStream_t)stream, features, center_grid,
                            offset, P, J, S2, beta, pose, maxprob);
     else

@@ -25,16 +25,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base,
 // of a wave cover 64/LPV consecutive pixels -> coalesced plane reads), writes
 // one float4 (a wave writes a contiguous 1 KiB run; NF > 1: runs of JP*4 B,
 // the NF frames of a group interleaved per pixel: [b/NF][V][H*W][NF][JP]).
+// (J joints of a slice; Jst = the planes per (frame, view) of the source)
 template <int LPV, typename T, int NF = 1>
 __global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict__ hm, float4 *__restrict__ cl, int J,
-                                                             int HW, int V, long long total_px) {
+                                                             int Jst, int HW, int V, long long total_px) {
     const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
     const long long pxg = gid / LPV;
     const int q = (int)(gid - pxg * LPV);
     if (pxg >= total_px) return;
     const long long bv = pxg / HW;
     const int pix = (int)(pxg - bv * HW);
-    const T *__restrict__ src = hm + (size_t)bv * J * HW + pix;
+    const T *__restrict__ src = hm + (size_t)bv * Jst * HW + pix;
     const int j = 4 * q;
     float4 o;
     o.x = (j + 0 < J) ? to_f32(src[(size_t)(j + 0) * HW]) : 0.f;
@@ -186,11 +187,11 @@ inline size_t cl_frame_bytes(int V, int J, int H, int W) {
 }
 
 template <int LPV, typename T, int NF = 1>
-inline void launch_layout(const T *hm, int nb, int V, int J, int H, int W, float *cl, hipStream_t s) {
+inline void launch_layout(const T *hm, int nb, int V, int J, int Jst, int H, int W, float *cl, hipStream_t s) {
     const long long px = (long long)nb * V * H * W;
     const long long threads = px * LPV;
     hipLaunchKernelGGL((heatmaps_to_cl_kernel<LPV, T, NF>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                       hm, reinterpret_cast<float4 *>(cl), J, H * W, V, px);
+                       hm, reinterpret_cast<float4 *>(cl), J, Jst, H * W, V, px);
 }
 
 }  // namespace fvp

@@ -98,6 +98,26 @@ __global__ __launch_bounds__(256) void max_planes_kernel(const float *__restrict
     }
 }
 
+// Planes of cubes deeper than 64 (one thread per plane cell, a loop over the
+// reduced axis; NaN-propagating like torch.max).
+__global__ __launch_bounds__(256) void max_planes_generic_kernel(const float *__restrict__ cubes,
+                                                                 float *__restrict__ planes, int P, int J, int S) {
+    const size_t SS = (size_t)S * S;
+    const size_t per_plane = (size_t)P * J * SS;
+    const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= 3 * per_plane) return;
+    const int k = (int)(e / per_plane);  // 0 xy (max z), 1 xz (max y), 2 yz (max x)
+    const size_t r = e - k * per_plane;
+    const size_t pj = r / SS;
+    const int a = (int)((r - pj * SS) / S), b = (int)(r - pj * SS - (size_t)a * S);
+    const float *__restrict__ c = cubes + pj * SS * S;
+    const size_t base = k == 0 ? ((size_t)a * S + b) * S : k == 1 ? (size_t)a * SS + b : (size_t)a * S + b;
+    const size_t step = k == 0 ? 1 : k == 1 ? (size_t)S : SS;
+    float m = -INFINITY;
+    for (int t = 0; t < S; ++t) m = nanmax(m, c[base + t * step]);
+    planes[e] = m;
+}
+
 // Channels-last per-person kernel (batched over frames, optional fused planes).
 // Block = (proposal p, group of YG y-rows); threads = 64 z-lanes x LPV joint
 // quads.  The block walks x = 0..S-1 and, for each x, its YG rows:
@@ -124,8 +144,9 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                                                              const float *__restrict__ props,
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
                                                              float *__restrict__ cubes, float *__restrict__ planes,
-                                                             float *__restrict__ offset, int P, int V, int J, int H,
-                                                             int W, int xmap, int xsplit, unsigned pix_bytes) {
+                                                             float *__restrict__ offset, int P, int V, int J, int Jst,
+                                                             int H, int W, int xmap, int xsplit, int zsplit,
+                                                             unsigned pix_bytes) {
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
@@ -135,18 +156,20 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     // with round-robin placement)
     const int L = xmap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     // block -> (proposal, row group, x part): a proposal's blocks stay contiguous
-    const int p = L / (ngroups * xsplit);
-    const int rem = L - p * ngroups * xsplit;
-    const int yg0 = (rem / xsplit) * YG;
-    const int xpart = rem - (rem / xsplit) * xsplit;
+    const int parts = xsplit * zsplit;  // x parts x 64-deep z chunks per row group
+    const int p = L / (ngroups * parts);
+    const int rem = L - p * ngroups * parts;
+    const int yg0 = (rem / parts) * YG;
+    const int part = rem - (rem / parts) * parts;
+    const int xpart = part % xsplit, zc = part / xsplit;
     const Window w = person_window(props + (size_t)p * 7, s);
-    if (offset && yg0 == 0 && xpart == 0 && threadIdx.x < 3) {
+    if (offset && yg0 == 0 && part == 0 && threadIdx.x < 3) {
         const int a = threadIdx.x;
         offset[(size_t)p * 3 + a] =
             ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
     }
     const int lane = threadIdx.x & 63;
-    const int zl = threadIdx.x / LPV, q = threadIdx.x % LPV;
+    const int zl = zc * 64 + (int)threadIdx.x / LPV, q = threadIdx.x % LPV;
     const int b = frame_of ? frame_of[p] : 0;
     const unsigned HW = (unsigned)(H * W);
     const unsigned img = HW * pix_bytes;  // pix_bytes >= JP * 4: one channels-last pixel
@@ -169,9 +192,10 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     const char *__restrict__ frame_cl = (const char *)cl + (size_t)b * V * img;
     const size_t SS = (size_t)SY * SZ;
     const size_t S3 = (size_t)SX * SS;
-    float *xy_pl = planes ? planes + (size_t)p * J * SX * SY : nullptr;
-    float *xz_pl = planes ? planes + ((size_t)P + p) * J * SX * SZ : nullptr;
-    float *yz_pl = planes ? planes + ((size_t)2 * P + p) * J * SY * SZ : nullptr;
+    // (planes / cubes start at this joint slice; Jst joints per proposal)
+    float *xy_pl = planes ? planes + (size_t)p * Jst * SX * SY : nullptr;
+    float *xz_pl = planes ? planes + ((size_t)P + p) * Jst * SX * SZ : nullptr;
+    float *yz_pl = planes ? planes + ((size_t)2 * P + p) * Jst * SY * SZ : nullptr;
     const bool zok = zl < SZ;
     const int gz = w.ctl[2] + zl;
     const bool zin = zok && gz >= w.start[2] && gz < w.end[2];
@@ -290,7 +314,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             if (cubes && zok && y < SY) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (4 * q + k < J) cubes[((size_t)p * J + 4 * q + k) * S3 + ((size_t)x * SY + y) * SZ + zl] = o[k];
+                    if (4 * q + k < J) cubes[((size_t)p * Jst + 4 * q + k) * S3 + ((size_t)x * SY + y) * SZ + zl] = o[k];
             }
             if (planes) {
 #pragma unroll
@@ -346,7 +370,8 @@ static int person_xsplit(int P, int SY) {
 template <int LPV, bool OTF, bool CASC>
 static void launch_person_cl(const float *cl, const float *fgrid, const PersonCoords &pc, const float *props,
                              const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
-                             float *offset, int P, int V, int J, int H, int W, unsigned pix_bytes, hipStream_t st) {
+                             float *offset, int P, int V, int J, int Jst, int H, int W, unsigned pix_bytes,
+                             hipStream_t st) {
     const int SY = s.bins[1];
     // one y-row per block (the kernel also takes YG rows): with the planes-only
     // fast path for x-planes outside the window, rows are the finer and better
@@ -355,9 +380,12 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // the fast path).  XCD-aware placement keeps a proposal's rows on one XCD.
     // Small launches (per-frame calls) split each row's x walk over 2-4 blocks
     // (the yz maxima then go through atomics into a pre-zeroed plane).
-    const int xmap = 1, xsplit = person_xsplit(P, SY);
-    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF, CASC>), dim3((unsigned)(P * SY * xsplit)), dim3(64 * LPV), 0, st, cl,
-                       fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, H, W, xmap, xsplit, pix_bytes);
+    // Cubes deeper than 64 run as 64-deep z chunks, one block each (the xy and xz
+    // maxima already combine across blocks through atomics; yz is per (y, z)).
+    const int xmap = 1, xsplit = person_xsplit(P, SY), zsplit = (s.bins[2] + 63) / 64;
+    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF, CASC>), dim3((unsigned)((long long)P * SY * xsplit * zsplit)),
+                       dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H,
+                       W, xmap, xsplit, zsplit, pix_bytes);
 }
 
 }  // namespace fvp
@@ -365,7 +393,13 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
 extern "C" int fvp_max_planes(const float *cubes, int P, int J, int S, float *planes, void *stream) {
     if (!cubes || !planes) return FVP_ERR_NULL;
     if (P <= 0) return FVP_OK;
-    if (J <= 0 || S <= 0 || S > 64) return FVP_ERR_SHAPE;
+    if (J <= 0 || S <= 0 || S > 4096) return FVP_ERR_SHAPE;
+    if (S > 64) {
+        const size_t n = (size_t)3 * P * J * S * S;
+        hipLaunchKernelGGL(fvp::max_planes_generic_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, cubes, planes, P, J, S);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(fvp::max_planes_kernel, dim3(P * J), dim3(256), 0, (hipStream_t)stream, cubes, planes, P, J,
                        S);
     return (int)hipGetLastError();
@@ -373,13 +407,16 @@ extern "C" int fvp_max_planes(const float *cubes, int P, int J, int S, float *pl
 
 extern "C" size_t fvp_person_workspace_bytes(int B, int V, int J, int H, int W) {
     if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
-    return (size_t)B * fvp::cl_frame_bytes(V, J, H, W);
+    return (size_t)B * fvp::cl_frame_bytes(V, J < 32 ? J : 32, H, W);  // one joint slice at a time
 }
 
 namespace fvp {
 
 // heatmaps: planar [B][V][J][H][W] (cp == 0: re-laid out into the workspace
 // first) or channels-last [B][V][H][W][cp] (read in place, no workspace).
+// More than kPersonSlice joints run in joint slices (layout + launch each).
+constexpr int kPersonSlice = 32;
+
 static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J, int H, int W,
                              const float *fine_grid, const PersonCoords *pc, const fvp_person_spec *spec,
                              const float *proposals, const int32_t *frame_of, int P, float *cubes, float *planes,
@@ -390,22 +427,23 @@ static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J,
     if (B <= 0 || V <= 0 || V > FVP_MAX_VIEWS || J <= 0 || J > FVP_MAX_JOINTS || H < 2 || W < 2) return FVP_ERR_SHAPE;
     if (pc && V > 64) return FVP_ERR_SHAPE;  // camera records staged in LDS
     const int SX = spec->bins[0], SY = spec->bins[1], SZ = spec->bins[2];
-    if (SX <= 0 || SY <= 0 || SZ <= 0 || SZ > 64 || spec->fine[0] <= 1 || spec->fine[1] <= 1 || spec->fine[2] <= 1)
+    if (SX <= 0 || SY <= 0 || SZ <= 0 || SX > 4096 || SY > 4096 || SZ > 4096 || spec->fine[0] <= 1 ||
+        spec->fine[1] <= 1 || spec->fine[2] <= 1)
         return FVP_ERR_SHAPE;
     if (planes && !(SX == SY && SY == SZ)) return FVP_ERR_SHAPE;  // torch.cat of the planes needs a cubic volume
     // packed fine grid addressed with 32-bit byte offsets
     if (!pc && (long long)spec->fine[0] * spec->fine[1] * spec->fine[2] * FVP_GRID_SLOTS(V) * 8 > 0xfffff000LL)
         return FVP_ERR_SHAPE;
-    const int JP = 4 * lanes_per_voxel(J);
+    const int J1 = J < kPersonSlice ? J : kPersonSlice;
     if (cp) {
-        if (cp < JP || cp % 4 || (size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;
+        const int jl = ((J - 1) / kPersonSlice) * kPersonSlice;
+        if (cp % 4 || cp < jl + 4 * lanes_per_voxel(J - jl) || (size_t)H * W * cp * 4 > 0x7fffffffull)
+            return FVP_ERR_SHAPE;
     } else {
-        const size_t need = (size_t)B * cl_frame_bytes(V, J, H, W);
+        const size_t need = (size_t)B * cl_frame_bytes(V, J1, H, W);
         if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
     }
     hipStream_t st = (hipStream_t)stream;
-    const float *cl = cp ? heatmaps : reinterpret_cast<const float *>(workspace);
-    const unsigned pix_bytes = 4u * (unsigned)(cp ? cp : JP);
     if (planes) {  // xy, xz (and yz when x is split) are reduced with atomicMax over non-negative floats: from +0
         const size_t n = (person_xsplit(P, SY) > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
         const hipError_t e = hipMemsetAsync(planes, 0, n * 4, st);
@@ -413,28 +451,36 @@ static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J,
     }
     const PersonCoords none{};
     const PersonCoords &c = pc ? *pc : none;
+    const size_t HW = (size_t)H * W, S2 = (size_t)SX * SY, S3 = S2 * SZ;
+    for (int j0 = 0; j0 < J; j0 += kPersonSlice) {
+        const int Jc = J - j0 < kPersonSlice ? J - j0 : kPersonSlice;
+        const float *cl = cp ? heatmaps + j0 : reinterpret_cast<const float *>(workspace);
+        const unsigned pix_bytes = 4u * (unsigned)(cp ? cp : 4 * lanes_per_voxel(Jc));
+        float *cb = cubes ? cubes + j0 * S3 : nullptr;
+        float *pl = planes ? planes + j0 * S2 : nullptr;
 #define FVP_PERSON_CASE(L)                                                                                            \
-    if (!cp) launch_layout<L, float>(heatmaps, B, V, J, H, W, reinterpret_cast<float *>(workspace), st);             \
+    if (!cp) launch_layout<L, float>(heatmaps + j0 * HW, B, V, Jc, J, H, W, reinterpret_cast<float *>(workspace), st); \
     if (pc && V > 16)                                                                                                 \
-        launch_person_cl<L, true, true>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J, H, \
+        launch_person_cl<L, true, true>(cl, nullptr, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J, H,   \
                                         W, pix_bytes, st);                                                            \
     else if (pc)                                                                                                      \
-        launch_person_cl<L, true, false>(cl, nullptr, c, proposals, frame_of, *spec, cubes, planes, offset, P, V, J,  \
-                                         H, W, pix_bytes, st);                                                        \
+        launch_person_cl<L, true, false>(cl, nullptr, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J, H,  \
+                                         W, pix_bytes, st);                                                           \
     else if (V > 16)                                                                                                  \
-        launch_person_cl<L, false, true>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V,   \
-                                         J, H, W, pix_bytes, st);                                                     \
+        launch_person_cl<L, false, true>(cl, fine_grid, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J,   \
+                                         H, W, pix_bytes, st);                                                        \
     else                                                                                                              \
-        launch_person_cl<L, false, false>(cl, fine_grid, c, proposals, frame_of, *spec, cubes, planes, offset, P, V,  \
-                                          J, H, W, pix_bytes, st);                                                    \
+        launch_person_cl<L, false, false>(cl, fine_grid, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J,  \
+                                          H, W, pix_bytes, st);                                                       \
     break;
-    switch (lanes_per_voxel(J)) {
-        case 1: FVP_PERSON_CASE(1)
-        case 2: FVP_PERSON_CASE(2)
-        case 4: FVP_PERSON_CASE(4)
-        default: FVP_PERSON_CASE(8)
-    }
+        switch (lanes_per_voxel(Jc)) {
+            case 1: FVP_PERSON_CASE(1)
+            case 2: FVP_PERSON_CASE(2)
+            case 4: FVP_PERSON_CASE(4)
+            default: FVP_PERSON_CASE(8)
+        }
 #undef FVP_PERSON_CASE
+    }
     return (int)hipGetLastError();
 }
 

@@ -53,8 +53,8 @@ template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
-                                                       int H, int W, int X, int Y, int Z, int cols, int col_blocks,
-                                                       int SP, int band, unsigned pixb) {
+                                                       int Jst, int H, int W, int X, int Y, int Z, int cols,
+                                                       int col_blocks, int SP, int band, unsigned pixb) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
@@ -240,7 +240,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         const size_t bf = (size_t)(b + f);
         if (cube) {
             for (int j = 0; j < J; ++j) {
-                float *__restrict__ dst = cube + (bf * J + j) * N + n0;
+                float *__restrict__ dst = cube + (bf * Jst + j) * N + n0;
                 for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
             }
         }
@@ -250,7 +250,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 const float *s = fst + j * SP + cc * Z;
                 float m = -INFINITY;
                 for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
-                __builtin_nontemporal_store(m, xy + (bf * J + j) * XY + c0 + cc);
+                __builtin_nontemporal_store(m, xy + (bf * Jst + j) * XY + c0 + cc);
             }
         }
     }
@@ -265,22 +265,23 @@ template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __global__ __launch_bounds__(256, NF == 1 ? 8 : 5) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
-                                                          int J, int H, int W, int X, int Y, int Z, int cols,
-                                                          int col_blocks, int SP, int band, unsigned pixb) {
+                                                          int J, int Jst, int H, int W, int X, int Y, int Z,
+                                                          int cols, int col_blocks, int SP, int band, unsigned pixb) {
     static_assert(!OTF, "grid kernel");
-    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
-                                  band, pixb);
+    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
+                                            col_blocks, SP, band, pixb);
 }
 
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restrict__ tab, CoordSource src,
                                                             const int32_t *__restrict__ grid_index, int frame0,
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
-                                                            int J, int H, int W, int X, int Y, int Z, int cols,
-                                                            int col_blocks, int SP, int band, unsigned pixb) {
+                                                            int J, int Jst, int H, int W, int X, int Y, int Z,
+                                                            int cols, int col_blocks, int SP, int band,
+                                                            unsigned pixb) {
     static_assert(OTF, "on-the-fly kernel");
-    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, H, W, X, Y, Z, cols, col_blocks, SP,
-                                  band, pixb);
+    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
+                                            col_blocks, SP, band, pixb);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -358,61 +359,74 @@ static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg 
 
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 static void launch_gather(const void *tab, int f0, int nb, const GatherCfg &c, const CoordSource &src,
-                          const int32_t *grid_index, int V, int J, int H, int W, int X, int Y, int Z, float *cube,
-                          float *xy, unsigned pixb, hipStream_t s) {
+                          const int32_t *grid_index, int V, int J, int Jst, int H, int W, int X, int Y, int Z,
+                          float *cube, float *xy, unsigned pixb, hipStream_t s) {
     const dim3 grid((unsigned)(nb / NF * c.col_blocks));
     if constexpr (OTF)
         hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
-                           grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band, pixb);
+                           grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
+                           pixb);
     else
         hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
-                           grid_index, f0, cube, xy, V, J, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band, pixb);
+                           grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
+                           pixb);
 }
+
+// One voxelize call's shapes.  Heatmaps with more than kJointSlice joints run
+// in joint slices of kJointSlice (a layout pass + gather per slice): J is the
+// slice's joint count, Jst the full count (the frame stride of the input
+// planes and of the cube / xy outputs, whose pointers start at the slice).
+constexpr int kJointSlice = 32;
+
+struct VoxJob {
+    int V, J, Jst, H, W, X, Y, Z;
+    const int32_t *grid_index;
+    float *cube, *xy;
+};
 
 // Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
 // layout pass into the workspace, then the gather, NF frames per table entry.
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, typename T>
-static int run_chunks(const T *hm, int first, int last, int V, int J, int H, int W, const CoordSource &src,
-                      const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
+static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const CoordSource &src, void *ws,
+                      hipStream_t s) {
     const bool half = sizeof(T) == 2;
     const int B = last - first;
-    const int chunk = max(NF, chunk_frames(B, V, J, H, W, half) / NF * NF);
+    const int chunk = max(NF, chunk_frames(B, j.V, j.J, j.H, j.W, half) / NF * NF);
     GatherCfg c;
-    if (gather_cfg<LPV, OTF>(min(chunk, B), NF, V, X, Y, Z, c) != FVP_OK) return FVP_ERR_SHAPE;
-    const size_t frame_elems = (size_t)V * J * H * W;
+    if (gather_cfg<LPV, OTF>(min(chunk, B), NF, j.V, j.X, j.Y, j.Z, c) != FVP_OK) return FVP_ERR_SHAPE;
+    const size_t frame_elems = (size_t)j.V * j.Jst * j.H * j.W;
     for (int f0 = first; f0 < last; f0 += chunk) {
         const int nb = min(chunk, last - f0);
         const T *hsrc = hm + (size_t)f0 * frame_elems;
-        if constexpr (PAIR) {
-            const long long total = (long long)nb * V * H * (W + 1) * 4;
+        if constexpr (PAIR) {  // (J <= 16: never sliced)
+            const long long total = (long long)nb * j.V * j.H * (j.W + 1) * 4;
             hipLaunchKernelGGL((heatmaps_to_pairs_kernel<_Float16, NF>), dim3((unsigned)((total + 255) / 256)),
                                dim3(256), 0, s, reinterpret_cast<const _Float16 *>(hsrc), reinterpret_cast<uint4 *>(ws),
-                               J, H, W, V, total);
+                               j.J, j.H, j.W, j.V, total);
         } else {
-            launch_layout<LPV, T, NF>(hsrc, nb, V, J, H, W, reinterpret_cast<float *>(ws), s);
+            launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
         }
-        launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, grid_index, V, J, H, W, X, Y, Z, cube, xy,
-                                               4u * 4u * LPV, s);
+        launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
+                                               j.Z, j.cube, j.xy, 4u * 4u * LPV, s);
     }
     return (int)hipGetLastError();
 }
 
-// Heatmaps already channels-last ([B][V][H][W][cp] fp32, cp >= JP, e.g. the
-// PoseResNet backbone's NHWC output): the gather reads them in place, one
-// launch for the whole batch, no layout pass and no workspace.
+// Heatmaps already channels-last ([B][V][H][W][cp] fp32, the slice's joints
+// from hm_cl on, e.g. the PoseResNet backbone's NHWC output): the gather reads
+// them in place, one launch for the whole batch, no layout pass, no workspace.
 template <bool OTF, bool CASC>
-static int run_direct(const float *hm_cl, int cp, int B, int V, int J, int H, int W, const CoordSource &src,
-                      const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, hipStream_t s) {
+static int run_direct(const float *hm_cl, int cp, int B, const VoxJob &j, const CoordSource &src, hipStream_t s) {
     const unsigned pixb = (unsigned)cp * 4u;
     auto go = [&](auto lpv) -> int {
         constexpr int LPV = decltype(lpv)::value;
         GatherCfg c;
-        if (gather_cfg<LPV, OTF>(B, 1, V, X, Y, Z, c) != FVP_OK) return FVP_ERR_SHAPE;
-        launch_gather<LPV, false, OTF, CASC, 1>(hm_cl, 0, B, c, src, grid_index, V, J, H, W, X, Y, Z, cube, xy, pixb,
-                                               s);
+        if (gather_cfg<LPV, OTF>(B, 1, j.V, j.X, j.Y, j.Z, c) != FVP_OK) return FVP_ERR_SHAPE;
+        launch_gather<LPV, false, OTF, CASC, 1>(hm_cl, 0, B, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X,
+                                               j.Y, j.Z, j.cube, j.xy, pixb, s);
         return (int)hipGetLastError();
     };
-    switch (lanes_per_voxel(J)) {
+    switch (lanes_per_voxel(j.J)) {
         case 1: return go(std::integral_constant<int, 1>{});
         case 2: return go(std::integral_constant<int, 2>{});
         case 4: return go(std::integral_constant<int, 4>{});
@@ -428,46 +442,70 @@ static int run_direct(const float *hm_cl, int cp, int B, int V, int J, int H, in
 // doubles).  Frames of a pair must share one sampling grid, so batches that
 // mix sequences (grid_index given) and an odd last frame run at NF = 1.
 template <int LPV, bool PAIR, bool OTF, bool CASC, typename T>
-static int run_frames(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
-                      const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws, hipStream_t s) {
+static int run_frames(const T *hm, int B, const VoxJob &j, const CoordSource &src, void *ws, hipStream_t s) {
     if constexpr (PAIR) {
-        if (!grid_index && chunk_frames(B, V, J, H, W, sizeof(T) == 2) >= 2) {  // the workspace holds >= 2 frames
+        if (!j.grid_index && chunk_frames(B, j.V, j.J, j.H, j.W, sizeof(T) == 2) >= 2) {  // workspace holds >= 2 frames
             const int even = B & ~1;
-            const int st = run_chunks<LPV, PAIR, OTF, CASC, 2, T>(hm, 0, even, V, J, H, W, src, grid_index, X, Y, Z,
-                                                                  cube, xy, ws, s);
+            const int st = run_chunks<LPV, PAIR, OTF, CASC, 2, T>(hm, 0, even, j, src, ws, s);
             if (st != FVP_OK || even == B) return st;
-            return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, even, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
-                                                          ws, s);
+            return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, even, B, j, src, ws, s);
         }
     }
-    return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, 0, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+    return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, 0, B, j, src, ws, s);
 }
 
 template <bool OTF, bool CASC, typename T>
-static int voxelize_lpv(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
-                        const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws,
-                        hipStream_t s) {
+static int voxelize_lpv(const T *hm, int B, const VoxJob &j, const CoordSource &src, void *ws, hipStream_t s) {
     const bool half = sizeof(T) == 2;
-    if (use_pairs(J, half))
-        return run_frames<4, true, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-    switch (lanes_per_voxel(J)) {
-        case 1: return run_frames<1, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 2: return run_frames<2, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        case 4: return run_frames<4, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-        default: return run_frames<8, false, OTF, CASC, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+    if (use_pairs(j.Jst, half)) return run_frames<4, true, OTF, CASC, T>(hm, B, j, src, ws, s);
+    switch (lanes_per_voxel(j.J)) {
+        case 1: return run_frames<1, false, OTF, CASC, T>(hm, B, j, src, ws, s);
+        case 2: return run_frames<2, false, OTF, CASC, T>(hm, B, j, src, ws, s);
+        case 4: return run_frames<4, false, OTF, CASC, T>(hm, B, j, src, ws, s);
+        default: return run_frames<8, false, OTF, CASC, T>(hm, B, j, src, ws, s);
     }
 }
+
+// Joints of the first slice (all of them up to kJointSlice).
+static int slice_joints(int J) { return J < kJointSlice ? J : kJointSlice; }
 
 template <bool OTF, typename T>
 static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const CoordSource &src,
                         const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, void *ws,
                         size_t ws_bytes, hipStream_t s) {
     const bool half = sizeof(T) == 2;
-    const size_t need = (size_t)chunk_frames(B, V, J, H, W, half) * frame_bytes(V, J, H, W, half);
+    const int J1 = slice_joints(J);
+    const size_t need = (size_t)chunk_frames(B, V, J1, H, W, half) * frame_bytes(V, J1, H, W, half);
     if (!ws || ws_bytes < need) return FVP_ERR_WORKSPACE;
-    if (frame_bytes(1, J, H, W, half) > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets
-    if (V > 16) return voxelize_lpv<OTF, true, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
-    return voxelize_lpv<OTF, false, T>(hm, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, ws, s);
+    if (frame_bytes(1, J1, H, W, half) > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets
+    const size_t N = (size_t)X * Y * Z, XY = (size_t)X * Y, HW = (size_t)H * W;
+    for (int j0 = 0; j0 < J; j0 += kJointSlice) {
+        const VoxJob job{V, min(kJointSlice, J - j0), J, H, W, X, Y, Z, grid_index, cube ? cube + j0 * N : nullptr,
+                         xy ? xy + j0 * XY : nullptr};
+        const T *h = hm + j0 * HW;
+        const int st = V > 16 ? voxelize_lpv<OTF, true, T>(h, B, job, src, ws, s)
+                              : voxelize_lpv<OTF, false, T>(h, B, job, src, ws, s);
+        if (st != FVP_OK) return st;
+    }
+    return FVP_OK;
+}
+
+// Channels-last input: the slice's channels start at hm_cl + j0 (cp >= j0 + 4 * LPV(slice) for every slice).
+template <bool OTF>
+static int voxelize_cl_any(const float *hm_cl, int cp, int B, int V, int J, int H, int W, const CoordSource &src,
+                           const int32_t *grid_index, int X, int Y, int Z, float *cube, float *xy, hipStream_t s) {
+    const int jl = ((J - 1) / kJointSlice) * kJointSlice;  // first joint of the last slice
+    if (cp % 4 || cp < jl + 4 * lanes_per_voxel(J - jl)) return FVP_ERR_SHAPE;
+    if ((size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets per camera image
+    const size_t N = (size_t)X * Y * Z, XY = (size_t)X * Y;
+    for (int j0 = 0; j0 < J; j0 += kJointSlice) {
+        const VoxJob job{V, min(kJointSlice, J - j0), J, H, W, X, Y, Z, grid_index, cube ? cube + j0 * N : nullptr,
+                         xy ? xy + j0 * XY : nullptr};
+        const int st = V > 16 ? run_direct<OTF, true>(hm_cl + j0, cp, B, job, src, s)
+                              : run_direct<OTF, false>(hm_cl + j0, cp, B, job, src, s);
+        if (st != FVP_OK) return st;
+    }
+    return FVP_OK;
 }
 
 static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, const float *grids, int X, int Y, int Z) {
@@ -482,7 +520,8 @@ static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, c
 
 static size_t workspace_bytes(int B, int V, int J, int H, int W, bool half) {
     if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
-    return (size_t)chunk_frames(B, V, J, H, W, half) * frame_bytes(V, J, H, W, half);
+    const int J1 = slice_joints(J);  // one joint slice's copy at a time
+    return (size_t)chunk_frames(B, V, J1, H, W, half) * frame_bytes(V, J1, H, W, half);
 }
 
 }  // namespace fvp
@@ -558,16 +597,11 @@ extern "C" int fvp_voxelize_cl(const float *heatmaps_cl, int cp, int B, int V, i
                                float *xy, void *stream) {
     const int st = fvp::check_args(heatmaps_cl, B, V, J, H, W, packed_grids, X, Y, Z);
     if (st != FVP_OK) return st;
-    if (cp < 4 * fvp::lanes_per_voxel(J) || cp % 4) return FVP_ERR_SHAPE;
-    if ((size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;  // 32-bit tap offsets per camera image
     if (!cube && !xy) return FVP_OK;
     fvp::CoordSource src{};
     src.grids = packed_grids;
-    if (V > 16)
-        return fvp::run_direct<false, true>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
-                                            (hipStream_t)stream);
-    return fvp::run_direct<false, false>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
-                                         (hipStream_t)stream);
+    return fvp::voxelize_cl_any<false>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                       (hipStream_t)stream);
 }
 
 extern "C" int fvp_voxelize_cl_cams(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
@@ -579,17 +613,12 @@ extern "C" int fvp_voxelize_cl_cams(const float *heatmaps_cl, int cp, int B, int
     const int st = fvp::check_args(heatmaps_cl, B, V, J, H, W, cams, X, Y, Z);
     if (st != FVP_OK) return st;
     if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
-    if (cp < 4 * fvp::lanes_per_voxel(J) || cp % 4) return FVP_ERR_SHAPE;
-    if ((size_t)H * W * cp * 4 > 0x7fffffffull) return FVP_ERR_SHAPE;
     if (!cube && !xy) return FVP_OK;
     fvp::CoordSource src{};
     src.cams = cams;
     src.resize_t = resize_t;
     src.gs = *grid;
     src.im = *img;
-    if (V > 16)
-        return fvp::run_direct<true, true>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
-                                           (hipStream_t)stream);
-    return fvp::run_direct<true, false>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
-                                        (hipStream_t)stream);
+    return fvp::voxelize_cl_any<true>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
+                                      (hipStream_t)stream);
 }

@@ -126,7 +126,7 @@ def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Opt
     lib = _lib.load()
     ws_bytes = (lib.fvp_voxelize_f16_workspace_bytes if half else lib.fvp_voxelize_workspace_bytes)(B, V, J, H, W)
     if ws_bytes == 0:
-        raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+        raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 1024)")
     ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
     _lib.call("fvp_voxelize_f16" if half else "fvp_voxelize", _ptr(hm), B, V, J, H, W, _ptr(pg), _ptr(gi), X, Y, Z,
               _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _ptr(ws), ws_bytes, _stream(hm))
@@ -164,7 +164,7 @@ def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Option
     lib = _lib.load()
     ws_bytes = (lib.fvp_voxelize_f16_workspace_bytes if half else lib.fvp_voxelize_workspace_bytes)(B, V, J, H, W)
     if ws_bytes == 0:
-        raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+        raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 1024)")
     ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
     g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
     im = ImageSpec(ori_max, img_w, img_h, W, H)
@@ -392,7 +392,7 @@ def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: to
     if P > 0:
         ws_bytes = _lib.load().fvp_person_workspace_bytes(B, V, J, H, W)
         if ws_bytes == 0:
-            raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+            raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 1024)")
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
         spec = PersonSpec(_i3(fine), _f3(scale), _f3(bias), _f3(whole_size), _f3(ind_size), _i3(bins))
         _lib.call("fvp_person_planes", _ptr(hm), B, V, J, H, W, _ptr(fg), spec, _ptr(pc), _ptr(fo), P,
@@ -468,7 +468,7 @@ def person_planes_cams(heatmaps: torch.Tensor, cams: torch.Tensor, resize_t: tor
     if P > 0:
         ws_bytes = _lib.load().fvp_person_workspace_bytes(B, V, J, H, W)
         if ws_bytes == 0:
-            raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 32)")
+            raise _lib.FvpError(f"fvp: unsupported heatmap shape {tuple(hm.shape)} (J <= 1024)")
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
         spec = PersonSpec(_i3(fine), _f3(scale), _f3(bias), _f3(whole_size), _f3(ind_size), _i3(bins))
         g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(fine))

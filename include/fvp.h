@@ -32,7 +32,10 @@ extern "C" {
 #endif
 
 #define FVP_ABI_VERSION 8
-#define FVP_MAX_JOINTS 32  /* joints per heatmap set supported by fvp_voxelize */
+/* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
+ * per pass (one channels-last pixel of 32 floats per tap) and more in joint
+ * slices of 32. */
+#define FVP_MAX_JOINTS 1024
 /* Cameras per frame: torch's CPU mean over the views (the sum order every
  * kernel reproduces) folds blocks of 16 into a second accumulator, and past
  * 255 views into a third; up to 255 views are supported. */
@@ -105,7 +108,8 @@ int fvp_pack_grid(const float *sample_grid, int V, long long N, float *packed, v
  *   grid_index   device int32 [B] (grid of frame b) or NULL (all frames use grid 0)
  *   cube, xy     device outputs; either may be NULL to skip it
  *   workspace    device scratch of >= fvp_voxelize_workspace_bytes(B,V,J,H,W)
- *                bytes (channels-last copy of a chunk of frames); J <= FVP_MAX_JOINTS */
+ *                bytes (channels-last copy of a chunk of frames; of one 32-joint slice
+ *                when J > 32); J <= FVP_MAX_JOINTS */
 size_t fvp_voxelize_workspace_bytes(int B, int V, int J, int H, int W);
 int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W,
                  const float *packed_grids, const int32_t *grid_index,
@@ -193,7 +197,8 @@ int fvp_gather_bbox(const float *size, int B, int X, int Y,
  *   frame_of    device int32 [P]: frame of each proposal in [0,B) (NULL: all frame 0)
  *   cubes       device [P][J][SX][SY][SZ] or NULL (outside-window voxels are 0)
  *   planes      device [3P][J][S][S] or NULL: xy (max over z) for p < P, then xz
- *               (max over y), then yz (max over x); needs SX == SY == SZ <= 64
+ *               (max over y), then yz (max over x); needs SX == SY == SZ (any size:
+ *               cubes deeper than 64 run in 64-deep z chunks, joints in slices of 32)
  *   offset      device [P][3] or NULL
  *   workspace   >= fvp_person_workspace_bytes(B,V,J,H,W) bytes (channels-last frames) */
 size_t fvp_person_workspace_bytes(int B, int V, int J, int H, int W);
@@ -226,7 +231,7 @@ int fvp_person_planes_cl(const float *heatmaps_cl, int cp, int B, int V, int J, 
 /* xy / xz / yz max-projections of per-person cubes [P][J][S][S][S] into
  * planes [3P][J][S][S] (xy block first, then xz, then yz).
  * Replaces torch.cat([max(c,4), max(c,3), max(c,2)]) at
- * lib/models/joint_localization_net.py:158-160.  S <= 64. */
+ * lib/models/joint_localization_net.py:158-160.  S <= 4096 (S > 64: one thread per plane cell). */
 int fvp_max_planes(const float *cubes, int P, int J, int S, float *planes, void *stream);
 
 /* JLN soft-argmax of the per-plane joint maps plus the offset shift:

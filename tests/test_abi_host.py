@@ -40,12 +40,13 @@ def test_argument_validation_without_gpu():
     lib = _lib.load()
     assert lib.fvp_voxelize(None, 1, 5, 15, 128, 240, None, None, 80, 80, 20, None, None, None, 0, None) == 1001
     assert lib.fvp_voxelize(1, 0, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1002
-    assert lib.fvp_voxelize(1, 1, 5, 33, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1002  # J > 32
+    assert lib.fvp_voxelize(1, 1, 5, 1025, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1002  # J > 1024
     assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1003  # no workspace
     need = lib.fvp_voxelize_workspace_bytes(256, 5, 15, 128, 240)
     assert need == 8 * 5 * 128 * 240 * 16 * 4  # channels-last chunk of 8 frames (J padded to 16)
     assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, 1, 100, None) == 1003
-    assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 0
+    assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 4 * 5 * 128 * 240 * 32 * 4  # one 32-joint slice
+    assert lib.fvp_voxelize_workspace_bytes(4, 5, 1025, 128, 240) == 0
     # fp16, J <= 16: pixel-pair table [V][H][W+1] x 64 B, 2 frames of C5 per chunk
     assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 2 * 31 * 128 * 241 * 64
     # fp16, J > 16: the fp32 channels-last copy
@@ -57,7 +58,7 @@ def test_argument_validation_without_gpu():
     assert lib.fvp_nms_topk(None, 1, 80, 80, 0, 10, None, None, None, None) == 1001
     assert lib.fvp_nms_topk(1, 1, 2, 2, 0, 10, 1, 1, None, None) == 1002  # K > X*Y
     assert lib.fvp_nms_topk(1, 2, 8, 8, 10, 5, 1, 1, None, None) == 1002  # frame stride < X*Y
-    assert lib.fvp_max_planes(1, 1, 1, 65, 1, None) == 1002            # S > 64
+    assert lib.fvp_max_planes(1, 1, 1, 4097, 1, None) == 1002          # S > 4096
     spec = _lib.PersonSpec((253, 253, 64), (0.03, 0.03, 0.03), (0, 0, 0), (8000, 8000, 2000), (2000,) * 3, (64,) * 3)
     assert lib.fvp_person_planes(None, 1, 5, 15, 128, 240, 1, spec, 1, None, 1, None, 1, None, 1, 10, None) == 1001
     assert lib.fvp_person_planes(1, 1, 5, 15, 128, 240, 1, spec, 1, None, 1, None, 1, None, None, 0, None) == 1003

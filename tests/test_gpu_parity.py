@@ -475,13 +475,105 @@ def test_nms_on_channel_slice_without_copy(gpu_device):
     assert np.array_equal(v1.cpu().numpy(), ov) and np.array_equal(f1.cpu().numpy(), ofl)
 
 
-def test_more_than_32_joints_rejected(gpu_device):
-    from fvp import _lib
+@pytest.mark.parametrize("mode", ["f32", "f16", "cl", "onthefly"])
+def test_more_than_32_joints(gpu_device, mode):
+    """J = 40 runs as joint slices of 32 + 8 (layout pass + gather per slice; the
+    channels-last input read at the slice's channel offset) == the oracle bit for bit."""
+    import dataclasses
 
-    hm = torch.zeros((1, 1, 33, 8, 8), device=gpu_device)
-    sg = torch.zeros((8, 2, 2), device=gpu_device)  # packed [N, GV, 2]
-    with pytest.raises(_lib.FvpError, match="J <= 32"):
-        torch.ops.fvp.voxelize(hm, sg, None, 2, 2, 2, True, True)
+    from fvp import geometry
+    from fvp.heatmaps import ChannelsLastHeatmaps
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    J = 40
+    w = dataclasses.replace(WORKLOADS["c3"], num_joints=J, voxels_per_axis=(16, 12, 6))
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    layer.on_the_fly = mode == "onthefly"
+    cams, seq = w.cameras()
+    rt_np = geometry.resize_transform(w.ori_image_size, w.image_size).astype(np.float32)
+    rt = torch.from_numpy(rt_np).to(gpu_device)
+    Wh, Hh = w.heatmap_size
+    B = 2
+    hm = torch.rand((B, 5, J, Hh, Wh), generator=torch.Generator().manual_seed(40))
+    if mode == "f16":
+        hm = hm.half()
+    ref_in = hm.float().numpy()
+    hg = hm.to(gpu_device)
+    meta = {"seq": [seq] * B}
+    if mode == "cl":
+        cl = torch.full((B, 5, Hh, Wh, 48), 5.0, device=gpu_device)
+        cl[..., :J] = hg.permute(0, 1, 3, 4, 2)
+        hg = ChannelsLastHeatmaps(cl, J)
+    cube, xy = layer.forward_fused(hg, meta, cams, rt)
+    grid = O.compute_grid(w.space_size, w.space_center, w.voxels_per_axis)
+    sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, w.heatmap_size, rt_np)
+                   for c in cams[seq]])
+    for b in range(B):
+        ref = O.voxelize(ref_in[b], sg).reshape(cube.shape[1:])
+        _assert_same(cube[b].cpu().numpy(), ref, f"J=40 cube {mode} frame {b}")
+        _assert_same(xy[b].cpu().numpy(), O.xy_plane(ref), f"J=40 xy {mode} frame {b}")
+
+
+def _person_setup(gpu_device, J, S, space=2000.0):
+    """C3 cameras, a 2 m capture space (the fine grid stays small: S^3 x V slots)."""
+    import dataclasses
+
+    from fvp import geometry, synthetic
+    from fvp.project_individual import ProjectLayer
+    from fvp.workloads import WORKLOADS
+
+    w = dataclasses.replace(WORKLOADS["c3"], num_joints=J, space_size=(space, space, space),
+                            ind_space_size=(space, space, space), ind_voxels_per_axis=(S, S, S))
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 1)).to(gpu_device)
+    c = w.space_center
+    props = np.array([[c[0], c[1], c[2], 0, 0.9, 0.5, 0.5], [c[0] + 300, c[1] - 200, c[2] - 100, 0, 0.8, 0.2, 0.9],
+                      [c[0] - 700, c[1] + 500, c[2] + 300, 0, 0.7, 1.1, 0.3]], np.float32)
+    return w, layer, cams, seq, rt, hm, props
+
+
+@pytest.mark.parametrize("otf", [False, True], ids=["finegrid", "onthefly"])
+@pytest.mark.parametrize("J,S", [(40, 32), (5, 96), (3, 80)])
+def test_person_joint_slices_and_deep_cubes(gpu_device, J, S, otf):
+    """Person cubes / planes with J > 32 (joint slices) and S > 64 (64-deep z
+    chunks; max_planes beyond 64 on the per-cell kernel) == the oracle."""
+    w, layer, cams, seq, rt, hm, props = _person_setup(gpu_device, J, S)
+    layer.on_the_fly = otf
+    pg = torch.from_numpy(props).to(gpu_device)
+    meta = {"seq": [seq]}
+    planes, offset = layer.forward_planes(hm, 0, meta, pg, cams, rt)
+    cubes, off2 = layer(hm, 0, meta, pg, cams, rt)
+    ind = O.Individual(w.space_size, w.space_center, w.ind_space_size, w.ind_voxels_per_axis)
+    fsg = layer.build_sample_grid(cams, seq, rt, gpu_device).cpu().numpy()
+    ref_cubes, ref_off = ind.person_cubes(hm[0].cpu().numpy(), fsg, props)
+    _assert_same(cubes.cpu().numpy(), ref_cubes, f"cubes J={J} S={S}")
+    _assert_same(planes.cpu().numpy(), O.max_planes(ref_cubes), f"fused planes J={J} S={S}")
+    _assert_same(offset.cpu().numpy(), ref_off, "offset")
+    mp = torch.ops.fvp.max_planes(cubes)
+    _assert_same(mp.cpu().numpy(), O.max_planes(ref_cubes), f"max_planes S={S}")
+
+
+def test_soft_argmax_long_rows(gpu_device):
+    """Soft-argmax of 96 x 96 planes (9216 cells: the two-pass kernel) vs float64."""
+    from fvp import ops
+
+    P, J, S = 2, 3, 96
+    g = torch.Generator().manual_seed(3)
+    feat = torch.rand((3, P, J, S, S), generator=g)
+    grid = torch.rand((3, S * S, 2), generator=g) * 1000.0
+    off = torch.rand((P, 3), generator=g) * 10.0
+    pose, maxprob = ops.soft_argmax(feat.to(gpu_device), grid.to(gpu_device), off.to(gpu_device), 100.0)
+    ref_pose, _ = O.soft_argmax(feat.numpy(), grid.numpy(), 100.0)
+    ref_pose = O.add_offsets(ref_pose, off.numpy())
+    y = 100.0 * feat.numpy().reshape(3, P, J, -1).astype(np.float64)
+    ref_mp = 1.0 / np.exp(y - y.max(axis=3, keepdims=True)).sum(axis=3)  # max of the softmax
+    assert np.abs(pose.cpu().numpy() - ref_pose).max() <= 0.05
+    assert np.abs(maxprob.cpu().numpy() - ref_mp).max() <= 1e-5
 
 
 def _jln_setup(gpu_device, J=15, frames=3):

@@ -4,8 +4,8 @@
 One step = the hot path over one batch of B synthetic frames per GPU, inputs
 resident in HBM:
   fvp_voxelize (cube [B,J,X,Y,Z] + xy max-plane, one launch)
-  -> fvp_nms_topk on the root-joint xy plane (stand-in for CenterNet's map;
-     the dense CNN is out of scope) -> fvp_gather_columns [B,K,J,Z]
+  -> fvp_nms_topk_columns: NMS top-K on the root-joint xy plane (stand-in for
+     CenterNet's map) and the winners' z-columns [B,K,J,Z] in one launch
   -> (N > 1) one RCCL all_gather of the compact proposals.
 Frames are sharded across ranks (weak scaling).  Default workload: C2 =
 BASELINE configs[1] (Shelf calibration, 5 cams, J=15, 128x240 -> 80x80x20).
@@ -54,6 +54,11 @@ def parse():
                          "x-slab of each; strong scaling")
     ap.add_argument("--strong", action="store_true",
                     help="--batch is the whole job's frames, split over the ranks (strong scaling)")
+    ap.add_argument("--heatmap-layout", choices=["planar", "channels-last"], default="planar",
+                    help="planar: the reference's [B,V,J,H,W] heatmaps (the headline); channels-last: "
+                         "[B,V,H,W,Cp] as the fvp backbone writes them (no layout pass)")
+    ap.add_argument("--on-the-fly", choices=["auto", "on", "off"], default="auto",
+                    help="sampling coordinates from the cached grid (off) or projected in-kernel (on)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -78,7 +83,8 @@ def collect_traffic(args):
         d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=out_root)
         cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--child", "--steps", str(CHILD_OPS - 1), "--warmup", "1",
-               "--workload", args.workload, "--traffic", "off", "--cpu-baseline", "off"]
+               "--workload", args.workload, "--traffic", "off", "--cpu-baseline", "off",
+               "--heatmap-layout", args.heatmap_layout, "--on-the-fly", args.on_the_fly]
         if args.batch:
             cmd += ["--batch", str(args.batch)]
         if args.slabs:
@@ -189,7 +195,7 @@ def main():
 
     from fvp import geometry, parallel, synthetic
     from fvp.project_whole import ProjectLayer
-    from fvp.proposal import nms2D, gather_columns
+    from fvp.proposal import nms2D, nms2D_columns
     from fvp.workloads import WORKLOADS
 
     local_rank %= max(1, torch.cuda.device_count())  # identity with one rank per GPU
@@ -226,6 +232,7 @@ def main():
 
     layer = ProjectLayer(w.cfg(str(dev)))
     layer.verbose = False
+    layer.on_the_fly = {"auto": None, "on": True, "off": False}[args.on_the_fly]
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
     # large-frame mode: all ranks hold the same frames (x-slabs); otherwise own frames
     hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=0 if args.slabs else rank * B)
@@ -235,6 +242,21 @@ def main():
         hm = hm.half()
     del hm_host
     meta = {"seq": [seq] * B}
+
+    def channels_last(planar):
+        """[B,V,J,H,W] -> ChannelsLastHeatmaps [B,V,H,W,Cp] (the fvp backbone's output layout)."""
+        from fvp.heatmaps import ChannelsLastHeatmaps
+
+        cp = 16 * ((J + 15) // 16)
+        t = torch.zeros(planar.shape[:2] + planar.shape[3:] + (cp,), dtype=torch.float32, device=dev)
+        t[..., :J] = planar.permute(0, 1, 3, 4, 2)
+        return ChannelsLastHeatmaps(t, J)
+
+    hm_planar = hm
+    if args.heatmap_layout == "channels-last":
+        if hm.dtype != torch.float32:
+            raise SystemExit("--heatmap-layout channels-last: fp32 heatmaps only")
+        hm = channels_last(hm)
 
     # once-per-sequence cache build, timed separately (excluded from the step):
     # the first call also pays the library / code-object load; a second
@@ -249,7 +271,7 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record()
-    layer.prepare(hm[:1], {"seq": [seq_b]}, cams_b, rt)
+    layer.prepare(hm_planar[:1], {"seq": [seq_b]}, cams_b, rt)
     e1.record()
     torch.cuda.synchronize()
     cache_ms = {"first_call_ms": round(first_ms, 2), "sequence_build_ms": round((time.perf_counter() - t0) * 1e3, 3),
@@ -269,8 +291,8 @@ def main():
             xy = parallel.gather_xy_slabs(xy, X)
             vals, idx, flat = nms2D(xy[:, root:root + 1], K)
             return vals, flat, parallel.columns_from_slab(cube, flat, x0)
-        vals, idx, flat = nms2D(xy[:, root:root + 1], K)
-        return vals, flat, gather_columns(cube, flat)
+        vals, idx, flat, cols = nms2D_columns(xy[:, root:root + 1], K, cube)  # one launch
+        return vals, flat, cols
 
     if args.graph == "on" and args.slabs and world > 1:
         raise SystemExit("--graph on captures GPU-local work only; the slab collectives sit inside post()")
@@ -324,7 +346,8 @@ def main():
     frames = (1 if args.slabs else world) * B * args.steps
     fps = frames / el
     Xs = x1 - x0  # this rank's x-rows (X unless --slabs)
-    per_frame = V * J * Hd * Wd * hm.element_size() + J * Xs * Y * Z * 4 + J * Xs * Y * 4
+    # (channels-last input: the J joints' bytes are counted, not the zero padding)
+    per_frame = V * J * Hd * Wd * hm_planar.element_size() + J * Xs * Y * Z * 4 + J * Xs * Y * 4
     alg_bytes = B * per_frame
     achieved = alg_bytes / (vox_ms * 1e-3) / 1e9
 
@@ -332,7 +355,7 @@ def main():
     # per frame, against the per-CU vector-memory (texture addresser / L1) rate of
     # 64 B/clk: 16 fp32 joint-taps/clk/CU, 32 with the fp16 pixel-pair table.
     taps = B * Xs * Y * Z * V * J * 4
-    tap_bytes = 2 if (hm.element_size() == 2 and J <= 16) else 4
+    tap_bytes = 2 if (hm_planar.element_size() == 2 and J <= 16) else 4
     tap_peak = 256 * 2.4e9 * 64 / tap_bytes / 1e12
     tap_rate = taps / (vox_ms * 1e-3) / 1e12
 
@@ -356,12 +379,34 @@ def main():
         torch.cuda.synchronize()
         extra["copy_gbs"] = 2 * nbytes * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
         del src, dst
-        hm1, meta1 = hm[:1], {"seq": [seq]}
+        # the same voxelize op on channels-last heatmaps (as the fvp backbone
+        # writes them: the gather alone, no layout pass), same frames and events
+        if args.heatmap_layout == "planar" and hm_planar.dtype == torch.float32 and not args.slabs:
+            hcl = channels_last(hm_planar)
+            for _ in range(2):
+                layer.forward_fused(hcl, meta, cams, rt)
+            evs = []
+            for _ in range(args.steps):
+                a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                layer.forward_fused(hcl, meta, cams, rt)
+                b_.record(stream)
+                evs.append((a, b_))
+            torch.cuda.synchronize()
+            cl_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
+            extra["channels_last"] = {"kernel_ms": round(cl_ms, 4),
+                                      "achieved": round(alg_bytes / (cl_ms * 1e-3) / 1e9, 1),
+                                      "frac": round(alg_bytes / (cl_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "frames_per_s_op_only": round(B / (cl_ms * 1e-3), 1),
+                                      "what": "the same op on [B,V,H,W,16] heatmaps as fvp.backbone writes them "
+                                              "(fvp_voxelize_cl: no layout pass); bit-identical outputs"}
+            del hcl
+        hm1, meta1 = (hm_planar[:1] if args.heatmap_layout == "planar" else channels_last(hm_planar[:1])), \
+            {"seq": [seq]}
 
         def step1():
             cube, xy = layer.forward_fused(hm1, meta1, cams, rt, want_cube=True, want_xy=True)
-            vals, idx, flat = nms2D(xy[:, root:root + 1], K)
-            return gather_columns(cube, flat)
+            return nms2D_columns(xy[:, root:root + 1], K, cube)[3]
 
         for _ in range(3):
             step1()
@@ -418,7 +463,9 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "fvp_voxelize op = layout pass (heatmaps_to_cl / heatmaps_to_pairs) + voxelize_kernel per frame chunk",
+                "kernel": ("fvp_voxelize op = layout pass (heatmaps_to_cl / heatmaps_to_pairs) + voxelize_kernel per "
+                           "frame chunk" if args.heatmap_layout == "planar" else
+                           "fvp_voxelize_cl op = voxelize_kernel on channels-last heatmaps (no layout pass)"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -438,6 +485,10 @@ def main():
             "execution": "hipGraph replay of the GPU-local step" if args.graph == "on" else "eager",
             "cache_build": cache_ms,
         }
+        if "channels_last" in extra:
+            line["roofline"]["channels_last_input"] = extra["channels_last"]
+        if args.heatmap_layout != "planar":
+            line["config"]["heatmap_layout"] = "channels-last [B,V,H,W,16] (fvp backbone output)"
         if traffic is not None:
             line["roofline"]["traffic_detail"] = {k: round(v, 1) for k, v in traffic.items()}
         elif traffic_note:

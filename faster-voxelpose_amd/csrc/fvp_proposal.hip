@@ -179,11 +179,62 @@ constexpr int kSelCap = 4096;                   // candidate list capacity
 // A list longer than kSelCap (only for adversarial value layouts) falls back
 // to K block-wide extraction rounds of the largest key below the previous
 // winner (no taken bitmap: keys are unique).
+// K extraction rounds, each the largest key below the previous winner (the
+// select kernel's path for candidate lists longer than kSelCap).
+template <int E>
+__device__ __forceinline__ void select_fallback(const unsigned long long (&key)[E], const float (&val)[E], int b,
+                                                int K, int X, float *__restrict__ vals, int64_t *__restrict__ flat,
+                                                int64_t *__restrict__ xy, unsigned long long *wmax, float &wval,
+                                                int *widx) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long prev = ~0ull;
+    for (int r = 0; r < K; ++r) {
+        unsigned long long mine = 0;
+        float mv = 0.0f;
+#pragma unroll
+        for (int i = 0; i < E; ++i)
+            if (key[i] < prev && key[i] > mine) {
+                mine = key[i];
+                mv = val[i];
+            }
+        const unsigned long long wm = wave_max_key(mine);
+        if (lane == 0) wmax[wave] = wm;
+        __syncthreads();
+        unsigned long long w = 0;
+#pragma unroll
+        for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
+        if (mine == w && mine != 0) wval = mv;  // exactly one owner (unique keys)
+        __syncthreads();
+        if (tid == 0) {
+            const int idx = (int)~(unsigned)w;
+            const size_t o = (size_t)b * K + r;
+            vals[o] = wval;
+            flat[o] = idx;
+            widx[r] = idx;
+            if (xy) {
+                xy[o * 2 + 0] = (int64_t)(idx / X);
+                xy[o * 2 + 1] = (int64_t)(idx % X);
+            }
+        }
+        prev = w;
+        __syncthreads();
+    }
+}
+
+// Optionally fused with the column gather of the winners (cols != null:
+// cols[b,k,j,:] = cube[b,j,flat[b,k],:], human_detection_net.py:199-200), so a
+// frame's proposals and their z-columns come from one launch.
+struct ColGather {
+    const float *cube;  // [B][J][X*Y][Z]
+    float *cols;        // [B][K][J][Z]
+    int J, Z;
+};
+
 template <int E>
 __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__restrict__ prob, long long stride,
                                                                  int X, int Y, int K, float *__restrict__ vals,
                                                                  int64_t *__restrict__ flat,
-                                                                 int64_t *__restrict__ xy) {
+                                                                 int64_t *__restrict__ xy, ColGather cg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int M = X * Y;
     float *map = reinterpret_cast<float *>(smem);                                             // [M]
@@ -193,6 +244,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     __shared__ unsigned long long thr;
     __shared__ int count;
     __shared__ float wval;
+    __shared__ int widx[kSelWaves];  // winners' flat indices (K <= kSelWaves)
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const float *__restrict__ p = prob + (size_t)b * stride;
@@ -290,45 +342,23 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
                 const size_t o = (size_t)b * K + rank;
                 vals[o] = lval[c];
                 flat[o] = idx;
+                widx[rank] = idx;
                 if (xy) {
                     xy[o * 2 + 0] = (int64_t)(idx / X);
                     xy[o * 2 + 1] = (int64_t)(idx % X);
                 }
             }
         }
-        return;
+    } else {
+        select_fallback<E>(key, val, b, K, X, vals, flat, xy, wmax, wval, widx);
     }
-    // fallback: K rounds, each the largest key below the previous winner
-    unsigned long long prev = ~0ull;
-    for (int r = 0; r < K; ++r) {
-        unsigned long long mine = 0;
-        float mv = 0.0f;
-#pragma unroll
-        for (int i = 0; i < E; ++i)
-            if (key[i] < prev && key[i] > mine) {
-                mine = key[i];
-                mv = val[i];
-            }
-        const unsigned long long wm = wave_max_key(mine);
-        if (lane == 0) wmax[wave] = wm;
-        __syncthreads();
-        unsigned long long w = 0;
-#pragma unroll
-        for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
-        if (mine == w && mine != 0) wval = mv;  // exactly one owner (unique keys)
-        __syncthreads();
-        if (tid == 0) {
-            const int idx = (int)~(unsigned)w;
-            const size_t o = (size_t)b * K + r;
-            vals[o] = wval;
-            flat[o] = idx;
-            if (xy) {
-                xy[o * 2 + 0] = (int64_t)(idx / X);
-                xy[o * 2 + 1] = (int64_t)(idx % X);
-            }
-        }
-        prev = w;
-        __syncthreads();
+    if (!cg.cols) return;
+    __syncthreads();
+    const int JZ = cg.J * cg.Z, KJZ = K * JZ;
+    for (int e = tid; e < KJZ; e += kSelThreads) {
+        const int k = e / JZ, r = e - k * JZ;
+        const int j = r / cg.Z, z = r - j * cg.Z;
+        cg.cols[(size_t)b * KJZ + e] = cg.cube[(((size_t)b * cg.J + j) * M + widx[k]) * cg.Z + z];
     }
 }
 
@@ -347,7 +377,8 @@ __global__ __launch_bounds__(256) void gather_columns_kernel(const float *__rest
     const int k = (int)(r % K);
     const long long b = r / K;
     const int64_t f = flat[b * K + k];
-    out[gid] = cube[((b * J + j) * XY + f) * Z + z];
+    // an index outside the map reads nothing and yields NaN (torch.gather raises)
+    out[gid] = (f >= 0 && f < XY) ? cube[((b * J + j) * XY + f) * Z + z] : __builtin_nanf("");
 }
 
 __global__ __launch_bounds__(256) void gather_bbox_kernel(const float *__restrict__ size,
@@ -358,7 +389,8 @@ __global__ __launch_bounds__(256) void gather_bbox_kernel(const float *__restric
     const int c = (int)(gid & 1);
     const long long bk = gid >> 1;
     const long long b = bk / K;
-    out[gid] = size[(b * 2 + c) * XY + flat[bk]];
+    const int64_t f = flat[bk];
+    out[gid] = (f >= 0 && f < XY) ? size[(b * 2 + c) * XY + f] : __builtin_nanf("");
 }
 
 // ProposalLayer.forward in test mode (human_detection_net.py:36-37, 99-124)
@@ -402,8 +434,9 @@ __global__ __launch_bounds__(256) void proposal_centers_kernel(const int64_t *__
 
 }  // namespace fvp
 
-extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
-                            int64_t *flat, int64_t *xy, void *stream) {
+namespace fvp {
+static int nms_any(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals, int64_t *flat,
+                   int64_t *xy, const ColGather &cg, int Xc, int Yc, void *stream) {
     if (!prob || !vals || !flat) return FVP_ERR_NULL;
     if (B <= 0 || X <= 0 || Y <= 0 || K <= 0 || K > X * Y) return FVP_ERR_SHAPE;
     const size_t M = (size_t)X * Y;
@@ -411,21 +444,42 @@ extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long fr
     if (lds > 150 * 1024) return FVP_ERR_SHAPE;
     if (frame_stride == 0) frame_stride = (long long)M;
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
-    const int E = (int)((M + fvp::kSelThreads - 1) / fvp::kSelThreads);
-    if (K <= fvp::kSelWaves && E <= 16) {
-        const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)fvp::kSelCap * 12;
-        const dim3 g(B), blk(fvp::kSelThreads);
-        hipStream_t st = (hipStream_t)stream;
-        if (E <= 1) hipLaunchKernelGGL((fvp::nms_select_kernel<1>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
-        else if (E <= 2) hipLaunchKernelGGL((fvp::nms_select_kernel<2>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
-        else if (E <= 4) hipLaunchKernelGGL((fvp::nms_select_kernel<4>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
-        else if (E <= 8) hipLaunchKernelGGL((fvp::nms_select_kernel<8>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
-        else hipLaunchKernelGGL((fvp::nms_select_kernel<16>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy);
+    hipStream_t st = (hipStream_t)stream;
+    const int E = (int)((M + kSelThreads - 1) / kSelThreads);
+    if (K <= kSelWaves && E <= 16) {
+        const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)kSelCap * 12;
+        const dim3 g(B), blk(kSelThreads);
+        if (E <= 1) hipLaunchKernelGGL((nms_select_kernel<1>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        else if (E <= 2) hipLaunchKernelGGL((nms_select_kernel<2>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        else if (E <= 4) hipLaunchKernelGGL((nms_select_kernel<4>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        else if (E <= 8) hipLaunchKernelGGL((nms_select_kernel<8>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        else hipLaunchKernelGGL((nms_select_kernel<16>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
         return (int)hipGetLastError();
     }
-    hipLaunchKernelGGL(fvp::nms_topk_kernel, dim3(B), dim3(fvp::kNmsThreads), lds, (hipStream_t)stream, prob,
-                       frame_stride, X, Y, K, vals, flat, xy);
+    hipLaunchKernelGGL(nms_topk_kernel, dim3(B), dim3(kNmsThreads), lds, st, prob, frame_stride, X, Y, K, vals, flat,
+                       xy);
+    if (cg.cols) {  // K > 16: the column gather as its own launch
+        const long long total = (long long)B * K * cg.J * cg.Z;
+        hipLaunchKernelGGL(gather_columns_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cg.cube,
+                           flat, cg.cols, cg.J, Xc * Yc, cg.Z, K, total);
+    }
     return (int)hipGetLastError();
+}
+}  // namespace fvp
+
+extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
+                            int64_t *flat, int64_t *xy, void *stream) {
+    return fvp::nms_any(prob, B, X, Y, frame_stride, K, vals, flat, xy, fvp::ColGather{nullptr, nullptr, 0, 0}, 0, 0,
+                        stream);
+}
+
+extern "C" int fvp_nms_topk_columns(const float *prob, int B, int X, int Y, long long frame_stride, int K,
+                                    float *vals, int64_t *flat, int64_t *xy, const float *cube, int J, int Z,
+                                    float *columns, void *stream) {
+    if (!cube || !columns) return FVP_ERR_NULL;
+    if (J <= 0 || Z <= 0) return FVP_ERR_SHAPE;
+    return fvp::nms_any(prob, B, X, Y, frame_stride, K, vals, flat, xy, fvp::ColGather{cube, columns, J, Z}, X, Y,
+                        stream);
 }
 
 extern "C" int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z, const int64_t *flat, int K,

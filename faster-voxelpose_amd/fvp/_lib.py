@@ -53,6 +53,8 @@ SIGNATURES = {
     "fvp_voxelize_cl_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                              ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p, c_void_p, c_void_p],
     "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fvp_nms_topk_columns": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_int, c_int, c_void_p, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_proposal_centers": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,

@@ -127,9 +127,9 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     batch_size = heatmaps.shape[0]
     cubes, xy = self.project_layer.forward_fused(heatmaps, meta, cameras, resize_transform)
     hm2d, bbox_preds = center_net_from_xy(self.center_net, xy)
-    confs_2d, index_2d, flat = proposal.nms2D(hm2d.detach(), self.max_people)
+    # nms2D and the z-column gather of its winners in one launch (:188, :199-200)
+    confs_2d, index_2d, flat, columns = proposal.nms2D_columns(hm2d, self.max_people, cubes)  # columns [B,K,J,Z]
     match_bbox = proposal.gather_bbox(bbox_preds, flat)
-    columns = proposal.gather_columns(cubes, flat)                        # [B, K, J, Z]
     c2c = self.c2c_net
     if USE_FVP_CNN and not c2c.training:
         c2c = fvp_cnn.cached(c2c, FVP_CNN_DTYPE)

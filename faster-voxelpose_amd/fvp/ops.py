@@ -114,11 +114,7 @@ def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Opt
     if pg.shape[1:] != (N, grid_slots(V), 2):
         raise _lib.FvpError(f"fvp: packed grid {tuple(pg.shape)} does not match V={V}, N={N} "
                             f"(expected [S,{N},{grid_slots(V)},2] from pack_grid)")
-    gi = None
-    if grid_index is not None:
-        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
-        if gi.numel() != B:
-            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    gi = _grid_index(grid_index, B, pg.shape[0], hm.device)
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
     if B == 0:  # an empty batch: the reference's loop over frames yields empty outputs
@@ -152,11 +148,7 @@ def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Option
     if cm.shape[1] != V:
         raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
     X, Y, Z = bins
-    gi = None
-    if grid_index is not None:
-        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
-        if gi.numel() != B:
-            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    gi = _grid_index(grid_index, B, cm.shape[0], hm.device)
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
     if B == 0:  # an empty batch: the reference's loop over frames yields empty outputs
@@ -188,6 +180,19 @@ def _(heatmaps, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
             heatmaps.new_empty((B, J, X, Y) if want_xy else (0,)))
 
 
+def _grid_index(grid_index: Optional[torch.Tensor], B: int, S: int, device) -> Optional[torch.Tensor]:
+    """int32 [B] sequence index of every frame on `device`.  A host tensor is
+    range-checked here, before the copy (no device sync); a device tensor's
+    values are the caller's precondition (0 <= g < S, include/fvp.h)."""
+    if grid_index is None:
+        return None
+    if grid_index.numel() != B:
+        raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    if grid_index.device.type == "cpu" and B and (int(grid_index.min()) < 0 or int(grid_index.max()) >= S):
+        raise _lib.FvpError(f"fvp: grid_index values must lie in [0, {S})")
+    return grid_index.to(device=device, dtype=torch.int32, non_blocking=True).contiguous()
+
+
 def _cl_input(heatmaps_cl: torch.Tensor, J: int) -> torch.Tensor:
     if heatmaps_cl.device.type != "cuda":
         raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps_cl.device}")
@@ -209,11 +214,7 @@ def voxelize_cl(heatmaps_cl: torch.Tensor, J: int, packed_grids: torch.Tensor, g
         pg = pg.unsqueeze(0)
     if pg.shape[1:] != (N, grid_slots(V), 2):
         raise _lib.FvpError(f"fvp: packed grid {tuple(pg.shape)} does not match V={V}, N={N}")
-    gi = None
-    if grid_index is not None:
-        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
-        if gi.numel() != B:
-            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    gi = _grid_index(grid_index, B, pg.shape[0], hm.device)
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
     if B == 0:
@@ -245,11 +246,7 @@ def voxelize_cl_cams(heatmaps_cl: torch.Tensor, J: int, cams: torch.Tensor, grid
     if cm.shape[1] != V:
         raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
     X, Y, Z = bins
-    gi = None
-    if grid_index is not None:
-        gi = grid_index.to(device=hm.device, dtype=torch.int32).contiguous()
-        if gi.numel() != B:
-            raise _lib.FvpError("fvp: grid_index must have one entry per frame")
+    gi = _grid_index(grid_index, B, cm.shape[0], hm.device)
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
     if B == 0:
@@ -293,6 +290,41 @@ def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, to
         return vals, xy, flat
     _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
     return vals, xy, flat
+
+
+@torch.library.custom_op("fvp::nms_topk_columns", mutates_args=(), device_types="cuda")
+def nms_topk_columns(prob: torch.Tensor, K: int,
+                     cube: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """nms_topk + gather_columns in one launch (fvp_nms_topk_columns): the map's
+    top-K and the winners' z-columns [B,K,J,Z] of cube [B,J,X,Y,Z]."""
+    if prob.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: prob_map must be on a HIP device, got {prob.device}")
+    c = _dev_f32(cube, "feature_cubes")
+    B, X, Y = prob.shape[0], prob.shape[-2], prob.shape[-1]
+    if prob.numel() != B * X * Y or c.dim() != 5 or tuple(c.shape[0:1]) + tuple(c.shape[2:4]) != (B, X, Y):
+        raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map over the cube's [B, J, X, Y, Z] grid")
+    p = prob
+    if not (p.dtype == torch.float32 and p.stride()[-1] == 1 and p.stride()[-2] == Y
+            and (B <= 1 or p.stride()[0] >= X * Y)):
+        p = p.to(torch.float32).contiguous()
+    stride = p.stride()[0] if B > 1 else X * Y
+    J, Z = c.shape[1], c.shape[4]
+    vals = torch.empty((B, K), dtype=torch.float32, device=p.device)
+    flat = torch.empty((B, K), dtype=torch.int64, device=p.device)
+    xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
+    cols = torch.empty((B, K, J, Z), dtype=torch.float32, device=p.device)
+    if B == 0 or cols.numel() == 0:
+        return vals, xy, flat, cols
+    _lib.call("fvp_nms_topk_columns", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _ptr(c), J, Z,
+              _ptr(cols), _stream(p))
+    return vals, xy, flat, cols
+
+
+@nms_topk_columns.register_fake
+def _(prob, K, cube):
+    B = prob.shape[0]
+    return (prob.new_empty((B, K)), prob.new_empty((B, K, 2), dtype=torch.int64),
+            prob.new_empty((B, K), dtype=torch.int64), prob.new_empty((B, K, cube.shape[1], cube.shape[4])))
 
 
 @nms_topk.register_fake

@@ -17,8 +17,6 @@ proposal of a batch of frames in one launch.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 import torch.nn as nn
@@ -30,9 +28,8 @@ from .heatmaps import ChannelsLastHeatmaps, channels_last_of
 # Fine-grid sampling coordinates: read from the per-sequence packed fine grid
 # (197 MB for 5 cameras; measured faster: C3, 320 proposals, 10.7 vs 11.7 us
 # each) unless that grid would exceed this size (e.g. 31 cameras: 1 GB), then
-# projected on the fly (fvp_person_planes_cams).  FVP_PERSON_OTF=1/0 forces.
+# projected on the fly (fvp_person_planes_cams).  layer.on_the_fly forces.
 PERSON_OTF_GRID_BYTES = 512 << 20
-PERSON_ON_THE_FLY = {"1": True, "0": False}.get(os.environ.get("FVP_PERSON_OTF", ""))
 
 
 class ProjectLayer(nn.Module):
@@ -121,8 +118,6 @@ class ProjectLayer(nn.Module):
     def _otf(self, V: int) -> bool:
         if self.on_the_fly is not None:
             return bool(self.on_the_fly)
-        if PERSON_ON_THE_FLY is not None:
-            return PERSON_ON_THE_FLY
         fine = [int(v) for v in self._const["fine"]]
         return fine[0] * fine[1] * fine[2] * ops.grid_slots(V) * 8 > PERSON_OTF_GRID_BYTES
 

@@ -13,8 +13,6 @@ Registers no parameters or buffers, so checkpoints load unchanged.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 import torch.nn as nn
@@ -29,8 +27,6 @@ from .heatmaps import channels_last_of
 # cached vs 2.07 on the fly, V=24 (314 MB) 2.77 vs ~3.0, V=31 (406 MB) 3.76 vs
 # 3.84 (B=32: 2,124 vs 2,106 frames/s) -- a tie, so the 406 MB grid is not kept.
 ON_THE_FLY_GRID_BYTES = 384 << 20
-# "1"/"0" forces the choice for every layer (A/B measurements)
-ON_THE_FLY = {"1": True, "0": False}.get(os.environ.get("FVP_OTF", ""))
 
 
 def _as_list3(v, kind=float):
@@ -53,6 +49,7 @@ class ProjectLayer(nn.Module):
         self.sample_grid = {}  # seq -> [V, 1, N, 2] fp32 (the reference's cache layout; a view of _packed)
         self._packed = {}      # seq -> [N, GV, 2] voxel-major copy read by the voxelize kernel
         self._cams = {}        # seq -> [V, FVP_CAM_STRIDE] camera records (on-the-fly projection)
+        self._stacked = (None, None)  # (key, [S,N,GV,2]) grids of the last mixed-sequence batch
         self.on_the_fly = None  # None: decide by grid size; True/False: force
         self.verbose = True
 
@@ -114,15 +111,24 @@ class ProjectLayer(nn.Module):
         uniq = list(dict.fromkeys(seqs))
         if len(uniq) == 1:
             return self._packed_grid(uniq[0]), None
-        grids = torch.stack([self._packed_grid(s) for s in uniq])
         index = torch.tensor([uniq.index(s) for s in seqs], dtype=torch.int32).to(device, non_blocking=True)
-        return grids, index
+        return self._stacked_grids(uniq), index
+
+    def _stacked_grids(self, uniq, n0: int = 0, n1: int | None = None) -> torch.Tensor:
+        """[S, n1-n0, GV, 2]: the packed grids of the sequences `uniq` (voxels
+        n0..n1) in one tensor for the kernel, kept across calls while the same
+        sequences come back (a stack is a full copy of every grid)."""
+        grids = [self._packed_grid(s) for s in uniq]
+        n1 = grids[0].shape[0] if n1 is None else n1
+        key = (tuple(uniq), tuple(g.data_ptr() for g in grids), n0, n1)
+        if self._stacked[0] != key:
+            self._stacked = (None, None)  # release the previous stack first
+            self._stacked = (key, torch.stack([g[n0:n1] for g in grids]))
+        return self._stacked[1]
 
     def _project_on_the_fly(self, V) -> bool:
         if self.on_the_fly is not None:
             return bool(self.on_the_fly)
-        if ON_THE_FLY is not None:
-            return ON_THE_FLY
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         return X * Y * Z * ops.grid_slots(V) * 8 > ON_THE_FLY_GRID_BYTES
 
@@ -199,7 +205,13 @@ class ProjectLayer(nn.Module):
             return self._empty(heatmaps, x_end - x_begin, want_cube, want_xy)
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
         n0, n1 = x_begin * Y * Z, x_end * Y * Z
-        slab = grids[n0:n1] if grids.dim() == 3 else grids[:, n0:n1].contiguous()
+        if grids.dim() == 3:
+            slab = grids[n0:n1]
+        else:  # mixed sequences: the stacked slab rows (kept across calls)
+            slab = self._stacked_grids(list(dict.fromkeys(list(meta["seq"])[: heatmaps.shape[0]])), n0, n1)
+        cl = channels_last_of(heatmaps)
+        if cl is not None:
+            return ops.voxelize_cl(cl.t, cl.J, slab, index, x_end - x_begin, Y, Z, want_cube, want_xy)
         return ops.voxelize(heatmaps, slab, index, x_end - x_begin, Y, Z, want_cube, want_xy)
 
     def forward(self, heatmaps, meta, cameras, resize_transform):

@@ -32,6 +32,12 @@ def nms2D(prob_map: torch.Tensor, max_num: int):
     return vals, xy, flat
 
 
+def nms2D_columns(prob_map: torch.Tensor, max_num: int, feature_cubes: torch.Tensor):
+    """nms2D followed by gather_columns at its winners (human_detection_net.py:188,
+    :199-200) in one launch: (topk_values, topk_index, topk_flatten_index, feature_1d [B,K,J,Z])."""
+    return ops.nms_topk_columns(prob_map.detach(), int(max_num), feature_cubes)
+
+
 def gather_columns(feature_cubes: torch.Tensor, topk_flatten_index: torch.Tensor) -> torch.Tensor:
     """feature_1d [B,K,J,Z] of human_detection_net.py:199-200."""
     return ops.gather_columns(feature_cubes, topk_flatten_index)

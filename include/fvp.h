@@ -105,7 +105,8 @@ int fvp_pack_grid(const float *sample_grid, int V, long long N, float *packed, v
  * Replaces ProjectLayer.forward (project_whole.py:119-168) and the first line
  * of CenterNet.forward (lib/models/cnns_2d.py:291).
  *   packed_grids device [n_grids][N][FVP_GRID_SLOTS(V)][2] (fvp_pack_grid)
- *   grid_index   device int32 [B] (grid of frame b) or NULL (all frames use grid 0)
+ *   grid_index   device int32 [B] (grid of frame b, 0 <= g < n_grids: a precondition,
+ *                checked by fvp.ops on host tensors) or NULL (all frames use grid 0)
  *   cube, xy     device outputs; either may be NULL to skip it
  *   workspace    device scratch of >= fvp_voxelize_workspace_bytes(B,V,J,H,W)
  *                bytes (channels-last copy of a chunk of frames; of one 32-joint slice
@@ -177,12 +178,19 @@ int fvp_proposal_centers(const int64_t *index, int index_dims, const float *hm1d
                          const float *bbox, int B, int K, int Z, const float *scale3, const float *bias3,
                          float min_score, float *centers, void *stream);
 
+/* fvp_nms_topk fused with fvp_gather_columns for a map of the cube's own
+ * X x Y grid: the winners' z-columns columns[b,k,j,:] = cube[b,j,flat[b,k],:]
+ * come from the same launch (K <= 16; larger K: two launches).
+ *   cube device [B][J][X][Y][Z];  columns device [B][K][J][Z] */
+int fvp_nms_topk_columns(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
+                         int64_t *flat, int64_t *xy, const float *cube, int J, int Z, float *columns, void *stream);
 /* z-columns of the top-K proposals: columns[b,k,j,:] = cube[b,j,flat[b,k],:]
+ * (an index outside [0, X*Y) reads nothing and yields NaN; torch.gather raises)
  * Replaces the torch.gather at lib/models/human_detection_net.py:199-200. */
 int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z,
                        const int64_t *flat, int K, float *columns, void *stream);
 
-/* bbox sizes at the top-K: out[b,k,c] = size[b,c,flat[b,k]] (c = 0,1)
+/* bbox sizes at the top-K: out[b,k,c] = size[b,c,flat[b,k]] (c = 0,1; NaN for an index outside the map)
  * Replaces the torch.gather at lib/models/human_detection_net.py:191-192. */
 int fvp_gather_bbox(const float *size, int B, int X, int Y,
                     const int64_t *flat, int K, float *out, void *stream);

@@ -200,7 +200,8 @@ def _custom_workload(**kw):
 
 
 @pytest.mark.parametrize("bins,J,hm_size", [((13, 11, 7), 3, (240, 128)), ((8, 8, 1), 32, (64, 48)),
-                                            ((24, 16, 5), 17, (200, 152)), ((1, 1, 9), 2, (2, 2))])
+                                            ((24, 16, 5), 17, (200, 152)), ((1, 1, 9), 2, (2, 2)),
+                                            ((10, 9, 4), 15, (61, 33)), ((6, 7, 5), 20, (45, 31))])
 def test_ragged_shapes_vs_oracle(gpu_device, bins, J, hm_size):
     from fvp import geometry, synthetic
     from fvp.project_whole import ProjectLayer
@@ -920,3 +921,41 @@ def test_forward_batch_mixed_sequences(gpu_device):
     ref = torch.cat(rows, dim=1).reshape(3 * P, *planes.shape[1:])
     assert torch.equal(planes, ref) and torch.equal(offset, torch.cat(offs))
     assert frame_of.tolist() == mask.nonzero()[:, 0].tolist()
+
+
+def test_out_of_range_indices(gpu_device):
+    """Gathers at an index outside the map read nothing and return NaN (the
+    reference's torch.gather raises); a host grid_index out of range is rejected."""
+    from fvp import _lib
+    from fvp.proposal import gather_bbox, gather_columns
+
+    cube = torch.rand((2, 3, 4, 5, 6), device=gpu_device)
+    flat = torch.tensor([[0, 19, 20], [-1, 3, 7]], device=gpu_device)
+    cols = gather_columns(cube, flat)
+    assert torch.isnan(cols[0, 2]).all() and torch.isnan(cols[1, 0]).all()
+    assert torch.equal(cols[0, 1], cube[0, :, 3, 4]) and torch.equal(cols[1, 2], cube[1, :, 1, 2])
+    bb = gather_bbox(torch.rand((2, 2, 4, 5), device=gpu_device), flat)
+    assert torch.isnan(bb[0, 2]).all() and not torch.isnan(bb[0, 1]).any()
+    hm = torch.zeros((2, 1, 2, 8, 8), device=gpu_device)
+    pg = torch.zeros((1, 8, 2, 2), device=gpu_device)
+    with pytest.raises(_lib.FvpError, match="grid_index"):
+        torch.ops.fvp.voxelize(hm, pg, torch.tensor([0, 1], dtype=torch.int32), 2, 2, 2, True, True)
+
+
+@pytest.mark.parametrize("K", [10, 17])
+def test_nms_topk_columns_fused(gpu_device, K):
+    """fvp_nms_topk_columns == fvp_nms_topk then fvp_gather_columns (K <= 16 one
+    launch; K = 17 the two-launch path), on the C2 golden cube's root-joint plane."""
+    from fvp.proposal import gather_columns, nms2D, nms2D_columns
+
+    g = torch.Generator().manual_seed(K)
+    cube = torch.rand((3, 15, 80, 80, 20), generator=g).to(gpu_device)
+    xy = cube.max(dim=4)[0]
+    prob = xy[:, 2:3]
+    v1, i1, f1 = nms2D(prob, K)
+    c1 = gather_columns(cube, f1)
+    v2, i2, f2, c2 = nms2D_columns(prob, K, cube)
+    assert torch.equal(v1, v2) and torch.equal(i1, i2) and torch.equal(f1, f2) and torch.equal(c1, c2)
+    ov, _, ofl = O.nms2d(prob.cpu().numpy(), K)
+    assert np.array_equal(v2.cpu().numpy(), ov)
+    assert np.array_equal(c2.cpu().numpy(), O.gather_columns(cube.cpu().numpy(), f2.cpu().numpy()))

@@ -50,6 +50,7 @@ struct ConvArgs {
     int sy, sx, py, px;     // stride and top/left zero padding: input = row * s - p + tap
     int ks;                 // split-K blocks per parity group (gridDim.z = groups * ks)
     float *part;            // split-K: raw partial sums [gridDim.z][M][Ntot] (no epilogue), else null
+    int in_bf16, out_bf16;  // bf16 kernel only: activations (in; out + residuals) stored as bf16
 };
 
 __host__ __device__ __forceinline__ int conv_groups(int up2) { return up2 == 3 ? 4 : 1; }
@@ -163,9 +164,15 @@ __device__ __forceinline__ size_t conv_out_offset(const ConvArgs &a, int m, int 
 // wait per group instead of one per element).  rowm(l) maps the block-local
 // row l to its row-grid pixel m (or -1 past the image); m must grow with l
 // inside an MFMA tile (the output offsets then grow too).
-template <int TM, int TN, int NACC, int MS, typename AccT, typename RowM>
+// BFO: the output (and the residuals) may be bf16 (a.out_bf16, bf16 kernel).
+template <int TM, int TN, int NACC, int MS, bool BFO = false, typename AccT, typename RowM>
 __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM][TN], const RowM &rowm, int mw,
                                          int nw, int lane, int g) {
+    const bool bfo = BFO && a.out_bf16;
+    const size_t es = bfo ? 2 : 4;  // bytes per output element
+    auto ld = [&](const char *p, unsigned rel) -> float {
+        return bfo ? (float)reinterpret_cast<const __bf16 *>(p)[rel] : reinterpret_cast<const float *>(p)[rel];
+    };
     constexpr int EPI = 4;
     const int Ctot = conv_cols(a.up2, a.Cpo);
     auto rowof = [&](int r) { return MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r; };
@@ -184,9 +191,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
             // offsets grow with m, so rows are addressed relative to the tile's first (32-bit)
             int c_;
             const size_t ob = conv_out_offset(a, mt, nn, g, c_) - co;
-            float *__restrict__ out = a.out + ob;
-            const float *__restrict__ rpre = a.res_pre ? a.res_pre + ob : nullptr;
-            const float *__restrict__ rpost = a.res_post ? a.res_post + ob : nullptr;
+            char *__restrict__ out = reinterpret_cast<char *>(a.out) + ob * es;
+            const char *__restrict__ rpre = a.res_pre ? reinterpret_cast<const char *>(a.res_pre) + ob * es : nullptr;
+            const char *__restrict__ rpost =
+                a.res_post ? reinterpret_cast<const char *>(a.res_post) + ob * es : nullptr;
 #pragma unroll
             for (int r0 = 0; r0 < NACC; r0 += EPI) {
                 unsigned rel[EPI];
@@ -200,11 +208,11 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
                 }
                 if (rpre) {
 #pragma unroll
-                    for (int r = 0; r < EPI; ++r) pre[r] = rpre[rel[r]];
+                    for (int r = 0; r < EPI; ++r) pre[r] = ld(rpre, rel[r]);
                 }
                 if (rpost) {
 #pragma unroll
-                    for (int r = 0; r < EPI; ++r) post[r] = rpost[rel[r]];
+                    for (int r = 0; r < EPI; ++r) post[r] = ld(rpost, rel[r]);
                 }
 #pragma unroll
                 for (int r = 0; r < EPI; ++r) {
@@ -212,7 +220,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const AccT (&acc)[TM
                     if (rpre) v = v + pre[r];
                     if (a.relu) v = fmaxf(v, 0.0f);
                     if (rpost) v = v + post[r];
-                    if (ok[r]) out[rel[r]] = v;
+                    if (ok[r]) {
+                        if (bfo) reinterpret_cast<__bf16 *>(out)[rel[r]] = (__bf16)v;
+                        else reinterpret_cast<float *>(out)[rel[r]] = v;
+                    }
                 }
             }
         }
@@ -525,10 +536,11 @@ struct TileB {
     static_assert(TM >= 1 && TN >= 1, "tile");
 };
 
-template <class TL>
+template <class TL, bool INBF>
 __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
     constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, P = TL::P;
-    constexpr int AE = BM * KC / 4, AV = AE >= 256 ? AE / 256 : 1;  // A: float4 (4 channels) per element
+    constexpr int CPE = INBF ? 8 : 4;                               // channels per A element (16 B bf16 / float4)
+    constexpr int AE = BM * KC / CPE, AV = AE >= 256 ? AE / 256 : 1;
     constexpr int BE = BN * KC / 8, BV = BE >= 256 ? BE / 256 : 1;  // B: 8 bf16 per element
     __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * P];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * P];  // [column][k]
@@ -542,6 +554,8 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
     const size_t Ktot = (size_t)a.KH * a.KW * a.Cpi;
     const __bf16 *__restrict__ w = wb + (size_t)g * a.Cpo_w * Ktot;
     const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
+    // input image rows: fp32 or bf16 elements
+    const size_t esz = INBF ? 2 : 4;
     f32x16 acc[TL::TM][TL::TN];
 #pragma unroll
     for (int i = 0; i < TL::TM; ++i)
@@ -549,22 +563,32 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
         for (int j = 0; j < TL::TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    PixRef pr[AV];
+    int pyx[AV][2];
+    const char *pbase[AV];
 #pragma unroll
-    for (int u = 0; u < AV; ++u) pix_ref(a, m0 + ((u * 256 + t) / (KC / 4)), M, py, px, pr[u]);
-    float4 av[AV];
+    for (int u = 0; u < AV; ++u) {
+        PixRef pr;
+        pix_ref(a, m0 + ((u * 256 + t) / (KC / CPE)), M, py, px, pr);
+        pyx[u][0] = pr.y;
+        pyx[u][1] = pr.x;
+        // pix_ref's row base assumes fp32 elements: recompute for the element size
+        const int m = m0 + ((u * 256 + t) / (KC / CPE));
+        const int img = m < M ? m / (a.Hm * a.Wm) : 0;
+        pbase[u] = reinterpret_cast<const char *>(a.in) + (size_t)img * a.H * a.W * a.Cpi * esz;
+    }
+    uint4 av[AV];  // INBF: 8 bf16; else the bits of a float4
     uint4 bv[BV];
     auto load = [&](int chunk) {
         const int tap = chunk / cpc, c = chunk - tap * cpc;
         const int ky = tap / a.KW, kx = tap - ky * a.KW;
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
-            const int e = u * 256 + t;  // -> (pixel e/(KC/4), 4 channels)
-            const int y = pr[u].y + ky, x = pr[u].x + kx;
-            av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            const int e = u * 256 + t;  // -> (pixel e/(KC/CPE), CPE channels)
+            const int y = pyx[u][0] + ky, x = pyx[u][1] + kx;
+            av[u] = make_uint4(0u, 0u, 0u, 0u);
             if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-                av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * KC +
-                                                         (e % (KC / 4)) * 4);
+                av[u] = *reinterpret_cast<const uint4 *>(
+                    pbase[u] + (((size_t)y * a.W + x) * a.Cpi + c * KC + (e % (KC / CPE)) * CPE) * esz);
         }
 #pragma unroll
         for (int u = 0; u < BV; ++u) {
@@ -581,9 +605,16 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
         for (int u = 0; u < AV; ++u) {
             const int e = u * 256 + t;
             if (e < AE) {
-                bf16x4 h;
-                h[0] = (__bf16)av[u].x; h[1] = (__bf16)av[u].y; h[2] = (__bf16)av[u].z; h[3] = (__bf16)av[u].w;
-                *reinterpret_cast<bf16x4 *>(&As[buf][(e / (KC / 4)) * P + (e % (KC / 4)) * 4]) = h;
+                if constexpr (INBF) {
+                    *reinterpret_cast<uint4 *>(&As[buf][(e / (KC / 8)) * P + (e % (KC / 8)) * 8]) = av[u];
+                } else {
+                    bf16x4 h;
+                    h[0] = (__bf16)__builtin_bit_cast(float, av[u].x);
+                    h[1] = (__bf16)__builtin_bit_cast(float, av[u].y);
+                    h[2] = (__bf16)__builtin_bit_cast(float, av[u].z);
+                    h[3] = (__bf16)__builtin_bit_cast(float, av[u].w);
+                    *reinterpret_cast<bf16x4 *>(&As[buf][(e / (KC / 4)) * P + (e % (KC / 4)) * 4]) = h;
+                }
             }
         }
 #pragma unroll
@@ -613,7 +644,7 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
     }
 
     auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
-    epilogue<TL::TM, TL::TN, 16, 32>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane, g);
+    epilogue<TL::TM, TL::TN, 16, 32, true>(a, acc, rowm, wr * TL::WTM, n0 + wc * TL::WTN, lane, g);
 }
 
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
@@ -807,10 +838,14 @@ static size_t conv_ws_bytes(int N, int Cpi, int KH, int KW, int Cpo, const ConvG
     return p.ks > 1 ? (size_t)conv_groups(g.mode) * p.ks * N * g.Hm * g.Wm * Ntot * sizeof(float) : 0;
 }
 
+// bf16 flags: FVP_CONV_BF16 (operands), FVP_CONV_BF16_IN / _OUT (activations stored as bf16;
+// the output's residuals likewise) -- the last two only with bf16 operands.
 static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void *wpack, int KH, int KW, int Cpo,
                        int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                        const float *res_post, int relu, const ConvGeom &g, float *out, int bf16, int algo, void *ws,
                        size_t ws_bytes, void *stream) {
+    if (bf16 & ~(FVP_CONV_BF16 | FVP_CONV_BF16_IN | FVP_CONV_BF16_OUT)) return FVP_ERR_SHAPE;
+    if ((bf16 & (FVP_CONV_BF16_IN | FVP_CONV_BF16_OUT)) && !(bf16 & FVP_CONV_BF16)) return FVP_ERR_SHAPE;
     if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || Cpo <= 0 || Cpo % 16) return FVP_ERR_SHAPE;
     if (algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return FVP_ERR_SHAPE;
@@ -821,15 +856,22 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
         return FVP_ERR_SHAPE;
     const int G = conv_groups(g.mode);
     fvp::ConvArgs a{in, reinterpret_cast<const float *>(wpack), scale, shift, res_pre, res_post, out, N, H, W, Cpi,
-                    KH, KW, Cpo, Cpo_w, relu, g.mode, g.Hm, g.Wm, g.sy, g.sx, g.py, g.px, 1, nullptr};
+                    KH, KW, Cpo, Cpo_w, relu, g.mode, g.Hm, g.Wm, g.sy, g.sx, g.py, g.px, 1, nullptr,
+                    (bf16 & FVP_CONV_BF16_IN) ? 1 : 0, (bf16 & FVP_CONV_BF16_OUT) ? 1 : 0};
     hipStream_t st = (hipStream_t)stream;
     if (bf16) {  // chunks of one tap x 16 / 32 channels, no split
         if (Cpi % 16) return FVP_ERR_SHAPE;
         const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
 #define FVP_CONVB(BM, BN, WR, KC)                                                                                 \
-    hipLaunchKernelGGL((fvp::conv_bf16_kernel<fvp::TileB<BM, BN, WR, KC>>),                                      \
-                       dim3((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G),       \
-                       dim3(256), 0, st, a, wb)
+    do {                                                                                                          \
+        const dim3 gr((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);             \
+        if (a.in_bf16)                                                                                            \
+            hipLaunchKernelGGL((fvp::conv_bf16_kernel<fvp::TileB<BM, BN, WR, KC>, true>), gr, dim3(256), 0, st, a, \
+                               wb);                                                                               \
+        else                                                                                                      \
+            hipLaunchKernelGGL((fvp::conv_bf16_kernel<fvp::TileB<BM, BN, WR, KC>, false>), gr, dim3(256), 0, st,  \
+                               a, wb);                                                                            \
+    } while (0)
         const bool k32 = Cpi % 32 == 0;
         const long long b128 = G * ((M + 127) / 128) * ((Ntot + 63) / 64);
         if (Ntot <= 32) {
@@ -938,7 +980,7 @@ extern "C" int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cp
     const int st = fvp::legacy_geom(H, W, Cpi, KH, KW, upsample2, g);
     if (st != FVP_OK) return st;
     return fvp::conv_launch(in, N, H, W, Cpi, wpack_bf16, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu,
-                            g, out, 1, FVP_CONV_AUTO, nullptr, 0, stream);
+                            g, out, FVP_CONV_BF16, FVP_CONV_AUTO, nullptr, 0, stream);
 }
 
 extern "C" int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px,
@@ -970,7 +1012,7 @@ extern "C" int fvp_conv2d_nhwc_ex(const float *in, int N, int H, int W, int Cpi,
     const int st = fvp::conv_geom(H, W, Cpi, KH, KW, mode, sy, sx, py, px, g);
     if (st != FVP_OK) return st;
     return fvp::conv_launch(in, N, H, W, Cpi, wpack, KH, KW, Cpo, Cpo_w, scale, shift, res_pre, res_post, relu, g,
-                            out, bf16 ? 1 : 0, algo, workspace, workspace_bytes, stream);
+                            out, bf16, algo, workspace, workspace_bytes, stream);
 }
 
 extern "C" int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int S, int P, float *out,

@@ -8,7 +8,7 @@
 // deterministic.  Indices decode as get_index2D does, dividing by
 // shape[1] == X (proposal.py:27-29,75).
 //
-// nms_select_kernel (K <= 16, X*Y <= 16384): one 1024-thread block per frame,
+// nms_select_kernel (K <= 16, X*Y <= 32640): one 1024-thread block per frame,
 // the elements' 64-bit order keys in registers; a threshold from the wave
 // maxima bounds the candidates, which are compacted and ranked (below).
 // nms_topk_kernel (K > 16): one 256-thread block per frame, the masked map in
@@ -164,61 +164,27 @@ __device__ __forceinline__ unsigned long long wave_max_key(unsigned long long k)
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / kWave;  // 16 >= K
 constexpr int kSelCap = 4096;                   // candidate list capacity
+constexpr int kSelMaxE = 32;                    // elements per thread: maps up to 32768 (C5's 160 x 160)
 
-// Top-K (K <= 16) of one frame's masked map by threshold selection, one
-// 1024-thread block per frame, each thread owning E elements (e = tid + i*1024)
-// as 64-bit order keys in registers (cand_key: NaN first, value descending,
-// index ascending; every key of a real element is > 0):
-//   1. t = the K-th largest of the 16 wave maxima.  Those K maxima are distinct
-//      elements >= t, so at least K elements are >= t, and the top-K are among
-//      the elements >= t.
-//   2. the elements >= t are compacted into an LDS list by wave ballots (a map
-//      typically has tens; an all-equal plateau at most 64*(K-1)+1),
-//   3. every listed candidate counts the listed keys above its own: that rank
-//      is its output slot when < K.
-// A list longer than kSelCap (only for adversarial value layouts) falls back
-// to K block-wide extraction rounds of the largest key below the previous
-// winner (no taken bitmap: keys are unique).
-// K extraction rounds, each the largest key below the previous winner (the
-// select kernel's path for candidate lists longer than kSelCap).
-template <int E>
-__device__ __forceinline__ void select_fallback(const unsigned long long (&key)[E], const float (&val)[E], int b,
-                                                int K, int X, float *__restrict__ vals, int64_t *__restrict__ flat,
-                                                int64_t *__restrict__ xy, unsigned long long *wmax, float &wval,
-                                                int *widx) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned long long prev = ~0ull;
-    for (int r = 0; r < K; ++r) {
-        unsigned long long mine = 0;
-        float mv = 0.0f;
+// Element e of the masked map (max_pool2d 3x3/s1/p1 keep mask, proposal.py:34-52,
+// 66-70): the value itself where it is its neighbourhood's maximum, else
+// 0 * value (max_pool2d propagates NaN; NaN == m is false -> 0 * NaN).
+__device__ __forceinline__ float masked_value(const float *map, int e, int X, int Y) {
+    const int ex = e / Y, ey = e - (e / Y) * Y;
+    const float c = map[e];
+    float m = -INFINITY;
+    bool nan = false;
 #pragma unroll
-        for (int i = 0; i < E; ++i)
-            if (key[i] < prev && key[i] > mine) {
-                mine = key[i];
-                mv = val[i];
-            }
-        const unsigned long long wm = wave_max_key(mine);
-        if (lane == 0) wmax[wave] = wm;
-        __syncthreads();
-        unsigned long long w = 0;
+    for (int dx = -1; dx <= 1; ++dx)
 #pragma unroll
-        for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
-        if (mine == w && mine != 0) wval = mv;  // exactly one owner (unique keys)
-        __syncthreads();
-        if (tid == 0) {
-            const int idx = (int)~(unsigned)w;
-            const size_t o = (size_t)b * K + r;
-            vals[o] = wval;
-            flat[o] = idx;
-            widx[r] = idx;
-            if (xy) {
-                xy[o * 2 + 0] = (int64_t)(idx / X);
-                xy[o * 2 + 1] = (int64_t)(idx % X);
-            }
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int xx = ex + dx, yy = ey + dy;
+            const bool ok = (unsigned)xx < (unsigned)X && (unsigned)yy < (unsigned)Y;
+            const float q = map[ok ? xx * Y + yy : e];  // -inf padding: outside taps ignored
+            nan |= ok && (q != q);
+            m = ok ? fmaxf(m, q) : m;
         }
-        prev = w;
-        __syncthreads();
-    }
+    return ((!nan && c == m) ? 1.0f : 0.0f) * c;
 }
 
 // Optionally fused with the column gather of the winners (cols != null:
@@ -230,6 +196,33 @@ struct ColGather {
     int J, Z;
 };
 
+__device__ __forceinline__ void write_winner(int b, int K, int slot, int idx, float v, int X, float *__restrict__ vals,
+                                             int64_t *__restrict__ flat, int64_t *__restrict__ xy, int *widx) {
+    const size_t o = (size_t)b * K + slot;
+    vals[o] = v;
+    flat[o] = idx;
+    widx[slot] = idx;
+    if (xy) {
+        xy[o * 2 + 0] = (int64_t)(idx / X);
+        xy[o * 2 + 1] = (int64_t)(idx % X);
+    }
+}
+
+// Top-K (K <= 16) of one frame's masked map by threshold selection, one
+// 1024-thread block per frame, each thread owning E elements (e = tid + i*1024)
+// as 64-bit order keys in registers (cand_key: NaN first, value descending,
+// index ascending; every key of a real element is > 0; the masked values are
+// recomputed from the staged map for the few candidates):
+//   1. t = the K-th largest of the 16 wave maxima.  Those K maxima are distinct
+//      elements >= t, so at least K elements are >= t, and the top-K are among
+//      the elements >= t.
+//   2. the elements >= t are compacted into an LDS list by wave ballots (a map
+//      typically has tens; an all-equal plateau at most 64*(K-1)+1),
+//   3. every listed candidate counts the listed keys above its own: that rank
+//      is its output slot when < K.
+// A list longer than kSelCap (only for adversarial value layouts) falls back
+// to K block-wide extraction rounds of the largest key below the previous
+// winner (no taken bitmap: keys are unique).
 template <int E>
 __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__restrict__ prob, long long stride,
                                                                  int X, int Y, int K, float *__restrict__ vals,
@@ -239,11 +232,9 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     const int M = X * Y;
     float *map = reinterpret_cast<float *>(smem);                                             // [M]
     unsigned long long *lkey = reinterpret_cast<unsigned long long *>(smem + (((size_t)M * 4 + 15) & ~(size_t)15));
-    float *lval = reinterpret_cast<float *>(lkey + kSelCap);                                  // [kSelCap]
     __shared__ unsigned long long wmax[kSelWaves];
     __shared__ unsigned long long thr;
     __shared__ int count;
-    __shared__ float wval;
     __shared__ int widx[kSelWaves];  // winners' flat indices (K <= kSelWaves)
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -263,44 +254,13 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     }
     __syncthreads();
 
-    // masked values (max_pool2d 3x3/s1/p1 keep mask, proposal.py:34-52, 66-70) and keys
     unsigned long long key[E];
-    float val[E];
     unsigned long long best = 0;
-    {
-        int e = tid, ex = tid / Y, ey = tid - (tid / Y) * Y;
-        const int dX = kSelThreads / Y, dY = kSelThreads - (kSelThreads / Y) * Y;
 #pragma unroll
-        for (int i = 0; i < E; ++i) {
-            key[i] = 0;
-            val[i] = 0.0f;
-            if (e < M) {
-                const float c = map[e];
-                float m = -INFINITY;
-                bool nan = false;
-#pragma unroll
-                for (int dx = -1; dx <= 1; ++dx)
-#pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy) {
-                        const int xx = ex + dx, yy = ey + dy;
-                        const bool ok = (unsigned)xx < (unsigned)X && (unsigned)yy < (unsigned)Y;
-                        const float q = map[ok ? xx * Y + yy : e];  // -inf padding: outside taps ignored
-                        nan |= ok && (q != q);
-                        m = ok ? fmaxf(m, q) : m;
-                    }
-                // max_pool2d propagates NaN; (c == NaN) is false -> keep = 0 -> 0*c.
-                val[i] = ((!nan && c == m) ? 1.0f : 0.0f) * c;
-                key[i] = cand_key(Cand{val[i], e});
-                best = key[i] > best ? key[i] : best;
-            }
-            e += kSelThreads;
-            ex += dX;
-            ey += dY;
-            if (ey >= Y) {
-                ey -= Y;
-                ++ex;
-            }
-        }
+    for (int i = 0; i < E; ++i) {
+        const int e = tid + i * kSelThreads;
+        key[i] = e < M ? cand_key(Cand{masked_value(map, e, X, Y), e}) : 0ull;
+        best = key[i] > best ? key[i] : best;
     }
     best = wave_max_key(best);
     if (lane == 0) wmax[wave] = best;
@@ -325,10 +285,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
         base = __builtin_amdgcn_readfirstlane(base);
         const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-        if (pred && pos < kSelCap) {
-            lkey[pos] = key[i];
-            lval[pos] = val[i];
-        }
+        if (pred && pos < kSelCap) lkey[pos] = key[i];
     }
     __syncthreads();
     const int C = count;
@@ -339,18 +296,29 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             for (int j = 0; j < C; ++j) rank += lkey[j] > k;
             if (rank < K) {
                 const int idx = (int)~(unsigned)k;
-                const size_t o = (size_t)b * K + rank;
-                vals[o] = lval[c];
-                flat[o] = idx;
-                widx[rank] = idx;
-                if (xy) {
-                    xy[o * 2 + 0] = (int64_t)(idx / X);
-                    xy[o * 2 + 1] = (int64_t)(idx % X);
-                }
+                write_winner(b, K, rank, idx, masked_value(map, idx, X, Y), X, vals, flat, xy, widx);
             }
         }
-    } else {
-        select_fallback<E>(key, val, b, K, X, vals, flat, xy, wmax, wval, widx);
+    } else {  // K rounds, each the largest key below the previous winner
+        unsigned long long prev = ~0ull;
+        for (int r = 0; r < K; ++r) {
+            unsigned long long mine = 0;
+#pragma unroll
+            for (int i = 0; i < E; ++i)
+                if (key[i] < prev && key[i] > mine) mine = key[i];
+            const unsigned long long wm = wave_max_key(mine);
+            if (lane == 0) wmax[wave] = wm;
+            __syncthreads();
+            unsigned long long w = 0;
+#pragma unroll
+            for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
+            if (tid == 0) {
+                const int idx = (int)~(unsigned)w;
+                write_winner(b, K, r, idx, masked_value(map, idx, X, Y), X, vals, flat, xy, widx);
+            }
+            prev = w;
+            __syncthreads();
+        }
     }
     if (!cg.cols) return;
     __syncthreads();
@@ -446,14 +414,15 @@ static int nms_any(const float *prob, int B, int X, int Y, long long frame_strid
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
     hipStream_t st = (hipStream_t)stream;
     const int E = (int)((M + kSelThreads - 1) / kSelThreads);
-    if (K <= kSelWaves && E <= 16) {
-        const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)kSelCap * 12;
+    const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)kSelCap * 8;
+    if (K <= kSelWaves && E <= kSelMaxE && sel_lds <= 159 * 1024) {
         const dim3 g(B), blk(kSelThreads);
         if (E <= 1) hipLaunchKernelGGL((nms_select_kernel<1>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
         else if (E <= 2) hipLaunchKernelGGL((nms_select_kernel<2>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
         else if (E <= 4) hipLaunchKernelGGL((nms_select_kernel<4>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
         else if (E <= 8) hipLaunchKernelGGL((nms_select_kernel<8>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
-        else hipLaunchKernelGGL((nms_select_kernel<16>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        else if (E <= 16) hipLaunchKernelGGL((nms_select_kernel<16>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        else hipLaunchKernelGGL((nms_select_kernel<32>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(nms_topk_kernel, dim3(B), dim3(kNmsThreads), lds, st, prob, frame_stride, X, Y, K, vals, flat,

@@ -54,6 +54,10 @@ class _Block:
 
     def __call__(self, x: Act) -> Act:
         residual = x if self.down is None else self.down(x, relu=False)
+        last = self.convs[-1]
+        want = torch.bfloat16 if (last.bf16 and last.act_bf16) else torch.float32
+        if residual.t.dtype != want:  # the identity residual of the first bf16 block reads the fp32 max pool
+            residual = Act(residual.t.to(want), residual.C)
         y = x
         for c in self.convs[:-1]:
             y = c(y, relu=True)
@@ -67,7 +71,7 @@ class FvpPoseResNet:
     """Eval-mode PoseResNet: ``FvpPoseResNet(resnet)(images[N,3,H,W]) -> heatmaps[N,J,H/4,W/4]``.
 
     dtype torch.bfloat16: bf16 operands with fp32 accumulation on every layer
-    but the RGB stem (opt-in precision).  Weights are read once at construction;
+    but the RGB stem, bf16 activations between the layers (opt-in precision).  Weights are read once at construction;
     rebuild after loading a new state_dict."""
 
     def __init__(self, module: nn.Module, dtype=torch.float32):
@@ -99,6 +103,10 @@ class FvpPoseResNet:
             i += 3
         self.final = ConvLayer(module.final_layer, None, dtype)
         self.num_joints = module.final_layer.out_channels
+        # bf16: activations between the layers stay bf16 in HBM (half the bytes,
+        # no per-chunk conversion); the stem, max pool and the heatmaps are fp32
+        for c in self.layers()[1:-1]:
+            c.act_bf16 = c.bf16
 
     def layers(self):
         out = [self.stem]

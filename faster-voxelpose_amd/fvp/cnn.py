@@ -138,6 +138,7 @@ class ConvLayer:
         self.wpack = pack.contiguous()
         self._ws = {}  # (N, H, W, algo) -> split-K scratch bytes
         self.bf16 = dtype == torch.bfloat16 and self.Cpi % 16 == 0  # an RGB stem stays fp32
+        self.act_bf16 = False  # bf16 operands only: write the output (and read residuals) as bf16
         if self.bf16:  # [G][Cpo_w][K], k contiguous
             self.wpack_bf16 = pack[:, :taps * self.Cpi].transpose(1, 2).contiguous().to(torch.bfloat16)
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
@@ -164,12 +165,20 @@ class ConvLayer:
                  out: torch.Tensor | None = None) -> Act:
         """out: optional preallocated [N, Ho, Wo, Cpo] fp32 destination (e.g. a slice of a larger buffer)."""
         assert x.Cp == self.Cpi, (x.Cp, self.Cpi)
+        if x.t.dtype == torch.bfloat16 and not self.bf16:  # the fp32 kernels read fp32 activations
+            x = Act(x.t.float(), x.C)
         Ho, Wo = self.out_hw(x.H, x.W)
+        odt = torch.bfloat16 if (self.bf16 and self.act_bf16) else torch.float32
         if out is None:
-            out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=torch.float32, device=x.t.device)
-        assert tuple(out.shape) == (x.N, Ho, Wo, self.Cpo) and out.is_contiguous(), (tuple(out.shape), Ho, Wo)
+            out = torch.empty((x.N, Ho, Wo, self.Cpo), dtype=odt, device=x.t.device)
+        assert tuple(out.shape) == (x.N, Ho, Wo, self.Cpo) and out.is_contiguous() and out.dtype == odt, \
+            (tuple(out.shape), Ho, Wo, out.dtype)
         for r in (res_pre, res_post):
-            assert r is None or tuple(r.t.shape) == tuple(out.shape), (None if r is None else r.t.shape, out.shape)
+            assert r is None or (tuple(r.t.shape) == tuple(out.shape) and r.t.dtype == odt), \
+                (None if r is None else (r.t.shape, r.t.dtype), out.shape)
+        flags = 0
+        if self.bf16:  # FVP_CONV_BF16 | _IN | _OUT (include/fvp.h)
+            flags = 1 | (2 if x.t.dtype == torch.bfloat16 else 0) | (4 if odt == torch.bfloat16 else 0)
         key = (x.N, x.H, x.W, CONV_ALGO)
         if key not in self._ws:  # split-K scratch for under-filled launches (0 bytes: the layer does not split)
             self._ws[key] = 0 if self.bf16 else _lib.load().fvp_conv2d_ex_workspace_bytes(
@@ -181,7 +190,7 @@ class ConvLayer:
         _lib.call("fvp_conv2d_nhwc_ex", _ptr(x.t), x.N, x.H, x.W, x.Cp,
                   _ptr(self.wpack_bf16 if self.bf16 else self.wpack), self.KH, self.KW, self.Cpo, self.Cpo_w,
                   _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
-                  _ptr(res_post.t) if res_post else None, int(relu), *self.geom(), int(self.bf16), CONV_ALGO,
+                  _ptr(res_post.t) if res_post else None, int(relu), *self.geom(), flags, CONV_ALGO,
                   _ptr(out), _ptr(ws), nws, _stream(out))
         return Act(out, self.Cout)
 

@@ -326,8 +326,10 @@ int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const vo
  *   in     device [N][H][W][Cpi]: Cpi % 16 == 0, or Cpi in {4, 8, 12} (an RGB
  *          input padded to 4 channels; a K chunk then spans several taps)
  *   wpack  fp32: [G][Krows][Cpo_w], Krows = KH*KW*Cpi rounded up to 16 (zero
- *          rows), G = 4 for mode 3 else 1;  bf16 != 0: bf16 [G][Cpo_w][KH*KW*Cpi]
- *          (Cpi % 16 == 0, no split-K)
+ *          rows), G = 4 for mode 3 else 1;  bf16 & FVP_CONV_BF16: bf16 operands,
+ *          wpack bf16 [G][Cpo_w][KH*KW*Cpi] (Cpi % 16 == 0, no split-K); with
+ *          them, FVP_CONV_BF16_IN: `in` holds bf16 activations, FVP_CONV_BF16_OUT:
+ *          `out`, res_pre and res_post hold bf16 (the pointers are reinterpreted)
  *   out    device [N][Ho][Wo][Cpo];  res_pre / res_post likewise or NULL
  *   algo   FVP_CONV_* (the halo kernel serves stride-1 "same" fp32 convolutions);
  *   workspace as fvp_conv2d_nhwc_ws, sized by fvp_conv2d_ex_workspace_bytes. */
@@ -335,6 +337,9 @@ int fvp_conv2d_nhwc_ex(const float *in, int N, int H, int W, int Cpi, const void
                        int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                        const float *res_post, int relu, int mode, int sy, int sx, int py, int px, int bf16,
                        int algo, float *out, void *workspace, size_t workspace_bytes, void *stream);
+#define FVP_CONV_BF16 1
+#define FVP_CONV_BF16_IN 2
+#define FVP_CONV_BF16_OUT 4
 size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int mode, int sy,
                                      int sx, int py, int px, int algo);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */

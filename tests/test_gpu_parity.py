@@ -959,3 +959,18 @@ def test_nms_topk_columns_fused(gpu_device, K):
     ov, _, ofl = O.nms2d(prob.cpu().numpy(), K)
     assert np.array_equal(v2.cpu().numpy(), ov)
     assert np.array_equal(c2.cpu().numpy(), O.gather_columns(cube.cpu().numpy(), f2.cpu().numpy()))
+
+
+@pytest.mark.parametrize("side", [160, 180, 190])
+def test_nms_large_maps_vs_oracle(gpu_device, side):
+    """C5-sized detection maps: 160^2 and 180^2 through the select kernel (32
+    elements per thread), 190^2 through the K-round kernel; ties included (a
+    quantised map has plateaus)."""
+    from fvp.proposal import nms2D
+
+    g = torch.Generator().manual_seed(side)
+    p = (torch.rand((2, 1, side, side), generator=g) * 64).floor() / 64
+    v, xy, fl = nms2D(p.to(gpu_device), 10)
+    ov, oxy, ofl = O.nms2d(p.numpy(), 10)
+    assert np.array_equal(v.cpu().numpy(), ov) and np.array_equal(fl.cpu().numpy(), ofl)
+    assert np.array_equal(xy.cpu().numpy(), oxy)

@@ -9,7 +9,12 @@ its fused kernel (install(cnn=True)), all with the reference architectures
 (tests/cnn_arch.py) and seeded weights; --torch-cnn runs the same modules on
 torch.  Reports frames/s and a per-stage breakdown (HIP events).
 
-    python tools/bench_pipeline.py [--frames 8] [--steps 10]
+    python tools/bench_pipeline.py [--frames 8] [--steps 10] [--views]
+
+--views starts from the camera images instead: the PoseResNet-50 backbone
+(seeded weights) on B x V images of the IMAGE_SIZE (fvp.backbone: all views
+in one pass, heatmaps written channels-last and read in place by the HDN / JLN;
+with --torch-cnn the reference flow: per-view torch backbone + torch.stack).
 """
 import argparse
 import json
@@ -30,6 +35,7 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--torch-cnn", action="store_true", help="CNNs on torch's convolution instead of fvp")
     ap.add_argument("--bf16", action="store_true", help="fvp CNNs with bf16 operands (opt-in precision)")
+    ap.add_argument("--views", action="store_true", help="start from the images: PoseResNet-50 backbone first")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -83,16 +89,33 @@ def main():
     jl.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
     integration.USE_FVP_CNN = not args.torch_cnn
     integration.FVP_CNN_DTYPE = torch.bfloat16 if args.bf16 else torch.float32
+    backbone = None
+    if args.views:
+        from fvp.backbone import FvpPoseResNet
+
+        rn = cnn_arch.PoseResNet(50, J).eval()
+        rn.load_state_dict(synthetic.seeded_state_dict(rn, 21))
+        rn = rn.to(dev)
+        Wi, Hi = w.image_size
+        views = torch.randn((B, len(cams[seq]), 3, Hi, Wi), generator=torch.Generator().manual_seed(2)).to(dev)
+        if args.torch_cnn:  # the reference flow (faster_voxelpose.py:75)
+            backbone = lambda: torch.stack([rn(views[:, c]) for c in range(views.shape[1])], dim=1)  # noqa: E731
+        else:
+            fb = FvpPoseResNet(rn, torch.bfloat16 if args.bf16 else torch.float32)
+            backbone = lambda: fb.heatmaps_cl(views).planar()  # noqa: E731  (channels-last copy attached)
 
     def step(record=None):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if record is not None else None
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record is not None else None
+        if ev:
+            ev[3].record()
+        heat = backbone() if backbone is not None else hm
         if ev:
             ev[0].record()
-        _, _, centers, _ = integration.fused_hdn_forward(hdn, hm, meta, cams, rt)
+        _, _, centers, _ = integration.fused_hdn_forward(hdn, heat, meta, cams, rt)
         if ev:
             ev[1].record()
         mask = centers[:, :, 3] >= 0
-        fused, _ = jln.fused_jln_forward(jl, meta, hm, centers, mask, cams, rt)
+        fused, _ = jln.fused_jln_forward(jl, meta, heat, centers, mask, cams, rt)
         if ev:
             ev[2].record()
             record.append(ev)
@@ -114,10 +137,13 @@ def main():
             reps.append((e0.elapsed_time(e1) / args.steps, evs))
     reps.sort(key=lambda r: r[0])
     ms, evs = reps[1]
-    hdn_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
-    jln_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    hdn_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in evs]))
+    jln_ms = float(np.mean([b.elapsed_time(c) for _, b, c, _ in evs]))
+    bb_ms = float(np.mean([d.elapsed_time(a) for a, _, _, d in evs]))
     print(json.dumps({
-        "metric": "HDN+JLN inference after the backbone (heatmaps -> fused 3-D poses)", "unit": "frames/s",
+        "metric": ("views -> backbone -> HDN+JLN (images -> fused 3-D poses)" if args.views else
+                   "HDN+JLN inference after the backbone (heatmaps -> fused 3-D poses)"), "unit": "frames/s",
+        "backbone_ms": round(bb_ms, 3) if args.views else None,
         "value": round(B / (ms * 1e-3), 1), "ms_per_batch": round(ms, 3),
         "ms_per_batch_repeats": [round(r[0], 3) for r in reps], "frames": B, "proposals_per_frame": K,
         "hdn_ms": round(hdn_ms, 3), "jln_ms": round(jln_ms, 3),

@@ -39,6 +39,8 @@ def main():
     cams, seq = w.cameras()
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float32, device=dev)
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 1)).to(dev)
+    if w.dtype == "float16":  # C5: fp16 heatmaps, as bench.py
+        hm = hm.half()
     J = w.num_joints
     if args.layout == "channels-last":
         t = torch.zeros(hm.shape[:2] + hm.shape[3:] + (16 * ((J + 15) // 16),), device=dev)

@@ -57,6 +57,12 @@ def main():
     meta = {"seq": [seq] * B}
 
     class Proposal(nn.Module):  # test-mode ProposalLayer (human_detection_net.py:99-124)
+        # the constants the fused HDN's proposal_centers kernel reads; min_score -1:
+        # every proposal valid, so the JLN runs at full K (stand-in confidences)
+        scale = [float(s) / (float(n) - 1) for s, n in zip(w.space_size, w.voxels_per_axis)]
+        bias = [float(c) - float(s) / 2.0 for c, s in zip(w.space_center, w.space_size)]
+        min_score = -1.0
+
         def forward(self, topk_index, topk_confs, match_bbox, meta):
             scale = torch.tensor(w.space_size, device=dev) / (torch.tensor(w.voxels_per_axis, device=dev) - 1)
             bias = torch.tensor(w.space_center, device=dev) - torch.tensor(w.space_size, device=dev) / 2.0
@@ -112,6 +118,7 @@ def main():
         if ev:
             ev[0].record()
         _, _, centers, _ = integration.fused_hdn_forward(hdn, heat, meta, cams, rt)
+        centers[:, :, 5:7].clamp_(0.3, 0.8)  # seeded bbox head: keep every person window non-empty
         if ev:
             ev[1].record()
         mask = centers[:, :, 3] >= 0

@@ -244,6 +244,20 @@ __device__ __forceinline__ void epilogue_staged(const ConvArgs &a, const AccT (&
     }
 }
 
+// Output tile of this workgroup.  Workgroups are dealt round robin over the 8
+// XCDs (each with its own L2): the dispatch index is regrouped so that every
+// XCD gets a contiguous run of logical tiles, and the logical order walks the
+// column tiles of one row tile together, so a row tile's activations come from
+// HBM once and from that XCD's L2 for its other column tiles (a 2-D grid in
+// hardware order re-read them from HBM once per column tile).
+__device__ __forceinline__ void conv_tile(int &mt, int &nt) {
+    const unsigned T = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned q = T >> 3, r = T & 7, x = lin & 7, loc = lin >> 3;
+    const unsigned id = x < r ? x * (q + 1) + loc : r * (q + 1) + (x - r) * q + loc;
+    nt = (int)(id % gridDim.y);
+    mt = (int)(id / gridDim.y);
+}
+
 template <class TL>
 __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, AP = TL::AP, MS = TL::MS;
@@ -255,7 +269,9 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     float (*As)[BM * AP] = reinterpret_cast<float (*)[BM * AP]>(smem);
     float (*Bs)[KC * BN] = reinterpret_cast<float (*)[KC * BN]>(smem + 2 * BM * AP);
     const int M = a.N * a.Hm * a.Wm;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    int mt, nt;
+    conv_tile(mt, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave % TL::WR, wc = wave / TL::WR;
     const int g = blockIdx.z / a.ks, kz = blockIdx.z - g * a.ks;  // parity group, split-K slice
@@ -402,9 +418,11 @@ __global__ __launch_bounds__(256, 4) void conv_halo_kernel(ConvArgs a, int tiles
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave % TL::WR, wc = wave / TL::WR;
     const int per_img = tiles_x * tiles_y;
-    const int img = blockIdx.x / per_img, tr = blockIdx.x - img * per_img;
+    int mt, nt;
+    conv_tile(mt, nt);
+    const int img = mt / per_img, tr = mt - img * per_img;
     const int y0 = (tr / tiles_x) * TH, x0 = (tr - (tr / tiles_x) * tiles_x) * TW;
-    const int n0 = blockIdx.y * BN;
+    const int n0 = nt * BN;
     const int HWd = TW + a.KW - 1, HP = (TH + a.KH - 1) * HWd;
     const int hy0 = y0 - (a.KH - 1) / 2, hx0 = x0 - (a.KW - 1) / 2;
     const float *__restrict__ inimg = a.in + (size_t)img * a.H * a.W * a.Cpi;
@@ -567,13 +585,20 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
     __bf16 (*As)[BM * P] = reinterpret_cast<__bf16 (*)[BM * P]>(smem);
     __bf16 (*Bs)[BN * P] = reinterpret_cast<__bf16 (*)[BN * P]>(reinterpret_cast<__bf16 *>(smem) + 2 * BM * P);  // [column][k]
     const int M = a.N * a.Hm * a.Wm;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    int mt, nt;
+    conv_tile(mt, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave % TL::WR, wc = wave / TL::WR;
     const int g = blockIdx.z;  // parity group (mode 3), else 0
-    const int cpc = a.Cpi / KC;
-    const int nchunks = a.KH * a.KW * cpc;
-    const size_t Ktot = (size_t)a.KH * a.KW * a.Cpi;
+    // Cpi % KC == 0: a chunk is one tap x KC channels; an RGB input at a 4 / 8 /
+    // 12-channel pitch (fp32) instead spans several taps per chunk, each
+    // element its own tap, with the weight rows zero padded to 16 (KC = 16)
+    const bool small = a.Cpi % KC != 0;
+    const int cpc = small ? 1 : a.Cpi / KC;
+    const int ntaps = a.KH * a.KW;
+    const size_t Ktot = small ? (size_t)conv_krows(a.KH, a.KW, a.Cpi) : (size_t)ntaps * a.Cpi;  // weight row
+    const int nchunks = (int)(Ktot / KC);
     const __bf16 *__restrict__ w = wb + (size_t)g * a.Cpo_w * Ktot;
     const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
     // input image rows: fp32 or bf16 elements
@@ -602,22 +627,27 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
     uint4 bv[BV];
     auto load = [&](int chunk) {
         const int tap = chunk / cpc, c = chunk - tap * cpc;
-        const int ky = tap / a.KW, kx = tap - ky * a.KW;
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
             const int e = u * 256 + t;  // -> (pixel e/(KC/CPE), CPE channels)
+            int tp = tap, ci = c * KC + (e % (KC / CPE)) * CPE;
+            if (!INBF && small) {  // this element's own tap (k past the taps reads 0)
+                const int k = chunk * KC + (e % (KC / CPE)) * CPE;
+                tp = k / a.Cpi;
+                ci = k - tp * a.Cpi;
+            }
+            const int ky = tp / a.KW, kx = tp - (tp / a.KW) * a.KW;
             const int y = pyx[u][0] + ky, x = pyx[u][1] + kx;
             av[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
-                av[u] = *reinterpret_cast<const uint4 *>(
-                    pbase[u] + (((size_t)y * a.W + x) * a.Cpi + c * KC + (e % (KC / CPE)) * CPE) * esz);
+            if (e < AE && tp < ntaps && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
+                av[u] = *reinterpret_cast<const uint4 *>(pbase[u] + (((size_t)y * a.W + x) * a.Cpi + ci) * esz);
         }
 #pragma unroll
         for (int u = 0; u < BV; ++u) {
             const int e = u * 256 + t;  // -> (column e/(KC/8), 8 k)
             if (e < BE)
-                bv[u] = *reinterpret_cast<const uint4 *>(w + (size_t)(n0 + e / (KC / 8)) * Ktot +
-                                                        (size_t)tap * a.Cpi + c * KC + (e % (KC / 8)) * 8);
+                bv[u] = *reinterpret_cast<const uint4 *>(w + (size_t)(n0 + e / (KC / 8)) * Ktot + (size_t)chunk * KC +
+                                                        (e % (KC / 8)) * 8);
         }
     };
     load(0);
@@ -882,8 +912,8 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
                     KH, KW, Cpo, Cpo_w, relu, g.mode, g.Hm, g.Wm, g.sy, g.sx, g.py, g.px, 1, nullptr,
                     (bf16 & FVP_CONV_BF16_IN) ? 1 : 0, (bf16 & FVP_CONV_BF16_OUT) ? 1 : 0};
     hipStream_t st = (hipStream_t)stream;
-    if (bf16) {  // chunks of one tap x 16 / 32 channels, no split
-        if (Cpi % 16) return FVP_ERR_SHAPE;
+    if (bf16) {  // chunks of one tap x 16 / 32 channels (or several taps of a 4/8/12-channel input), no split
+        if (Cpi % 16 && (bf16 & FVP_CONV_BF16_IN)) return FVP_ERR_SHAPE;
         const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
 #define FVP_CONVB(BM, BN, WR, KC)                                                                                 \
     do {                                                                                                          \

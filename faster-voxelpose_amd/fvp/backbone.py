@@ -70,8 +70,8 @@ class _Block:
 class FvpPoseResNet:
     """Eval-mode PoseResNet: ``FvpPoseResNet(resnet)(images[N,3,H,W]) -> heatmaps[N,J,H/4,W/4]``.
 
-    dtype torch.bfloat16: bf16 operands with fp32 accumulation on every layer
-    but the RGB stem, bf16 activations between the layers (opt-in precision).  Weights are read once at construction;
+    dtype torch.bfloat16: bf16 operands with fp32 accumulation on every layer,
+    bf16 activations between the layers (opt-in precision).  Weights are read once at construction;
     rebuild after loading a new state_dict."""
 
     def __init__(self, module: nn.Module, dtype=torch.float32):
@@ -104,7 +104,8 @@ class FvpPoseResNet:
         self.final = ConvLayer(module.final_layer, None, dtype)
         self.num_joints = module.final_layer.out_channels
         # bf16: activations between the layers stay bf16 in HBM (half the bytes,
-        # no per-chunk conversion); the stem, max pool and the heatmaps are fp32
+        # no per-chunk conversion); the RGB input, the stem's output (max pool)
+        # and the heatmaps are fp32
         for c in self.layers()[1:-1]:
             c.act_bf16 = c.bf16
 

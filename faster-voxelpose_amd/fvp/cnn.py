@@ -137,10 +137,10 @@ class ConvLayer:
             pack = torch.cat([pack, pack.new_zeros((self.G, krows - taps * self.Cpi, self.Cpo_w))], dim=1)
         self.wpack = pack.contiguous()
         self._ws = {}  # (N, H, W, algo) -> split-K scratch bytes
-        self.bf16 = dtype == torch.bfloat16 and self.Cpi % 16 == 0  # an RGB stem stays fp32
+        self.bf16 = dtype == torch.bfloat16
         self.act_bf16 = False  # bf16 operands only: write the output (and read residuals) as bf16
-        if self.bf16:  # [G][Cpo_w][K], k contiguous
-            self.wpack_bf16 = pack[:, :taps * self.Cpi].transpose(1, 2).contiguous().to(torch.bfloat16)
+        if self.bf16:  # [G][Cpo_w][Krows], k contiguous (rows past the taps zero)
+            self.wpack_bf16 = pack.transpose(1, 2).contiguous().to(torch.bfloat16)
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
         if bn is not None:  # eval BatchNorm: (x - mean) / sqrt(var + eps) * gamma + beta
             s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
@@ -165,7 +165,7 @@ class ConvLayer:
                  out: torch.Tensor | None = None) -> Act:
         """out: optional preallocated [N, Ho, Wo, Cpo] fp32 destination (e.g. a slice of a larger buffer)."""
         assert x.Cp == self.Cpi, (x.Cp, self.Cpi)
-        if x.t.dtype == torch.bfloat16 and not self.bf16:  # the fp32 kernels read fp32 activations
+        if x.t.dtype == torch.bfloat16 and (not self.bf16 or self.Cpi % 16):  # fp32 kernels / 4-12 channel input
             x = Act(x.t.float(), x.C)
         Ho, Wo = self.out_hw(x.H, x.W)
         odt = torch.bfloat16 if (self.bf16 and self.act_bf16) else torch.float32

@@ -327,7 +327,8 @@ int fvp_conv2d_nhwc_bf16(const float *in, int N, int H, int W, int Cpi, const vo
  *          input padded to 4 channels; a K chunk then spans several taps)
  *   wpack  fp32: [G][Krows][Cpo_w], Krows = KH*KW*Cpi rounded up to 16 (zero
  *          rows), G = 4 for mode 3 else 1;  bf16 & FVP_CONV_BF16: bf16 operands,
- *          wpack bf16 [G][Cpo_w][KH*KW*Cpi] (Cpi % 16 == 0, no split-K); with
+ *          wpack bf16 [G][Cpo_w][Krows] (no split-K; a 4/8/12-channel input
+ *          must be fp32); with
  *          them, FVP_CONV_BF16_IN: `in` holds bf16 activations, FVP_CONV_BF16_OUT:
  *          `out`, res_pre and res_post hold bf16 (the pointers are reinterpreted)
  *   out    device [N][Ho][Wo][Cpo];  res_pre / res_post likewise or NULL

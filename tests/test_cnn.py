@@ -156,6 +156,30 @@ def test_bf16_conv_layer_vs_torch(gpu_device, cin, cout, k, hw, up):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cpi,k,stride,hw", [(3, 4, 7, 2, (67, 45)), (3, 8, 3, 1, (20, 33)),
+                                                 (10, 12, 5, 2, (31, 30)), (4, 4, 1, 1, (9, 9))])
+def test_bf16_small_channel_conv_vs_torch(gpu_device, cin, cpi, k, stride, hw):
+    """bf16 operands on a 4 / 8 / 12-channel fp32 input (the RGB stem,
+    resnet.py:222-224): one K chunk spans several taps; within 2e-2 of the
+    output scale of torch's fp32 convolution."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    seq = nn.Sequential(nn.Conv2d(cin, 64, k, stride=stride, padding=k // 2, bias=False), nn.BatchNorm2d(64)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin * 11 + k))
+    seq = seq.to(gpu_device)
+    x = torch.rand((2, cin) + hw, generator=torch.Generator().manual_seed(k)).to(gpu_device)
+    with torch.no_grad():
+        ref = torch.relu(seq(x))
+    layer = cnn.ConvLayer(seq[0], seq[1], torch.bfloat16, cpi=cpi)
+    assert layer.bf16
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x, cpi), relu=True))
+    err = float((got - ref).abs().max()) / float(ref.abs().max())
+    assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
 def test_bf16_p2pnet_vs_reference(gpu_device):
     """Whole P2PNet with bf16 operands against the reference's fp32 golden:
     within 5e-2 of the output scale (errors compound over 20 convolutions)."""

@@ -30,7 +30,7 @@
 // next chunk's global loads issued before the current chunk's MFMAs.
 #include <type_traits>
 
-#include "fvp_device.h"
+#include "fvp_layout.h"  // fvp_device.h, buffer descriptors (uniform_rsrc, kOOB)
 
 namespace fvp {
 
@@ -166,11 +166,13 @@ __device__ __forceinline__ size_t conv_out_offset(const ConvArgs &a, int m, int 
 // lane-per-channel epilogue straight from the MFMA registers issues 2-4 B per
 // lane: the wide 1x1 "expand" convolutions and their residual reads ran at
 // ~1.4 TB/s; bf16 ResNet-50 19.0 -> 14.6 ms, P2PNet 1.89 -> 1.78 ms.)
+template <int BM, int BN, bool BFO, typename RowM>
+__device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &rowm, int n0, int g, const float *cs);
+
 template <int BM, int BN, int TM, int TN, int NACC, int MS, bool BFO, typename AccT, typename RowM>
 __device__ __forceinline__ void epilogue_staged(const ConvArgs &a, const AccT (&acc)[TM][TN], const RowM &rowm,
                                                 int mw, int nwl, int n0, int lane, int g, float *cs) {
     constexpr int CP = BN + 4;  // row pitch (floats): 16-B aligned rows
-    constexpr int G = BN / 8;   // 8-channel groups per row
     auto rowof = [&](int r) { return MS == 32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r; };
     __syncthreads();  // every wave is past its last LDS read of the K loop
 #pragma unroll
@@ -181,21 +183,34 @@ __device__ __forceinline__ void epilogue_staged(const ConvArgs &a, const AccT (&
             for (int r = 0; r < NACC; ++r)
                 cs[(mw + i * MS + rowof(r)) * CP + nwl + j * MS + (lane % MS)] = acc[i][j][r];
     __syncthreads();
+    epilogue_write<BM, BN, BFO>(a, rowm, n0, g, cs);
+}
+
+// The write half: each thread takes (pixel, 8 output channels) units of the
+// staged [BM][BN + 4] fp32 tile; a thread's units share one channel group
+// (256 % (BN / 8) == 0), so its scale / shift are loaded once.
+template <int BM, int BN, bool BFO, typename RowM>
+__device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &rowm, int n0, int g, const float *cs) {
+    constexpr int CP = BN + 4;
+    constexpr int G = BN / 8;  // 8-channel groups per row
+    static_assert(256 % G == 0, "one channel group per thread");
     const bool bfo = BFO && a.out_bf16;
     const int Ctot = conv_cols(a.up2, a.Cpo);
-    for (int u = threadIdx.x; u < BM * G; u += 256) {
-        const int row = u / G, cg = u - (u / G) * G;
+    const int cg = threadIdx.x % G;
+    const int n = n0 + cg * 8;
+    if (n >= Ctot) return;  // Ctot is a multiple of 16: whole groups
+    const int co = (a.up2 == 1 || a.up2 == 2) ? n % a.Cpo : n;
+    const float4 s0 = *reinterpret_cast<const float4 *>(a.scale + co);
+    const float4 s1 = *reinterpret_cast<const float4 *>(a.scale + co + 4);
+    const float4 h0 = *reinterpret_cast<const float4 *>(a.shift + co);
+    const float4 h1 = *reinterpret_cast<const float4 *>(a.shift + co + 4);
+    for (int row = threadIdx.x / G; row < BM; row += 256 / G) {
         const int m = rowm(row);
-        const int n = n0 + cg * 8;
-        if (m < 0 || n >= Ctot) continue;  // Ctot is a multiple of 16: whole groups
-        int co;
-        const size_t off = conv_out_offset(a, m, n, g, co);  // 8 consecutive output channels from off
+        if (m < 0) continue;
+        int co_;
+        const size_t off = conv_out_offset(a, m, n, g, co_);  // 8 consecutive output channels from off
         const float4 c0 = *reinterpret_cast<const float4 *>(cs + row * CP + cg * 8);
         const float4 c1 = *reinterpret_cast<const float4 *>(cs + row * CP + cg * 8 + 4);
-        const float4 s0 = *reinterpret_cast<const float4 *>(a.scale + co);
-        const float4 s1 = *reinterpret_cast<const float4 *>(a.scale + co + 4);
-        const float4 h0 = *reinterpret_cast<const float4 *>(a.shift + co);
-        const float4 h1 = *reinterpret_cast<const float4 *>(a.shift + co + 4);
         float v[8] = {c0.x * s0.x + h0.x, c0.y * s0.y + h0.y, c0.z * s0.z + h0.z, c0.w * s0.w + h0.w,
                       c1.x * s1.x + h1.x, c1.y * s1.y + h1.y, c1.z * s1.z + h1.z, c1.w * s1.w + h1.w};
         auto load8 = [&](const float *base, float (&o)[8]) {
@@ -700,6 +715,173 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
                                                          smem);
 }
 
+// ---- bf16 activations, Cpi % 64 == 0: LDS-DMA staged implicit GEMM -------------
+// The backbone's bf16 layers (bf16 NHWC in, weights bf16 [G][Cpo_w][K]).  A
+// K step is one tap x 64 channels = one 128-B row per pixel / output column.
+// Both operands go global -> LDS by buffer_load_dwordx4 ... lds (no VGPR
+// staging, no LDS write pass): one wave instruction moves 8 whole rows (1 KiB, lane l
+// -> row l/8, 16-B slot l%8).  The LDS image is lane-linear, so the bank
+// swizzle is applied on the SOURCE side: slot s of row r holds the row's
+// 16-B chunk s ^ ((r >> 1) & 7), which makes the ds_read_b128 fragment reads
+// of v_mfma_f32_32x32x16_bf16 (lane -> row lane&31, chunk 2*kk + lane/32)
+// conflict-free.  Padding taps and rows past M read zeros (range check).  Two
+// stages: step s+1 is in flight while step s feeds the MFMAs (counted vmcnt,
+// raw s_barrier: a __syncthreads() would drain the prefetch).  Tile 128 x BN,
+// waves 2 x 2 (64 x BN/2 each).  Measured before it (register-staged
+// conv_bf16_kernel, 3x3 64->64 at 40 x 128 x 240): 18 VALU + 17 SALU per
+// MFMA, 41 % of wave time parked on waits, 33 % of LDS cycles bank conflicts.
+
+#define FVP_WAIT_BARRIER(vm) asm volatile("s_waitcnt vmcnt(" #vm ")\n\ts_barrier" ::: "memory")
+
+template <int BN>
+__global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
+    constexpr int BM = 128, WTN = BN / 2, TN = WTN / 32, NBI = BN / 32;  // NBI: B row groups of 8 per wave
+    constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;
+    constexpr int KLDS = 2 * STAGE, CLDS = BM * (BN + 4) * 4;
+    static_assert(NBI == 2 || NBI == 4, "BN 64 or 128");
+    __shared__ __attribute__((aligned(16))) float smem[(KLDS > CLDS ? KLDS : CLDS) / 4];
+    char *lds = reinterpret_cast<char *>(smem);
+    const int M = a.N * a.Hm * a.Wm;
+    int mt, nt;
+    conv_tile(mt, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wr = wave & 1, wc = wave >> 1;
+    const int g = blockIdx.z;  // parity group (mode 3), else 0
+    const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
+    const int cpc = a.Cpi >> 6, nks = a.KH * a.KW * cpc;
+    const size_t Ktot = (size_t)a.KH * a.KW * a.Cpi;
+    const int slot = lane & 7;
+    // Both operands through buffer descriptors (32-bit offsets; the host keeps
+    // the activations under 2 GiB): a padding tap or a row past M reads at
+    // kOOB, which the range check turns into zeros.  Per row, the input offset
+    // of tap (0, 0) and a bit mask of the taps inside the image are decoded
+    // once (quotients by a float reciprocal + one correction: M < 2^24).
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(a.in, (unsigned)((size_t)a.N * a.H * a.W * a.Cpi * 2));
+    const __amdgpu_buffer_rsrc_t rb =
+        uniform_rsrc(wb + (size_t)g * a.Cpo_w * Ktot, (unsigned)((size_t)a.Cpo_w * Ktot * 2));
+    const int HWm = a.Hm * a.Wm;
+    const float inv_hw = 1.0f / (float)HWm, inv_w = 1.0f / (float)a.Wm;
+    auto qdiv = [](int n, int d, float inv) {
+        int q = (int)((float)n * inv);
+        const int r = n - q * d;
+        return q + (r >= d) - (r < 0);
+    };
+    unsigned rep = 0;  // bit ky*KW set for every tap row (uniform)
+    for (int ky = 0; ky < a.KH; ++ky) rep |= 1u << (ky * a.KW);
+    int voa[4];
+    unsigned tmask[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+        const int m = m0 + r, mm = m < M ? m : 0;
+        const int img = qdiv(mm, HWm, inv_hw), rr = mm - img * HWm;
+        const int oy = qdiv(rr, a.Wm, inv_w), ox = rr - oy * a.Wm;
+        const int y0 = oy * a.sy - py, x0 = ox * a.sx - px;
+        // taps inside the image: ky in [max(0, -y0), min(KH, H - y0)), likewise kx
+        const int ylo = min(max(-y0, 0), a.KH), yhi = min(max(a.H - y0, 0), a.KH);
+        const int xlo = min(max(-x0, 0), a.KW), xhi = min(max(a.W - x0, 0), a.KW);
+        const unsigned xm = ((1u << xhi) - 1u) & ~((1u << xlo) - 1u);  // KW <= 32 bits
+        // tap rows ylo..yhi-1 of the all-rows pattern rep = sum 2^(ky*KW): mask = xm * rep(rows)
+        const unsigned rows = (unsigned)(((1ull << (yhi * a.KW)) - 1ull) & ~((1ull << (ylo * a.KW)) - 1ull));
+        tmask[i] = m < M ? xm * (rep & rows) : 0u;
+        const int c = slot ^ ((r >> 1) & 7);
+        voa[i] = (((img * a.H + y0) * a.W + x0) * a.Cpi + c * 8) * 2;  // may be negative: only valid taps use it
+    }
+    int vob[NBI];
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+        const int r = (wave * NBI + i) * 8 + (lane >> 3);
+        vob[i] = ((n0 + r) * (int)Ktot + (slot ^ ((r >> 1) & 7)) * 8) * 2;
+    }
+    typedef __attribute__((address_space(3))) void *lds_ptr;
+    auto issue = [&](int ks, int tap, int d, int buf) {
+        char *sa = lds + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned vo = (tmask[i] >> tap) & 1u ? (unsigned)(voa[i] + d) : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(sa + (wave * 4 + i) * 1024), 16, vo, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < NBI; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(sa + ABYTES + (wave * NBI + i) * 1024), 16,
+                                                     (unsigned)(vob[i] + ks * 128), 0, 0, 0);
+    };
+    f32x16 acc[2][TN];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    int tap = 0, kx = 0, cc = 0, d = 0;  // tap, its column and channel chunk, byte delta of the next step
+    auto advance = [&]() {
+        d += 128;
+        if (++cc == cpc) {
+            cc = 0;
+            ++tap;
+            if (++kx == a.KW) {
+                kx = 0;
+                d += (a.W - a.KW) * a.Cpi * 2;  // next tap row
+            }
+        }
+    };
+    issue(0, 0, 0, 0);
+    advance();
+    for (int ks = 0; ks < nks; ++ks) {
+        const int buf = ks & 1;
+        if (ks + 1 < nks) {  // buf ^ 1 was last read in step ks - 1, before its closing barrier
+            issue(ks + 1, tap, d, buf ^ 1);
+            advance();
+            if constexpr (NBI == 4) FVP_WAIT_BARRIER(8);  // step ks landed (this wave's), then everyone's
+            else FVP_WAIT_BARRIER(6);
+        } else {
+            FVP_WAIT_BARRIER(0);
+        }
+        const char *sa = lds + buf * STAGE, *sb = sa + ABYTES;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int c = kk * 2 + (lane >> 5);
+            bf16x8 fa[2], fb[TN];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = wr * 64 + i * 32 + (lane & 31);
+                fa[i] = *reinterpret_cast<const bf16x8 *>(sa + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = wc * WTN + j * 32 + (lane & 31);
+                fb[j] = *reinterpret_cast<const bf16x8 *>(sb + col * 128 + ((c ^ ((col >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)  // D = W x A^T: lane -> pixel, 4 consecutive registers -> 4 channels
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buf is free for step ks + 2
+    }
+    // stage [pixel][channel] with one 16-B write per 4 accumulators (register
+    // r of tile (i, j): pixel i*32 + lane%32, channel j*32 + 8*(r/4) + 4*(lane/32) + r%4)
+    {
+        constexpr int CP = BN + 4;
+        float *cs = smem + (wr * 64 + (lane & 31)) * CP + wc * WTN + 4 * (lane >> 5);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4 *>(cs + i * 32 * CP + j * 32 + q * 8) =
+                        make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+    }
+    __syncthreads();
+    auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
+    epilogue_write<BM, BN, true>(a, rowm, n0, g, smem);
+}
+#undef FVP_WAIT_BARRIER
+
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
 // cnns_2d.py Pool2DBlock; F.max_pool1d(x, 2, 2) on H == 1 rows, cnns_1d.py Pool1DBlock)
 template <int KH, int KW>
@@ -915,7 +1097,22 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
     if (bf16) {  // chunks of one tap x 16 / 32 channels (or several taps of a 4/8/12-channel input), no split
         if (Cpi % 16 && (bf16 & FVP_CONV_BF16_IN)) return FVP_ERR_SHAPE;
         const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
-#define FVP_CONVB(BM, BN, WR, KC)                                                                                 \
+        // LDS-DMA kernel, except on the wide 1x1 "expand" layers over large maps
+        // (Ntot >= 4 K: 1-4 K steps, output-bound), which keep the register-staged
+        // kernel's 4 blocks per CU (measured: ResNet-50's 64->256 at 128x240 0.43 vs
+        // 0.58 ms, 3x3 64->64 0.21 -> 0.17 ms, deconv 256->256 at 64x120 1.21 -> 0.84 ms)
+        const long long Kd = (long long)KH * KW * Cpi;
+        const bool expand = Ntot >= 4 * Kd && M >= 65536;
+        const bool fits = (long long)N * H * W * Cpi * 2 < (1LL << 31) && (long long)Cpo_w * Kd * 2 < (1LL << 31) &&
+                          KH * KW <= 32 && M < (1 << 24);  // 32-bit buffer offsets, tap masks, row decode
+        if (a.in_bf16 && Cpi % 64 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && !expand && fits) {
+            const int BN = Ntot > 64 ? 128 : 64;
+            const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
+            if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128>), gr, dim3(256), 0, st, a, wb);
+            else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64>), gr, dim3(256), 0, st, a, wb);
+            return (int)hipGetLastError();
+        }
+#define FVP_CONVB(BM, BN, WR, KC)                                                                               \
     do {                                                                                                          \
         const dim3 gr((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);             \
         if (a.in_bf16)                                                                                            \

@@ -180,6 +180,53 @@ def test_bf16_small_channel_conv_vs_torch(gpu_device, cin, cpi, k, stride, hw):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,stride,hw,deconv,res", [(64, 64, 3, 1, (33, 47), False, False),
+                                                             (128, 256, 3, 2, (30, 17), False, True),
+                                                             (256, 64, 1, 1, (20, 21), False, True),
+                                                             (64, 512, 1, 2, (19, 23), False, False),
+                                                             (256, 128, 4, 2, (9, 11), True, False),
+                                                             (192, 96, 3, 1, (7, 130), False, False)])
+def test_bf16_dma_conv_matches_register_staged(gpu_device, cin, cout, k, stride, hw, deconv, res):
+    """bf16 activations with Cpi % 64 == 0 run the LDS-DMA kernel
+    (conv_bf16_dma_kernel); CONV_PER_TAP_NOSPLIT keeps such layers on the
+    register-staged conv_bf16_kernel.  Both walk k in the same order with the
+    same MFMA instruction, so the outputs are bit-identical; and within 2e-2 of
+    the output scale of torch's fp32 convolution of the bf16-rounded input."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    conv = (nn.ConvTranspose2d(cin, cout, 4, stride=2, padding=1) if deconv
+            else nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False))
+    seq = nn.Sequential(conv, nn.BatchNorm2d(cout)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin + 3 * cout + k))
+    seq = seq.to(gpu_device)
+    gen = torch.Generator().manual_seed(cin + k)
+    x = torch.rand((3, cin) + hw, generator=gen).to(gpu_device).to(torch.bfloat16).float()
+    layer = cnn.ConvLayer(seq[0], seq[1], torch.bfloat16)
+    layer.act_bf16 = True
+    xn = cnn.to_nhwc(x)
+    xa = cnn.Act(xn.t.to(torch.bfloat16), xn.C)
+    Ho, Wo = layer.out_hw(*hw)
+    r = None
+    if res:
+        rt = torch.zeros((3, Ho, Wo, layer.Cpo), dtype=torch.bfloat16, device=gpu_device)
+        rt[..., :cout] = torch.randn((3, Ho, Wo, cout), generator=gen).to(gpu_device).to(torch.bfloat16)
+        r = cnn.Act(rt, cout)
+    y_dma = layer(xa, relu=True, res_post=r)
+    with cnn.conv_algo(cnn.CONV_PER_TAP_NOSPLIT):
+        y_reg = layer(xa, relu=True, res_post=r)
+    assert torch.equal(y_dma.t, y_reg.t)
+    with torch.no_grad():
+        ref = torch.relu(seq(x))
+        if res:
+            ref = ref + r.t[..., :cout].float().permute(0, 3, 1, 2)
+    got = y_dma.t[..., :cout].float().permute(0, 3, 1, 2)
+    err = float((got - ref).abs().max()) / float(ref.abs().max())
+    assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
 def test_bf16_p2pnet_vs_reference(gpu_device):
     """Whole P2PNet with bf16 operands against the reference's fp32 golden:
     within 5e-2 of the output scale (errors compound over 20 convolutions)."""

@@ -204,34 +204,61 @@ __device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &ro
     const float4 s1 = *reinterpret_cast<const float4 *>(a.scale + co + 4);
     const float4 h0 = *reinterpret_cast<const float4 *>(a.shift + co);
     const float4 h1 = *reinterpret_cast<const float4 *>(a.shift + co + 4);
-    for (int row = threadIdx.x / G; row < BM; row += 256 / G) {
-        const int m = rowm(row);
-        if (m < 0) continue;
+    // all of this thread's units' output offsets and residual loads are issued
+    // before the first is used (a unit-by-unit loop exposed one global round
+    // trip per unit: the wide 1x1 "expand" layers are output / residual bound)
+    constexpr int U = (BM * G + 255) / 256;  // units per thread (the last may be past the tile: BM * G < 256)
+    size_t off[U];
+    bool ok[U];
+    uint4 rpre[U][2], rpost[U][2];  // 8 channels: bf16 in [0], fp32 in [0..1]
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = threadIdx.x / G + u * (256 / G);
+        const int m = row < BM ? rowm(row) : -1;
+        ok[u] = m >= 0;
         int co_;
-        const size_t off = conv_out_offset(a, m, n, g, co_);  // 8 consecutive output channels from off
+        off[u] = conv_out_offset(a, ok[u] ? m : rowm(0), n, g, co_);  // 8 consecutive output channels from off
+    }
+    auto load8 = [&](const float *base, size_t o, uint4 (&r)[2]) {
+        if (bfo) {
+            r[0] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const __bf16 *>(base) + o);
+        } else {
+            r[0] = *reinterpret_cast<const uint4 *>(base + o);
+            r[1] = *reinterpret_cast<const uint4 *>(base + o + 4);
+        }
+    };
+    auto unpack8 = [&](const uint4 (&r)[2], float (&o)[8]) {
+        if (bfo) {
+            const unsigned w4[4] = {r[0].x, r[0].y, r[0].z, r[0].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[2 * k] = __builtin_bit_cast(float, w4[k] << 16);
+                o[2 * k + 1] = __builtin_bit_cast(float, w4[k] & 0xffff0000u);
+            }
+        } else {
+            const unsigned w8[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] = __builtin_bit_cast(float, w8[k]);
+        }
+    };
+    if (a.res_pre) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load8(a.res_pre, off[u], rpre[u]);
+    }
+    if (a.res_post) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load8(a.res_post, off[u], rpost[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = min(threadIdx.x / G + u * (256 / G), BM - 1);
         const float4 c0 = *reinterpret_cast<const float4 *>(cs + row * CP + cg * 8);
         const float4 c1 = *reinterpret_cast<const float4 *>(cs + row * CP + cg * 8 + 4);
         float v[8] = {c0.x * s0.x + h0.x, c0.y * s0.y + h0.y, c0.z * s0.z + h0.z, c0.w * s0.w + h0.w,
                       c1.x * s1.x + h1.x, c1.y * s1.y + h1.y, c1.z * s1.z + h1.z, c1.w * s1.w + h1.w};
-        auto load8 = [&](const float *base, float (&o)[8]) {
-            if (bfo) {
-                const uint4 q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const __bf16 *>(base) + off);
-                const unsigned w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    o[2 * k] = (float)__builtin_bit_cast(__bf16, (unsigned short)(w4[k] & 0xffffu));
-                    o[2 * k + 1] = (float)__builtin_bit_cast(__bf16, (unsigned short)(w4[k] >> 16));
-                }
-            } else {
-                const float4 p0 = *reinterpret_cast<const float4 *>(base + off);
-                const float4 p1 = *reinterpret_cast<const float4 *>(base + off + 4);
-                o[0] = p0.x; o[1] = p0.y; o[2] = p0.z; o[3] = p0.w;
-                o[4] = p1.x; o[5] = p1.y; o[6] = p1.z; o[7] = p1.w;
-            }
-        };
         if (a.res_pre) {
             float r8[8];
-            load8(a.res_pre, r8);
+            unpack8(rpre[u], r8);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = v[k] + r8[k];
         }
@@ -241,20 +268,22 @@ __device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &ro
         }
         if (a.res_post) {
             float r8[8];
-            load8(a.res_post, r8);
+            unpack8(rpost[u], r8);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = v[k] + r8[k];
         }
+        if (!ok[u]) continue;
         if (bfo) {
             unsigned w4[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 w4[k] = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[2 * k]) |
                         ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[2 * k + 1]) << 16);
-            *reinterpret_cast<uint4 *>(reinterpret_cast<__bf16 *>(a.out) + off) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            *reinterpret_cast<uint4 *>(reinterpret_cast<__bf16 *>(a.out) + off[u]) =
+                make_uint4(w4[0], w4[1], w4[2], w4[3]);
         } else {
-            *reinterpret_cast<float4 *>(a.out + off) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4 *>(a.out + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            *reinterpret_cast<float4 *>(a.out + off[u]) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4 *>(a.out + off[u] + 4) = make_float4(v[4], v[5], v[6], v[7]);
         }
     }
 }
@@ -946,6 +975,47 @@ __global__ __launch_bounds__(256) void maxpool_pad_kernel(const float *__restric
     reinterpret_cast<float4 *>(out)[gid] = m;
 }
 
+// The same on bf16 activations (C % 8 == 0): 8 channels (16 B) per thread; the
+// maximum of bf16 values is one of them, so the result is exact.
+__global__ __launch_bounds__(256) void maxpool_pad_bf16_kernel(const uint4 *__restrict__ in, uint4 *__restrict__ out,
+                                                               int N, int H, int W, int C, int K, int S, int P, int Ho,
+                                                               int Wo) {
+    const int C8 = C / 8;
+    const long long total = (long long)N * Ho * Wo * C8;
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int c8 = (int)(gid % C8);
+    long long r = gid / C8;
+    const int x = (int)(r % Wo);
+    r /= Wo;
+    const int y = (int)(r % Ho);
+    const long long img = r / Ho;
+    const uint4 *base = in + (size_t)img * H * W * C8 + c8;
+    float m[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = -INFINITY;
+    for (int ky = 0; ky < K; ++ky) {
+        const int iy = y * S - P + ky;
+        if ((unsigned)iy >= (unsigned)H) continue;
+        for (int kx = 0; kx < K; ++kx) {
+            const int ix = x * S - P + kx;
+            if ((unsigned)ix >= (unsigned)W) continue;
+            const uint4 b = base[((size_t)iy * W + ix) * C8];
+            const unsigned w4[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                m[2 * k] = nanmax(m[2 * k], __builtin_bit_cast(float, w4[k] << 16));
+                m[2 * k + 1] = nanmax(m[2 * k + 1], __builtin_bit_cast(float, w4[k] & 0xffff0000u));
+            }
+        }
+    }
+    unsigned o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)  // exact: the low halves of bf16-valued floats are zero
+        o[k] = (__builtin_bit_cast(unsigned, m[2 * k]) >> 16) | (__builtin_bit_cast(unsigned, m[2 * k + 1]) & 0xffff0000u);
+    out[gid] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // NCHW (C channels) -> NHWC with Cp >= C channels (zero padded), and back.
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float *__restrict__ in, float *__restrict__ out,
                                                            int N, int C, int HW, int Cp) {
@@ -1097,15 +1167,14 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
     if (bf16) {  // chunks of one tap x 16 / 32 channels (or several taps of a 4/8/12-channel input), no split
         if (Cpi % 16 && (bf16 & FVP_CONV_BF16_IN)) return FVP_ERR_SHAPE;
         const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
-        // LDS-DMA kernel, except on the wide 1x1 "expand" layers over large maps
-        // (Ntot >= 4 K: 1-4 K steps, output-bound), which keep the register-staged
-        // kernel's 4 blocks per CU (measured: ResNet-50's 64->256 at 128x240 0.43 vs
-        // 0.58 ms, 3x3 64->64 0.21 -> 0.17 ms, deconv 256->256 at 64x120 1.21 -> 0.84 ms)
+        // LDS-DMA kernel (measured against the register-staged one on ResNet-50
+        // at 40 x 960 x 512: 3x3 64->64 0.21 -> 0.15 ms, deconv 256->256 at 64x120
+        // 1.21 -> 0.76 ms, 1x1 256->1024 at 32x60 0.15 -> 0.11 ms; the 64->256
+        // expand layers at 128x240 tie at 0.31 ms, output bound)
         const long long Kd = (long long)KH * KW * Cpi;
-        const bool expand = Ntot >= 4 * Kd && M >= 65536;
         const bool fits = (long long)N * H * W * Cpi * 2 < (1LL << 31) && (long long)Cpo_w * Kd * 2 < (1LL << 31) &&
                           KH * KW <= 32 && M < (1 << 24);  // 32-bit buffer offsets, tap masks, row decode
-        if (a.in_bf16 && Cpi % 64 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && !expand && fits) {
+        if (a.in_bf16 && Cpi % 64 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && fits) {
             const int BN = Ntot > 64 ? 128 : 64;
             const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
             if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128>), gr, dim3(256), 0, st, a, wb);
@@ -1274,6 +1343,19 @@ extern "C" int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C,
     const long long total = (long long)N * Ho * Wo * (C / 4);
     hipLaunchKernelGGL(fvp::maxpool_pad_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, in, out, N, H, W, C, K, S, P, Ho, Wo);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_maxpool_pad_nhwc_bf16(const void *in, int N, int H, int W, int C, int K, int S, int P, void *out,
+                                         void *stream) {
+    if (!in || !out) return FVP_ERR_NULL;
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || K < 1 || S < 1 || P < 0 || 2 * P > K) return FVP_ERR_SHAPE;
+    if (H + 2 * P < K || W + 2 * P < K) return FVP_ERR_SHAPE;
+    const int Ho = (H + 2 * P - K) / S + 1, Wo = (W + 2 * P - K) / S + 1;
+    const long long total = (long long)N * Ho * Wo * (C / 8);
+    hipLaunchKernelGGL(fvp::maxpool_pad_bf16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, reinterpret_cast<const uint4 *>(in), reinterpret_cast<uint4 *>(out), N, H,
+                       W, C, K, S, P, Ho, Wo);
     return (int)hipGetLastError();
 }
 

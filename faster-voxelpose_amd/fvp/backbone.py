@@ -56,7 +56,7 @@ class _Block:
         residual = x if self.down is None else self.down(x, relu=False)
         last = self.convs[-1]
         want = torch.bfloat16 if (last.bf16 and last.act_bf16) else torch.float32
-        if residual.t.dtype != want:  # the identity residual of the first bf16 block reads the fp32 max pool
+        if residual.t.dtype != want:  # an identity residual whose dtype differs from the block's output
             residual = Act(residual.t.to(want), residual.C)
         y = x
         for c in self.convs[:-1]:
@@ -104,9 +104,9 @@ class FvpPoseResNet:
         self.final = ConvLayer(module.final_layer, None, dtype)
         self.num_joints = module.final_layer.out_channels
         # bf16: activations between the layers stay bf16 in HBM (half the bytes,
-        # no per-chunk conversion); the RGB input, the stem's output (max pool)
-        # and the heatmaps are fp32
-        for c in self.layers()[1:-1]:
+        # no per-chunk conversion), the stem's output and its max pool included;
+        # the RGB input and the heatmaps are fp32
+        for c in self.layers()[:-1]:
             c.act_bf16 = c.bf16
 
     def layers(self):

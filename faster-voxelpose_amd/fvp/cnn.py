@@ -209,10 +209,11 @@ def maxpool2(x: Act, dim: int = 2) -> Act:
 
 
 def maxpool_pad(x: Act, k: int, s: int, p: int) -> Act:
-    """MaxPool2d(k, s, p) with -inf padding (resnet.py:109)."""
+    """MaxPool2d(k, s, p) with -inf padding (resnet.py:109); fp32 or bf16 activations (same dtype out)."""
     Ho, Wo = (x.H + 2 * p - k) // s + 1, (x.W + 2 * p - k) // s + 1
-    out = torch.empty((x.N, Ho, Wo, x.Cp), dtype=torch.float32, device=x.t.device)
-    _lib.call("fvp_maxpool_pad_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, k, s, p, _ptr(out), _stream(out))
+    out = torch.empty((x.N, Ho, Wo, x.Cp), dtype=x.t.dtype, device=x.t.device)
+    fn = "fvp_maxpool_pad_nhwc_bf16" if x.t.dtype == torch.bfloat16 else "fvp_maxpool_pad_nhwc"
+    _lib.call(fn, _ptr(x.t), x.N, x.H, x.W, x.Cp, k, s, p, _ptr(out), _stream(out))
     return Act(out, x.C)
 
 

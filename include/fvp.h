@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 8
+#define FVP_ABI_VERSION 9
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -348,6 +348,10 @@ int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf
  * padding, NaN-propagating (resnet.py:109: 3, 2, 1).  Ho = (H + 2P - K)/S + 1. */
 int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int S, int P, float *out, void *stream);
+/* The same on bf16 NHWC activations (C % 8 == 0; exact: the maximum is one
+ * of the inputs) -- the bf16 backbone's max pool after its bf16 stem. */
+int fvp_maxpool_pad_nhwc_bf16(const void *in, int N, int H, int W, int C, int K, int S, int P, void *out,
+                              void *stream);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */
 int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, void *stream);
 /* KH x KW / stride-(KH, KW) max pool, KH, KW in {1, 2} (floor); KH = 1, KW = 2

@@ -147,6 +147,23 @@ def test_maxpool_pad_matches_torch(gpu_device):
 
 
 @pytest.mark.gpu
+def test_maxpool_pad_bf16_matches_torch(gpu_device):
+    """bf16 NHWC max pool (the bf16 backbone's, after its bf16 stem): exact."""
+    from fvp.cnn import Act, maxpool_pad
+
+    x = torch.randn((2, 37, 43, 64), device=gpu_device).to(torch.bfloat16)
+    x[0, 0, 0, 3] = float("nan")
+    x[1, :, :, 5] = -float("inf")
+    got = maxpool_pad(Act(x, 64), 3, 2, 1).t
+    assert got.dtype == torch.bfloat16
+    ref = F.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).to(torch.bfloat16)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    assert torch.equal(torch.nan_to_num(got.float(), 7.0), torch.nan_to_num(ref.float(), 7.0))
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tag", ["r50", "r18"])
 def test_fvp_pose_resnet_matches_reference(gpu_device, tag):
     from fvp.backbone import FvpPoseResNet
@@ -170,14 +187,18 @@ def test_fvp_pose_resnet_matches_reference(gpu_device, tag):
 
 
 @pytest.mark.gpu
-def test_fvp_pose_resnet_bf16(gpu_device):
+@pytest.mark.parametrize("tag", ["r50", "r18"])
+def test_fvp_pose_resnet_bf16(gpu_device, tag):
+    """bf16 operands and activations (opt-in): within 5e-2 of the heatmap scale
+    of the reference's fp32 output (ResNet-50's Bottleneck layers run the
+    LDS-DMA kernel, the stem the small-channel bf16 path)."""
     from fvp.backbone import FvpPoseResNet
 
-    m, x, y = _net("r18")
+    m, x, y = _net(tag)
     got = FvpPoseResNet(m.to(gpu_device), torch.bfloat16)(torch.from_numpy(x).to(gpu_device))
     torch.cuda.synchronize()
     err = _rel_err(got.cpu().numpy(), y)
-    print(f"bf16 ResNet-18: {err:.3g} of the heatmap scale")
+    print(f"bf16 {tag}: {err:.3g} of the heatmap scale")
     assert err <= 5e-2
 
 

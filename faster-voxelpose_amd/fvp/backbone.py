@@ -8,6 +8,8 @@ BasicBlock stages, the deconvolution head, the final conv) into
 
 * conv1 7x7/s2/p3 + BN + ReLU on the RGB input padded to 4 channels (a K chunk
   of the implicit GEMM spans 4 taps, so no MFMA work goes to padding channels);
+  with bf16 operands a dedicated kernel reads the NCHW images directly
+  (``fvp_conv_stem7_bf16``: halo tile in LDS, no NHWC conversion pass);
 * MaxPool2d(3, 2, 1) (``fvp_maxpool_pad_nhwc``);
 * each Bottleneck (resnet.py:57-95) as three launches -- 1x1 + BN + ReLU, 3x3
   (stride) + BN + ReLU, 1x1 + BN with the residual add and the ReLU fused into
@@ -29,6 +31,7 @@ import torch.nn as nn
 
 from . import _lib
 from .cnn import Act, ConvLayer, maxpool_pad, to_nchw, to_nhwc
+from .ops import _ptr, _stream
 from .heatmaps import ChannelsLastHeatmaps
 
 RGB_PITCH = 4  # input channel pitch of conv1 (3 colour channels + one zero)
@@ -83,6 +86,16 @@ class FvpPoseResNet:
         if module.conv1.in_channels > RGB_PITCH:
             raise _lib.FvpError(f"FvpPoseResNet: {module.conv1.in_channels} input channels (RGB expected)")
         self.stem = ConvLayer(module.conv1, module.bn1, dtype, cpi=RGB_PITCH)
+        # bf16: the 7x7/s2/p3 -> 64 stem runs its own kernel straight from the
+        # NCHW images (fvp_conv_stem7_bf16), weights packed [64][7][8][4]
+        c1 = module.conv1
+        self.stem7 = None
+        if (dtype == torch.bfloat16 and tuple(c1.kernel_size) == (7, 7) and tuple(c1.stride) == (2, 2)
+                and tuple(c1.padding) == (3, 3) and c1.out_channels == 64 and c1.groups == 1
+                and tuple(c1.dilation) == (1, 1)):
+            w = torch.zeros((64, 7, 8, 4), dtype=torch.float32, device=c1.weight.device)
+            w[:, :, :7, :c1.in_channels] = c1.weight.detach().float().permute(0, 2, 3, 1)
+            self.stem7 = w.reshape(64, 224).to(torch.bfloat16).contiguous()
         mp = module.maxpool
         k, s, p = (mp.kernel_size, mp.stride, mp.padding)
         k, s, p = (v if isinstance(v, int) else v[0] for v in (k, s, p))
@@ -121,13 +134,24 @@ class FvpPoseResNet:
         out: optional [N,h,w,Cp] destination of the final layer."""
         if images.device.type != "cuda":
             raise _lib.FvpError(f"fvp: images must be on a HIP device, got {images.device}")
-        x = self.stem(to_nhwc(images, RGB_PITCH), relu=True)
+        if self.stem7 is not None:
+            x = self._stem7(images)
+        else:
+            x = self.stem(to_nhwc(images, RGB_PITCH), relu=True)
         x = maxpool_pad(x, *self.pool)
         for b in self.blocks:
             x = b(x)
         for d in self.deconvs:
             x = d(x, relu=True)
         return self.final(x, relu=False, out=out)
+
+    def _stem7(self, images: torch.Tensor) -> Act:
+        x = images.float().contiguous()
+        N, C, H, W = x.shape
+        out = torch.empty((N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64), dtype=torch.bfloat16, device=x.device)
+        _lib.call("fvp_conv_stem7_bf16", _ptr(x), N, C, H, W, _ptr(self.stem7), _ptr(self.stem.scale),
+                  _ptr(self.stem.shift), _ptr(out), _stream(out))
+        return Act(out, 64)
 
     def __call__(self, images: torch.Tensor) -> torch.Tensor:
         """ResNet.forward (resnet.py:187-201): [N,3,H,W] -> [N,J,h,w] fp32."""

@@ -350,6 +350,14 @@ int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int
 int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int S, int P, float *out, void *stream);
 /* The same on bf16 NHWC activations (C % 8 == 0; exact: the maximum is one
  * of the inputs) -- the bf16 backbone's max pool after its bf16 stem. */
+/* PoseResNet's conv1 + BN + ReLU (resnet.py:105-107, 109: 7x7, stride 2,
+ * pad 3, C <= 4 input channels -> 64) on bf16 MFMA straight from the NCHW
+ * fp32 images [N][C][H][W] to bf16 NHWC [N][Ho][Wo][64], Ho = (H - 1)/2 + 1.
+ * wpack: bf16 [64][7][8][4] = W[co][c][ky][kx] at (co, ky, kx, c), zero for
+ * kx = 7 and c >= C; scale / shift: fp32 [64] (BN folded).  Opt-in precision
+ * (bf16 operands, fp32 accumulation). */
+int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W, const void *wpack, const float *scale,
+                        const float *shift, void *out, void *stream);
 int fvp_maxpool_pad_nhwc_bf16(const void *in, int N, int H, int W, int C, int K, int S, int P, void *out,
                               void *stream);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */

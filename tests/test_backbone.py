@@ -187,6 +187,32 @@ def test_fvp_pose_resnet_matches_reference(gpu_device, tag):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,hw", [(3, (512, 960)), (3, (37, 70)), (4, (21, 33)), (1, (64, 100))])
+def test_stem7_bf16_vs_torch(gpu_device, cin, hw):
+    """fvp_conv_stem7_bf16 (7x7/s2/p3 -> 64 + BN + ReLU from NCHW images, bf16
+    operands): within 2e-2 of the output scale of torch's fp32 conv of the
+    bf16-rounded input, ragged tiles included."""
+    import cnn_arch
+    from fvp import synthetic
+    from fvp.backbone import FvpPoseResNet
+
+    m = cnn_arch.PoseResNet(18, 15).eval()
+    m.conv1 = nn.Conv2d(cin, 64, 7, 2, 3, bias=False)
+    m.load_state_dict(synthetic.seeded_state_dict(m, 3 + cin))
+    m = m.to(gpu_device)
+    bb = FvpPoseResNet(m, torch.bfloat16)
+    assert bb.stem7 is not None
+    x = torch.rand((2, cin) + hw, generator=torch.Generator().manual_seed(cin)).to(gpu_device)
+    x = x.to(torch.bfloat16).float()
+    got = bb._stem7(x).t.float().permute(0, 3, 1, 2)
+    with torch.no_grad():
+        ref = torch.relu(m.bn1(m.conv1(x)))
+    assert got.shape == ref.shape
+    err = float((got - ref).abs().max()) / float(ref.abs().max())
+    assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tag", ["r50", "r18"])
 def test_fvp_pose_resnet_bf16(gpu_device, tag):
     """bf16 operands and activations (opt-in): within 5e-2 of the heatmap scale

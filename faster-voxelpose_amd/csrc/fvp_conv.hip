@@ -1058,6 +1058,52 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const float *__restrict__ 
     reinterpret_cast<float4 *>(out)[gid] = m;
 }
 
+// The same on bf16 activations (C % 8 == 0): 8 channels (16 B) per thread,
+// exact (the maximum is one of the inputs).
+__device__ __forceinline__ void bf16x8_max(float (&m)[8], const uint4 b) {
+    const unsigned w4[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[2 * k] = nanmax(m[2 * k], __builtin_bit_cast(float, w4[k] << 16));
+        m[2 * k + 1] = nanmax(m[2 * k + 1], __builtin_bit_cast(float, w4[k] & 0xffff0000u));
+    }
+}
+
+__device__ __forceinline__ uint4 bf16x8_pack(const float (&m)[8]) {  // exact: low halves are zero
+    unsigned o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        o[k] = (__builtin_bit_cast(unsigned, m[2 * k]) >> 16) | (__builtin_bit_cast(unsigned, m[2 * k + 1]) & 0xffff0000u);
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int KH, int KW>
+__global__ __launch_bounds__(256) void maxpool_bf16_kernel(const uint4 *__restrict__ in, uint4 *__restrict__ out, int N,
+                                                           int H, int W, int C) {
+    const int Ho = H / KH, Wo = W / KW, C8 = C / 8;
+    const long long total = (long long)N * Ho * Wo * C8;
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int c8 = (int)(gid % C8);
+    long long r = gid / C8;
+    const int x = (int)(r % Wo);
+    r /= Wo;
+    const int y = (int)(r % Ho);
+    const long long img = r / Ho;
+    const uint4 *p = in + (((size_t)img * H + KH * y) * W + KW * x) * C8 + c8;
+    const size_t rs = (size_t)W * C8;
+    float m[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = -INFINITY;
+    bf16x8_max(m, p[0]);
+    if (KW == 2) bf16x8_max(m, p[C8]);
+    if (KH == 2) {
+        bf16x8_max(m, p[rs]);
+        if (KW == 2) bf16x8_max(m, p[rs + C8]);
+    }
+    out[gid] = bf16x8_pack(m);
+}
+
 // MaxPool2d(K, S, P) of NHWC activations with implicit -inf padding
 // (resnet.py:109: kernel 3, stride 2, padding 1), NaN-propagating like torch.
 __global__ __launch_bounds__(256) void maxpool_pad_kernel(const float *__restrict__ in, float *__restrict__ out,
@@ -1115,20 +1161,10 @@ __global__ __launch_bounds__(256) void maxpool_pad_bf16_kernel(const uint4 *__re
         for (int kx = 0; kx < K; ++kx) {
             const int ix = x * S - P + kx;
             if ((unsigned)ix >= (unsigned)W) continue;
-            const uint4 b = base[((size_t)iy * W + ix) * C8];
-            const unsigned w4[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                m[2 * k] = nanmax(m[2 * k], __builtin_bit_cast(float, w4[k] << 16));
-                m[2 * k + 1] = nanmax(m[2 * k + 1], __builtin_bit_cast(float, w4[k] & 0xffff0000u));
-            }
+            bf16x8_max(m, base[((size_t)iy * W + ix) * C8]);
         }
     }
-    unsigned o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)  // exact: the low halves of bf16-valued floats are zero
-        o[k] = (__builtin_bit_cast(unsigned, m[2 * k]) >> 16) | (__builtin_bit_cast(unsigned, m[2 * k + 1]) & 0xffff0000u);
-    out[gid] = make_uint4(o[0], o[1], o[2], o[3]);
+    out[gid] = bf16x8_pack(m);
 }
 
 // NCHW (C channels) -> NHWC with Cp >= C channels (zero padded), and back.
@@ -1471,6 +1507,23 @@ extern "C" int fvp_maxpool_pad_nhwc_bf16(const void *in, int N, int H, int W, in
     hipLaunchKernelGGL(fvp::maxpool_pad_bf16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, reinterpret_cast<const uint4 *>(in), reinterpret_cast<uint4 *>(out), N, H,
                        W, C, K, S, P, Ho, Wo);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_maxpool_nhwc_bf16(const void *in, int N, int H, int W, int C, int KH, int KW, void *out,
+                                     void *stream) {
+    if (!in || !out) return FVP_ERR_NULL;
+    if (KH < 1 || KH > 2 || KW < 1 || KW > 2) return FVP_ERR_SHAPE;
+    if (N <= 0 || H < KH || W < KW || C <= 0 || C % 8) return FVP_ERR_SHAPE;
+    const long long total = (long long)N * (H / KH) * (W / KW) * (C / 8);
+    const dim3 g((unsigned)((total + 255) / 256)), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    const uint4 *i4 = reinterpret_cast<const uint4 *>(in);
+    uint4 *o4 = reinterpret_cast<uint4 *>(out);
+    if (KH == 2 && KW == 2) hipLaunchKernelGGL((fvp::maxpool_bf16_kernel<2, 2>), g, b, 0, st, i4, o4, N, H, W, C);
+    else if (KH == 1 && KW == 2) hipLaunchKernelGGL((fvp::maxpool_bf16_kernel<1, 2>), g, b, 0, st, i4, o4, N, H, W, C);
+    else if (KH == 2) hipLaunchKernelGGL((fvp::maxpool_bf16_kernel<2, 1>), g, b, 0, st, i4, o4, N, H, W, C);
+    else hipLaunchKernelGGL((fvp::maxpool_bf16_kernel<1, 1>), g, b, 0, st, i4, o4, N, H, W, C);
     return (int)hipGetLastError();
 }
 

@@ -89,6 +89,7 @@ SIGNATURES = {
     "fvp_maxpool_pad_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_maxpool_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_weight_net": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_copy_f4": [c_void_p, c_void_p, ctypes.c_size_t, c_void_p],

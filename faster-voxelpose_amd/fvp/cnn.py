@@ -201,10 +201,11 @@ class ConvLayer:
 
 
 def maxpool2(x: Act, dim: int = 2) -> Act:
-    """max_pool2d(x, 2, 2) (dim 2) or max_pool1d(x, 2, 2) along W (dim 1)."""
+    """max_pool2d(x, 2, 2) (dim 2) or max_pool1d(x, 2, 2) along W (dim 1); fp32 or bf16 (same dtype out)."""
     kh = 2 if dim == 2 else 1
-    out = torch.empty((x.N, x.H // kh, x.W // 2, x.Cp), dtype=torch.float32, device=x.t.device)
-    _lib.call("fvp_maxpool_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, kh, 2, _ptr(out), _stream(out))
+    out = torch.empty((x.N, x.H // kh, x.W // 2, x.Cp), dtype=x.t.dtype, device=x.t.device)
+    fn = "fvp_maxpool_nhwc_bf16" if x.t.dtype == torch.bfloat16 else "fvp_maxpool_nhwc"
+    _lib.call(fn, _ptr(x.t), x.N, x.H, x.W, x.Cp, kh, 2, _ptr(out), _stream(out))
     return Act(out, x.C)
 
 
@@ -259,6 +260,19 @@ class _Plan:
     def __init__(self, m: nn.Module, dtype=torch.float32, dim: int = 2):
         self.dtype, self.dim = dtype, dim
         self.kind, self.parts = self._compile(m)
+
+    def layers(self):
+        """Every ConvLayer of the plan."""
+        k, p = self.kind, self.parts
+        if k == "res":
+            return [c for c in p if c is not None]
+        if k == "seq":
+            return [c for c, _ in p]
+        if k == "chain":
+            return [c for sub in p for c in sub.layers()]
+        if k == "encdec":
+            return [c for sub in p.values() for c in sub.layers()]
+        return []
 
     def _compile(self, m):
         if hasattr(m, "res_branch"):  # Res2DBlock (cnns_2d.py:32-64) / Res1DBlock (cnns_1d.py:37-74)
@@ -349,6 +363,14 @@ class FvpCNN:
         else:
             self.kind = "plain"
             self.plan = _Plan(module, dtype)
+        if dtype == torch.bfloat16 and self.kind != "plain":
+            # bf16 activations between the layers (half the bytes, no per-chunk
+            # conversion); the heads' last convs write the fp32 outputs
+            inner = self.front.layers() + self.encdec.layers()
+            if self.kind == "centernet":
+                inner += [c for c, _ in self.hm[:-1]] + [c for c, _ in self.size[:-1]]
+            for c in inner:
+                c.act_bf16 = c.bf16
 
     @staticmethod
     def _run_seq(seq, x):

@@ -365,6 +365,8 @@ int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, float *out, v
 /* KH x KW / stride-(KH, KW) max pool, KH, KW in {1, 2} (floor); KH = 1, KW = 2
  * is F.max_pool1d(x, 2, 2) of Pool1DBlock (cnns_1d.py:77-93) on H == 1 rows. */
 int fvp_maxpool_nhwc(const float *in, int N, int H, int W, int C, int KH, int KW, float *out, void *stream);
+/* The same on bf16 NHWC activations (C % 8 == 0; exact) -- the bf16 CNNs' pools. */
+int fvp_maxpool_nhwc_bf16(const void *in, int N, int H, int W, int C, int KH, int KW, void *out, void *stream);
 
 /* WeightNet.forward (lib/models/weight_net.py:48-80) fused into one launch,
  * one block per joint map:

@@ -744,9 +744,11 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
                                                          smem);
 }
 
-// ---- bf16 activations, Cpi % 64 == 0: LDS-DMA staged implicit GEMM -------------
-// The backbone's bf16 layers (bf16 NHWC in, weights bf16 [G][Cpo_w][K]).  A
-// K step is one tap x 64 channels = one 128-B row per pixel / output column.
+// ---- bf16 activations, Cpi % 32 == 0: LDS-DMA staged implicit GEMM -------------
+// The bf16 layers (bf16 NHWC in, weights bf16 [G][Cpo_w][K]).  A K step is
+// one tap x BK channels = one 128-B (BK 64) or 64-B (BK 32) row per pixel /
+// output column (below for BK 64; BK 32: 16 rows per wave load, swizzle
+// s ^ ((r >> 2) & 3)).
 // Both operands go global -> LDS by buffer_load_dwordx4 ... lds (no VGPR
 // staging, no LDS write pass): one wave instruction moves 8 whole rows (1 KiB, lane l
 // -> row l/8, 16-B slot l%8).  The LDS image is lane-linear, so the bank
@@ -762,14 +764,18 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
 
 #define FVP_WAIT_BARRIER(vm) asm volatile("s_waitcnt vmcnt(" #vm ")\n\ts_barrier" ::: "memory")
 
-template <int BN>
+template <int BN, int BK>
 __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
-    constexpr int BM = 128, WTN = BN / 2, TN = WTN / 32, NBI = BN / 32;  // NBI: B row groups of 8 per wave
-    constexpr int ABYTES = BM * 128, STAGE = ABYTES + BN * 128;
+    constexpr int BM = 128, WTN = BN / 2, TN = WTN / 32;
+    constexpr int RB = BK * 2, SPR = RB / 16, RPI = 1024 / RB;  // row bytes, 16-B slots per row, rows per wave load
+    constexpr int NAI = BM / (4 * RPI), NBI = BN / (4 * RPI), NPS = NAI + NBI;  // wave loads per K step
+    constexpr int ABYTES = BM * RB, STAGE = ABYTES + BN * RB;
     constexpr int KLDS = 2 * STAGE, CLDS = BM * (BN + 4) * 4;
-    static_assert(NBI == 2 || NBI == 4, "BN 64 or 128");
+    static_assert((BK == 32 || BK == 64) && (BN == 64 || BN == 128), "tile");
     __shared__ __attribute__((aligned(16))) float smem[(KLDS > CLDS ? KLDS : CLDS) / 4];
     char *lds = reinterpret_cast<char *>(smem);
+    // conflict-free ds_read_b128 fragment reads: 16-B slot s of row r holds chunk s ^ swz(r)
+    auto swz = [](int r) { return RB == 128 ? (r >> 1) & 7 : (r >> 2) & 3; };
     const int M = a.N * a.Hm * a.Wm;
     int mt, nt;
     conv_tile(mt, nt);
@@ -779,9 +785,9 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
     const int wr = wave & 1, wc = wave >> 1;
     const int g = blockIdx.z;  // parity group (mode 3), else 0
     const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
-    const int cpc = a.Cpi >> 6, nks = a.KH * a.KW * cpc;
+    const int cpc = a.Cpi / BK, nks = a.KH * a.KW * cpc;
     const size_t Ktot = (size_t)a.KH * a.KW * a.Cpi;
-    const int slot = lane & 7;
+    const int slot = lane % SPR;
     // Both operands through buffer descriptors (32-bit offsets; the host keeps
     // the activations under 2 GiB): a padding tap or a row past M reads at
     // kOOB, which the range check turns into zeros.  Per row, the input offset
@@ -799,11 +805,11 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
     };
     unsigned rep = 0;  // bit ky*KW set for every tap row (uniform)
     for (int ky = 0; ky < a.KH; ++ky) rep |= 1u << (ky * a.KW);
-    int voa[4];
-    unsigned tmask[4];
+    int voa[NAI];
+    unsigned tmask[NAI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = (wave * 4 + i) * 8 + (lane >> 3);
+    for (int i = 0; i < NAI; ++i) {
+        const int r = (wave * NAI + i) * RPI + lane / SPR;
         const int m = m0 + r, mm = m < M ? m : 0;
         const int img = qdiv(mm, HWm, inv_hw), rr = mm - img * HWm;
         const int oy = qdiv(rr, a.Wm, inv_w), ox = rr - oy * a.Wm;
@@ -815,27 +821,26 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
         // tap rows ylo..yhi-1 of the all-rows pattern rep = sum 2^(ky*KW): mask = xm * rep(rows)
         const unsigned rows = (unsigned)(((1ull << (yhi * a.KW)) - 1ull) & ~((1ull << (ylo * a.KW)) - 1ull));
         tmask[i] = m < M ? xm * (rep & rows) : 0u;
-        const int c = slot ^ ((r >> 1) & 7);
-        voa[i] = (((img * a.H + y0) * a.W + x0) * a.Cpi + c * 8) * 2;  // may be negative: only valid taps use it
+        voa[i] = (((img * a.H + y0) * a.W + x0) * a.Cpi + (slot ^ swz(r)) * 8) * 2;  // < 0 only for unused taps
     }
     int vob[NBI];
 #pragma unroll
     for (int i = 0; i < NBI; ++i) {
-        const int r = (wave * NBI + i) * 8 + (lane >> 3);
-        vob[i] = ((n0 + r) * (int)Ktot + (slot ^ ((r >> 1) & 7)) * 8) * 2;
+        const int r = (wave * NBI + i) * RPI + lane / SPR;
+        vob[i] = ((n0 + r) * (int)Ktot + (slot ^ swz(r)) * 8) * 2;
     }
     typedef __attribute__((address_space(3))) void *lds_ptr;
     auto issue = [&](int ks, int tap, int d, int buf) {
         char *sa = lds + buf * STAGE;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NAI; ++i) {
             const unsigned vo = (tmask[i] >> tap) & 1u ? (unsigned)(voa[i] + d) : kOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(sa + (wave * 4 + i) * 1024), 16, vo, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(sa + (wave * NAI + i) * 1024), 16, vo, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < NBI; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(sa + ABYTES + (wave * NBI + i) * 1024), 16,
-                                                     (unsigned)(vob[i] + ks * 128), 0, 0, 0);
+                                                     (unsigned)(vob[i] + ks * RB), 0, 0, 0);
     };
     f32x16 acc[2][TN];
 #pragma unroll
@@ -846,7 +851,7 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     int tap = 0, kx = 0, cc = 0, d = 0;  // tap, its column and channel chunk, byte delta of the next step
     auto advance = [&]() {
-        d += 128;
+        d += RB;
         if (++cc == cpc) {
             cc = 0;
             ++tap;
@@ -863,25 +868,27 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
         if (ks + 1 < nks) {  // buf ^ 1 was last read in step ks - 1, before its closing barrier
             issue(ks + 1, tap, d, buf ^ 1);
             advance();
-            if constexpr (NBI == 4) FVP_WAIT_BARRIER(8);  // step ks landed (this wave's), then everyone's
-            else FVP_WAIT_BARRIER(6);
+            if constexpr (NPS == 8) FVP_WAIT_BARRIER(8);  // step ks landed (this wave's), then everyone's
+            else if constexpr (NPS == 6) FVP_WAIT_BARRIER(6);
+            else if constexpr (NPS == 4) FVP_WAIT_BARRIER(4);
+            else FVP_WAIT_BARRIER(3);
         } else {
             FVP_WAIT_BARRIER(0);
         }
         const char *sa = lds + buf * STAGE, *sb = sa + ABYTES;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
+        for (int kk = 0; kk < BK / 16; ++kk) {
             const int c = kk * 2 + (lane >> 5);
             bf16x8 fa[2], fb[TN];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int row = wr * 64 + i * 32 + (lane & 31);
-                fa[i] = *reinterpret_cast<const bf16x8 *>(sa + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+                fa[i] = *reinterpret_cast<const bf16x8 *>(sa + row * RB + ((c ^ swz(row)) << 4));
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int col = wc * WTN + j * 32 + (lane & 31);
-                fb[j] = *reinterpret_cast<const bf16x8 *>(sb + col * 128 + ((c ^ ((col >> 1) & 7)) << 4));
+                fb[j] = *reinterpret_cast<const bf16x8 *>(sb + col * RB + ((c ^ swz(col)) << 4));
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -1325,11 +1332,16 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
         const long long Kd = (long long)KH * KW * Cpi;
         const bool fits = (long long)N * H * W * Cpi * 2 < (1LL << 31) && (long long)Cpo_w * Kd * 2 < (1LL << 31) &&
                           KH * KW <= 32 && M < (1 << 24);  // 32-bit buffer offsets, tap masks, row decode
-        if (a.in_bf16 && Cpi % 64 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && fits) {
+        if (a.in_bf16 && Cpi % 32 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && fits) {
             const int BN = Ntot > 64 ? 128 : 64;
             const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
-            if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128>), gr, dim3(256), 0, st, a, wb);
-            else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64>), gr, dim3(256), 0, st, a, wb);
+            if (Cpi % 64 == 0) {  // K steps of one tap x 64 channels (128-B rows)
+                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 64>), gr, dim3(256), 0, st, a, wb);
+                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 64>), gr, dim3(256), 0, st, a, wb);
+            } else {  // the HDN / JLN CNNs' 32-channel layers: 64-B rows
+                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 32>), gr, dim3(256), 0, st, a, wb);
+                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 32>), gr, dim3(256), 0, st, a, wb);
+            }
             return (int)hipGetLastError();
         }
 #define FVP_CONVB(BM, BN, WR, KC)                                                                               \

@@ -160,7 +160,7 @@ def test_bf16_conv_layer_vs_torch(gpu_device, cin, cout, k, hw, up):
                                                  (10, 12, 5, 2, (31, 30)), (4, 4, 1, 1, (9, 9))])
 def test_bf16_small_channel_conv_vs_torch(gpu_device, cin, cpi, k, stride, hw):
     """bf16 operands on a 4 / 8 / 12-channel fp32 input (the RGB stem,
-    resnet.py:222-224): one K chunk spans several taps; within 2e-2 of the
+    resnet.py:105-107): one K chunk spans several taps; within 2e-2 of the
     output scale of torch's fp32 convolution."""
     import torch.nn as nn
 
@@ -185,10 +185,13 @@ def test_bf16_small_channel_conv_vs_torch(gpu_device, cin, cpi, k, stride, hw):
                                                              (256, 64, 1, 1, (20, 21), False, True),
                                                              (64, 512, 1, 2, (19, 23), False, False),
                                                              (256, 128, 4, 2, (9, 11), True, False),
-                                                             (192, 96, 3, 1, (7, 130), False, False)])
+                                                             (192, 96, 3, 1, (7, 130), False, False),
+                                                             (32, 64, 3, 1, (64, 64), False, True),
+                                                             (96, 32, 3, 2, (21, 19), False, False),
+                                                             (32, 32, 1, 1, (17, 40), False, True)])
 def test_bf16_dma_conv_matches_register_staged(gpu_device, cin, cout, k, stride, hw, deconv, res):
-    """bf16 activations with Cpi % 64 == 0 run the LDS-DMA kernel
-    (conv_bf16_dma_kernel); CONV_PER_TAP_NOSPLIT keeps such layers on the
+    """bf16 activations with Cpi % 32 == 0 run the LDS-DMA kernel
+    (conv_bf16_dma_kernel, 64- or 32-deep K steps); CONV_PER_TAP_NOSPLIT keeps such layers on the
     register-staged conv_bf16_kernel.  Both walk k in the same order with the
     same MFMA instruction, so the outputs are bit-identical; and within 2e-2 of
     the output scale of torch's fp32 convolution of the bf16-rounded input."""

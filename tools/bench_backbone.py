@@ -82,6 +82,17 @@ def main():
             t_t = timeit(lambda: m(imgs))
             out.update(torch_f32_ms=round(t_t, 3), torch_f32_tflops=round(gflop / t_t, 1),
                        speedup_f32_vs_torch=round(t_t / t_f, 3))
+            # torch's bf16 forward of the same module (MIOpen bf16 convolutions), NCHW and channels_last
+            import copy
+            mb = copy.deepcopy(m).to(torch.bfloat16)
+            ib = imgs.to(torch.bfloat16)
+            t_tb = timeit(lambda: mb(ib))
+            mbc = copy.deepcopy(mb).to(memory_format=torch.channels_last)
+            ibc = ib.contiguous(memory_format=torch.channels_last)
+            t_tbc = timeit(lambda: mbc(ibc))
+            out.update(torch_bf16_ms=round(t_tb, 3), torch_bf16_channels_last_ms=round(t_tbc, 3),
+                       speedup_bf16_vs_torch_bf16=round(min(t_tb, t_tbc) / t_b, 3))
+            del mb, mbc
 
         # views -> cube at C2's voxel geometry
         layer = ProjectLayer(w.cfg(str(dev)))

@@ -930,106 +930,129 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
 // an even x, so ds_read_b128 stays aligned).  Wave w owns output rows 2w, 2w+1
 // (32 pixels each) x 64 channels; the accumulators come out Wᵀ-major (lane ->
 // pixel, 4 consecutive registers -> 4 channels), get BN + ReLU in registers
-// and go through LDS to 16-B row stores.  Replaces the NCHW -> NHWC pass and
-// the register-staged small-channel path (0.23 + 0.68 ms per 40 images).
+// and go through LDS to 16-B row stores.  Persistent blocks (2 per CU) walk
+// the tiles: the weights are staged once per block, and the next tile's halo
+// is loaded into registers while the current one runs its MFMAs, epilogue and
+// stores.  Replaces the NCHW -> NHWC pass and the register-staged
+// small-channel path (0.23 + 0.68 ms per 40 images).
 constexpr int kStemTH = 8, kStemTW = 32, kStemHR = 2 * kStemTH + 5, kStemHX = 2 * kStemTW + 6;
 constexpr int kStemWP = 232;  // weight row pitch (bf16): 224 + 8, conflict-free ds_read_b128
 constexpr int kStemOP = 72;   // output staging pitch (bf16)
+constexpr int kStemHE = (kStemHR * kStemHX + 255) / 256;  // halo pixels per thread
 
 __global__ __launch_bounds__(256, 2) void conv_stem7_bf16_kernel(const float *__restrict__ img, int C, int H, int W,
                                                                   int Ho, int Wo, int tiles_x, int tiles_y,
-                                                                  const __bf16 *__restrict__ wpk,
+                                                                  int ntiles, const __bf16 *__restrict__ wpk,
                                                                   const float *__restrict__ scale,
                                                                   const float *__restrict__ shift,
                                                                   __bf16 *__restrict__ out) {
     constexpr int HALO_B = kStemHR * kStemHX * 8, W_B = 64 * kStemWP * 2;
     constexpr int OUT_B = kStemTH * kStemTW * kStemOP * 2;
-    constexpr int LDS_B = (HALO_B + W_B) > OUT_B ? (HALO_B + W_B) : OUT_B;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_B];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[HALO_B + W_B + OUT_B];
     __bf16 *halo = reinterpret_cast<__bf16 *>(smem);
     __bf16 *wl = reinterpret_cast<__bf16 *>(smem + HALO_B);
+    __bf16 *st = reinterpret_cast<__bf16 *>(smem + HALO_B + W_B);
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int px = lane & 31, h = lane >> 5;
     const int per_img = tiles_x * tiles_y;
-    const int n = blockIdx.x / per_img, tr = blockIdx.x - n * per_img;
-    const int oy0 = (tr / tiles_x) * kStemTH, ox0 = (tr - (tr / tiles_x) * tiles_x) * kStemTW;
-    const int iy0 = 2 * oy0 - 3, ix0 = 2 * ox0 - 3;
-    // halo: pixel (r, c) of the tile's input window, C planes -> 4 bf16
-    const float *__restrict__ src = img + (size_t)n * C * H * W;
-    for (int e = t; e < kStemHR * kStemHX; e += 256) {
-        const int r = e / kStemHX, c = e - (e / kStemHX) * kStemHX;
-        const int y = iy0 + r, x = ix0 + c;
-        const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-        const size_t o = (size_t)(in ? y : 0) * W + (in ? x : 0);
-        float v[4];
-#pragma unroll
-        for (int ch = 0; ch < 4; ++ch) v[ch] = (in && ch < C) ? src[(size_t)ch * H * W + o] : 0.0f;
-        bf16x4 h;
-#pragma unroll
-        for (int ch = 0; ch < 4; ++ch) h[ch] = (__bf16)v[ch];
-        *reinterpret_cast<bf16x4 *>(halo + e * 4) = h;
-    }
-    // weights [64][224] -> LDS rows of kStemWP
+    // weights [64][224] -> LDS rows of kStemWP, once per block
     for (int e = t; e < 64 * 28; e += 256) {
         const int co = e / 28, q = e - (e / 28) * 28;
         *reinterpret_cast<uint4 *>(wl + co * kStemWP + q * 8) = *reinterpret_cast<const uint4 *>(wpk + co * 224 + q * 8);
     }
-    __syncthreads();
-    f32x16 acc[2][2];
+    float hv[kStemHE][3];  // the next tile's halo pixels (up to 3 planes; a 4th would be a C = 4 input)
+    float hv4[kStemHE];
+    auto load_halo = [&](int tile) {
+        const int n = tile / per_img, tr = tile - n * per_img;
+        const int iy0 = 2 * ((tr / tiles_x) * kStemTH) - 3, ix0 = 2 * ((tr - (tr / tiles_x) * tiles_x) * kStemTW) - 3;
+        const float *__restrict__ src = img + (size_t)n * C * H * W;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int u = 0; u < kStemHE; ++u) {
+            const int e = t + u * 256;
+            const int r = e / kStemHX, c = e - (e / kStemHX) * kStemHX;
+            const int y = iy0 + r, x = ix0 + c;
+            const bool in = e < kStemHR * kStemHX && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+            const size_t o = (size_t)(in ? y : 0) * W + (in ? x : 0);
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) hv[u][ch] = (in && ch < C) ? src[(size_t)ch * H * W + o] : 0.0f;
+            hv4[u] = (in && C > 3) ? src[(size_t)3 * H * W + o] : 0.0f;
+        }
+    };
+    int tile = blockIdx.x;
+    if (tile < ntiles) load_halo(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        // halo registers -> LDS (every wave finished the previous tile's MFMAs: barrier below)
+#pragma unroll
+        for (int u = 0; u < kStemHE; ++u) {
+            const int e = t + u * 256;
+            if (e < kStemHR * kStemHX) {
+                bf16x4 hb;
+                hb[0] = (__bf16)hv[u][0];
+                hb[1] = (__bf16)hv[u][1];
+                hb[2] = (__bf16)hv[u][2];
+                hb[3] = (__bf16)hv4[u];
+                *reinterpret_cast<bf16x4 *>(halo + e * 4) = hb;
+            }
+        }
+        __syncthreads();
+        const int n = tile / per_img, tr = tile - n * per_img;
+        const int oy0 = (tr / tiles_x) * kStemTH, ox0 = (tr - (tr / tiles_x) * tiles_x) * kStemTW;
+        if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);  // in flight during the MFMAs
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 7; ++ky) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int kx = 4 * s + 2 * h;  // this lane's two taps: kx, kx + 1
+                bf16x8 fa[2], fb[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int oyl = wave * 2 + i;
+                    fa[i] = *reinterpret_cast<const bf16x8 *>(halo + ((2 * oyl + ky) * kStemHX + 2 * px + kx) * 4);
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    fb[j] = *reinterpret_cast<const bf16x8 *>(wl + (j * 32 + px) * kStemWP + (ky * 8 + kx) * 4);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+            }
+        }
+        // BN + ReLU -> bf16 staging (its previous reads, the stores below, precede the barrier above)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int px = lane & 31, h = lane >> 5;
+            for (int q = 0; q < 4; ++q) {
+                const int co = j * 32 + 8 * q + 4 * h;  // channels co..co+3 of pixel px
+                const float4 sc = *reinterpret_cast<const float4 *>(scale + co);
+                const float4 sh = *reinterpret_cast<const float4 *>(shift + co);
 #pragma unroll
-    for (int ky = 0; ky < 7; ++ky) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int kx = 4 * s + 2 * h;  // this lane's two taps: kx, kx + 1
-            bf16x8 fa[2], fb[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int oyl = wave * 2 + i;
-                fa[i] = *reinterpret_cast<const bf16x8 *>(halo + ((2 * oyl + ky) * kStemHX + 2 * px + kx) * 4);
+                for (int i = 0; i < 2; ++i) {
+                    bf16x4 o;
+                    o[0] = (__bf16)fmaxf(acc[i][j][4 * q + 0] * sc.x + sh.x, 0.0f);
+                    o[1] = (__bf16)fmaxf(acc[i][j][4 * q + 1] * sc.y + sh.y, 0.0f);
+                    o[2] = (__bf16)fmaxf(acc[i][j][4 * q + 2] * sc.z + sh.z, 0.0f);
+                    o[3] = (__bf16)fmaxf(acc[i][j][4 * q + 3] * sc.w + sh.w, 0.0f);
+                    *reinterpret_cast<bf16x4 *>(st + ((wave * 2 + i) * kStemTW + px) * kStemOP + co) = o;
+                }
             }
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                fb[j] = *reinterpret_cast<const bf16x8 *>(wl + (j * 32 + px) * kStemWP + (ky * 8 + kx) * 4);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        __syncthreads();  // staging complete; every wave is past its halo reads
+        // 8 x 32 pixels x 128 B: 16-B pieces, a tile row's 32 pixels contiguous in NHWC
+        for (int e = t; e < kStemTH * kStemTW * 8; e += 256) {
+            const int pix = e >> 3, q = e & 7;
+            const int oy = oy0 + pix / kStemTW, ox = ox0 + (pix % kStemTW);
+            if (oy < Ho && ox < Wo)
+                *reinterpret_cast<uint4 *>(out + (((size_t)n * Ho + oy) * Wo + ox) * 64 + q * 8) =
+                    *reinterpret_cast<const uint4 *>(st + pix * kStemOP + q * 8);
         }
-    }
-    __syncthreads();  // halo / weights no longer read: the staging reuses the LDS
-    __bf16 *st = reinterpret_cast<__bf16 *>(smem);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int co = j * 32 + 8 * q + 4 * h;  // channels co..co+3 of pixel px
-            const float4 sc = *reinterpret_cast<const float4 *>(scale + co);
-            const float4 sh = *reinterpret_cast<const float4 *>(shift + co);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                bf16x4 o;
-                o[0] = (__bf16)fmaxf(acc[i][j][4 * q + 0] * sc.x + sh.x, 0.0f);
-                o[1] = (__bf16)fmaxf(acc[i][j][4 * q + 1] * sc.y + sh.y, 0.0f);
-                o[2] = (__bf16)fmaxf(acc[i][j][4 * q + 2] * sc.z + sh.z, 0.0f);
-                o[3] = (__bf16)fmaxf(acc[i][j][4 * q + 3] * sc.w + sh.w, 0.0f);
-                *reinterpret_cast<bf16x4 *>(st + ((wave * 2 + i) * kStemTW + px) * kStemOP + co) = o;
-            }
-        }
-    __syncthreads();
-    // 8 x 32 pixels x 128 B: 16-B pieces, a tile row's 32 pixels contiguous in NHWC
-    for (int e = t; e < kStemTH * kStemTW * 8; e += 256) {
-        const int pix = e >> 3, q = e & 7;
-        const int oy = oy0 + pix / kStemTW, ox = ox0 + (pix % kStemTW);
-        if (oy < Ho && ox < Wo)
-            *reinterpret_cast<uint4 *>(out + (((size_t)n * Ho + oy) * Wo + ox) * 64 + q * 8) =
-                *reinterpret_cast<const uint4 *>(st + pix * kStemOP + q * 8);
     }
 }
 
@@ -1574,8 +1597,12 @@ extern "C" int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W,
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2*3 - 7) / 2 + 1
     const int tx = (Wo + fvp::kStemTW - 1) / fvp::kStemTW, ty = (Ho + fvp::kStemTH - 1) / fvp::kStemTH;
     if ((long long)N * tx * ty > 0x7fffffffLL) return FVP_ERR_SHAPE;
-    hipLaunchKernelGGL(fvp::conv_stem7_bf16_kernel, dim3((unsigned)(N * tx * ty)), dim3(256), 0, (hipStream_t)stream,
-                       img, C, H, W, Ho, Wo, tx, ty, reinterpret_cast<const __bf16 *>(wpack), scale, shift,
+    const int ntiles = N * tx * ty;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;  // persistent: 2 blocks per CU walk the tiles
+    hipLaunchKernelGGL(fvp::conv_stem7_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, C,
+                       H, W, Ho, Wo, tx, ty, ntiles, reinterpret_cast<const __bf16 *>(wpack), scale, shift,
                        reinterpret_cast<__bf16 *>(out));
     return (int)hipGetLastError();
 }

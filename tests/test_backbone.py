@@ -69,6 +69,14 @@ def test_conv_geometry_host():
     assert lib.fvp_conv2d_geom(8, 8, 16, 3, 3, 3, 1, 1, 1, 1, hw) == 1002       # mode 3 needs 2x2 taps
     assert lib.fvp_conv2d_geom(2, 2, 16, 7, 7, 0, 1, 1, 0, 0, hw) == 1002       # kernel larger than the input
     assert lib.fvp_maxpool_pad_nhwc(1, 1, 8, 8, 16, 3, 2, 2, 1, None) == 1002  # 2P > K
+    # bf16 entry points: argument checks before any launch
+    assert lib.fvp_maxpool_pad_nhwc_bf16(1, 1, 8, 8, 12, 3, 2, 1, 1, None) == 1002  # C % 8
+    assert lib.fvp_maxpool_pad_nhwc_bf16(None, 1, 8, 8, 16, 3, 2, 1, 1, None) == 1001
+    assert lib.fvp_maxpool_nhwc_bf16(1, 1, 8, 8, 12, 2, 2, 1, None) == 1002         # C % 8
+    assert lib.fvp_maxpool_nhwc_bf16(1, 1, 8, 8, 16, 3, 2, 1, None) == 1002         # KH > 2
+    assert lib.fvp_conv_stem7_bf16(1, 1, 5, 64, 64, 1, 1, 1, 1, None) == 1002      # > 4 input channels
+    assert lib.fvp_conv_stem7_bf16(1, 0, 3, 64, 64, 1, 1, 1, 1, None) == 1002      # N = 0
+    assert lib.fvp_conv_stem7_bf16(None, 1, 3, 64, 64, 1, 1, 1, 1, None) == 1001
 
 
 def test_backbone_compile_rejects_train_mode():

@@ -166,7 +166,7 @@ __device__ __forceinline__ size_t conv_out_offset(const ConvArgs &a, int m, int 
 // lane-per-channel epilogue straight from the MFMA registers issues 2-4 B per
 // lane: the wide 1x1 "expand" convolutions and their residual reads ran at
 // ~1.4 TB/s; bf16 ResNet-50 19.0 -> 14.6 ms, P2PNet 1.89 -> 1.78 ms.)
-template <int BM, int BN, bool BFO, typename RowM>
+template <int BM, int BN, bool BFO, typename RowM, int NT = 256>
 __device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &rowm, int n0, int g, const float *cs);
 
 template <int BM, int BN, int TM, int TN, int NACC, int MS, bool BFO, typename AccT, typename RowM>
@@ -188,12 +188,12 @@ __device__ __forceinline__ void epilogue_staged(const ConvArgs &a, const AccT (&
 
 // The write half: each thread takes (pixel, 8 output channels) units of the
 // staged [BM][BN + 4] fp32 tile; a thread's units share one channel group
-// (256 % (BN / 8) == 0), so its scale / shift are loaded once.
-template <int BM, int BN, bool BFO, typename RowM>
+// (NT % (BN / 8) == 0), so its scale / shift are loaded once.  NT: threads per block.
+template <int BM, int BN, bool BFO, typename RowM, int NT>
 __device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &rowm, int n0, int g, const float *cs) {
     constexpr int CP = BN + 4;
     constexpr int G = BN / 8;  // 8-channel groups per row
-    static_assert(256 % G == 0, "one channel group per thread");
+    static_assert(NT % G == 0, "one channel group per thread");
     const bool bfo = BFO && a.out_bf16;
     const int Ctot = conv_cols(a.up2, a.Cpo);
     const int cg = threadIdx.x % G;
@@ -207,13 +207,13 @@ __device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &ro
     // all of this thread's units' output offsets and residual loads are issued
     // before the first is used (a unit-by-unit loop exposed one global round
     // trip per unit: the wide 1x1 "expand" layers are output / residual bound)
-    constexpr int U = (BM * G + 255) / 256;  // units per thread (the last may be past the tile: BM * G < 256)
+    constexpr int U = (BM * G + NT - 1) / NT;  // units per thread (the last may be past the tile: BM * G < NT)
     size_t off[U];
     bool ok[U];
     uint4 rpre[U][2], rpost[U][2];  // 8 channels: bf16 in [0], fp32 in [0..1]
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int row = threadIdx.x / G + u * (256 / G);
+        const int row = threadIdx.x / G + u * (NT / G);
         const int m = row < BM ? rowm(row) : -1;
         ok[u] = m >= 0;
         int co_;
@@ -251,7 +251,7 @@ __device__ __forceinline__ void epilogue_write(const ConvArgs &a, const RowM &ro
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int row = min(threadIdx.x / G + u * (256 / G), BM - 1);
+        const int row = min(threadIdx.x / G + u * (NT / G), BM - 1);
         const float4 c0 = *reinterpret_cast<const float4 *>(cs + row * CP + cg * 8);
         const float4 c1 = *reinterpret_cast<const float4 *>(cs + row * CP + cg * 8 + 4);
         float v[8] = {c0.x * s0.x + h0.x, c0.y * s0.y + h0.y, c0.z * s0.z + h0.z, c0.w * s0.w + h0.w,
@@ -758,20 +758,23 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
 // conflict-free.  Padding taps and rows past M read zeros (range check).  Two
 // stages: step s+1 is in flight while step s feeds the MFMAs (counted vmcnt,
 // raw s_barrier: a __syncthreads() would drain the prefetch).  Tile 128 x BN,
-// waves 2 x 2 (64 x BN/2 each).  Measured before it (register-staged
+// waves 2 x NW/2 (64 x 32 each at BN 128 with 8 waves: 108 VGPRs, 4 waves per
+// SIMD; 4 waves of 64 x 64 took 184 VGPRs and ran 2.6 % slower over ResNet-50).  Measured before it (register-staged
 // conv_bf16_kernel, 3x3 64->64 at 40 x 128 x 240): 18 VALU + 17 SALU per
 // MFMA, 41 % of wave time parked on waits, 33 % of LDS cycles bank conflicts.
 
 #define FVP_WAIT_BARRIER(vm) asm volatile("s_waitcnt vmcnt(" #vm ")\n\ts_barrier" ::: "memory")
 
-template <int BN, int BK>
-__global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
-    constexpr int BM = 128, WTN = BN / 2, TN = WTN / 32;
+template <int BN, int BK, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void conv_bf16_dma_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
+    constexpr int NT = NW * 64, WCN = NW / 2;  // threads; waves 2 (rows) x WCN (columns)
+    constexpr int BM = 128, WTN = BN / WCN, TN = WTN / 32;
     constexpr int RB = BK * 2, SPR = RB / 16, RPI = 1024 / RB;  // row bytes, 16-B slots per row, rows per wave load
-    constexpr int NAI = BM / (4 * RPI), NBI = BN / (4 * RPI), NPS = NAI + NBI;  // wave loads per K step
+    constexpr int NAI = BM / (NW * RPI), NBI = BN / (NW * RPI), NPS = NAI + NBI;  // wave loads per K step
     constexpr int ABYTES = BM * RB, STAGE = ABYTES + BN * RB;
     constexpr int KLDS = 2 * STAGE, CLDS = BM * (BN + 4) * 4;
-    static_assert((BK == 32 || BK == 64) && (BN == 64 || BN == 128), "tile");
+    static_assert((BK == 32 || BK == 64) && (BN == 64 || BN == 128) && (NW == 4 || NW == 8) && TN >= 1 &&
+                  NAI >= 1 && NBI >= 1, "tile");
     __shared__ __attribute__((aligned(16))) float smem[(KLDS > CLDS ? KLDS : CLDS) / 4];
     char *lds = reinterpret_cast<char *>(smem);
     // conflict-free ds_read_b128 fragment reads: 16-B slot s of row r holds chunk s ^ swz(r)
@@ -871,7 +874,8 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
             if constexpr (NPS == 8) FVP_WAIT_BARRIER(8);  // step ks landed (this wave's), then everyone's
             else if constexpr (NPS == 6) FVP_WAIT_BARRIER(6);
             else if constexpr (NPS == 4) FVP_WAIT_BARRIER(4);
-            else FVP_WAIT_BARRIER(3);
+            else if constexpr (NPS == 3) FVP_WAIT_BARRIER(3);
+            else FVP_WAIT_BARRIER(2);
         } else {
             FVP_WAIT_BARRIER(0);
         }
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void conv_bf16_dma_kernel(ConvArgs a, const
     }
     __syncthreads();
     auto rowm = [&](int l) { return m0 + l < M ? m0 + l : -1; };
-    epilogue_write<BM, BN, true>(a, rowm, n0, g, smem);
+    epilogue_write<BM, BN, true, decltype(rowm), NT>(a, rowm, n0, g, smem);
 }
 #undef FVP_WAIT_BARRIER
 
@@ -1359,11 +1363,11 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
             const int BN = Ntot > 64 ? 128 : 64;
             const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
             if (Cpi % 64 == 0) {  // K steps of one tap x 64 channels (128-B rows)
-                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 64>), gr, dim3(256), 0, st, a, wb);
-                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 64>), gr, dim3(256), 0, st, a, wb);
+                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 64, 8>), gr, dim3(512), 0, st, a, wb);
+                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 64, 4>), gr, dim3(256), 0, st, a, wb);
             } else {  // the HDN / JLN CNNs' 32-channel layers: 64-B rows
-                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 32>), gr, dim3(256), 0, st, a, wb);
-                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 32>), gr, dim3(256), 0, st, a, wb);
+                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 32, 8>), gr, dim3(512), 0, st, a, wb);
+                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 32, 4>), gr, dim3(256), 0, st, a, wb);
             }
             return (int)hipGetLastError();
         }

@@ -1060,6 +1060,99 @@ __global__ __launch_bounds__(256, 2) void conv_stem7_bf16_kernel(const float *__
     }
 }
 
+// ---- the CNNs' 7x7 J -> 16 front conv on bf16 MFMA, from the NCHW maps -------
+// Basic2DBlock(J, 16, 7) of P2PNet / CenterNet (cnns_2d.py:12-29, 185-232,
+// 235-295): 7x7, stride 1, pad 3, C <= 16 input planes -> 16 channels + BN +
+// ReLU, bf16 NHWC16 out.  On the generic path it was the slowest layer of the
+// bf16 P2PNet (16 output columns on a 32-wide MFMA tile, a conversion pass
+// before it).  A block owns an 8 x 32 output tile: the 14 x 38 input halo of
+// the C planes goes to LDS once as bf16 [row][x][16 channels] (48-B pixel
+// pitch: conflict-free fragment reads), the weights [16][50 taps][16] (tap 49
+// and channels >= C zero) beside it.  v_mfma_f32_16x16x32_bf16 with the
+// weights as the A operand: K step = 2 taps x 16 channels, a lane's 8 k values
+// = 8 channels of one tap (16 contiguous bytes), and the output comes out with
+// lane -> pixel, 4 registers -> 4 consecutive channels.
+constexpr int kFrTH = 8, kFrTW = 32, kFrHR = kFrTH + 6, kFrHX = kFrTW + 6, kFrPB = 48;  // pixel pitch (B)
+constexpr int kFrWP = 50 * 16 + 8;                                                      // weight row (bf16)
+
+__global__ __launch_bounds__(256) void conv_front7_bf16_kernel(const float *__restrict__ x, int C, int H, int W,
+                                                               int tiles_x, int tiles_y,
+                                                               const __bf16 *__restrict__ wpk,
+                                                               const float *__restrict__ scale,
+                                                               const float *__restrict__ shift,
+                                                               __bf16 *__restrict__ out) {
+    constexpr int HALO_B = kFrHR * kFrHX * kFrPB, W_B = 16 * kFrWP * 2, OUT_B = kFrTH * kFrTW * 16 * 2;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[HALO_B + W_B + OUT_B];
+    unsigned char *halo = smem;
+    __bf16 *wl = reinterpret_cast<__bf16 *>(smem + HALO_B);
+    __bf16 *st = reinterpret_cast<__bf16 *>(smem + HALO_B + W_B);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int per_img = tiles_x * tiles_y;
+    const int n = blockIdx.x / per_img, tr = blockIdx.x - n * per_img;
+    const int oy0 = (tr / tiles_x) * kFrTH, ox0 = (tr - (tr / tiles_x) * tiles_x) * kFrTW;
+    const float *__restrict__ src = x + (size_t)n * C * H * W;
+    // halo (r, c) <- input (oy0 - 3 + r, ox0 - 3 + c), C planes -> 16 bf16 (zeros past C / outside)
+    for (int e = t; e < kFrHR * kFrHX; e += 256) {
+        const int r = e / kFrHX, c = e - (e / kFrHX) * kFrHX;
+        const int y = oy0 - 3 + r, xx = ox0 - 3 + c;
+        const bool in = (unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const size_t o = (size_t)(in ? y : 0) * W + (in ? xx : 0);
+        bf16x8 h0, h1;
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch) {
+            h0[ch] = (__bf16)((in && ch < C) ? src[(size_t)ch * H * W + o] : 0.0f);
+            h1[ch] = (__bf16)((in && ch + 8 < C) ? src[(size_t)(ch + 8) * H * W + o] : 0.0f);
+        }
+        *reinterpret_cast<bf16x8 *>(halo + e * kFrPB) = h0;
+        *reinterpret_cast<bf16x8 *>(halo + e * kFrPB + 16) = h1;
+    }
+    for (int e = t; e < 16 * 100; e += 256) {  // weights: 16 rows x 100 pieces of 8
+        const int co = e / 100, q = e - (e / 100) * 100;
+        *reinterpret_cast<uint4 *>(wl + co * kFrWP + q * 8) = *reinterpret_cast<const uint4 *>(wpk + co * 800 + q * 8);
+    }
+    __syncthreads();
+    const int px = lane & 15, g = lane >> 4;  // pixel of a 16-pixel M tile; k group
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // wave w: output rows 2w, 2w+1 x 32 columns = 4 tiles of 16 pixels (i: row i/2, columns 16*(i%2)..)
+#pragma unroll 5
+    for (int s = 0; s < 25; ++s) {
+        const int tap = 2 * s + (g >> 1), half = g & 1;  // this lane's tap (49: zero weights) and channel half
+        const int ky = tap / 7, kx = tap - (tap / 7) * 7;
+        const bf16x8 fw = *reinterpret_cast<const bf16x8 *>(wl + px * kFrWP + tap * 16 + half * 8);
+        const int tky = tap < 49 ? ky : 0, tkx = tap < 49 ? kx : 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int oyl = wave * 2 + (i >> 1), oxl = (i & 1) * 16 + px;
+            const bf16x8 fa = *reinterpret_cast<const bf16x8 *>(halo + ((oyl + tky) * kFrHX + oxl + tkx) * kFrPB +
+                                                                  half * 16);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw, fa, acc[i], 0, 0, 0);
+        }
+    }
+    // D[co][pixel]: lane -> pixel px of tile i, registers r -> channel 4g + r
+    const float4 sc = *reinterpret_cast<const float4 *>(scale + 4 * g);
+    const float4 sh = *reinterpret_cast<const float4 *>(shift + 4 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int pix = (wave * 2 + (i >> 1)) * kFrTW + (i & 1) * 16 + px;
+        bf16x4 o;
+        o[0] = (__bf16)fmaxf(acc[i][0] * sc.x + sh.x, 0.0f);
+        o[1] = (__bf16)fmaxf(acc[i][1] * sc.y + sh.y, 0.0f);
+        o[2] = (__bf16)fmaxf(acc[i][2] * sc.z + sh.z, 0.0f);
+        o[3] = (__bf16)fmaxf(acc[i][3] * sc.w + sh.w, 0.0f);
+        *reinterpret_cast<bf16x4 *>(st + pix * 16 + 4 * g) = o;
+    }
+    __syncthreads();
+    for (int e = t; e < kFrTH * kFrTW * 2; e += 256) {  // 16-B halves of the 32-B pixels
+        const int pix = e >> 1, hh = e & 1;
+        const int oy = oy0 + pix / kFrTW, ox = ox0 + (pix % kFrTW);
+        if (oy < H && ox < W)
+            *reinterpret_cast<uint4 *>(out + (((size_t)n * H + oy) * W + ox) * 16 + hh * 8) =
+                *reinterpret_cast<const uint4 *>(st + pix * 16 + hh * 8);
+    }
+}
+
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
 // cnns_2d.py Pool2DBlock; F.max_pool1d(x, 2, 2) on H == 1 rows, cnns_1d.py Pool1DBlock)
 template <int KH, int KW>
@@ -1607,6 +1700,18 @@ extern "C" int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W,
     const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;  // persistent: 2 blocks per CU walk the tiles
     hipLaunchKernelGGL(fvp::conv_stem7_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, C,
                        H, W, Ho, Wo, tx, ty, ntiles, reinterpret_cast<const __bf16 *>(wpack), scale, shift,
+                       reinterpret_cast<__bf16 *>(out));
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_conv_front7_bf16(const float *x, int N, int C, int H, int W, const void *wpack,
+                                    const float *scale, const float *shift, void *out, void *stream) {
+    if (!x || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
+    if (N <= 0 || C < 1 || C > 16 || H < 1 || W < 1) return FVP_ERR_SHAPE;
+    const int tx = (W + fvp::kFrTW - 1) / fvp::kFrTW, ty = (H + fvp::kFrTH - 1) / fvp::kFrTH;
+    if ((long long)N * tx * ty > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    hipLaunchKernelGGL(fvp::conv_front7_bf16_kernel, dim3((unsigned)(N * tx * ty)), dim3(256), 0, (hipStream_t)stream,
+                       x, C, H, W, tx, ty, reinterpret_cast<const __bf16 *>(wpack), scale, shift,
                        reinterpret_cast<__bf16 *>(out));
     return (int)hipGetLastError();
 }

@@ -85,6 +85,7 @@ SIGNATURES = {
     "fvp_conv2d_ex_workspace_bytes": [c_int] * 13,
     "fvp_conv2d_geom": [c_int] * 10 + [ctypes.POINTER(c_int)],
     "fvp_maxpool_pad_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv_front7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_stem7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_maxpool_pad_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -363,6 +363,7 @@ class FvpCNN:
         else:
             self.kind = "plain"
             self.plan = _Plan(module, dtype)
+        self.front7 = None
         if dtype == torch.bfloat16 and self.kind != "plain":
             # bf16 activations between the layers (half the bytes, no per-chunk
             # conversion); the heads' last convs write the fp32 outputs
@@ -371,6 +372,37 @@ class FvpCNN:
                 inner += [c for c, _ in self.hm[:-1]] + [c for c, _ in self.size[:-1]]
             for c in inner:
                 c.act_bf16 = c.bf16
+            self._compile_front7()
+
+    def _compile_front7(self):
+        """The front Basic2DBlock(J <= 16, 16, 7) as fvp_conv_front7_bf16 straight
+        from the NCHW maps (2-D nets, bf16): weights [16][50 taps][16]."""
+        f = self.front
+        if f.kind != "chain" or not f.parts or f.parts[0].kind != "seq" or len(f.parts[0].parts) != 1:
+            return
+        c, relu = f.parts[0].parts[0]
+        if not (relu and c.mode == 0 and (c.KH, c.KW) == (7, 7) and c.stride == (1, 1) and c.pad == (3, 3)
+                and c.Cin <= 16 and c.Cpo == 16):
+            return
+        w = self.module.front_layers[0].block[0].weight.detach().float()  # [Cout][Cin][7][7]
+        wp = torch.zeros((16, 50, 16), dtype=torch.float32, device=w.device)
+        wp[:c.Cout, :49, :c.Cin] = w.permute(0, 2, 3, 1).reshape(c.Cout, 49, c.Cin)
+        self.front7 = (wp.reshape(16, 800).to(torch.bfloat16).contiguous(), c)
+
+    def _front(self, x: torch.Tensor) -> Act:
+        """front_layers(x) for NCHW fp32 maps x."""
+        if self.front7 is None:
+            return self.front(to_nhwc(x))
+        wp, c = self.front7
+        x = x.float().contiguous()
+        N, C, H, W = x.shape
+        out = torch.empty((N, H, W, 16), dtype=torch.bfloat16, device=x.device)
+        _lib.call("fvp_conv_front7_bf16", _ptr(x), N, C, H, W, _ptr(wp), _ptr(c.scale), _ptr(c.shift), _ptr(out),
+                  _stream(out))
+        a = Act(out, c.Cout)
+        for sub in self.front.parts[1:]:
+            a = sub(a)
+        return a
 
     @staticmethod
     def _run_seq(seq, x):
@@ -383,17 +415,16 @@ class FvpCNN:
         if self.kind == "c2c":  # [N, C, L] as [N, C, 1, L]
             y = self.out(self.encdec(self.front(to_nhwc(x.unsqueeze(2)))), relu=False)
             return to_nchw(y).squeeze(2)
-        a = to_nhwc(x)
         if self.kind == "p2p":
-            return to_nchw(self.out(self.encdec(self.front(a)), relu=False))
+            return to_nchw(self.out(self.encdec(self._front(x)), relu=False))
         if self.kind == "centernet":
             return self.from_xy(x)
-        return to_nchw(self.plan(a))
+        return to_nchw(self.plan(to_nhwc(x)))
 
     @torch.no_grad()
     def from_xy(self, xy: torch.Tensor):
         assert self.kind == "centernet"
-        f = self.encdec(self.front(to_nhwc(xy)))
+        f = self.encdec(self._front(xy))
         return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
 
 

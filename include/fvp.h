@@ -358,6 +358,13 @@ int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int
  * (bf16 operands, fp32 accumulation). */
 int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W, const void *wpack, const float *scale,
                         const float *shift, void *out, void *stream);
+/* The CNNs' front Basic2DBlock (cnns_2d.py: 7x7, stride 1, pad 3, C <= 16
+ * planes -> 16 channels) + BN + ReLU on bf16 MFMA, straight from the NCHW
+ * fp32 maps [N][C][H][W] to bf16 NHWC [N][H][W][16].  wpack: bf16
+ * [16][50][16] = W[co][c][ky][kx] at (co, 7*ky + kx, c), zero for tap 49 and
+ * c >= C; scale / shift: fp32 [16].  Opt-in precision. */
+int fvp_conv_front7_bf16(const float *x, int N, int C, int H, int W, const void *wpack, const float *scale,
+                         const float *shift, void *out, void *stream);
 int fvp_maxpool_pad_nhwc_bf16(const void *in, int N, int H, int W, int C, int K, int S, int P, void *out,
                               void *stream);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */

@@ -230,6 +230,36 @@ def test_bf16_dma_conv_matches_register_staged(gpu_device, cin, cout, k, stride,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,hw", [(15, (64, 64)), (15, (37, 50)), (3, (80, 80)), (16, (9, 70))])
+def test_bf16_front7_vs_torch(gpu_device, cin, hw):
+    """fvp_conv_front7_bf16 (the bf16 nets' Basic2DBlock(J, 16, 7) from the NCHW
+    maps): within 2e-2 of the output scale of torch's fp32 Basic2DBlock on the
+    bf16-rounded input, ragged tiles included."""
+    import cnn_arch
+    from fvp import cnn, synthetic
+
+    p2p = cnn_arch.P2PNet(cin, 15).eval()
+    p2p.load_state_dict(synthetic.seeded_state_dict(p2p, 40 + cin))
+    p2p = p2p.to(gpu_device)
+    f = cnn.FvpCNN(p2p, torch.bfloat16)
+    assert f.front7 is not None
+    x = torch.rand((3, cin) + hw, generator=torch.Generator().manual_seed(cin)).to(gpu_device)
+    x = x.to(torch.bfloat16).float()
+    wp, c = f.front7
+    out = torch.empty((3,) + hw + (16,), dtype=torch.bfloat16, device=gpu_device)
+    from fvp import _lib
+    from fvp.ops import _ptr, _stream
+
+    _lib.call("fvp_conv_front7_bf16", _ptr(x), 3, cin, hw[0], hw[1], _ptr(wp), _ptr(c.scale), _ptr(c.shift),
+              _ptr(out), _stream(out))
+    with torch.no_grad():
+        ref = p2p.front_layers[0](x)
+    got = out.float().permute(0, 3, 1, 2)
+    err = float((got - ref).abs().max()) / float(ref.abs().max())
+    assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
 def test_bf16_p2pnet_vs_reference(gpu_device):
     """Whole P2PNet with bf16 operands against the reference's fp32 golden:
     within 5e-2 of the output scale (errors compound over 20 convolutions)."""

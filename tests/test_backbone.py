@@ -77,6 +77,8 @@ def test_conv_geometry_host():
     assert lib.fvp_conv_stem7_bf16(1, 1, 5, 64, 64, 1, 1, 1, 1, None) == 1002      # > 4 input channels
     assert lib.fvp_conv_stem7_bf16(1, 0, 3, 64, 64, 1, 1, 1, 1, None) == 1002      # N = 0
     assert lib.fvp_conv_stem7_bf16(None, 1, 3, 64, 64, 1, 1, 1, 1, None) == 1001
+    assert lib.fvp_conv_front7_bf16(1, 1, 17, 64, 64, 1, 1, 1, 1, None) == 1002     # > 16 input planes
+    assert lib.fvp_conv_front7_bf16(None, 1, 15, 64, 64, 1, 1, 1, 1, None) == 1001
 
 
 def test_backbone_compile_rejects_train_mode():

@@ -112,13 +112,18 @@ def main():
         def fvp_flow():
             return layer.forward_fused(f32.heatmaps_cl(views), meta, cams, rt)
 
+        def fvp_flow_bf16():  # bf16 backbone (opt-in precision), fp32 heatmaps and voxelize
+            return layer.forward_fused(b16.heatmaps_cl(views), meta, cams, rt)
+
         t_vox_planar = timeit(lambda: layer.forward_fused(planar, meta, cams, rt), 20)
         t_vox_cl = timeit(lambda: layer.forward_fused(cl, meta, cams, rt), 20)
-        t_ref, t_fvp = timeit(ref_flow), timeit(fvp_flow)
+        t_ref, t_fvp, t_fvp_b = timeit(ref_flow), timeit(fvp_flow), timeit(fvp_flow_bf16)
         out["views_to_cube"] = {
             "frames": B, "geometry": "c2 (5 Shelf cams, 80x80x20, J=15)",
             "reference_flow_ms": round(t_ref, 3), "fvp_flow_ms": round(t_fvp, 3),
             "reference_flow_frames_per_s": round(B / t_ref * 1e3, 1), "fvp_flow_frames_per_s": round(B / t_fvp * 1e3, 1),
+            "fvp_flow_bf16_backbone_ms": round(t_fvp_b, 3),
+            "fvp_flow_bf16_backbone_frames_per_s": round(B / t_fvp_b * 1e3, 1),
             "voxelize_planar_ms": round(t_vox_planar, 4), "voxelize_channels_last_ms": round(t_vox_cl, 4),
             "layout_pass_removed_ms": round(t_vox_planar - t_vox_cl, 4)}
     print(json.dumps({"metric": f"PoseResNet-{args.layers} backbone on fp32 MFMA + views->cube",

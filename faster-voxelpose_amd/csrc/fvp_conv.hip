@@ -765,15 +765,16 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
 
 #define FVP_WAIT_BARRIER(vm) asm volatile("s_waitcnt vmcnt(" #vm ")\n\ts_barrier" ::: "memory")
 
-template <int BN, int BK, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void conv_bf16_dma_kernel(ConvArgs a, const __bf16 *__restrict__ wb) {
+template <int BN, int BK, int NW, bool F32>
+__global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const void *__restrict__ wb) {
     constexpr int NT = NW * 64, WCN = NW / 2;  // threads; waves 2 (rows) x WCN (columns)
     constexpr int BM = 128, WTN = BN / WCN, TN = WTN / 32;
-    constexpr int RB = BK * 2, SPR = RB / 16, RPI = 1024 / RB;  // row bytes, 16-B slots per row, rows per wave load
+    constexpr int ES = F32 ? 4 : 2;                             // operand bytes
+    constexpr int RB = BK * ES, SPR = RB / 16, RPI = 1024 / RB;  // row bytes, 16-B slots per row, rows per wave load
     constexpr int NAI = BM / (NW * RPI), NBI = BN / (NW * RPI), NPS = NAI + NBI;  // wave loads per K step
     constexpr int ABYTES = BM * RB, STAGE = ABYTES + BN * RB;
     constexpr int KLDS = 2 * STAGE, CLDS = BM * (BN + 4) * 4;
-    static_assert((BK == 32 || BK == 64) && (BN == 64 || BN == 128) && (NW == 4 || NW == 8) && TN >= 1 &&
+    static_assert((RB == 64 || RB == 128) && (BN == 64 || BN == 128) && (NW == 4 || NW == 8) && TN >= 1 &&
                   NAI >= 1 && NBI >= 1, "tile");
     __shared__ __attribute__((aligned(16))) float smem[(KLDS > CLDS ? KLDS : CLDS) / 4];
     char *lds = reinterpret_cast<char *>(smem);
@@ -796,9 +797,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_bf16_dma_kernel(ConvArgs a, c
     // kOOB, which the range check turns into zeros.  Per row, the input offset
     // of tap (0, 0) and a bit mask of the taps inside the image are decoded
     // once (quotients by a float reciprocal + one correction: M < 2^24).
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(a.in, (unsigned)((size_t)a.N * a.H * a.W * a.Cpi * 2));
-    const __amdgpu_buffer_rsrc_t rb =
-        uniform_rsrc(wb + (size_t)g * a.Cpo_w * Ktot, (unsigned)((size_t)a.Cpo_w * Ktot * 2));
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(a.in, (unsigned)((size_t)a.N * a.H * a.W * a.Cpi * ES));
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(reinterpret_cast<const char *>(wb) + (size_t)g * a.Cpo_w * Ktot * ES,
+                                                   (unsigned)((size_t)a.Cpo_w * Ktot * ES));
     const int HWm = a.Hm * a.Wm;
     const float inv_hw = 1.0f / (float)HWm, inv_w = 1.0f / (float)a.Wm;
     auto qdiv = [](int n, int d, float inv) {
@@ -824,13 +825,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_bf16_dma_kernel(ConvArgs a, c
         // tap rows ylo..yhi-1 of the all-rows pattern rep = sum 2^(ky*KW): mask = xm * rep(rows)
         const unsigned rows = (unsigned)(((1ull << (yhi * a.KW)) - 1ull) & ~((1ull << (ylo * a.KW)) - 1ull));
         tmask[i] = m < M ? xm * (rep & rows) : 0u;
-        voa[i] = (((img * a.H + y0) * a.W + x0) * a.Cpi + (slot ^ swz(r)) * 8) * 2;  // < 0 only for unused taps
+        voa[i] = ((img * a.H + y0) * a.W + x0) * a.Cpi * ES + (slot ^ swz(r)) * 16;  // < 0 only for unused taps
     }
     int vob[NBI];
 #pragma unroll
     for (int i = 0; i < NBI; ++i) {
         const int r = (wave * NBI + i) * RPI + lane / SPR;
-        vob[i] = ((n0 + r) * (int)Ktot + (slot ^ swz(r)) * 8) * 2;
+        vob[i] = (n0 + r) * (int)Ktot * ES + (slot ^ swz(r)) * 16;
     }
     typedef __attribute__((address_space(3))) void *lds_ptr;
     auto issue = [&](int ks, int tap, int d, int buf) {
@@ -860,7 +861,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_bf16_dma_kernel(ConvArgs a, c
             ++tap;
             if (++kx == a.KW) {
                 kx = 0;
-                d += (a.W - a.KW) * a.Cpi * 2;  // next tap row
+                d += (a.W - a.KW) * a.Cpi * ES;  // next tap row
             }
         }
     };
@@ -881,24 +882,48 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_bf16_dma_kernel(ConvArgs a, c
         }
         const char *sa = lds + buf * STAGE, *sb = sa + ABYTES;
 #pragma unroll
-        for (int kk = 0; kk < BK / 16; ++kk) {
+        for (int kk = 0; kk < RB / 32; ++kk) {  // a lane half reads one 16-B chunk of each row
             const int c = kk * 2 + (lane >> 5);
-            bf16x8 fa[2], fb[TN];
+            const char *pa[2], *pb[TN];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int row = wr * 64 + i * 32 + (lane & 31);
-                fa[i] = *reinterpret_cast<const bf16x8 *>(sa + row * RB + ((c ^ swz(row)) << 4));
+                pa[i] = sa + row * RB + ((c ^ swz(row)) << 4);
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int col = wc * WTN + j * 32 + (lane & 31);
-                fb[j] = *reinterpret_cast<const bf16x8 *>(sb + col * RB + ((c ^ swz(col)) << 4));
+                pb[j] = sb + col * RB + ((c ^ swz(col)) << 4);
             }
+            if constexpr (F32) {
+                // fp32: chunk c of lane half h holds k = 8 kk + 4 h + q, q < 4, so the
+                // q-th v_mfma_f32_32x32x2f32 sums the k pair {8 kk + q, 8 kk + 4 + q}
+                // (both operands agree on it): one ds_read_b128 per operand feeds 4
+                // MFMAs.  Every product is summed in fp32 as before, in another order.
+                float4 fa[2], fb[TN];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const float4 *>(pa[i]);
 #pragma unroll
-                for (int j = 0; j < TN; ++j)  // D = W x A^T: lane -> pixel, 4 consecutive registers -> 4 channels
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const float4 *>(pb[j]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][q], fa[i][q], acc[i][j], 0, 0, 0);
+            } else {
+                bf16x8 fa[2], fb[TN];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const bf16x8 *>(pa[i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8 *>(pb[j]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)  // D = W x A^T: lane -> pixel, 4 consecutive registers -> 4 channels
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buf is free for step ks + 2
     }
@@ -1427,8 +1452,9 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
                        int Cpo_w, const float *scale, const float *shift, const float *res_pre,
                        const float *res_post, int relu, const ConvGeom &g, float *out, int bf16, int algo, void *ws,
                        size_t ws_bytes, void *stream) {
-    if (bf16 & ~(FVP_CONV_BF16 | FVP_CONV_BF16_IN | FVP_CONV_BF16_OUT)) return FVP_ERR_SHAPE;
+    if (bf16 & ~(FVP_CONV_BF16 | FVP_CONV_BF16_IN | FVP_CONV_BF16_OUT | FVP_CONV_F32_KC)) return FVP_ERR_SHAPE;
     if ((bf16 & (FVP_CONV_BF16_IN | FVP_CONV_BF16_OUT)) && !(bf16 & FVP_CONV_BF16)) return FVP_ERR_SHAPE;
+    if ((bf16 & FVP_CONV_F32_KC) && (bf16 & FVP_CONV_BF16)) return FVP_ERR_SHAPE;
     if (!in || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || Cpo <= 0 || Cpo % 16) return FVP_ERR_SHAPE;
     if (algo < FVP_CONV_AUTO || algo > FVP_CONV_PER_TAP_NOSPLIT) return FVP_ERR_SHAPE;
@@ -1442,6 +1468,29 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
                     KH, KW, Cpo, Cpo_w, relu, g.mode, g.Hm, g.Wm, g.sy, g.sx, g.py, g.px, 1, nullptr,
                     (bf16 & FVP_CONV_BF16_IN) ? 1 : 0, (bf16 & FVP_CONV_BF16_OUT) ? 1 : 0};
     hipStream_t st = (hipStream_t)stream;
+    // LDS-DMA kernel: one K step = one tap x a 128-B (or 64-B) row of channels
+    const int es = (bf16 & FVP_CONV_BF16) ? 2 : 4;
+    const long long Kd = (long long)KH * KW * Cpi;
+    const bool fits = (long long)N * H * W * Cpi * es < (1LL << 31) && (long long)Cpo_w * Kd * es < (1LL << 31) &&
+                      KH * KW <= 32 && M < (1 << 24);  // 32-bit buffer offsets, tap masks, row decode
+    auto dma = [&](auto f32) {
+        constexpr bool F = decltype(f32)::value;
+        constexpr int E = F ? 4 : 2;
+        const int BN = Ntot > 64 ? 128 : 64;
+        const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
+        if (Cpi * E % 128 == 0) {  // 128-B rows
+            if (BN == 128) hipLaunchKernelGGL((fvp::conv_dma_kernel<128, 128 / E, 8, F>), gr, dim3(512), 0, st, a, wpack);
+            else hipLaunchKernelGGL((fvp::conv_dma_kernel<64, 128 / E, 4, F>), gr, dim3(256), 0, st, a, wpack);
+        } else {  // 64-B rows (32 bf16 / 16 fp32 channels)
+            if (BN == 128) hipLaunchKernelGGL((fvp::conv_dma_kernel<128, 64 / E, 8, F>), gr, dim3(512), 0, st, a, wpack);
+            else hipLaunchKernelGGL((fvp::conv_dma_kernel<64, 64 / E, 4, F>), gr, dim3(256), 0, st, a, wpack);
+        }
+        return (int)hipGetLastError();
+    };
+    if (bf16 & FVP_CONV_F32_KC) {  // fp32 operands, weights [G][Cpo_w][Krows]: the DMA kernel or nothing
+        if (Cpi % 16 || !fits) return FVP_ERR_SHAPE;
+        return dma(std::true_type{});
+    }
     if (bf16) {  // chunks of one tap x 16 / 32 channels (or several taps of a 4/8/12-channel input), no split
         if (Cpi % 16 && (bf16 & FVP_CONV_BF16_IN)) return FVP_ERR_SHAPE;
         const __bf16 *wb = reinterpret_cast<const __bf16 *>(wpack);
@@ -1449,21 +1498,7 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
         // at 40 x 960 x 512: 3x3 64->64 0.21 -> 0.15 ms, deconv 256->256 at 64x120
         // 1.21 -> 0.76 ms, 1x1 256->1024 at 32x60 0.15 -> 0.11 ms; the 64->256
         // expand layers at 128x240 tie at 0.31 ms, output bound)
-        const long long Kd = (long long)KH * KW * Cpi;
-        const bool fits = (long long)N * H * W * Cpi * 2 < (1LL << 31) && (long long)Cpo_w * Kd * 2 < (1LL << 31) &&
-                          KH * KW <= 32 && M < (1 << 24);  // 32-bit buffer offsets, tap masks, row decode
-        if (a.in_bf16 && Cpi % 32 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && fits) {
-            const int BN = Ntot > 64 ? 128 : 64;
-            const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
-            if (Cpi % 64 == 0) {  // K steps of one tap x 64 channels (128-B rows)
-                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 64, 8>), gr, dim3(512), 0, st, a, wb);
-                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 64, 4>), gr, dim3(256), 0, st, a, wb);
-            } else {  // the HDN / JLN CNNs' 32-channel layers: 64-B rows
-                if (BN == 128) hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<128, 32, 8>), gr, dim3(512), 0, st, a, wb);
-                else hipLaunchKernelGGL((fvp::conv_bf16_dma_kernel<64, 32, 4>), gr, dim3(256), 0, st, a, wb);
-            }
-            return (int)hipGetLastError();
-        }
+        if (a.in_bf16 && Cpi % 32 == 0 && algo != FVP_CONV_PER_TAP_NOSPLIT && fits) return dma(std::false_type{});
 #define FVP_CONVB(BM, BN, WR, KC)                                                                               \
     do {                                                                                                          \
         const dim3 gr((unsigned)((M + BM - 1) / BM), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);             \

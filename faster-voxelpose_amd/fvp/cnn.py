@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -29,9 +30,14 @@ from .ops import _ptr, _stream
 
 
 # Kernel selection passed to fvp_conv2d_nhwc_ws (include/fvp.h FVP_CONV_*):
-# AUTO in the product; tests run every choice through conv_algo().
-CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT = 0, 1, 2, 3
+# AUTO in the product; tests run every choice through conv_algo().  CONV_DMA
+# (host side only) runs every eligible fp32 layer on the LDS-DMA kernel
+# (FVP_CONV_F32_KC); AUTO picks it for the launches that fill the chip.
+CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA = 0, 1, 2, 3, 4
 CONV_ALGO = CONV_AUTO
+# AUTO may pick the fp32 LDS-DMA kernel (FVP_F32_DMA=0: A/B against the [Krows][Cpo_w] kernels)
+F32_DMA_AUTO = os.environ.get("FVP_F32_DMA", "1") != "0"
+FVP_CONV_F32_KC = 8
 
 
 @contextlib.contextmanager
@@ -141,6 +147,8 @@ class ConvLayer:
         self.act_bf16 = False  # bf16 operands only: write the output (and read residuals) as bf16
         if self.bf16:  # [G][Cpo_w][Krows], k contiguous (rows past the taps zero)
             self.wpack_bf16 = pack.transpose(1, 2).contiguous().to(torch.bfloat16)
+        elif self.Cpi % 16 == 0 and taps <= 32:  # the same layout in fp32 for the LDS-DMA kernel
+            self.wpack_kc = pack.transpose(1, 2).contiguous()
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
         if bn is not None:  # eval BatchNorm: (x - mean) / sqrt(var + eps) * gamma + beta
             s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
@@ -176,23 +184,53 @@ class ConvLayer:
         for r in (res_pre, res_post):
             assert r is None or (tuple(r.t.shape) == tuple(out.shape) and r.t.dtype == odt), \
                 (None if r is None else (r.t.shape, r.t.dtype), out.shape)
-        flags = 0
+        flags, wp = 0, self.wpack
         if self.bf16:  # FVP_CONV_BF16 | _IN | _OUT (include/fvp.h)
             flags = 1 | (2 if x.t.dtype == torch.bfloat16 else 0) | (4 if odt == torch.bfloat16 else 0)
+            wp = self.wpack_bf16
         key = (x.N, x.H, x.W, CONV_ALGO)
-        if key not in self._ws:  # split-K scratch for under-filled launches (0 bytes: the layer does not split)
-            self._ws[key] = 0 if self.bf16 else _lib.load().fvp_conv2d_ex_workspace_bytes(
-                x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo, *self.geom(), CONV_ALGO)
-        nws = self._ws[key]
+        if key not in self._ws:  # (split-K scratch bytes, LDS-DMA kernel) of this input size
+            self._ws[key] = self._plan(x)
+        nws, dma = self._ws[key]
+        if dma:
+            flags, wp = FVP_CONV_F32_KC, self.wpack_kc
         # allocated per call: the caching allocator is stream-ordered, so two
         # streams running this layer never share partial sums
         ws = torch.empty(((nws + 3) // 4,), dtype=torch.float32, device=out.device) if nws else None
         _lib.call("fvp_conv2d_nhwc_ex", _ptr(x.t), x.N, x.H, x.W, x.Cp,
-                  _ptr(self.wpack_bf16 if self.bf16 else self.wpack), self.KH, self.KW, self.Cpo, self.Cpo_w,
+                  _ptr(wp), self.KH, self.KW, self.Cpo, self.Cpo_w,
                   _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
-                  _ptr(res_post.t) if res_post else None, int(relu), *self.geom(), flags, CONV_ALGO,
-                  _ptr(out), _ptr(ws), nws, _stream(out))
+                  _ptr(res_post.t) if res_post else None, int(relu), *self.geom(), flags,
+                  CONV_AUTO if CONV_ALGO == CONV_DMA else CONV_ALGO, _ptr(out), _ptr(ws), nws, _stream(out))
         return Act(out, self.Cout)
+
+    def _plan(self, x: Act) -> tuple[int, bool]:
+        """(split-K scratch bytes, use the fp32 LDS-DMA kernel) for input x under CONV_ALGO."""
+        if self.bf16:
+            return 0, False
+        dma = hasattr(self, "wpack_kc") and (CONV_ALGO == CONV_DMA or (CONV_ALGO == CONV_AUTO and F32_DMA_AUTO))
+        if dma:  # the kernel's limits (fvp.h FVP_CONV_F32_KC): 32-bit offsets, row decode
+            Ho, Wo = self.out_hw(x.H, x.W)
+            M = x.N * (x.H * x.W if self.mode else Ho * Wo)
+            dma = (M < 1 << 24 and x.N * x.H * x.W * x.Cp * 4 < 1 << 31
+                   and self.wpack_kc.numel() // self.G * 4 < 1 << 31)
+            if dma and CONV_ALGO == CONV_AUTO:
+                # measured on ResNet-50 at 40 x 960 x 512 (profiles/round2/conv_f32_dma): the
+                # DMA kernel wins wherever its launch fills the chip (no split-K) and
+                # has 64+ columns (the 15-joint head: 0.28 -> 0.39 ms on 64-wide tiles);
+                # a "same" KxK layer under two waves of blocks stays on the halo
+                # kernel (3x3 512->512 at 16x30: 0.83 vs 0.89 ms)
+                ncols = self.nq * self.Cpo
+                bn = 128 if ncols > 64 else 64
+                blocks = -(-M // 128) * -(-ncols // bn) * self.G
+                same = (self.mode == 0 and self.stride == (1, 1) and (self.KH > 1 or self.KW > 1)
+                        and 2 * self.pad[0] == self.KH - 1 and 2 * self.pad[1] == self.KW - 1)
+                dma = ncols >= 64 and blocks >= (1024 if same else 256)
+        if dma:
+            return 0, True
+        algo = CONV_AUTO if CONV_ALGO == CONV_DMA else CONV_ALGO
+        return _lib.load().fvp_conv2d_ex_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo,
+                                                         *self.geom(), algo), False
 
     def flops(self, x: Act) -> int:
         Ho, Wo = self.out_hw(x.H, x.W)

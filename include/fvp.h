@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 9
+#define FVP_ABI_VERSION 10
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -341,6 +341,12 @@ int fvp_conv2d_nhwc_ex(const float *in, int N, int H, int W, int Cpi, const void
 #define FVP_CONV_BF16 1
 #define FVP_CONV_BF16_IN 2
 #define FVP_CONV_BF16_OUT 4
+/* fp32 operands with the weights given k-contiguous, wpack fp32
+ * [G][Cpo_w][Krows] (the bf16 layout): runs the LDS-DMA staged kernel
+ * (Cpi % 16 == 0, activations and weights under 2 GiB, KH*KW <= 32, N*Hm*Wm
+ * < 2^24, else FVP_ERR_SHAPE; no split-K, algo ignored).  Same fp32 products,
+ * summed in another order than the [Krows][Cpo_w] kernels. */
+#define FVP_CONV_F32_KC 8
 size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int mode, int sy,
                                      int sx, int py, int px, int algo);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */

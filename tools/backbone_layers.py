@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=40)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--no-dma", action="store_true", help="fp32: keep AUTO off the LDS-DMA kernel")
     args = ap.parse_args()
     import torch
 
@@ -27,6 +28,7 @@ def main():
     from fvp import cnn, synthetic
     from fvp.backbone import FvpPoseResNet
 
+    cnn.F32_DMA_AUTO = not args.no_dma
     dev = torch.device("cuda:0")
     m = cnn_arch.PoseResNet(50, 15).eval()
     m.load_state_dict(synthetic.seeded_state_dict(m, 21))
@@ -58,6 +60,7 @@ def main():
         tot_ms += ms
         tot_gf += fl / 1e9
         rows.append({"k": f"{l.KH}x{l.KW}", "mode": l.mode, "stride": l.stride[0], "in": [H, W, Cp], "cout": l.Cout,
+                     "dma": any(v[1] for v in l._ws.values()),
                      "ms": round(ms, 3), "gflop": round(fl / 1e9, 1), "tflops": round(fl / 1e9 / ms, 1)})
     agg = {}
     for r in rows:
@@ -65,7 +68,8 @@ def main():
         a = agg.setdefault(key, [0.0, 0.0])
         a[0] += r["ms"]
         a[1] += r["gflop"]
-    print(json.dumps({"images": args.images, "dtype": "bf16" if args.bf16 else "fp32", "total_ms": round(tot_ms, 2),
+    print(json.dumps({"images": args.images, "dtype": "bf16" if args.bf16 else "fp32", "f32_dma": not args.no_dma,
+                      "total_ms": round(tot_ms, 2),
                       "total_tflops": round(tot_gf / tot_ms, 1),
                       "by_kind": {k: {"ms": round(v[0], 2), "tflops": round(v[1] / v[0], 1)} for k, v in agg.items()},
                       "layers": rows}))

@@ -191,7 +191,7 @@ def test_bf16_small_channel_conv_vs_torch(gpu_device, cin, cpi, k, stride, hw):
                                                              (32, 32, 1, 1, (17, 40), False, True)])
 def test_bf16_dma_conv_matches_register_staged(gpu_device, cin, cout, k, stride, hw, deconv, res):
     """bf16 activations with Cpi % 32 == 0 run the LDS-DMA kernel
-    (conv_bf16_dma_kernel, 64- or 32-deep K steps); CONV_PER_TAP_NOSPLIT keeps such layers on the
+    (conv_dma_kernel, 64- or 32-deep K steps); CONV_PER_TAP_NOSPLIT keeps such layers on the
     register-staged conv_bf16_kernel.  Both walk k in the same order with the
     same MFMA instruction, so the outputs are bit-identical; and within 2e-2 of
     the output scale of torch's fp32 convolution of the bf16-rounded input."""

@@ -97,6 +97,32 @@ def test_conv_layer_vs_torch(gpu_device, conv_kernel, cin, cout, k, hw, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,hw,res", [(64, 128, 3, (256, 250), True), (256, 512, 1, (100, 90), False),
+                                               (48, 96, 1, (160, 150), True)])
+def test_auto_takes_f32_dma_kernel(gpu_device, cin, cout, k, hw, res):
+    """AUTO (the product setting) on launches that fill the chip runs the fp32
+    LDS-DMA kernel (FVP_CONV_F32_KC, k-paired MFMA order): fp32 tolerance vs torch."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    seq = nn.Sequential(nn.Conv2d(cin, cout, k, padding=(k - 1) // 2), nn.BatchNorm2d(cout)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin * cout))
+    seq = seq.to(gpu_device)
+    g = torch.Generator().manual_seed(cin)
+    x = torch.rand((3, cin) + hw, generator=g).to(gpu_device) - 0.5
+    r = torch.rand((3, cout) + hw, generator=g).to(gpu_device) if res else None
+    with torch.no_grad():
+        ref = seq(x)
+        ref = torch.relu(ref + r) if res else torch.relu(ref)
+    layer = cnn.ConvLayer(seq[0], seq[1])
+    assert cnn.CONV_ALGO == cnn.CONV_AUTO and cnn.F32_DMA_AUTO
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=cnn.to_nhwc(r) if res else None))
+    assert any(dma for _, dma in layer._ws.values()), "AUTO did not pick the LDS-DMA kernel"
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv {cin}->{cout} k{k} (DMA)")
+
+
+@pytest.mark.gpu
 def test_transposed_conv_and_pool_vs_torch(gpu_device):
     import torch.nn as nn
     import torch.nn.functional as F

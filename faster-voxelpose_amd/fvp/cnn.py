@@ -51,6 +51,16 @@ def conv_algo(algo: int):
         CONV_ALGO = prev
 
 
+_CUS = {}
+
+
+def _cus(dev: torch.device) -> int:
+    """Compute units of a device (cached)."""
+    if dev not in _CUS:
+        _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CUS[dev]
+
+
 def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
@@ -215,17 +225,22 @@ class ConvLayer:
             dma = (M < 1 << 24 and x.N * x.H * x.W * x.Cp * 4 < 1 << 31
                    and self.wpack_kc.numel() // self.G * 4 < 1 << 31)
             if dma and CONV_ALGO == CONV_AUTO:
-                # measured on ResNet-50 at 40 x 960 x 512 (profiles/round2/conv_f32_dma): the
-                # DMA kernel wins wherever its launch fills the chip (no split-K) and
-                # has 64+ columns (the 15-joint head: 0.28 -> 0.39 ms on 64-wide tiles);
-                # a "same" KxK layer under two waves of blocks stays on the halo
-                # kernel (3x3 512->512 at 16x30: 0.83 vs 0.89 ms)
+                # measured on ResNet-50 at 40 x 960 x 512 and the P2PNet / CenterNet
+                # layers (profiles/round2/conv_f32_dma): the DMA kernel wins wherever its
+                # launch fills the chip (no split-K) and has 64+ columns (the 15-joint
+                # head: 0.28 -> 0.39 ms on 64-wide tiles, 32-column 3x3 layers 0.21 ->
+                # 0.36 ms); a "same" KxK layer whose last round of blocks would run
+                # mostly empty stays on the halo kernel (3x3 512->512 at 16x30: 600
+                # blocks on 512 slots, 0.83 vs 0.89 ms; P2PNet's 3x3 128->128 at 16x16,
+                # 480 blocks: DMA 0.175 vs 0.191 ms)
                 ncols = self.nq * self.Cpo
                 bn = 128 if ncols > 64 else 64
                 blocks = -(-M // 128) * -(-ncols // bn) * self.G
                 same = (self.mode == 0 and self.stride == (1, 1) and (self.KH > 1 or self.KW > 1)
                         and 2 * self.pad[0] == self.KH - 1 and 2 * self.pad[1] == self.KW - 1)
-                dma = ncols >= 64 and blocks >= (1024 if same else 256)
+                slots = _cus(x.t.device) * (2 if bn == 128 else 3)  # resident blocks (VGPRs / LDS)
+                fill = blocks / (-(-blocks // slots) * slots)  # occupancy of the block rounds
+                dma = ncols >= 64 and blocks >= 256 and (not same or fill >= 0.7)
         if dma:
             return 0, True
         algo = CONV_AUTO if CONV_ALGO == CONV_DMA else CONV_ALGO

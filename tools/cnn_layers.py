@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--net", choices=["p2p", "centernet"], default="p2p")
     ap.add_argument("--images", type=int, default=240)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--algo", choices=["auto", "dma", "halo", "pertap"], default="auto",
+                    help="fp32 kernel choice (fvp.cnn.conv_algo)")
     args = ap.parse_args()
     import torch
 
@@ -48,7 +50,8 @@ def main():
         rec.append((self, a.H, a.W, a.Cp, a.t.dtype, e0, e1, self.flops(a)))
         return y
 
-    with torch.no_grad():
+    algo = {"auto": cnn.CONV_AUTO, "dma": cnn.CONV_DMA, "halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP}[args.algo]
+    with torch.no_grad(), cnn.conv_algo(algo):
         run()
         torch.cuda.synchronize()
         cnn.ConvLayer.__call__ = timed
@@ -62,8 +65,9 @@ def main():
         ms = e0.elapsed_time(e1)
         tot += ms
         rows.append({"k": f"{l.KH}x{l.KW}", "mode": l.mode, "in": [H, W, Cp], "in_dtype": str(dt).split(".")[-1],
-                     "cout": l.Cout, "ms": round(ms, 4), "tflops": round(fl / 1e9 / ms, 1)})
-    print(json.dumps({"net": args.net, "images": args.images, "dtype": "bf16" if args.bf16 else "fp32",
+                     "cout": l.Cout, "dma": any(v[1] for v in l._ws.values()), "ms": round(ms, 4),
+                     "tflops": round(fl / 1e9 / ms, 1)})
+    print(json.dumps({"net": args.net, "images": args.images, "dtype": "bf16" if args.bf16 else "fp32", "algo": args.algo,
                       "total_ms": round(tot, 3), "layers": rows}))
 
 

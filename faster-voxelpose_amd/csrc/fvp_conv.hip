@@ -767,15 +767,16 @@ __global__ __launch_bounds__(256, 4) void conv_bf16_kernel(ConvArgs a, const __b
 
 template <int BN, int BK, int NW, bool F32>
 __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const void *__restrict__ wb) {
-    constexpr int NT = NW * 64, WCN = NW / 2;  // threads; waves 2 (rows) x WCN (columns)
-    constexpr int BM = 128, WTN = BN / WCN, TN = WTN / 32;
+    // waves WRN (rows) x WCN (columns): 2 x NW/2 of 64 x BN/(NW/2), or NW x 1 of 32 x 32 at BN 32
+    constexpr int NT = NW * 64, WCN = BN == 32 ? 1 : NW / 2, WRN = NW / WCN;
+    constexpr int BM = 128, WTM = BM / WRN, TM = WTM / 32, WTN = BN / WCN, TN = WTN / 32;
     constexpr int ES = F32 ? 4 : 2;                             // operand bytes
     constexpr int RB = BK * ES, SPR = RB / 16, RPI = 1024 / RB;  // row bytes, 16-B slots per row, rows per wave load
     constexpr int NAI = BM / (NW * RPI), NBI = BN / (NW * RPI), NPS = NAI + NBI;  // wave loads per K step
     constexpr int ABYTES = BM * RB, STAGE = ABYTES + BN * RB;
     constexpr int KLDS = 2 * STAGE, CLDS = BM * (BN + 4) * 4;
-    static_assert((RB == 64 || RB == 128) && (BN == 64 || BN == 128) && (NW == 4 || NW == 8) && TN >= 1 &&
-                  NAI >= 1 && NBI >= 1, "tile");
+    static_assert((RB == 64 || RB == 128) && (BN == 32 || BN == 64 || BN == 128) && (NW == 4 || NW == 8) &&
+                  TM >= 1 && TN >= 1 && NAI >= 1 && NBI >= 1, "tile");
     __shared__ __attribute__((aligned(16))) float smem[(KLDS > CLDS ? KLDS : CLDS) / 4];
     char *lds = reinterpret_cast<char *>(smem);
     // conflict-free ds_read_b128 fragment reads: 16-B slot s of row r holds chunk s ^ swz(r)
@@ -786,7 +787,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
     const int m0 = mt * BM, n0 = nt * BN;
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int wr = wave & 1, wc = wave >> 1;
+    const int wr = wave % WRN, wc = wave / WRN;
     const int g = blockIdx.z;  // parity group (mode 3), else 0
     const int py = a.up2 == 3 ? 1 - (g >> 1) : a.py, px = a.up2 == 3 ? 1 - (g & 1) : a.px;
     const int cpc = a.Cpi / BK, nks = a.KH * a.KW * cpc;
@@ -846,9 +847,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(sa + ABYTES + (wave * NBI + i) * 1024), 16,
                                                      (unsigned)(vob[i] + ks * RB), 0, 0, 0);
     };
-    f32x16 acc[2][TN];
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -874,9 +875,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
             advance();
             if constexpr (NPS == 8) FVP_WAIT_BARRIER(8);  // step ks landed (this wave's), then everyone's
             else if constexpr (NPS == 6) FVP_WAIT_BARRIER(6);
+            else if constexpr (NPS == 5) FVP_WAIT_BARRIER(5);
             else if constexpr (NPS == 4) FVP_WAIT_BARRIER(4);
             else if constexpr (NPS == 3) FVP_WAIT_BARRIER(3);
-            else FVP_WAIT_BARRIER(2);
+            else {
+                static_assert(NPS == 2, "wave loads per step");
+                FVP_WAIT_BARRIER(2);
+            }
         } else {
             FVP_WAIT_BARRIER(0);
         }
@@ -884,10 +889,10 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
 #pragma unroll
         for (int kk = 0; kk < RB / 32; ++kk) {  // a lane half reads one 16-B chunk of each row
             const int c = kk * 2 + (lane >> 5);
-            const char *pa[2], *pb[TN];
+            const char *pa[TM], *pb[TN];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int row = wr * 64 + i * 32 + (lane & 31);
+            for (int i = 0; i < TM; ++i) {
+                const int row = wr * WTM + i * 32 + (lane & 31);
                 pa[i] = sa + row * RB + ((c ^ swz(row)) << 4);
             }
 #pragma unroll
@@ -900,26 +905,26 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
                 // q-th v_mfma_f32_32x32x2f32 sums the k pair {8 kk + q, 8 kk + 4 + q}
                 // (both operands agree on it): one ds_read_b128 per operand feeds 4
                 // MFMAs.  Every product is summed in fp32 as before, in another order.
-                float4 fa[2], fb[TN];
+                float4 fa[TM], fb[TN];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const float4 *>(pa[i]);
+                for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const float4 *>(pa[i]);
 #pragma unroll
                 for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const float4 *>(pb[j]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < TM; ++i)
 #pragma unroll
                         for (int j = 0; j < TN; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][q], fa[i][q], acc[i][j], 0, 0, 0);
             } else {
-                bf16x8 fa[2], fb[TN];
+                bf16x8 fa[TM], fb[TN];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const bf16x8 *>(pa[i]);
+                for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8 *>(pa[i]);
 #pragma unroll
                 for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8 *>(pb[j]);
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)  // D = W x A^T: lane -> pixel, 4 consecutive registers -> 4 channels
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
@@ -931,9 +936,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
     // r of tile (i, j): pixel i*32 + lane%32, channel j*32 + 8*(r/4) + 4*(lane/32) + r%4)
     {
         constexpr int CP = BN + 4;
-        float *cs = smem + (wr * 64 + (lane & 31)) * CP + wc * WTN + 4 * (lane >> 5);
+        float *cs = smem + (wr * WTM + (lane & 31)) * CP + wc * WTN + 4 * (lane >> 5);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -1476,9 +1481,12 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
     auto dma = [&](auto f32) {
         constexpr bool F = decltype(f32)::value;
         constexpr int E = F ? 4 : 2;
-        const int BN = Ntot > 64 ? 128 : 64;
+        // 32-column tiles (4 waves of 32 x 32) for the <= 32-channel layers, 128-B rows only
+        const int BN = Ntot > 64 ? 128 : (Ntot > 32 || Cpi * E % 128) ? 64 : 32;
         const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
-        if (Cpi * E % 128 == 0) {  // 128-B rows
+        if (BN == 32) {
+            hipLaunchKernelGGL((fvp::conv_dma_kernel<32, 128 / E, 4, F>), gr, dim3(256), 0, st, a, wpack);
+        } else if (Cpi * E % 128 == 0) {  // 128-B rows
             if (BN == 128) hipLaunchKernelGGL((fvp::conv_dma_kernel<128, 128 / E, 8, F>), gr, dim3(512), 0, st, a, wpack);
             else hipLaunchKernelGGL((fvp::conv_dma_kernel<64, 128 / E, 4, F>), gr, dim3(256), 0, st, a, wpack);
         } else {  // 64-B rows (32 bf16 / 16 fp32 channels)

@@ -214,7 +214,9 @@ def test_bf16_small_channel_conv_vs_torch(gpu_device, cin, cpi, k, stride, hw):
                                                              (192, 96, 3, 1, (7, 130), False, False),
                                                              (32, 64, 3, 1, (64, 64), False, True),
                                                              (96, 32, 3, 2, (21, 19), False, False),
-                                                             (32, 32, 1, 1, (17, 40), False, True)])
+                                                             (32, 32, 1, 1, (17, 40), False, True),
+                                                             (64, 16, 3, 1, (33, 29), False, True),
+                                                             (256, 15, 1, 1, (20, 21), False, False)])
 def test_bf16_dma_conv_matches_register_staged(gpu_device, cin, cout, k, stride, hw, deconv, res):
     """bf16 activations with Cpi % 32 == 0 run the LDS-DMA kernel
     (conv_dma_kernel, 64- or 32-deep K steps); CONV_PER_TAP_NOSPLIT keeps such layers on the

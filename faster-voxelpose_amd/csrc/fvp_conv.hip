@@ -1738,8 +1738,10 @@ extern "C" int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W,
     const int tx = (Wo + fvp::kStemTW - 1) / fvp::kStemTW, ty = (Ho + fvp::kStemTH - 1) / fvp::kStemTH;
     if ((long long)N * tx * ty > 0x7fffffffLL) return FVP_ERR_SHAPE;
     const int ntiles = N * tx * ty;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
     const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;  // persistent: 2 blocks per CU walk the tiles
     hipLaunchKernelGGL(fvp::conv_stem7_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, C,
                        H, W, Ho, Wo, tx, ty, ntiles, reinterpret_cast<const __bf16 *>(wpack), scale, shift,

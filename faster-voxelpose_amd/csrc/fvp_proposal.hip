@@ -169,8 +169,17 @@ constexpr int kSelMaxE = 32;                    // elements per thread: maps up 
 // Element e of the masked map (max_pool2d 3x3/s1/p1 keep mask, proposal.py:34-52,
 // 66-70): the value itself where it is its neighbourhood's maximum, else
 // 0 * value (max_pool2d propagates NaN; NaN == m is false -> 0 * NaN).
-__device__ __forceinline__ float masked_value(const float *map, int e, int X, int Y) {
-    const int ex = e / Y, ey = e - (e / Y) * Y;
+// e / Y for 0 <= e < 2^16 without an integer division: a float estimate
+// (off by at most one) and one correction step.
+__device__ __forceinline__ int div_small(int e, int Y, float rY) {
+    int q = (int)((float)e * rY);
+    const int r = e - q * Y;
+    q += (r >= Y) - (r < 0);
+    return q;
+}
+
+__device__ __forceinline__ float masked_value(const float *map, int e, int X, int Y, float rY) {
+    const int ex = div_small(e, Y, rY), ey = e - ex * Y;
     const float c = map[e];
     float m = -INFINITY;
     bool nan = false;
@@ -238,6 +247,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     __shared__ int widx[kSelWaves];  // winners' flat indices (K <= kSelWaves)
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float rY = 1.0f / (float)Y;
     const float *__restrict__ p = prob + (size_t)b * stride;
     {
         // all E loads in flight before the first LDS store (clamped addresses, no branches)
@@ -259,7 +269,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
 #pragma unroll
     for (int i = 0; i < E; ++i) {
         const int e = tid + i * kSelThreads;
-        key[i] = e < M ? cand_key(Cand{masked_value(map, e, X, Y), e}) : 0ull;
+        key[i] = e < M ? cand_key(Cand{masked_value(map, e, X, Y, rY), e}) : 0ull;
         best = key[i] > best ? key[i] : best;
     }
     best = wave_max_key(best);
@@ -296,7 +306,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             for (int j = 0; j < C; ++j) rank += lkey[j] > k;
             if (rank < K) {
                 const int idx = (int)~(unsigned)k;
-                write_winner(b, K, rank, idx, masked_value(map, idx, X, Y), X, vals, flat, xy, widx);
+                write_winner(b, K, rank, idx, masked_value(map, idx, X, Y, rY), X, vals, flat, xy, widx);
             }
         }
     } else {  // K rounds, each the largest key below the previous winner
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
             if (tid == 0) {
                 const int idx = (int)~(unsigned)w;
-                write_winner(b, K, r, idx, masked_value(map, idx, X, Y), X, vals, flat, xy, widx);
+                write_winner(b, K, r, idx, masked_value(map, idx, X, Y, rY), X, vals, flat, xy, widx);
             }
             prev = w;
             __syncthreads();

@@ -32,6 +32,8 @@
 // tap and the camera sum order are the reference's (fvp_device.h: torch's
 // CPU mean over the views folds complete blocks of 16 cameras, CASC = V > 16),
 // so the result is bit-exact.
+#include <type_traits>
+
 #include "fvp_layout.h"
 
 namespace fvp {
@@ -523,6 +525,145 @@ static size_t workspace_bytes(int B, int V, int J, int H, int W, bool half) {
     const int J1 = slice_joints(J);  // one joint slice's copy at a time
     return (size_t)chunk_frames(B, V, J1, H, W, half) * frame_bytes(V, J1, H, W, half);
 }
+
+// -- winners' columns without the cube ----------------------------------------
+// columns[b,k,j,z] = cube[b,j,flat[b,k],z] (human_detection_net.py:199-200)
+// recomputed for the K winners only, so an HDN forward that needs the cube
+// just for these columns can skip writing it (7.7 MB per C2 frame): the same
+// per-voxel arithmetic as voxelize_body -- coordinates from the packed grid or
+// projected on the fly, setup_taps, fma(d,w3, fma(c,w2, fma(b,w1, a*w0))) per
+// camera in view order with the 16-camera block fold, + 0 / + blocks, / V,
+// clamp -- hence bit-identical to the cube's voxels.  The heatmaps are read
+// in place through strides: planar [B][V][J][H][W] (joint stride H*W, pixel
+// stride 1) or channels-last [B][V][H][W][cp] (joint stride 1, pixel stride
+// cp).  One thread per output element (z fastest).
+template <typename T, bool OTF, bool CASC>
+__global__ __launch_bounds__(256) void voxel_columns_kernel(const T *__restrict__ hm, long long vstride,
+                                                            long long jstride, int pstride, CoordSource src,
+                                                            const int32_t *__restrict__ grid_index,
+                                                            const int64_t *__restrict__ flat, int K, int V, int J,
+                                                            int H, int W, int X, int Y, int Z,
+                                                            float *__restrict__ cols, long long total) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int z = (int)(gid % Z);
+    long long r = gid / Z;
+    const int j = (int)(r % J);
+    r /= J;
+    const int k = (int)(r % K);
+    const long long b = r / K;
+    const int64_t f = flat[b * K + k];
+    if (f < 0 || f >= (int64_t)X * Y) {  // an index outside the map reads nothing (as gather_columns)
+        cols[gid] = __builtin_nanf("");
+        return;
+    }
+    const long long n = f * Z + z;
+    const long long N = (long long)X * Y * Z;
+    const int GV = V + (V & 1);
+    const int gsel = grid_index ? grid_index[b] : 0;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    float wx_ = 0.f, wy_ = 0.f, wz_ = 0.f, rt[6];
+    if constexpr (OTF) {
+        wx_ = axis_coord(src.gs.start[0], src.gs.end[0], X, (int)(f / Y), src.gs.center[0]);
+        wy_ = axis_coord(src.gs.start[1], src.gs.end[1], Y, (int)(f % Y), src.gs.center[1]);
+        wz_ = axis_coord(src.gs.start[2], src.gs.end[2], Z, z, src.gs.center[2]);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) rt[q] = src.resize_t[q];
+    }
+    // cameras in groups of 8: all coordinates, then all 32 taps in flight, then
+    // the sums in view order (the latency of one group instead of one per camera)
+    constexpr int G = 8;
+    float acc = 0.0f, blk = 0.0f;
+    for (int v0 = 0; v0 < V; v0 += G) {
+        float tv[G][4], w[G][4];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int v = min(v0 + u, V - 1);
+            float gx, gy;
+            if constexpr (OTF) {
+                const Cam c = load_cam(src.cams + ((size_t)gsel * V + v) * FVP_CAM_STRIDE);
+                float px, py;
+                project_point(c, wx_, wy_, wz_, px, py);
+                pixel_to_sample(px, py, rt, src.im.ori_max, src.im.img_w, src.im.img_h, (float)src.im.hm_w,
+                                (float)src.im.hm_h, gx, gy);
+            } else {
+                const float2 gp = *reinterpret_cast<const float2 *>(src.grids + (((size_t)gsel * N + n) * GV + v) * 2);
+                gx = gp.x;
+                gy = gp.y;
+            }
+            const Taps4<false> t = setup_taps<false>(gx, gy, sxs, sys, W, H, 1u);  // offsets in pixels
+            const T *__restrict__ im = hm + ((size_t)b * V + v) * vstride + (size_t)j * jstride;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                w[u][m] = t.w[m];
+                tv[u][m] = t.o[m] == kOOB ? 0.0f : to_f32(im[(size_t)t.o[m] * pstride]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int v = v0 + u;
+            if (v >= V) break;
+            if (CASC && (v & 15) == 0 && v > 0) {  // a complete block of 16 cameras (fvp_device.h)
+                blk = blk + acc;
+                acc = 0.0f;
+            }
+            acc = acc + __builtin_fmaf(tv[u][3], w[u][3],
+                                       __builtin_fmaf(tv[u][2], w[u][2], __builtin_fmaf(tv[u][1], w[u][1], tv[u][0] * w[u][0])));
+        }
+    }
+    acc = acc + (CASC ? blk : 0.0f);
+    cols[gid] = clampf(acc / (float)V, 0.0f, 1.0f);
+}
+
+}  // namespace fvp
+
+extern "C" int fvp_voxel_columns(const void *heatmaps, int half, long long view_stride, long long joint_stride,
+                                 int pix_stride, int B, int V, int J, int H, int W, const float *packed_grids,
+                                 const float *cams, const float *resize_t, const fvp_grid_spec *grid,
+                                 const fvp_image_spec *img, const int32_t *grid_index, int X, int Y, int Z,
+                                 const int64_t *flat, int K, float *columns, void *stream) {
+    if (!heatmaps || !flat || !columns) return FVP_ERR_NULL;
+    if (B < 0 || K < 0 || V <= 0 || V > FVP_MAX_VIEWS || J <= 0 || H < 2 || W < 2 || X <= 0 || Y <= 0 || Z <= 0 ||
+        view_stride <= 0 || joint_stride <= 0 || pix_stride <= 0)
+        return FVP_ERR_SHAPE;
+    if ((long long)H * W > 0x7fffffffLL) return FVP_ERR_SHAPE;  // 32-bit pixel offsets
+    fvp::CoordSource src{};
+    const bool otf = packed_grids == nullptr;
+    if (otf) {
+        if (!cams || !resize_t || !grid || !img) return FVP_ERR_NULL;
+        if (grid->bins[0] != X || grid->bins[1] != Y || grid->bins[2] != Z || img->hm_w != W || img->hm_h != H)
+            return FVP_ERR_SHAPE;
+        src.cams = cams;
+        src.resize_t = resize_t;
+        src.gs = *grid;
+        src.im = *img;
+    } else {
+        src.grids = packed_grids;
+    }
+    const long long total = (long long)B * K * J * Z;
+    if (total == 0) return FVP_OK;
+    const dim3 g((unsigned)((total + 255) / 256)), blk(256);
+    hipStream_t st = (hipStream_t)stream;
+    auto go = [&](auto tag, auto o, auto c) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((fvp::voxel_columns_kernel<T, decltype(o)::value, decltype(c)::value>), g, blk, 0, st,
+                           reinterpret_cast<const T *>(heatmaps), view_stride, joint_stride, pix_stride, src,
+                           grid_index, flat, K, V, J, H, W, X, Y, Z, columns, total);
+    };
+    using TT = std::true_type;
+    using FF = std::false_type;
+    const bool casc = V > 16;
+    if (half) {
+        if (otf) casc ? go(_Float16{}, TT{}, TT{}) : go(_Float16{}, TT{}, FF{});
+        else casc ? go(_Float16{}, FF{}, TT{}) : go(_Float16{}, FF{}, FF{});
+    } else {
+        if (otf) casc ? go(0.0f, TT{}, TT{}) : go(0.0f, TT{}, FF{});
+        else casc ? go(0.0f, FF{}, TT{}) : go(0.0f, FF{}, FF{});
+    }
+    return (int)hipGetLastError();
+}
+
+namespace fvp {
 
 }  // namespace fvp
 

@@ -56,6 +56,9 @@ SIGNATURES = {
     "fvp_nms_topk_columns": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_int, c_int, c_void_p, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
+    "fvp_voxel_columns": [c_void_p, c_int, ctypes.c_longlong, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int,
+                          c_int, c_void_p, c_void_p, c_void_p, ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec),
+                          c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_gather_bbox": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_proposal_centers": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                              c_float, c_void_p, c_void_p],
@@ -98,7 +101,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _LIB = None
 
 

@@ -37,6 +37,8 @@ from __future__ import annotations
 
 import sys
 
+import os
+
 import torch
 
 from . import backbone as fvp_backbone
@@ -46,6 +48,14 @@ from . import jln, project_individual, project_whole, proposal
 USE_FVP_CNN = False  # set by install(cnn=True)
 FVP_CNN_DTYPE = torch.float32
 USE_FVP_BACKBONE = False  # set by install(backbone=True)
+# fused_hdn_forward: write no cube and recompute the K winners' z-columns from the
+# heatmaps instead (fvp_voxel_columns, bit-identical to gathering them from the
+# cube).  None = when the batch's cube would exceed RECOMPUTE_CUBE_BYTES (a
+# memory saving: the TD-bound gather hides the cube writes, so below that the
+# one-launch NMS + column gather is as fast or faster).
+_env = os.environ.get("FVP_RECOMPUTE_COLUMNS")
+RECOMPUTE_COLUMNS = None if _env is None else _env != "0"
+RECOMPUTE_CUBE_BYTES = 512 << 20
 FVP_BACKBONE_DTYPE = torch.float32
 
 
@@ -125,10 +135,22 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     proposal_heatmaps_1d [B,K,Z], proposal_centers [B,K,7], bbox_preds [B,X*Y,2]).
     """
     batch_size = heatmaps.shape[0]
-    cubes, xy = self.project_layer.forward_fused(heatmaps, meta, cameras, resize_transform)
-    hm2d, bbox_preds = center_net_from_xy(self.center_net, xy)
-    # nms2D and the z-column gather of its winners in one launch (:188, :199-200)
-    confs_2d, index_2d, flat, columns = proposal.nms2D_columns(hm2d, self.max_people, cubes)  # columns [B,K,J,Z]
+    pl_ = self.project_layer
+    recompute = RECOMPUTE_COLUMNS
+    if recompute is None:
+        X, Y, Z = (int(v) for v in pl_.voxels_per_axis)
+        recompute = batch_size * heatmaps.shape[2] * X * Y * Z * 4 > RECOMPUTE_CUBE_BYTES
+    if recompute:
+        # no cube: the xy plane only, then the winners' columns recomputed (:162-200)
+        _, xy = pl_.forward_fused(heatmaps, meta, cameras, resize_transform, want_cube=False, want_xy=True)
+        hm2d, bbox_preds = center_net_from_xy(self.center_net, xy)
+        confs_2d, index_2d, flat = proposal.nms2D(hm2d, self.max_people)
+        columns = pl_.columns(heatmaps, meta, cameras, resize_transform, flat)  # [B,K,J,Z]
+    else:
+        cubes, xy = pl_.forward_fused(heatmaps, meta, cameras, resize_transform)
+        hm2d, bbox_preds = center_net_from_xy(self.center_net, xy)
+        # nms2D and the z-column gather of its winners in one launch (:188, :199-200)
+        confs_2d, index_2d, flat, columns = proposal.nms2D_columns(hm2d, self.max_people, cubes)
     match_bbox = proposal.gather_bbox(bbox_preds, flat)
     c2c = self.c2c_net
     if USE_FVP_CNN and not c2c.training:

@@ -354,6 +354,68 @@ def _(cube, flat):
     return cube.new_empty((B, flat.shape[1], J, Z))
 
 
+@torch.library.custom_op("fvp::voxel_columns", mutates_args=(), device_types="cuda")
+def voxel_columns(heatmaps: torch.Tensor, cl_joints: int, packed_grids: Optional[torch.Tensor],
+                  cams: Optional[torch.Tensor], grid_index: Optional[torch.Tensor], resize_t: Optional[torch.Tensor],
+                  start: list[float], end: list[float], center: list[float], bins: list[int], ori_max: float,
+                  img_w: float, img_h: float, flat: torch.Tensor) -> torch.Tensor:
+    """columns[b,k,j,:] = cube[b,j,flat[b,k],:] of the cube voxelize (packed_grids)
+    or voxelize_cams (cams) would produce, recomputed for the K winners only
+    (fvp_voxel_columns; bit-identical).  heatmaps: planar [B,V,J,H,W] fp32/fp16
+    (cl_joints = 0) or channels-last [B,V,H,W,cp] fp32 with cl_joints = J."""
+    if heatmaps.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps.device}")
+    if cl_joints:
+        hm = _cl_input(heatmaps, cl_joints)
+        B, V, H, W, cp = hm.shape
+        J, half, strides = cl_joints, False, (H * W * cp, 1, cp)
+    else:
+        half = heatmaps.dtype == torch.float16
+        hm = heatmaps.contiguous() if half else _dev_f32(heatmaps, "heatmaps")
+        B, V, J, H, W = hm.shape
+        strides = (J * H * W, H * W, 1)
+    X, Y, Z = (int(b) for b in bins)
+    f = flat.to(device=hm.device, dtype=torch.int64).contiguous()
+    if f.dim() != 2 or f.shape[0] != B:
+        raise _lib.FvpError(f"fvp: flat must be [B={B}, K], got {tuple(f.shape)}")
+    K = f.shape[1]
+    g = im = None
+    if packed_grids is not None:
+        pg = _dev_f32(packed_grids, "packed_grids")
+        if pg.dim() == 3:
+            pg = pg.unsqueeze(0)
+        if pg.shape[1:] != (X * Y * Z, grid_slots(V), 2):
+            raise _lib.FvpError(f"fvp: packed grid {tuple(pg.shape)} does not match V={V}, bins={X, Y, Z}")
+        S, cm, rt = pg.shape[0], None, None
+    else:
+        if cams is None or resize_t is None:
+            raise _lib.FvpError("fvp: voxel_columns needs packed_grids, or cams and resize_t")
+        pg = None
+        cm = _dev_f32(cams, "cams")
+        if cm.dim() == 2:
+            cm = cm.unsqueeze(0)
+        if cm.shape[1] != V:
+            raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
+        S, rt = cm.shape[0], _dev_f32(resize_t, "resize_transform")
+        g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
+        im = ImageSpec(ori_max, img_w, img_h, W, H)
+    gi = _grid_index(grid_index, B, S, hm.device)
+    out = torch.empty((B, K, J, Z), dtype=torch.float32, device=hm.device)
+    if out.numel() == 0:
+        return out
+    _lib.call("fvp_voxel_columns", _ptr(hm), int(half), strides[0], strides[1], strides[2], B, V, J, H, W,
+              _ptr(pg) if pg is not None else None, _ptr(cm) if cm is not None else None,
+              _ptr(rt) if rt is not None else None, g, im, _ptr(gi), X, Y, Z, _ptr(f), K, _ptr(out), _stream(hm))
+    return out
+
+
+@voxel_columns.register_fake
+def _(heatmaps, cl_joints, packed_grids, cams, grid_index, resize_t, start, end, center, bins, ori_max, img_w, img_h,
+      flat):
+    J = cl_joints if cl_joints else heatmaps.shape[2]
+    return heatmaps.new_empty((heatmaps.shape[0], flat.shape[1], J, int(bins[2])), dtype=torch.float32)
+
+
 @torch.library.custom_op("fvp::gather_bbox", mutates_args=(), device_types="cuda")
 def gather_bbox(size: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
     s = _dev_f32(size, "bbox_preds")

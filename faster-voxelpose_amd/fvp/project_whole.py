@@ -179,6 +179,24 @@ class ProjectLayer(nn.Module):
             return ops.voxelize_cl(cl.t, cl.J, grids, index, X, Y, Z, want_cube, want_xy)
         return ops.voxelize(heatmaps, grids, index, X, Y, Z, want_cube, want_xy)
 
+    def columns(self, heatmaps, meta, cameras, resize_transform, flat):
+        """columns[b,k,j,:] = forward_fused(...)[0][b,j,flat[b,k],:] -- the z-columns
+        at the proposals (human_detection_net.py:199-200) recomputed for the K
+        winners only, bit-identical, so the cube need not be written."""
+        X, Y, Z = _as_list3(self.voxels_per_axis, int)
+        cl = channels_last_of(heatmaps)
+        src, J = (cl.t, cl.J) if cl is not None else (heatmaps, 0)
+        if self._project_on_the_fly(heatmaps.shape[1]):
+            cams, index = self._cams_for_batch(heatmaps, meta, cameras)
+            start, end, center, nb = self.grid_spec()
+            rt = resize_transform.to(device=heatmaps.device, dtype=torch.float32)
+            return ops.voxel_columns(src, J, None, cams, index, rt, start, end, center, nb,
+                                     float(max(self.ori_image_size[0], self.ori_image_size[1])),
+                                     float(self.image_size[0]), float(self.image_size[1]), flat)
+        grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
+        return ops.voxel_columns(src, J, grids, None, index, None, [0.0] * 3, [0.0] * 3, [0.0] * 3, [X, Y, Z],
+                                 0.0, 0.0, 0.0, flat)
+
     def _empty(self, heatmaps, X, want_cube, want_xy):
         _, Y, Z = _as_list3(self.voxels_per_axis, int)
         J = heatmaps.shape[2]

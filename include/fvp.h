@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 10
+#define FVP_ABI_VERSION 11
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -189,6 +189,22 @@ int fvp_nms_topk_columns(const float *prob, int B, int X, int Y, long long frame
  * Replaces the torch.gather at lib/models/human_detection_net.py:199-200. */
 int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z,
                        const int64_t *flat, int K, float *columns, void *stream);
+
+/* The same z-columns recomputed from the heatmaps for the K winners only, so
+ * a caller that needs the cube just for them (HumanDetectionNet.forward,
+ * human_detection_net.py:162-200) can run fvp_voxelize without the cube:
+ * bit-identical to fvp_gather_columns on the cube fvp_voxelize (packed_grids
+ * != NULL) or fvp_voxelize_cams (packed_grids == NULL: cams, resize_t, grid,
+ * img as there) would write.  Heatmaps are read in place through strides, in
+ * elements: planar [B][V][J][H][W] -> (J*H*W, H*W, 1), channels-last
+ * [B][V][H][W][cp] -> (H*W*cp, 1, cp) (from the first joint's element);
+ * half = fp16 heatmaps.  columns device [B][K][J][Z] (NaN for an index
+ * outside the map). */
+int fvp_voxel_columns(const void *heatmaps, int half, long long view_stride, long long joint_stride,
+                      int pix_stride, int B, int V, int J, int H, int W, const float *packed_grids,
+                      const float *cams, const float *resize_t, const fvp_grid_spec *grid,
+                      const fvp_image_spec *img, const int32_t *grid_index, int X, int Y, int Z,
+                      const int64_t *flat, int K, float *columns, void *stream);
 
 /* bbox sizes at the top-K: out[b,k,c] = size[b,c,flat[b,k]] (c = 0,1; NaN for an index outside the map)
  * Replaces the torch.gather at lib/models/human_detection_net.py:191-192. */

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 10
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 11
     assert lib.fvp_status_string(0) == b"success"
 
 
@@ -66,6 +66,10 @@ def test_argument_validation_without_gpu():
     bad = _lib.PersonSpec((253, 253, 64), (0.03,) * 3, (0,) * 3, (8000,) * 3, (2000,) * 3, (64, 64, 32))
     assert lib.fvp_person_planes(1, 1, 5, 15, 128, 240, 1, bad, 1, None, 1, None, 1, None, 1, 1 << 30, None) == 1002
     assert lib.fvp_gather_columns(None, 1, 1, 1, 1, 1, None, 1, None, None) == 1001
+    vc = lib.fvp_voxel_columns  # (hm, half, strides x3, B, V, J, H, W, grids, cams, rt, grid, img, gi, X, Y, Z, flat, K, cols)
+    assert vc(None, 0, 1, 1, 1, 1, 5, 15, 128, 240, 1, None, None, None, None, None, 80, 80, 20, 1, 10, 1, None) == 1001
+    assert vc(1, 0, 1, 1, 1, 1, 0, 15, 128, 240, 1, None, None, None, None, None, 80, 80, 20, 1, 10, 1, None) == 1002
+    assert vc(1, 0, 1, 1, 1, 1, 5, 15, 128, 240, None, None, None, None, None, None, 80, 80, 20, 1, 10, 1, None) == 1001
     # split-K scratch: CenterNet's 20x20 128->128 level at 8 frames (200 blocks, 72 K-chunks -> 3-way)
     assert lib.fvp_conv2d_workspace_bytes(8, 20, 20, 128, 3, 3, 128, 0, 0) == 3 * 3200 * 128 * 4
     assert lib.fvp_conv2d_workspace_bytes(120, 64, 64, 32, 3, 3, 32, 0, 0) == 0  # enough blocks: no split

@@ -225,7 +225,12 @@ __global__ __launch_bounds__(256) void weight_net_kernel(const float *__restrict
                 const f32x2 scv = {sc, sc}, shv = {sh, sh};
                 v[0] = v[0] * scv + shv;
                 v[1] = v[1] * scv + shv;
-                const float m = nanmax(nanmax(v[0][0], v[0][1]), nanmax(v[1][0], v[1][1]));
+                // the 2x2 pool as two v_maximum3_f32 (IEEE maximum: NaN propagates as
+                // in max_pool2d; +0 / -0 may differ from torch's pick, which the ReLU
+                // and the +0-started sum below make invisible)
+                const float m = __builtin_elementwise_maximum(
+                    __builtin_elementwise_maximum(v[0][0], v[0][1]),
+                    __builtin_elementwise_maximum(v[1][0], v[1][1]));
                 acc[c] += m < 0.0f ? 0.0f : m;  // ReLU after the pool; NaN passes through as in torch
             }
         }

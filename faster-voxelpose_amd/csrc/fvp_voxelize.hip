@@ -570,9 +570,9 @@ __global__ __launch_bounds__(256) void voxel_columns_kernel(const T *__restrict_
 #pragma unroll
         for (int q = 0; q < 6; ++q) rt[q] = src.resize_t[q];
     }
-    // cameras in groups of 8: all coordinates, then all 32 taps in flight, then
+    // cameras in groups of G: all coordinates, then all 4G taps in flight, then
     // the sums in view order (the latency of one group instead of one per camera)
-    constexpr int G = 8;
+    constexpr int G = OTF ? 4 : 8;  // (OTF: 21 floats of camera record per camera in registers)
     float acc = 0.0f, blk = 0.0f;
     for (int v0 = 0; v0 < V; v0 += G) {
         float tv[G][4], w[G][4];

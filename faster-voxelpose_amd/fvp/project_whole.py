@@ -13,6 +13,8 @@ Registers no parameters or buffers, so checkpoints load unchanged.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -33,6 +35,13 @@ def _as_list3(v, kind=float):
     if isinstance(v, (int, float)):
         return [kind(v)] * 3
     return [kind(x) for x in v]
+
+
+# ProjectLayer.columns: project the winners' voxels from the camera records even
+# when a packed grid is cached (bit-identical; measured slower at C3 B=8, 15.1
+# vs 11.6 us: the projection's VALU and 21-float records outweigh the round
+# trip it saves), FVP_COLUMNS_ON_THE_FLY=1
+COLUMNS_ON_THE_FLY = os.environ.get("FVP_COLUMNS_ON_THE_FLY", "0") != "0"
 
 
 class ProjectLayer(nn.Module):
@@ -186,7 +195,9 @@ class ProjectLayer(nn.Module):
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         cl = channels_last_of(heatmaps)
         src, J = (cl.t, cl.J) if cl is not None else (heatmaps, 0)
-        if self._project_on_the_fly(heatmaps.shape[1]):
+        if self._project_on_the_fly(heatmaps.shape[1]) or COLUMNS_ON_THE_FLY:
+            # the coordinates projected from the camera records (bit-identical to the
+            # packed grid; their loads do not wait for `flat`)
             cams, index = self._cams_for_batch(heatmaps, meta, cameras)
             start, end, center, nb = self.grid_spec()
             rt = resize_transform.to(device=heatmaps.device, dtype=torch.float32)

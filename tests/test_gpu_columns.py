@@ -45,11 +45,15 @@ def _check(layer, hm, meta, cams, rt, flat, src=None):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cols_otf", [False, True], ids=["cols-grid", "cols-otf"])
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16], ids=["f32", "f16"])
-def test_columns_match_cube_c2(gpu_device, otf, dtype):
-    from fvp import synthetic
+def test_columns_match_cube_c2(gpu_device, otf, dtype, cols_otf, monkeypatch):
+    """The columns' coordinates from the packed grid or projected on the fly
+    (ProjectLayer.columns' default) against the cube of either voxelize path."""
+    from fvp import project_whole, synthetic
 
+    monkeypatch.setattr(project_whole, "COLUMNS_ON_THE_FLY", cols_otf)
     w, layer, cams, seq, rt = _layer(gpu_device, "c2", otf=otf)
     B, K = 3, 10
     hm = synthetic.uniform_heatmaps(w, B, seed=5).to(dtype).to(gpu_device)

@@ -192,6 +192,7 @@ class ProjectLayer(nn.Module):
         """columns[b,k,j,:] = forward_fused(...)[0][b,j,flat[b,k],:] -- the z-columns
         at the proposals (human_detection_net.py:199-200) recomputed for the K
         winners only, bit-identical, so the cube need not be written."""
+        ops.forward_only(heatmaps)
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         cl = channels_last_of(heatmaps)
         src, J = (cl.t, cl.J) if cl is not None else (heatmaps, 0)

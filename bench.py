@@ -44,9 +44,8 @@ def parse():
     ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
                     help="collect FETCH_SIZE/WRITE_SIZE with rocprofv3 child runs (N=1, rank 0)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU-baseline threads (default: OMP_NUM_THREADS = the pool's per-GPU CPU share)")
+                    help="the CPU baseline's pool-share line (default: OMP_NUM_THREADS)")
     ap.add_argument("--graph", choices=["on", "off"], default="off",
                     help="replay the GPU-local part of the step from captured hipGraphs (the collective stays eager)")
     ap.add_argument("--slabs", action="store_true",
@@ -123,20 +122,33 @@ def host_cores():
     return phys, len(os.sched_getaffinity(0))
 
 
-def cpu_baseline_threads(requested):
-    """Threads for the CPU baseline: --cpu-threads, else the pool's per-GPU CPU
-    share (OMP_NUM_THREADS, 16 on the MI355X pool, which forbids more), else
-    every CPU this process may run on."""
-    if requested:
-        return requested
-    env = os.environ.get("OMP_NUM_THREADS", "")
-    if env.isdigit() and int(env) > 0:
-        return int(env)
-    return host_cores()[1]
+def cgroup_cpu_limit():
+    """The cgroup v2 CPU quota of this process ("max" or "<quota> <period>"), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            pass
+    return None
 
 
-def cpu_baseline_run(w, sample_grid_cpu, seconds, threads):
-    """Reference op sequence on the host cores (oracle/torch_cpu.py), bounded."""
+def cpu_quota_cpus(limit):
+    """CPUs' worth of time the quota allows (None when unlimited / unknown)."""
+    if not limit or limit.startswith("max"):
+        return None
+    try:
+        q, per = limit.split()[:2]
+        return int(q) / int(per)
+    except ValueError:
+        return None
+
+
+def cpu_baseline_run(w, sample_grid_cpu, threads, runs=10, warmup=2, budget_s=30.0):
+    """Reference op sequence on the host cores (oracle/torch_cpu.py): `warmup`
+    untimed calls, then the median of `runs` timed calls of 4 frames each
+    (SURVEY.md §8(d)); fewer runs only if one call would blow `budget_s`."""
+    import numpy as np
     import torch
     from fvp import synthetic
     from oracle import torch_cpu
@@ -144,27 +156,47 @@ def cpu_baseline_run(w, sample_grid_cpu, seconds, threads):
     torch.set_num_threads(threads)
     frames = 4
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, frames, first_frame=10_000))
-    torch_cpu.hot_path(hm, sample_grid_cpu, w.voxels_per_axis, w.max_people)  # warm-up
-    done, t0 = 0, time.perf_counter()
-    while True:
+    for _ in range(warmup):
+        t0 = time.perf_counter()
         torch_cpu.hot_path(hm, sample_grid_cpu, w.voxels_per_axis, w.max_people)
-        done += frames
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return done, el
+        one = time.perf_counter() - t0
+    runs = max(3, min(runs, int(budget_s / max(one, 1e-6))))
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        torch_cpu.hot_path(hm, sample_grid_cpu, w.voxels_per_axis, w.max_people)
+        ts.append(time.perf_counter() - t0)
+    return frames / float(np.median(ts)), frames, runs
 
 
-def cpu_baseline(w, sample_grid_cpu, seconds, threads):
+def cpu_baseline(w, sample_grid_cpu, threads_req):
+    """the reference's CPU op order timed on the box's host
+    cores -- at every physical core, at 8 threads (the survey container's
+    count), and at the pool's per-GPU share (OMP_NUM_THREADS).  A cgroup CPU
+    quota is recorded as found; where it caps the process below the physical
+    core count, the all-core line runs at the quota's CPUs instead (more
+    threads than the quota only queue)."""
     phys, avail = host_cores()
-    done, el = cpu_baseline_run(w, sample_grid_cpu, seconds, threads)
-    d8, e8 = cpu_baseline_run(w, sample_grid_cpu, seconds / 2, 8)
-    return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
-            "host_physical_cores": phys, "host_logical_cpus_available": avail,
-            "value_8_threads": d8 / e8,
-            "sample": f"{done} frames of {w.name} in {el:.1f} s on {threads} threads ({d8} frames in {e8:.1f} s on "
-                      f"8 threads): torch-CPU restatement of project_whole.forward (per-frame F.grid_sample, mean, "
-                      f"clamp) + max(dim=4) + nms2D + column gather (oracle/torch_cpu.py), sample grid prebuilt"}
+    limit = cgroup_cpu_limit()
+    quota = cpu_quota_cpus(limit)
+    share = threads_req or (int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit()
+                            else avail)
+    all_cores = min(x for x in (phys or avail, avail, int(quota) if quota else 10 ** 9) if x)
+    lines = {}
+    for tag, th in (("all_cores", all_cores), ("8_threads", 8), ("pool_share", share)):
+        if th in [v["threads"] for v in lines.values()]:
+            lines[tag] = dict(next(v for v in lines.values() if v["threads"] == th))
+            continue
+        fps, frames, runs = cpu_baseline_run(w, sample_grid_cpu, th)
+        lines[tag] = {"threads": th, "frames_per_s": round(fps, 2), "runs": runs}
+    main_line = lines["all_cores"]
+    return {"value": main_line["frames_per_s"], "unit": "frames/s", "cores": main_line["threads"], "kind": "port",
+            "host_physical_cores": phys, "host_logical_cpus_available": avail, "cgroup_cpu_max": limit,
+            "value_8_threads": lines["8_threads"]["frames_per_s"],
+            "value_pool_share": lines["pool_share"]["frames_per_s"], "pool_share_threads": share,
+            "sample": f"{w.name}, 4 frames per call, 2 warm-up calls then the median of {main_line['runs']} timed calls "
+                      f"per thread count: torch-CPU restatement of project_whole.forward (per-frame F.grid_sample, "
+                      f"mean, clamp) + max(dim=4) + nms2D + column gather (oracle/torch_cpu.py), sample grid prebuilt"}
 
 
 def note(msg):
@@ -198,13 +230,19 @@ def main():
     from fvp.proposal import nms2D, nms2D_columns
     from fvp.workloads import WORKLOADS
 
-    local_rank %= max(1, torch.cuda.device_count())  # identity with one rank per GPU
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    # FVP_BENCH_BACKEND=gloo: plumbing rehearsal of N ranks (not a measurement).
+    # FVP_BENCH_BACKEND=gloo: plumbing rehearsal of N ranks that may share a
+    # device (not a measurement; labelled as such).  Otherwise one rank per GPU
+    # over RCCL, and more ranks than GPUs is an error, never a silent wrap.
     # One process group at every N (a one-rank RCCL group when launched without
     # torchrun), so the timed step runs the same all-gather code at N = 1.
     backend = os.environ.get("FVP_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend != "gloo" and (world > ndev or local_rank >= ndev):
+        raise SystemExit(f"bench: {world} ranks (local rank {local_rank}) but {ndev} visible GPU(s); "
+                         f"one rank per GPU (FVP_BENCH_BACKEND=gloo for a shared-device rehearsal)")
+    local_rank %= max(1, ndev)  # (gloo rehearsal only: ranks share devices)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
     pg_kw = {"device_id": dev} if backend == "nccl" else {}
     if world > 1 or "MASTER_ADDR" in os.environ:
         dist.init_process_group(backend, **pg_kw)
@@ -215,6 +253,10 @@ def main():
         # earlier makes the store's cleanup at exit wait forever)
         dist.init_process_group(backend, store=dist.FileStore(store_path, 1), rank=0, world_size=1, **pg_kw)
     grouped = dist.is_initialized()
+    pg_backend = dist.get_backend() if grouped else None
+    collective = {"nccl": "RCCL", "gloo": "gloo"}.get(pg_backend, str(pg_backend))
+    rehearsal = pg_backend == "gloo"
+    n_devices = min(world, ndev) if rehearsal else world  # distinct GPUs doing the work
 
     w = WORKLOADS[args.workload]
     B = args.batch or DEFAULT_BATCH.get(args.workload, 64)
@@ -235,7 +277,9 @@ def main():
     layer.on_the_fly = {"auto": None, "on": True, "off": False}[args.on_the_fly]
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
     # large-frame mode: all ranks hold the same frames (x-slabs); otherwise own frames
-    hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=0 if args.slabs else rank * B)
+    # weak scaling: rank r owns frames shard_frames(world*B, world, r) of the job
+    first = 0 if args.slabs else parallel.shard_frames(world * B, world, rank)[0]
+    hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=first)
     x0, x1 = parallel.shard_slab(X, world, rank) if args.slabs else (0, X)
     hm = torch.from_numpy(hm_host).to(dev)
     if w.dtype == "float16":  # C5: fp16 heatmaps (computed in fp32 by the kernels)
@@ -436,14 +480,14 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
         note("cpu baseline")
         sg_cpu = layer.build_sample_grid(cams, seq, rt, dev).cpu().contiguous()
-        cpu = cpu_baseline(w, sg_cpu, args.cpu_seconds, cpu_baseline_threads(args.cpu_threads))
+        cpu = cpu_baseline(w, sg_cpu, args.cpu_threads)
 
     if rank == 0:
         line = {
             "metric": METRIC,
             "value": round(fps, 1),
             "unit": "frames/s",
-            "n_gpus": world,
+            "n_gpus": n_devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -457,9 +501,11 @@ def main():
                             f"{Hd}x{Wd} heatmaps -> {X}x{Y}x{Z} voxels, K={K} proposals",
                 "frames_per_gpu_step": B,
                 "global_batch": B if args.slabs else world * B,
-                "parallelism": (f"x-slab x{world}" + (" + RCCL all_gather of xy slabs, all_reduce of columns"
-                                                      if world > 1 else "") if args.slabs else
-                                f"frame-sharded x{world}" + (" + RCCL all_gather of proposals" if grouped else "")),
+                "parallelism": ((f"x-slab x{world}" + (f" + {collective} all_gather of xy slabs, all_reduce of columns"
+                                                       if world > 1 else "") if args.slabs else
+                                 f"frame-sharded x{world}" + (f" + {collective} all_gather of proposals" if grouped else ""))
+                                + (f" -- rehearsal (gloo, {world} ranks on {n_devices} shared device(s)), not a measurement"
+                                   if rehearsal else "")),
             },
             "roofline": {
                 "bound": "hbm",

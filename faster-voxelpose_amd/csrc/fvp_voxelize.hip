@@ -335,26 +335,32 @@ struct GatherCfg {
 template <int LPV, bool OTF>
 static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg &c) {
     // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
-    int cols = OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z);
-    // latency (few frames): one pass of 256/LPV voxels per block, so a single
-    // frame spreads over enough blocks to fill the CUs -- or two passes when
-    // one-pass blocks would overflow one round of 8 blocks per CU by a few (C2/C3
-    // B = 1: 2,134 blocks, a tail round of 86; two passes: gather 16.8 -> 14.6 us;
-    // C4 / C5 unchanged, measured with tools/ab_few.sh)
-    if ((long long)frames / NF * ((X * Y + cols - 1) / cols) < 4 * 256) {
-        cols = max(1, (256 / LPV) / Z);
-        if ((long long)frames / NF * ((X * Y + cols - 1) / cols) > 8 * 256) cols = max(1, 2 * (256 / LPV) / Z);
-    }
     // Column groups that tile the x-rows exactly (largest divisor of Y, if it
     // keeps at least half the columns), so the blocks can be walked in bands of
     // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
     // x-y patch, whose heatmap footprint is smaller (C5 -8 %, C4 -4 %, C2 0).
     // Small grids (C1: 400 columns) keep their column groups (measured -6 % with bands).
     const bool big = (long long)X * Y >= 4096;
-    if (big) {
-        int cc = cols;
-        while (cc > 1 && Y % cc != 0) --cc;
-        if (2 * cc >= cols) cols = cc;
+    auto snap = [&](int c) {
+        if (big) {
+            int cc = c;
+            while (cc > 1 && Y % cc != 0) --cc;
+            if (2 * cc >= c) c = cc;
+        }
+        return c;
+    };
+    auto blocks = [&](int c) { return (long long)frames / NF * ((X * Y + c - 1) / c); };
+    int cols = snap(OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z));
+    // latency (few frames): one pass of 256/LPV voxels per block, so a single
+    // frame spreads over enough blocks to fill the CUs -- or two passes when
+    // one-pass blocks would overflow one round of 8 blocks per CU (the counts
+    // compared are those of the snapped column groups actually launched: C2/C3
+    // B = 1, 80x80x20, LPV 4: one pass = 2 columns, 3,200 blocks; two passes =
+    // 5 columns, 1,280 blocks -- 40 of a block's 64 voxel slots busy per pass
+    // at one pass, 100 of 128 at two)
+    if (blocks(cols) < 4 * 256) {
+        cols = snap(max(1, (256 / LPV) / Z));
+        if (blocks(cols) > 8 * 256) cols = snap(max(1, 2 * (256 / LPV) / Z));
     }
     c.cols = cols;
     c.band = (big && Y % cols == 0 && X > kBandRows) ? kBandRows : 0;

@@ -40,12 +40,12 @@ RGB_PITCH = 4  # input channel pitch of conv1 (3 colour channels + one zero)
 class _Block:
     """Bottleneck (3 convs) or BasicBlock (2 convs) with an optional downsample."""
 
-    def __init__(self, blk: nn.Module, dtype):
+    def __init__(self, blk: nn.Module, dtype, algo=None):
         if hasattr(blk, "conv3"):
-            self.convs = [ConvLayer(blk.conv1, blk.bn1, dtype), ConvLayer(blk.conv2, blk.bn2, dtype),
-                          ConvLayer(blk.conv3, blk.bn3, dtype)]
+            self.convs = [ConvLayer(blk.conv1, blk.bn1, dtype, algo=algo), ConvLayer(blk.conv2, blk.bn2, dtype, algo=algo),
+                          ConvLayer(blk.conv3, blk.bn3, dtype, algo=algo)]
         elif hasattr(blk, "conv2"):
-            self.convs = [ConvLayer(blk.conv1, blk.bn1, dtype), ConvLayer(blk.conv2, blk.bn2, dtype)]
+            self.convs = [ConvLayer(blk.conv1, blk.bn1, dtype, algo=algo), ConvLayer(blk.conv2, blk.bn2, dtype, algo=algo)]
         else:
             raise _lib.FvpError(f"FvpPoseResNet: unsupported block {type(blk).__name__}")
         self.down = None
@@ -53,7 +53,7 @@ class _Block:
             ds = list(blk.downsample.children())
             if not (len(ds) == 2 and isinstance(ds[0], nn.Conv2d) and isinstance(ds[1], nn.BatchNorm2d)):
                 raise _lib.FvpError("FvpPoseResNet: downsample must be Sequential(Conv2d, BatchNorm2d)")
-            self.down = ConvLayer(ds[0], ds[1], dtype)
+            self.down = ConvLayer(ds[0], ds[1], dtype, algo=algo)
 
     def __call__(self, x: Act) -> Act:
         residual = x if self.down is None else self.down(x, relu=False)
@@ -77,7 +77,7 @@ class FvpPoseResNet:
     bf16 activations between the layers (opt-in precision).  Weights are read once at construction;
     rebuild after loading a new state_dict."""
 
-    def __init__(self, module: nn.Module, dtype=torch.float32):
+    def __init__(self, module: nn.Module, dtype=torch.float32, algo: int | None = None):
         if dtype not in (torch.float32, torch.bfloat16):
             raise _lib.FvpError(f"FvpPoseResNet: dtype {dtype} (float32 or bfloat16)")
         if module.training:
@@ -85,7 +85,7 @@ class FvpPoseResNet:
         self.module, self.dtype = module, dtype
         if module.conv1.in_channels > RGB_PITCH:
             raise _lib.FvpError(f"FvpPoseResNet: {module.conv1.in_channels} input channels (RGB expected)")
-        self.stem = ConvLayer(module.conv1, module.bn1, dtype, cpi=RGB_PITCH)
+        self.stem = ConvLayer(module.conv1, module.bn1, dtype, cpi=RGB_PITCH, algo=algo)
         # bf16: the 7x7/s2/p3 -> 64 stem runs its own kernel straight from the
         # NCHW images (fvp_conv_stem7_bf16), weights packed [64][7][8][4]
         c1 = module.conv1
@@ -102,7 +102,7 @@ class FvpPoseResNet:
         if mp.ceil_mode or (mp.dilation not in (1, (1, 1))):
             raise _lib.FvpError("FvpPoseResNet: max pool must be floor mode without dilation")
         self.pool = (k, s, p)
-        self.blocks = [_Block(b, dtype) for name in ("layer1", "layer2", "layer3", "layer4")
+        self.blocks = [_Block(b, dtype, algo) for name in ("layer1", "layer2", "layer3", "layer4")
                        for b in getattr(module, name).children()]
         mods = list(module.deconv_layers.children())
         self.deconvs = []
@@ -112,9 +112,9 @@ class FvpPoseResNet:
             if not (isinstance(conv, nn.ConvTranspose2d) and isinstance(bn, nn.BatchNorm2d)
                     and isinstance(act, nn.ReLU)):
                 raise _lib.FvpError("FvpPoseResNet: deconv head must be (ConvTranspose2d, BatchNorm2d, ReLU)*")
-            self.deconvs.append(ConvLayer(conv, bn, dtype))
+            self.deconvs.append(ConvLayer(conv, bn, dtype, algo=algo))
             i += 3
-        self.final = ConvLayer(module.final_layer, None, dtype)
+        self.final = ConvLayer(module.final_layer, None, dtype, algo=algo)
         self.num_joints = module.final_layer.out_channels
         # bf16: activations between the layers stay bf16 in HBM (half the bytes,
         # no per-chunk conversion), the stem's output and its max pool included;
@@ -188,11 +188,11 @@ class FvpPoseResNet:
         return total
 
 
-def cached(module: nn.Module, dtype=torch.float32) -> FvpPoseResNet:
+def cached(module: nn.Module, dtype=torch.float32, algo: int | None = None) -> FvpPoseResNet:
     """FvpPoseResNet for ``module``, rebuilt whenever its parameters or buffers change."""
-    sig = (dtype,) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
+    sig = (dtype, algo) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
     hit = getattr(module, "_fvp_backbone", None)
     if hit is None or hit[0] != sig:
-        hit = (sig, FvpPoseResNet(module, dtype))
+        hit = (sig, FvpPoseResNet(module, dtype, algo))
         object.__setattr__(module, "_fvp_backbone", hit)
     return hit[1]

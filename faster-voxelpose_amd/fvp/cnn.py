@@ -18,7 +18,6 @@ one fused launch.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
 
@@ -29,26 +28,16 @@ from . import _lib
 from .ops import _ptr, _stream
 
 
-# Kernel selection passed to fvp_conv2d_nhwc_ws (include/fvp.h FVP_CONV_*):
-# AUTO in the product; tests run every choice through conv_algo().  CONV_DMA
-# (host side only) runs every eligible fp32 layer on the LDS-DMA kernel
-# (FVP_CONV_F32_KC); AUTO picks it for the launches that fill the chip.
-CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA = 0, 1, 2, 3, 4
-CONV_ALGO = CONV_AUTO
-# AUTO may pick the fp32 LDS-DMA kernel (FVP_F32_DMA=0: A/B against the [Krows][Cpo_w] kernels)
-F32_DMA_AUTO = os.environ.get("FVP_F32_DMA", "1") != "0"
+# Kernel selection passed to fvp_conv2d_nhwc_ws (include/fvp.h FVP_CONV_*),
+# fixed per compiled layer (``algo`` of ConvLayer / FvpCNN / FvpPoseResNet /
+# cached): AUTO in the product; the tests build layers with every choice.
+# CONV_DMA (host side only) runs every eligible fp32 layer on the LDS-DMA
+# kernel (FVP_CONV_F32_KC); AUTO picks it for the launches that fill the chip;
+# CONV_AUTO_NO_DMA is AUTO without it (the A/B arm against the [Krows][Cpo_w]
+# kernels; FVP_F32_DMA=0 makes it the default of layers built without ``algo``).
+CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA, CONV_AUTO_NO_DMA = 0, 1, 2, 3, 4, 5
+DEFAULT_ALGO = CONV_AUTO if os.environ.get("FVP_F32_DMA", "1") != "0" else CONV_AUTO_NO_DMA
 FVP_CONV_F32_KC = 8
-
-
-@contextlib.contextmanager
-def conv_algo(algo: int):
-    """Launch the fp32 convolutions inside the block with kernel choice `algo` (process-wide)."""
-    global CONV_ALGO
-    prev, CONV_ALGO = CONV_ALGO, algo
-    try:
-        yield
-    finally:
-        CONV_ALGO = prev
 
 
 _CUS = {}
@@ -95,8 +84,11 @@ class ConvLayer:
     Cin rounded up to 16; 4 / 8 / 12 for a network's RGB input).  dtype
     torch.bfloat16: bf16 operands, fp32 accumulation (opt-in precision)."""
 
-    def __init__(self, conv, bn=None, dtype=torch.float32, cpi: int | None = None):
+    def __init__(self, conv, bn=None, dtype=torch.float32, cpi: int | None = None, algo: int | None = None):
         dev = conv.weight.device
+        self.algo = DEFAULT_ALGO if algo is None else int(algo)
+        if self.algo not in (CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA, CONV_AUTO_NO_DMA):
+            raise _lib.FvpError(f"ConvLayer: kernel choice {algo}")
         w = conv.weight.detach().float()
         if isinstance(conv, (nn.Conv1d, nn.ConvTranspose1d)):  # 1-D: rows of height 1, kernel (1, k)
             w = w.unsqueeze(2)
@@ -152,7 +144,7 @@ class ConvLayer:
         if krows > taps * self.Cpi:  # K rounded up to whole 16-row chunks (zero rows)
             pack = torch.cat([pack, pack.new_zeros((self.G, krows - taps * self.Cpi, self.Cpo_w))], dim=1)
         self.wpack = pack.contiguous()
-        self._ws = {}  # (N, H, W, algo) -> split-K scratch bytes
+        self._ws = {}  # (N, H, W) -> (split-K scratch bytes, LDS-DMA kernel)
         self.bf16 = dtype == torch.bfloat16
         self.act_bf16 = False  # bf16 operands only: write the output (and read residuals) as bf16
         if self.bf16:  # [G][Cpo_w][Krows], k contiguous (rows past the taps zero)
@@ -198,7 +190,7 @@ class ConvLayer:
         if self.bf16:  # FVP_CONV_BF16 | _IN | _OUT (include/fvp.h)
             flags = 1 | (2 if x.t.dtype == torch.bfloat16 else 0) | (4 if odt == torch.bfloat16 else 0)
             wp = self.wpack_bf16
-        key = (x.N, x.H, x.W, CONV_ALGO)
+        key = (x.N, x.H, x.W)
         if key not in self._ws:  # (split-K scratch bytes, LDS-DMA kernel) of this input size
             self._ws[key] = self._plan(x)
         nws, dma = self._ws[key]
@@ -211,20 +203,24 @@ class ConvLayer:
                   _ptr(wp), self.KH, self.KW, self.Cpo, self.Cpo_w,
                   _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
                   _ptr(res_post.t) if res_post else None, int(relu), *self.geom(), flags,
-                  CONV_AUTO if CONV_ALGO == CONV_DMA else CONV_ALGO, _ptr(out), _ptr(ws), nws, _stream(out))
+                  self._abi_algo(), _ptr(out), _ptr(ws), nws, _stream(out))
         return Act(out, self.Cout)
 
+    def _abi_algo(self) -> int:
+        """The FVP_CONV_* value the C ABI takes (the DMA choices are made here on the host)."""
+        return CONV_AUTO if self.algo in (CONV_DMA, CONV_AUTO_NO_DMA) else self.algo
+
     def _plan(self, x: Act) -> tuple[int, bool]:
-        """(split-K scratch bytes, use the fp32 LDS-DMA kernel) for input x under CONV_ALGO."""
+        """(split-K scratch bytes, use the fp32 LDS-DMA kernel) for input x under self.algo."""
         if self.bf16:
             return 0, False
-        dma = hasattr(self, "wpack_kc") and (CONV_ALGO == CONV_DMA or (CONV_ALGO == CONV_AUTO and F32_DMA_AUTO))
+        dma = hasattr(self, "wpack_kc") and self.algo in (CONV_DMA, CONV_AUTO)
         if dma:  # the kernel's limits (fvp.h FVP_CONV_F32_KC): 32-bit offsets, row decode
             Ho, Wo = self.out_hw(x.H, x.W)
             M = x.N * (x.H * x.W if self.mode else Ho * Wo)
             dma = (M < 1 << 24 and x.N * x.H * x.W * x.Cp * 4 < 1 << 31
                    and self.wpack_kc.numel() // self.G * 4 < 1 << 31)
-            if dma and CONV_ALGO == CONV_AUTO:
+            if dma and self.algo == CONV_AUTO:
                 # measured on ResNet-50 at 40 x 960 x 512 and the P2PNet / CenterNet
                 # layers (profiles/round2/conv_f32_dma): the DMA kernel wins wherever its
                 # launch fills the chip (no split-K) and has 64+ columns (the 15-joint
@@ -243,9 +239,8 @@ class ConvLayer:
                 dma = ncols >= 64 and blocks >= 256 and (not same or fill >= 0.7)
         if dma:
             return 0, True
-        algo = CONV_AUTO if CONV_ALGO == CONV_DMA else CONV_ALGO
         return _lib.load().fvp_conv2d_ex_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo,
-                                                         *self.geom(), algo), False
+                                                         *self.geom(), self._abi_algo()), False
 
     def flops(self, x: Act) -> int:
         Ho, Wo = self.out_hw(x.H, x.W)
@@ -291,7 +286,7 @@ _CONVS = (nn.Conv2d, nn.ConvTranspose2d, nn.Conv1d, nn.ConvTranspose1d)
 _BNS = (nn.BatchNorm2d, nn.BatchNorm1d)
 
 
-def _seq_convs(seq: nn.Sequential, dtype=torch.float32):
+def _seq_convs(seq: nn.Sequential, dtype=torch.float32, algo: int | None = None):
     """[Conv(, BN)(, ReLU)]* of an nn.Sequential -> [(ConvLayer, relu)]."""
     mods = list(seq.children())
     out, i = [], 0
@@ -302,7 +297,7 @@ def _seq_convs(seq: nn.Sequential, dtype=torch.float32):
         bn = mods[i + 1] if i + 1 < len(mods) and isinstance(mods[i + 1], _BNS) else None
         j = i + 1 + (bn is not None)
         relu = j < len(mods) and isinstance(mods[j], nn.ReLU)
-        out.append((ConvLayer(m, bn, dtype), relu))
+        out.append((ConvLayer(m, bn, dtype, algo=algo), relu))
         i = j + relu
     return out
 
@@ -310,8 +305,8 @@ def _seq_convs(seq: nn.Sequential, dtype=torch.float32):
 class _Plan:
     """A compiled module: call(x: Act) -> Act."""
 
-    def __init__(self, m: nn.Module, dtype=torch.float32, dim: int = 2):
-        self.dtype, self.dim = dtype, dim
+    def __init__(self, m: nn.Module, dtype=torch.float32, dim: int = 2, algo: int | None = None):
+        self.dtype, self.dim, self.algo = dtype, dim, algo
         self.kind, self.parts = self._compile(m)
 
     def layers(self):
@@ -329,23 +324,23 @@ class _Plan:
 
     def _compile(self, m):
         if hasattr(m, "res_branch"):  # Res2DBlock (cnns_2d.py:32-64) / Res1DBlock (cnns_1d.py:37-74)
-            (c1, r1), (c2, _) = _seq_convs(m.res_branch, self.dtype)
-            skip = _seq_convs(m.skip_con, self.dtype) if len(list(m.skip_con.children())) else []
+            (c1, r1), (c2, _) = _seq_convs(m.res_branch, self.dtype, self.algo)
+            skip = _seq_convs(m.skip_con, self.dtype, self.algo) if len(list(m.skip_con.children())) else []
             return "res", (c1, c2, skip[0][0] if skip else None)
         if hasattr(m, "pool_size"):  # Pool2DBlock
             assert m.pool_size == 2
             return "pool", None
         if hasattr(m, "block"):  # Basic2DBlock / Upsample2DBlock: Sequential(conv, BN, ReLU)
-            return "seq", _seq_convs(m.block, self.dtype)
+            return "seq", _seq_convs(m.block, self.dtype, self.algo)
         if hasattr(m, "encoder_pool1") and hasattr(m, "skip_res1"):  # EncoderDecorder (:123-183)
             names = ["skip_res1", "encoder_pool1", "encoder_res1", "skip_res2", "encoder_pool2", "encoder_res2",
                      "mid_res", "decoder_res2", "decoder_upsample2", "decoder_res1", "decoder_upsample1"]
-            return "encdec", {n: _Plan(getattr(m, n), self.dtype, self.dim) for n in names}
+            return "encdec", {n: _Plan(getattr(m, n), self.dtype, self.dim, self.algo) for n in names}
         if isinstance(m, nn.Sequential):
             kids = list(m.children())
             if kids and all(isinstance(k, _CONVS + _BNS + (nn.ReLU,)) for k in kids):
-                return "seq", _seq_convs(m, self.dtype)
-            return "chain", [_Plan(k, self.dtype, self.dim) for k in kids]
+                return "seq", _seq_convs(m, self.dtype, self.algo)
+            return "chain", [_Plan(k, self.dtype, self.dim, self.algo) for k in kids]
         raise TypeError(f"FvpCNN: unsupported module {type(m).__name__}")
 
     def __call__(self, x: Act, res_post: Act | None = None) -> Act:
@@ -390,8 +385,9 @@ class FvpCNN:
     after its ``torch.max(x, dim=4)``, cnns_2d.py:291-295).  Weights are read
     once at construction; rebuild after loading a new state_dict."""
 
-    def __init__(self, module: nn.Module, dtype=torch.float32):
-        """dtype torch.bfloat16: bf16 operands with fp32 accumulation (opt-in; ~1e-2 relative)."""
+    def __init__(self, module: nn.Module, dtype=torch.float32, algo: int | None = None):
+        """dtype torch.bfloat16: bf16 operands with fp32 accumulation (opt-in; ~1e-2 relative);
+        algo: the fp32 kernel choice of every layer (CONV_*; default AUTO)."""
         if dtype not in (torch.float32, torch.bfloat16):
             raise _lib.FvpError(f"FvpCNN: dtype {dtype} (float32 or bfloat16)")
         if module.training:
@@ -399,23 +395,23 @@ class FvpCNN:
         self.module = module
         if isinstance(getattr(module, "output_hm", None), nn.Conv1d):  # C2CNet (cnns_1d.py:182-241)
             self.kind = "c2c"
-            self.front = _Plan(module.front_layers, dtype, dim=1)
-            self.encdec = _Plan(module.encoder_decoder, dtype, dim=1)
-            self.out = ConvLayer(module.output_hm, None, dtype)
+            self.front = _Plan(module.front_layers, dtype, dim=1, algo=algo)
+            self.encdec = _Plan(module.encoder_decoder, dtype, dim=1, algo=algo)
+            self.out = ConvLayer(module.output_hm, None, dtype, algo=algo)
         elif hasattr(module, "output_hm") and hasattr(module, "output_size"):  # CenterNet
             self.kind = "centernet"
-            self.front = _Plan(module.front_layers, dtype)
-            self.encdec = _Plan(module.encoder_decoder, dtype)
-            self.hm = _seq_convs(module.output_hm, dtype)
-            self.size = _seq_convs(module.output_size, dtype)
+            self.front = _Plan(module.front_layers, dtype, algo=algo)
+            self.encdec = _Plan(module.encoder_decoder, dtype, algo=algo)
+            self.hm = _seq_convs(module.output_hm, dtype, algo)
+            self.size = _seq_convs(module.output_size, dtype, algo)
         elif hasattr(module, "output_layer"):  # P2PNet
             self.kind = "p2p"
-            self.front = _Plan(module.front_layers, dtype)
-            self.encdec = _Plan(module.encoder_decoder, dtype)
-            self.out = ConvLayer(module.output_layer, None, dtype)
+            self.front = _Plan(module.front_layers, dtype, algo=algo)
+            self.encdec = _Plan(module.encoder_decoder, dtype, algo=algo)
+            self.out = ConvLayer(module.output_layer, None, dtype, algo=algo)
         else:
             self.kind = "plain"
-            self.plan = _Plan(module, dtype)
+            self.plan = _Plan(module, dtype, algo=algo)
         self.front7 = None
         if dtype == torch.bfloat16 and self.kind != "plain":
             # bf16 activations between the layers (half the bytes, no per-chunk
@@ -530,12 +526,13 @@ class FvpWeightNet:
         return out
 
 
-def cached(module: nn.Module, dtype=torch.float32):
+def cached(module: nn.Module, dtype=torch.float32, algo: int | None = None):
     """FvpCNN (or FvpWeightNet) for ``module``, rebuilt whenever its parameters
-    or buffers change (storage or in-place version), e.g. after load_state_dict."""
-    sig = (dtype,) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
+    or buffers change (storage or in-place version), e.g. after load_state_dict,
+    or the precision / kernel choice asked for differs."""
+    sig = (dtype, algo) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
     hit = getattr(module, "_fvp_cnn", None)
     if hit is None or hit[0] != sig:
-        hit = (sig, FvpWeightNet(module) if hasattr(module, "heatmap_feature_net") else FvpCNN(module, dtype))
+        hit = (sig, FvpWeightNet(module) if hasattr(module, "heatmap_feature_net") else FvpCNN(module, dtype, algo))
         object.__setattr__(module, "_fvp_cnn", hit)
     return hit[1]

@@ -35,9 +35,9 @@ work as before.
 """
 from __future__ import annotations
 
-import sys
-
+import dataclasses
 import os
+import sys
 
 import torch
 
@@ -45,18 +45,57 @@ from . import backbone as fvp_backbone
 from . import cnn as fvp_cnn
 from . import jln, project_individual, project_whole, proposal
 
-USE_FVP_CNN = False  # set by install(cnn=True)
-FVP_CNN_DTYPE = torch.float32
-USE_FVP_BACKBONE = False  # set by install(backbone=True)
-# fused_hdn_forward: write no cube and recompute the K winners' z-columns from the
-# heatmaps instead (fvp_voxel_columns, bit-identical to gathering them from the
-# cube).  None = when the batch's cube would exceed RECOMPUTE_CUBE_BYTES (a
-# memory saving: the TD-bound gather hides the cube writes, so below that the
-# one-launch NMS + column gather is as fast or faster).
-_env = os.environ.get("FVP_RECOMPUTE_COLUMNS")
-RECOMPUTE_COLUMNS = None if _env is None else _env != "0"
-RECOMPUTE_CUBE_BYTES = 512 << 20
-FVP_BACKBONE_DTYPE = torch.float32
+
+def _env_recompute():
+    v = os.environ.get("FVP_RECOMPUTE_COLUMNS")
+    return None if v is None else v != "0"
+
+
+@dataclasses.dataclass(frozen=True)
+class FvpOptions:
+    """How the fused forwards run, per model (no process-wide switches).
+
+    install() attaches one to the classes it patches; set_options(model, ...)
+    gives one model (and every submodule) its own; a forward reads the
+    options of the module it runs on (``options_of``), so two models in one
+    process can differ.
+
+    cnn / cnn_dtype: in eval mode run CenterNet, C2CNet, P2PNet on the fvp MFMA
+      convolutions (fvp/cnn.py) and WeightNet as one fused launch; bf16 =
+      bf16 operands with fp32 accumulation (opt-in, ~1e-2 relative).
+    backbone / backbone_dtype: the same for the PoseResNet backbone.
+    recompute_columns: fused_hdn_forward writes no cube and recomputes the K
+      winners' z-columns from the heatmaps (fvp_voxel_columns, bit-identical to
+      gathering them from the cube); None = only when the batch's cube would
+      exceed recompute_cube_bytes (a memory saving: the TD-bound gather hides
+      the cube writes, so below that the one-launch NMS + column gather is as
+      fast or faster).  Default from the environment variable
+      FVP_RECOMPUTE_COLUMNS (0 / 1) when set."""
+    cnn: bool = False
+    cnn_dtype: torch.dtype = torch.float32
+    backbone: bool = False
+    backbone_dtype: torch.dtype = torch.float32
+    recompute_columns: bool | None = dataclasses.field(default_factory=_env_recompute)
+    recompute_cube_bytes: int = 512 << 20
+
+
+DEFAULT_OPTIONS = FvpOptions()
+
+
+def options_of(module) -> FvpOptions:
+    """The FvpOptions a fused forward on `module` uses (its own, its class's, or the defaults)."""
+    opts = getattr(module, "fvp_options", None)
+    return opts if isinstance(opts, FvpOptions) else DEFAULT_OPTIONS
+
+
+def set_options(model, **changes) -> FvpOptions:
+    """Give `model` and every submodule (an nn.Module's modules(); or just the
+    object) its own options: the current ones with `changes` applied.  No
+    parameters or buffers are added, so state_dict is unchanged."""
+    opts = dataclasses.replace(options_of(model), **changes)
+    for m in (model.modules() if hasattr(model, "modules") else [model]):
+        object.__setattr__(m, "fvp_options", opts)  # plain attribute (not a submodule / parameter)
+    return opts
 
 
 def install(fused: bool = True, modules=None, cnn: bool = False, backbone: bool = False) -> dict:
@@ -66,12 +105,11 @@ def install(fused: bool = True, modules=None, cnn: bool = False, backbone: bool 
     C2CNet and P2PNet on the fvp MFMA convolutions (fvp/cnn.py) instead of
     torch's, in fp32, and WeightNet as one fused launch; cnn="bf16": bf16
     operands with fp32 accumulation for the MFMA convolutions (opt-in, ~1e-2
-    relative).  backbone=True / "bf16": the same for the PoseResNet backbone."""
-    global USE_FVP_CNN, FVP_CNN_DTYPE, USE_FVP_BACKBONE, FVP_BACKBONE_DTYPE
-    USE_FVP_CNN = bool(cnn)
-    FVP_CNN_DTYPE = torch.bfloat16 if cnn == "bf16" else torch.float32
-    USE_FVP_BACKBONE = bool(backbone)
-    FVP_BACKBONE_DTYPE = torch.bfloat16 if backbone == "bf16" else torch.float32
+    relative).  backbone=True / "bf16": the same for the PoseResNet backbone.
+    These become the FvpOptions of the patched classes (per-model overrides:
+    set_options)."""
+    opts = FvpOptions(cnn=bool(cnn), cnn_dtype=torch.bfloat16 if cnn == "bf16" else torch.float32,
+                      backbone=bool(backbone), backbone_dtype=torch.bfloat16 if backbone == "bf16" else torch.float32)
     mods = modules if modules is not None else sys.modules
     patched = {}
 
@@ -81,6 +119,13 @@ def install(fused: bool = True, modules=None, cnn: bool = False, backbone: bool 
             setattr(m, attr, value)
             patched[f"{modname}.{attr}"] = value
 
+    for modname, cls in (("models.human_detection_net", "HumanDetectionNet"),
+                         ("models.joint_localization_net", "JointLocalizationNet"),
+                         ("models.resnet", "ResNet"), ("models.faster_voxelpose", "FasterVoxelPoseNet")):
+        m = mods.get(modname)
+        if m is not None and hasattr(m, cls):
+            getattr(m, cls).fvp_options = opts
+            patched[f"{modname}.{cls}.fvp_options"] = opts
     setattr_if("models.project_whole", "ProjectLayer", project_whole.ProjectLayer)
     setattr_if("models.human_detection_net", "ProjectLayer", project_whole.ProjectLayer)
     setattr_if("models.project_individual", "ProjectLayer", project_individual.ProjectLayer)
@@ -118,11 +163,11 @@ def install(fused: bool = True, modules=None, cnn: bool = False, backbone: bool 
     return patched
 
 
-def center_net_from_xy(center_net, xy: torch.Tensor):
+def center_net_from_xy(center_net, xy: torch.Tensor, opts: FvpOptions = DEFAULT_OPTIONS):
     """CenterNet.forward (cnns_2d.py:280-295) minus its first line, fed with
     the xy max-plane the voxelize kernel already produced."""
-    if USE_FVP_CNN and not center_net.training:
-        return fvp_cnn.cached(center_net, FVP_CNN_DTYPE).from_xy(xy)
+    if opts.cnn and not center_net.training:
+        return fvp_cnn.cached(center_net, opts.cnn_dtype).from_xy(xy)
     x = center_net.front_layers(xy)
     x = center_net.encoder_decoder(x)
     return center_net.output_hm(x), center_net.output_size(x)
@@ -135,26 +180,27 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     proposal_heatmaps_1d [B,K,Z], proposal_centers [B,K,7], bbox_preds [B,X*Y,2]).
     """
     batch_size = heatmaps.shape[0]
+    opts = options_of(self)
     pl_ = self.project_layer
-    recompute = RECOMPUTE_COLUMNS
+    recompute = opts.recompute_columns
     if recompute is None:
         X, Y, Z = (int(v) for v in pl_.voxels_per_axis)
-        recompute = batch_size * heatmaps.shape[2] * X * Y * Z * 4 > RECOMPUTE_CUBE_BYTES
+        recompute = batch_size * heatmaps.shape[2] * X * Y * Z * 4 > opts.recompute_cube_bytes
     if recompute:
         # no cube: the xy plane only, then the winners' columns recomputed (:162-200)
         _, xy = pl_.forward_fused(heatmaps, meta, cameras, resize_transform, want_cube=False, want_xy=True)
-        hm2d, bbox_preds = center_net_from_xy(self.center_net, xy)
+        hm2d, bbox_preds = center_net_from_xy(self.center_net, xy, opts)
         confs_2d, index_2d, flat = proposal.nms2D(hm2d, self.max_people)
         columns = pl_.columns(heatmaps, meta, cameras, resize_transform, flat)  # [B,K,J,Z]
     else:
         cubes, xy = pl_.forward_fused(heatmaps, meta, cameras, resize_transform)
-        hm2d, bbox_preds = center_net_from_xy(self.center_net, xy)
+        hm2d, bbox_preds = center_net_from_xy(self.center_net, xy, opts)
         # nms2D and the z-column gather of its winners in one launch (:188, :199-200)
         confs_2d, index_2d, flat, columns = proposal.nms2D_columns(hm2d, self.max_people, cubes)
     match_bbox = proposal.gather_bbox(bbox_preds, flat)
     c2c = self.c2c_net
-    if USE_FVP_CNN and not c2c.training:
-        c2c = fvp_cnn.cached(c2c, FVP_CNN_DTYPE)
+    if opts.cnn and not c2c.training:
+        c2c = fvp_cnn.cached(c2c, opts.cnn_dtype)
     hm1d = c2c(torch.flatten(columns, 0, 1)).view(batch_size, self.max_people, -1)
     pl = self.proposal_layer
     if pl.training and ("roots_3d" in meta and "num_person" in meta):  # GT matching (training)
@@ -166,8 +212,8 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     return hm2d, hm1d, centers, torch.flatten(bbox_preds, 2, 3).permute(0, 2, 1)
 
 
-def _fvp_backbone_ok(module, x) -> bool:
-    return (USE_FVP_BACKBONE and not module.training and isinstance(x, torch.Tensor) and x.is_cuda
+def _fvp_backbone_ok(module, x, opts: FvpOptions) -> bool:
+    return (opts.backbone and not module.training and isinstance(x, torch.Tensor) and x.is_cuda
             and not (torch.is_grad_enabled() and x.requires_grad))
 
 
@@ -175,8 +221,9 @@ def fvp_resnet_forward(self, x):
     """ResNet.forward (resnet.py:187-201) on the fvp MFMA convolutions in eval
     mode; the reference's forward in training (BatchNorm batch statistics,
     autograd) and on CPU tensors."""
-    if _fvp_backbone_ok(self, x):
-        return fvp_backbone.cached(self, FVP_BACKBONE_DTYPE)(x)
+    opts = options_of(self)
+    if _fvp_backbone_ok(self, x, opts):
+        return fvp_backbone.cached(self, opts.backbone_dtype)(x)
     return type(self)._fvp_original_forward(self, x)
 
 
@@ -186,9 +233,10 @@ def fused_fvp_forward(self, backbone=None, views=None, meta=None, targets=None, 
     path on the fvp backbone in eval mode: all B*V views in one pass, heatmaps
     written channels-last once and handed to the HDN / JLN gathers in place
     (fvp.heatmaps.attach); everything after it is the reference's forward."""
+    opts = options_of(self)
     if (views is not None and backbone is not None and not self.training and hasattr(backbone, "deconv_layers")
-            and _fvp_backbone_ok(backbone, views)):
-        cl = fvp_backbone.cached(backbone, FVP_BACKBONE_DTYPE).heatmaps_cl(views)
+            and _fvp_backbone_ok(backbone, views, opts)):
+        cl = fvp_backbone.cached(backbone, opts.backbone_dtype).heatmaps_cl(views)
         input_heatmaps, views = cl.planar(), None  # [B,V,J,H,W], carrying the channels-last copy
     return type(self)._fvp_original_forward(self, backbone=backbone, views=views, meta=meta, targets=targets,
                                             input_heatmaps=input_heatmaps, cameras=cameras,

@@ -75,8 +75,9 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
         return
     from . import cnn, integration
 
-    use = integration.USE_FVP_CNN and not self.conv_net.training
-    conv = cnn.cached(self.conv_net, integration.FVP_CNN_DTYPE) if use else self.conv_net
+    opts = integration.options_of(self)
+    use = opts.cnn and not self.conv_net.training
+    conv = cnn.cached(self.conv_net, opts.cnn_dtype) if use else self.conv_net
     features = torch.stack(torch.chunk(conv(planes), 3), dim=0)                    # [3,P,J,S,S]
     pose, maxprob = ops.soft_argmax(features, self.project_layer.center_grid, offset,
                                     float(self.soft_argmax_layer.beta))

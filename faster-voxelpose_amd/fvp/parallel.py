@@ -45,12 +45,9 @@ def gather_proposals(vals: torch.Tensor, flat: torch.Tensor, group=None) -> tupl
     local = pack_proposals(vals, flat)
     world = dist.get_world_size(group)
     out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype, device=local.device)
-    try:
-        dist.all_gather_into_tensor(out, local, group=group)
-    except (RuntimeError, NotImplementedError):  # backends without the fused form (older gloo)
-        parts = [torch.empty_like(local) for _ in range(world)]
-        dist.all_gather(parts, local, group=group)
-        out = torch.cat(parts)
+    # (nccl = RCCL and gloo both implement the fused form; any failure, a
+    # timeout included, propagates -- no second collective is attempted)
+    dist.all_gather_into_tensor(out, local, group=group)
     return unpack_proposals(out, K)
 
 
@@ -70,12 +67,7 @@ def gather_xy_slabs(xy_slab: torch.Tensor, X: int, group=None) -> torch.Tensor:
     local = xy_slab.new_zeros((xm, B, J, Y))
     local[: xy_slab.shape[2]] = xy_slab.permute(2, 0, 1, 3)  # x-major so the gather concatenates slabs
     out = xy_slab.new_empty((world * xm, B, J, Y))
-    try:
-        dist.all_gather_into_tensor(out, local, group=group)
-    except (RuntimeError, NotImplementedError):
-        parts = [torch.empty_like(local) for _ in range(world)]
-        dist.all_gather(parts, local, group=group)
-        out = torch.cat(parts)
+    dist.all_gather_into_tensor(out, local, group=group)
     rows = torch.cat([out[r * xm: r * xm + (e - s)] for r, (s, e) in enumerate(spans)])
     return rows.permute(1, 2, 0, 3).contiguous()
 

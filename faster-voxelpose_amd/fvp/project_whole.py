@@ -37,11 +37,8 @@ def _as_list3(v, kind=float):
     return [kind(x) for x in v]
 
 
-# ProjectLayer.columns: project the winners' voxels from the camera records even
-# when a packed grid is cached (bit-identical; measured slower at C3 B=8, 15.1
-# vs 11.6 us: the projection's VALU and 21-float records outweigh the round
-# trip it saves), FVP_COLUMNS_ON_THE_FLY=1
-COLUMNS_ON_THE_FLY = os.environ.get("FVP_COLUMNS_ON_THE_FLY", "0") != "0"
+# default of ProjectLayer.columns_on_the_fly (FVP_COLUMNS_ON_THE_FLY=1)
+_COLUMNS_ON_THE_FLY_ENV = os.environ.get("FVP_COLUMNS_ON_THE_FLY", "0") != "0"
 
 
 class ProjectLayer(nn.Module):
@@ -60,6 +57,11 @@ class ProjectLayer(nn.Module):
         self._cams = {}        # seq -> [V, FVP_CAM_STRIDE] camera records (on-the-fly projection)
         self._stacked = (None, None)  # (key, [S,N,GV,2]) grids of the last mixed-sequence batch
         self.on_the_fly = None  # None: decide by grid size; True/False: force
+        # columns(): project the winners' voxels from the camera records even when
+        # a packed grid is cached (bit-identical; measured slower at C3 B=8, 15.1
+        # vs 11.6 us: the projection's VALU and 21-float records outweigh the
+        # round trip it saves)
+        self.columns_on_the_fly = _COLUMNS_ON_THE_FLY_ENV
         self.verbose = True
 
     # -- reference attribute: voxel centres [N,3] (compute_grid, :43-79) -------------
@@ -196,7 +198,7 @@ class ProjectLayer(nn.Module):
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         cl = channels_last_of(heatmaps)
         src, J = (cl.t, cl.J) if cl is not None else (heatmaps, 0)
-        if self._project_on_the_fly(heatmaps.shape[1]) or COLUMNS_ON_THE_FLY:
+        if self._project_on_the_fly(heatmaps.shape[1]) or self.columns_on_the_fly:
             # the coordinates projected from the camera records (bit-identical to the
             # packed grid; their loads do not wait for `flat`)
             cams, index = self._cams_for_batch(heatmaps, meta, cameras)

@@ -199,7 +199,10 @@ int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z,
  * elements: planar [B][V][J][H][W] -> (J*H*W, H*W, 1), channels-last
  * [B][V][H][W][cp] -> (H*W*cp, 1, cp) (from the first joint's element);
  * half = fp16 heatmaps.  columns device [B][K][J][Z] (NaN for an index
- * outside the map). */
+ * outside the map).  Precondition (as fvp_voxelize): a device grid_index holds
+ * 0 <= grid_index[b] < the number of sequences packed in packed_grids / cams;
+ * it is not range-checked on the device (the Python wrapper checks host
+ * indices). */
 int fvp_voxel_columns(const void *heatmaps, int half, long long view_stride, long long joint_stride,
                       int pix_stride, int B, int V, int J, int H, int W, const float *packed_grids,
                       const float *cams, const float *resize_t, const fvp_grid_spec *grid,

@@ -34,8 +34,33 @@ F64 = np.float64
 
 
 def fma32(a, b, c):
-    """fp32 fused multiply-add emulated in float64."""
-    return (np.asarray(a, F64) * np.asarray(b, F64) + np.asarray(c, F64)).astype(F32)
+    """fp32 fused multiply-add, correctly rounded, emulated in float64.
+
+    a*b of two fp32 values is exact in float64; the sum with c is taken
+    exactly as hi + lo (TwoSum), and hi is rounded to fp32.  That rounding is
+    wrong only when hi sits exactly on a midpoint between two fp32 values and
+    lo != 0 (the double-rounding case): then the sign of lo picks the side.
+    (Seen in the reference: resize_transform's 8.9e-18 off-diagonal term of
+    the Panoptic affine, transforms.py:59-63, breaks the tie of
+    0.47407407 * 192 -- project_grid at C5 moves by one ulp.)"""
+    a, b, c = np.broadcast_arrays(np.asarray(a, F64), np.asarray(b, F64), np.asarray(c, F64))
+    s = a * b
+    hi = s + c
+    bb = hi - s
+    with np.errstate(invalid="ignore", over="ignore"):
+        lo = (s - (hi - bb)) + (c - bb)
+        r = hi.astype(F32)
+        r64 = r.astype(F64)
+        diff = hi - r64
+        toward = np.where(diff > 0, F32(np.inf), F32(-np.inf)).astype(F32)
+        other = np.nextafter(r, toward)
+        tie = np.isfinite(hi) & np.isfinite(lo) & (diff != 0) & (hi == (r64 + other.astype(F64)) * 0.5)
+        # the exact value is hi + lo: past the midpoint toward `other` when lo has diff's sign
+        pick_other = tie & (lo != 0) & (np.sign(lo) == np.sign(diff))
+        pick_r = tie & (lo != 0) & (np.sign(lo) != np.sign(diff))
+        lower_side = np.where(pick_other, other, r)
+    out = np.where(pick_r, r, lower_side).astype(F32)
+    return out[()] if out.ndim == 0 else out
 
 
 def linspace32(start: float, end: float, n: int) -> np.ndarray:
@@ -346,3 +371,26 @@ def fuse_pose_preds(pose: np.ndarray, weights: np.ndarray) -> np.ndarray:
     y = yw[:, :, :1] * xy[:, :, 1:] + yw[:, :, 1:] * yz[:, :, :1]
     z = zw[:, :, :1] * xz[:, :, 1:] + zw[:, :, 1:] * yz[:, :, 1:]
     return np.concatenate([x, y, z], axis=2)
+
+
+CUBE_SLABS = 8  # per-x-slab digests localise a mismatch
+
+
+def cube_digests(cube: np.ndarray, slabs: int = CUBE_SLABS) -> np.ndarray:
+    """SHA-256 pins of whole fp32 cubes [B,J,X,Y,Z] (project_whole.py:166-167's
+    output layout): per frame, the digest of the frame's little-endian fp32
+    bytes (C order, so -0.0 vs +0.0 and NaN payloads count) followed by one
+    digest per x-slab (``slabs`` contiguous runs of x-rows, [J, x0:x1, Y, Z]).
+    Returns uint8 [B, 1 + slabs, 32]."""
+    import hashlib
+
+    cube = np.ascontiguousarray(cube, dtype="<f4")
+    B, X = cube.shape[0], cube.shape[2]
+    bounds = np.linspace(0, X, slabs + 1).round().astype(int)
+    out = np.zeros((B, 1 + slabs, 32), np.uint8)
+    for b in range(B):
+        out[b, 0] = np.frombuffer(hashlib.sha256(cube[b].tobytes()).digest(), np.uint8)
+        for s in range(slabs):
+            part = np.ascontiguousarray(cube[b, :, bounds[s]:bounds[s + 1]])
+            out[b, 1 + s] = np.frombuffer(hashlib.sha256(part.tobytes()).digest(), np.uint8)
+    return out

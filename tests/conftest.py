@@ -32,14 +32,13 @@ def gpu_device():
 
 @pytest.fixture(params=["halo", "pertap", "pertap-nosplit", "dma"])
 def conv_kernel(request):
-    """Run with the halo-tiled KxK kernel on every eligible layer (so small
-    test shapes take it too), with the per-tap kernel only (split-K where a
-    launch is under-filled), with neither halo nor split-K
-    (FVP_CONV_HALO / _PER_TAP / _PER_TAP_NOSPLIT of fvp_conv2d_nhwc_ws), and
-    with the LDS-DMA kernel on every layer it takes (FVP_CONV_F32_KC)."""
+    """The fp32 kernel choice a test builds its layers with (``algo`` of
+    fvp.cnn.ConvLayer / FvpCNN): the halo-tiled KxK kernel on every eligible
+    layer (so small test shapes take it too), the per-tap kernel only (split-K
+    where a launch is under-filled), neither halo nor split-K
+    (FVP_CONV_HALO / _PER_TAP / _PER_TAP_NOSPLIT of fvp_conv2d_nhwc_ws), and the
+    LDS-DMA kernel on every layer it takes (FVP_CONV_F32_KC)."""
     from fvp import cnn
 
-    algo = {"halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP, "pertap-nosplit": cnn.CONV_PER_TAP_NOSPLIT,
-            "dma": cnn.CONV_DMA}
-    with cnn.conv_algo(algo[request.param]):
-        yield request.param
+    return {"halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP, "pertap-nosplit": cnn.CONV_PER_TAP_NOSPLIT,
+            "dma": cnn.CONV_DMA}[request.param]

@@ -97,7 +97,7 @@ def test_backbone_compile_rejects_train_mode():
 
 
 # ------------------------------------------------------------------------- GPU
-def _conv_case(dev, conv, bn, x):
+def _conv_case(dev, conv, bn, x, algo=None):
     from fvp.cnn import ConvLayer, to_nchw, to_nhwc
 
     conv, bn = conv.to(dev).eval(), (bn.to(dev).eval() if bn is not None else None)
@@ -110,7 +110,7 @@ def _conv_case(dev, conv, bn, x):
         ref = conv(x) if bn is None else bn(conv(x))
         cin = conv.in_channels
         cpi = 4 if cin <= 4 else None
-        layer = ConvLayer(conv, bn, cpi=cpi)
+        layer = ConvLayer(conv, bn, cpi=cpi, algo=algo)
         got = to_nchw(layer(to_nhwc(x, layer.Cpi), relu=False))
     torch.cuda.synchronize()
     return got.cpu().numpy(), ref.cpu().numpy()
@@ -130,7 +130,7 @@ def test_strided_conv_matches_torch(gpu_device, conv_kernel, cin, cout, k, s, p,
     conv = nn.Conv2d(cin, cout, k, s, p, bias=cout == 17)
     bn = None if cout == 17 else nn.BatchNorm2d(cout)
     x = torch.randn((2, cin) + hw, device=gpu_device)
-    got, ref = _conv_case(gpu_device, conv, bn, x)
+    got, ref = _conv_case(gpu_device, conv, bn, x, conv_kernel)
     assert got.shape == ref.shape
     assert _rel_err(got, ref) <= 2e-5
 
@@ -142,7 +142,7 @@ def test_deconv4_matches_torch(gpu_device, conv_kernel, cin, cout, hw):
     torch.manual_seed(cin + cout)
     conv = nn.ConvTranspose2d(cin, cout, 4, 2, 1, 0, bias=False)
     x = torch.randn((2, cin) + hw, device=gpu_device)
-    got, ref = _conv_case(gpu_device, conv, nn.BatchNorm2d(cout), x)
+    got, ref = _conv_case(gpu_device, conv, nn.BatchNorm2d(cout), x, conv_kernel)
     assert got.shape == ref.shape == (2, cout, 2 * hw[0], 2 * hw[1])
     assert _rel_err(got, ref) <= 2e-5
 
@@ -360,6 +360,8 @@ def _restore(cls):
     if hasattr(cls, "_fvp_original_forward"):
         cls.forward = cls._fvp_original_forward
         del cls._fvp_original_forward
+    if "fvp_options" in cls.__dict__:  # install()'s per-class options
+        del cls.fvp_options
 
 
 def test_install_backbone_patches_and_falls_back_on_cpu():
@@ -382,7 +384,6 @@ def test_install_backbone_patches_and_falls_back_on_cpu():
     finally:
         _restore(ResNet)
         _restore(FVP)
-        integration.USE_FVP_BACKBONE = False
 
 
 @pytest.mark.gpu
@@ -418,7 +419,6 @@ def test_installed_views_path_matches_reference_flow(gpu_device):
         finally:
             _restore(ResNet)
             _restore(FVP)
-            integration.USE_FVP_BACKBONE = False
         planar = layer(hm.clone(), meta, cams, rt)
     torch.cuda.synchronize()
     assert torch.equal(cube, planar)

@@ -91,7 +91,7 @@ def test_conv_layer_vs_torch(gpu_device, conv_kernel, cin, cout, k, hw, res):
     with torch.no_grad():
         ref = seq(x)
         ref = torch.relu(ref + r) if res else torch.relu(ref)
-    layer = cnn.ConvLayer(seq[0], seq[1])
+    layer = cnn.ConvLayer(seq[0], seq[1], algo=conv_kernel)
     got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=cnn.to_nhwc(r) if res else None))
     _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv {cin}->{cout} k{k}")
 
@@ -116,7 +116,7 @@ def test_auto_takes_f32_dma_kernel(gpu_device, cin, cout, k, hw, res):
         ref = seq(x)
         ref = torch.relu(ref + r) if res else torch.relu(ref)
     layer = cnn.ConvLayer(seq[0], seq[1])
-    assert cnn.CONV_ALGO == cnn.CONV_AUTO and cnn.F32_DMA_AUTO
+    assert layer.algo == cnn.CONV_AUTO == cnn.DEFAULT_ALGO
     got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=cnn.to_nhwc(r) if res else None))
     assert any(dma for _, dma in layer._ws.values()), "AUTO did not pick the LDS-DMA kernel"
     _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv {cin}->{cout} k{k} (DMA)")
@@ -154,7 +154,7 @@ def test_fvp_cnn_large_batch_tiles_vs_torch(gpu_device, conv_kernel):
     x = torch.rand((24, 15, 64, 64), generator=torch.Generator().manual_seed(5)).to(gpu_device)
     with torch.no_grad():
         ref = p2p(x)
-    got = FvpCNN(p2p)(x)
+    got = FvpCNN(p2p, algo=conv_kernel)(x)
     _close(got.cpu().numpy(), ref.cpu().numpy(), "P2PNet, 24 images")
 
 
@@ -245,8 +245,9 @@ def test_bf16_dma_conv_matches_register_staged(gpu_device, cin, cout, k, stride,
         rt[..., :cout] = torch.randn((3, Ho, Wo, cout), generator=gen).to(gpu_device).to(torch.bfloat16)
         r = cnn.Act(rt, cout)
     y_dma = layer(xa, relu=True, res_post=r)
-    with cnn.conv_algo(cnn.CONV_PER_TAP_NOSPLIT):
-        y_reg = layer(xa, relu=True, res_post=r)
+    reg = cnn.ConvLayer(seq[0], seq[1], torch.bfloat16, algo=cnn.CONV_PER_TAP_NOSPLIT)
+    reg.act_bf16 = True
+    y_reg = reg(xa, relu=True, res_post=r)
     assert torch.equal(y_dma.t, y_reg.t)
     with torch.no_grad():
         ref = torch.relu(seq(x))

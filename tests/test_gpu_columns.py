@@ -48,13 +48,13 @@ def _check(layer, hm, meta, cams, rt, flat, src=None):
 @pytest.mark.parametrize("cols_otf", [False, True], ids=["cols-grid", "cols-otf"])
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16], ids=["f32", "f16"])
-def test_columns_match_cube_c2(gpu_device, otf, dtype, cols_otf, monkeypatch):
+def test_columns_match_cube_c2(gpu_device, otf, dtype, cols_otf):
     """The columns' coordinates from the packed grid or projected on the fly
     (ProjectLayer.columns' default) against the cube of either voxelize path."""
-    from fvp import project_whole, synthetic
+    from fvp import synthetic
 
-    monkeypatch.setattr(project_whole, "COLUMNS_ON_THE_FLY", cols_otf)
     w, layer, cams, seq, rt = _layer(gpu_device, "c2", otf=otf)
+    layer.columns_on_the_fly = cols_otf
     B, K = 3, 10
     hm = synthetic.uniform_heatmaps(w, B, seed=5).to(dtype).to(gpu_device)
     X, Y, _ = w.voxels_per_axis
@@ -96,7 +96,7 @@ def test_columns_channels_last_and_mixed_sequences(gpu_device):
 
 @pytest.mark.gpu
 def test_fused_hdn_without_cube_equals_with_cube(gpu_device):
-    """integration.fused_hdn_forward with RECOMPUTE_COLUMNS on and off: identical outputs."""
+    """integration.fused_hdn_forward with recompute_columns on and off: identical outputs."""
     import types
 
     import torch.nn as nn
@@ -110,14 +110,52 @@ def test_fused_hdn_without_cube_equals_with_cube(gpu_device):
                                 c2c_net=nn.Conv1d(w.num_joints, 1, 1).to(gpu_device).eval())
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 3)).to(gpu_device)
     meta = {"seq": [seq] * 3}
-    outs, keep = {}, integration.RECOMPUTE_COLUMNS
+    outs = {}
     with torch.no_grad():
         for flag in (False, True):
-            integration.RECOMPUTE_COLUMNS = flag
-            try:
-                outs[flag] = integration.fused_hdn_forward(net, hm, meta, cams, rt)
-            finally:
-                integration.RECOMPUTE_COLUMNS = keep
+            integration.set_options(net, recompute_columns=flag)
+            outs[flag] = integration.fused_hdn_forward(net, hm, meta, cams, rt)
     torch.cuda.synchronize()
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_fused_hdn_automatic_cube_free_choice_at_c5(gpu_device):
+    """FvpOptions.recompute_columns = None (the product default) decides by the
+    batch's cube size: with the threshold below one C5 frame's cube the
+    automatic choice takes the cube-free path at C5's full geometry (31 ring
+    cameras, 160x160x64, fp16, on-the-fly coordinates) and must give exactly
+    the outputs of the cube path."""
+    import types
+
+    import torch.nn as nn
+    from fvp import integration, synthetic
+    from test_integration import _CenterNet, _Proposal
+
+    torch.manual_seed(1)
+    w, layer, cams, seq, rt = _layer(gpu_device, "c5", otf=None)  # auto: C5 projects on the fly
+    net = types.SimpleNamespace(project_layer=layer, max_people=w.max_people, proposal_layer=_Proposal(w),
+                                center_net=_CenterNet(w.num_joints).to(gpu_device).eval(),
+                                c2c_net=nn.Conv1d(w.num_joints, 1, 1).to(gpu_device).eval())
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 2)).half().to(gpu_device)
+    meta = {"seq": [seq] * 2}
+    seen = []
+    orig = layer.columns
+
+    def spy(*a, **k):
+        seen.append(1)
+        return orig(*a, **k)
+
+    layer.columns = spy
+    with torch.no_grad():
+        integration.set_options(net, recompute_columns=False)
+        ref = integration.fused_hdn_forward(net, hm, meta, cams, rt)
+        assert not seen
+        X, Y, Z = w.voxels_per_axis
+        integration.set_options(net, recompute_columns=None, recompute_cube_bytes=w.num_joints * X * Y * Z * 4)
+        got = integration.fused_hdn_forward(net, hm, meta, cams, rt)  # 2 frames' cube > threshold: cube-free
+        assert seen, "the automatic size check did not take the cube-free path"
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(torch.nan_to_num(a, nan=-7.0), torch.nan_to_num(b, nan=-7.0))

@@ -43,7 +43,9 @@ def test_install_patches_reference_names():
     assert mods["core.proposal"].nms2D is proposal.nms2D
     assert mods["models.human_detection_net"].nms2D is proposal.nms2D
     assert HDN.forward is integration.fused_hdn_forward
-    assert len(patched) == 7
+    assert HDN.fvp_options == integration.FvpOptions()  # install()'s options, per patched class
+    assert integration.options_of(HDN()) is HDN.fvp_options
+    assert len(patched) == 8
 
 
 class _CenterNet(nn.Module):
@@ -261,11 +263,11 @@ def test_fused_forwards_with_fvp_cnn(gpu_device):
     hdn.c2c_net = hdn.c2c_net.to(gpu_device)
     hdn.proposal_layer = _Proposal(w)
     hdn.max_people = w.max_people
-    try:
+    if True:
         with torch.no_grad():
-            integration.USE_FVP_CNN = False
+            integration.set_options(hdn, cnn=False)
             ref = integration.fused_hdn_forward(hdn, hm, meta, cams, rt)
-            integration.USE_FVP_CNN = True
+            integration.set_options(hdn, cnn=True)
             got = integration.fused_hdn_forward(hdn, hm, meta, cams, rt)
         scale = float(ref[0].abs().max())
         assert float((got[0] - ref[0]).abs().max()) <= 2e-5 * scale
@@ -287,14 +289,12 @@ def test_fused_forwards_with_fvp_cnn(gpu_device):
         pc = torch.from_numpy(np.stack([synthetic.proposals_for_frame(w, f, 4) for f in range(2)])).to(gpu_device)
         mask = torch.ones((2, 4), dtype=torch.bool, device=gpu_device)
         with torch.no_grad():
-            integration.USE_FVP_CNN = False
+            integration.set_options(net, cnn=False)
             rf, rp = jln.fused_jln_forward(net, meta, hm, pc.clone(), mask, cams, rt)
-            integration.USE_FVP_CNN = True
+            integration.set_options(net, cnn=True)
             gf, gp = jln.fused_jln_forward(net, meta, hm, pc.clone(), mask, cams, rt)
         np.testing.assert_allclose(gp.cpu().numpy(), rp.cpu().numpy(), atol=0.5, rtol=0)
         np.testing.assert_allclose(gf.cpu().numpy(), rf.cpu().numpy(), atol=0.5, rtol=0)
-    finally:
-        integration.USE_FVP_CNN = False
 
 
 @pytest.mark.gpu
@@ -331,14 +331,11 @@ def test_fused_hdn_forward_trains_like_reference_flow(gpu_device):
     for flow in ("fused", "reference"):
         net.center_net = copy.deepcopy(cn).to(gpu_device).train()
         net.c2c_net = copy.deepcopy(c2c).to(gpu_device).train()
-        integration.USE_FVP_CNN = True  # ignored in train mode
-        try:
-            if flow == "fused":
-                hm2d, hm1d, centers, bbox = integration.fused_hdn_forward(net, hm, meta, cams, rt)
-            else:
-                hm2d, hm1d, centers, bbox = _reference_flow(net, hm, meta, cams, rt)
-        finally:
-            integration.USE_FVP_CNN = False
+        integration.set_options(net, cnn=True)  # ignored in train mode
+        if flow == "fused":
+            hm2d, hm1d, centers, bbox = integration.fused_hdn_forward(net, hm, meta, cams, rt)
+        else:
+            hm2d, hm1d, centers, bbox = _reference_flow(net, hm, meta, cams, rt)
         loss = (hm2d ** 2).mean() + (hm1d ** 2).mean() + bbox.abs().mean()
         loss.backward()
         grads.append({n: p.grad.detach().clone() for m in (net.center_net, net.c2c_net)

@@ -192,3 +192,47 @@ def test_c5_ring_cameras_bit_exact_on_sampled_voxels():
         R, T = np.asarray(c["R"], np.float64), np.asarray(c["T"], np.float64).reshape(3, 1)
         behind += int(((R @ (grid[d["sub"]].T.astype(np.float64) - T))[2] < 0).sum())
     assert behind > 0
+
+
+# whole-cube SHA-256 pins written by the reference's ProjectLayer (tests/digest_cases.py);
+# the oracle must reproduce every byte of every frame (C5's 31-camera cubes are
+# left to the GPU tests: minutes of numpy)
+@pytest.mark.parametrize("key", ["c1_g", "c1_u", "c2_g", "c2_u", "c3_g", "c3_u", "shelf_native_g", "c4_g", "c4_u", "c5_g", "c5_u"])
+def test_oracle_full_cube_digests(key):
+    import os
+
+    import digest_cases as dc
+
+    if key.startswith("c5") and os.environ.get("FVP_SLOW_ORACLE", "0") == "0":
+        pytest.skip("C5 oracle cube takes ~4 min of numpy: FVP_SLOW_ORACLE=1 (its sample grid is pinned below)")
+
+    d = golden("cube_digests.npz")
+    wname, _, frames = dc.CASES[key]
+    w = WORKLOADS[wname]
+    hm, _ = dc.inputs(key)
+    assert np.array_equal(dc.input_sha(hm), d[f"{key}_input_sha256"]), "regenerated input differs"
+    rt = np.asarray(geometry.resize_transform(w.ori_image_size, w.image_size), np.float32)
+    _, sg = _sample_grid(w, rt)
+    X, Y, Z = w.voxels_per_axis
+    cube = np.stack([O.voxelize(hm[b], sg).reshape(w.num_joints, X, Y, Z) for b in range(frames)])
+    got = O.cube_digests(cube)
+    bad = [(b, s) for b in range(frames) for s in range(got.shape[1]) if not np.array_equal(got[b, s], d[f"{key}_digests"][b, s])]
+    assert not bad, f"{key}: (frame, digest slot) mismatches {bad} (slot 0 = whole frame, 1.. = x-slabs)"
+    assert np.array_equal(cube.astype(np.float64).sum(axis=(1, 2, 3, 4)), d[f"{key}_sum64"])
+
+
+@pytest.mark.parametrize("wname", ["c1", "c2", "c3", "shelf_native", "c4", "c5"])
+def test_oracle_full_sample_grid_digests(wname):
+    """Every camera's whole per-sequence sample grid (project_whole.py:81-117,
+    cached at :151-156) against the SHA-256 of the reference's own cache --
+    at C5 this is where a one-ulp fp32 fma tie (resize_transform's 8.9e-18
+    off-diagonal term) used to slip past the strided samples."""
+    import digest_cases as dc
+
+    d = golden("cube_digests.npz")
+    w = WORKLOADS[wname]
+    rt = np.asarray(geometry.resize_transform(w.ori_image_size, w.image_size), np.float32)
+    _, sg = _sample_grid(w, rt)
+    ref = d[f"grid_{wname}_sha256"]
+    bad = [v for v in range(sg.shape[0]) if not np.array_equal(dc.input_sha(np.ascontiguousarray(sg[v], "<f4")), ref[v])]
+    assert not bad, f"{wname}: sample grid of cameras {bad} differs from the reference's"

@@ -96,6 +96,60 @@ def test_two_rank_gloo_sharded_proposals_match_single_process():
     assert np.array_equal(gf, rf.numpy())
 
 
+def _golden_worker(rank, world, port, q):
+    """bench.py's N > 1 step on CPU: rank r takes shard_frames(4, world, r) of
+    the golden C2 frames (tests/digest_cases.py "c2_g"), voxelises them (oracle
+    standing in for the HIP op; each frame's cube checked against the
+    reference's SHA-256), NMS on the root plane, then gather_proposals."""
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "faster-voxelpose_amd"), os.path.join(repo, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import digest_cases as dc
+        from fvp import geometry
+        from fvp.workloads import WORKLOADS
+        from oracle import fvp_oracle as O
+
+        w = WORKLOADS["c2"]
+        hm, _ = dc.inputs("c2_g")
+        s, e = parallel.shard_frames(hm.shape[0], world, rank)
+        cams, seq = w.cameras()
+        rt = geometry.resize_transform(w.ori_image_size, w.image_size).astype(np.float32)
+        grid = O.compute_grid(w.space_size, w.space_center, w.voxels_per_axis)
+        sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, w.heatmap_size, rt)
+                       for c in geometry.camera_list(cams, seq)])
+        cube = np.stack([O.voxelize(hm[b], sg).reshape(w.num_joints, *w.voxels_per_axis) for b in range(s, e)])
+        ref = np.load(os.path.join(repo, "tests", "golden", "cube_digests.npz"))["c2_g_digests"][s:e]
+        assert np.array_equal(O.cube_digests(cube)[:, 0], ref[:, 0]), f"rank {rank}: frames {s}..{e} differ"
+        vals, _, flat = O.nms2d(cube.max(axis=4)[:, 2:3], w.max_people)
+        gv, gf = parallel.gather_proposals(torch.from_numpy(vals), torch.from_numpy(flat))
+        q.put((rank, s, e, vals, flat, gv.numpy(), gf.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_golden_frames_gathered_in_rank_order():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_golden_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    own_v = np.concatenate([g[3] for g in got])
+    own_f = np.concatenate([g[4] for g in got])
+    assert [g[1:3] for g in got] == [(0, 2), (2, 4)]
+    for g in got:  # every rank holds all frames' proposals, rank 0's frames first
+        assert np.array_equal(g[5], own_v) and np.array_equal(g[6], own_f)
+
+
 def _slab_setup(world):
     import sys
 

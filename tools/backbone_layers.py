@@ -28,11 +28,11 @@ def main():
     from fvp import cnn, synthetic
     from fvp.backbone import FvpPoseResNet
 
-    cnn.F32_DMA_AUTO = not args.no_dma
     dev = torch.device("cuda:0")
     m = cnn_arch.PoseResNet(50, 15).eval()
     m.load_state_dict(synthetic.seeded_state_dict(m, 21))
-    bb = FvpPoseResNet(m.to(dev), torch.bfloat16 if args.bf16 else torch.float32)
+    bb = FvpPoseResNet(m.to(dev), torch.bfloat16 if args.bf16 else torch.float32,
+                       algo=cnn.CONV_AUTO_NO_DMA if args.no_dma else cnn.CONV_AUTO)
     x = torch.randn((args.images, 3, 512, 960), device=dev)
     rec = []
     orig = cnn.ConvLayer.__call__

@@ -29,11 +29,9 @@ def main():
     import torch
     from fvp import _lib
 
-    if os.environ.get("FVP_CONV_HALO") == "0":  # A/B: per-tap kernel only (FVP_CONV_SPLIT=0: never split)
+    cnn_algo = None  # A/B: FVP_CONV_HALO=0 -> per-tap kernel only (FVP_CONV_SPLIT=0: never split)
+    if os.environ.get("FVP_CONV_HALO") == "0":
         cnn_algo = 3 if os.environ.get("FVP_CONV_SPLIT") == "0" else 1
-        from fvp import cnn as _cnn
-
-        _cnn.CONV_ALGO = cnn_algo
 
     import cnn_arch
     from fvp import cnn, synthetic
@@ -48,7 +46,7 @@ def main():
     g = torch.Generator().manual_seed(0)
     x_jln = torch.rand((3 * args.proposals, J, 64, 64), generator=g).to(dev)
     x_hdn = torch.rand((args.frames, J, 80, 80), generator=g).to(dev)
-    f_p2p, f_cn = cnn.FvpCNN(p2p), cnn.FvpCNN(cn)
+    f_p2p, f_cn = cnn.FvpCNN(p2p, algo=cnn_algo), cnn.FvpCNN(cn, algo=cnn_algo)
     b_p2p, b_cn = cnn.FvpCNN(p2p, torch.bfloat16), cnn.FvpCNN(cn, torch.bfloat16)
 
     def flops(plan_net, x):

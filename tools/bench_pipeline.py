@@ -93,8 +93,9 @@ def main():
     jl.weight_net.load_state_dict(synthetic.seeded_state_dict(jl.weight_net, 15))
     jl.weight_net = jl.weight_net.to(dev)
     jl.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
-    integration.USE_FVP_CNN = not args.torch_cnn
-    integration.FVP_CNN_DTYPE = torch.bfloat16 if args.bf16 else torch.float32
+    for net in (hdn, jl):
+        integration.set_options(net, cnn=not args.torch_cnn,
+                                cnn_dtype=torch.bfloat16 if args.bf16 else torch.float32)
     backbone = None
     if args.views:
         from fvp.backbone import FvpPoseResNet

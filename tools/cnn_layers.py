@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--images", type=int, default=240)
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--algo", choices=["auto", "dma", "halo", "pertap"], default="auto",
-                    help="fp32 kernel choice (fvp.cnn.conv_algo)")
+                    help="fp32 kernel choice (algo of fvp.cnn.FvpCNN)")
     args = ap.parse_args()
     import torch
 
@@ -36,7 +36,8 @@ def main():
         m = cnn_arch.CenterNet(J, 1).eval()
         hw = (80, 80)
     m.load_state_dict(synthetic.seeded_state_dict(m, 11))
-    f = cnn.FvpCNN(m.to(dev), torch.bfloat16 if args.bf16 else torch.float32)
+    algo = {"auto": cnn.CONV_AUTO, "dma": cnn.CONV_DMA, "halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP}[args.algo]
+    f = cnn.FvpCNN(m.to(dev), torch.bfloat16 if args.bf16 else torch.float32, algo=algo)
     x = torch.rand((args.images, J) + hw, device=dev)
     run = (lambda: f(x)) if args.net == "p2p" else (lambda: f.from_xy(x))
     rec = []
@@ -50,8 +51,7 @@ def main():
         rec.append((self, a.H, a.W, a.Cp, a.t.dtype, e0, e1, self.flops(a)))
         return y
 
-    algo = {"auto": cnn.CONV_AUTO, "dma": cnn.CONV_DMA, "halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP}[args.algo]
-    with torch.no_grad(), cnn.conv_algo(algo):
+    with torch.no_grad():
         run()
         torch.cuda.synchronize()
         cnn.ConvLayer.__call__ = timed

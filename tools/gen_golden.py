@@ -110,6 +110,37 @@ def backbone_case(torch, synthetic):
     print("wrote backbone", {k: v.shape for k, v in d.items()})
 
 
+def digest_cases(torch, pw, geometry, WORKLOADS, make_cfg):
+    """Whole-cube pins: for every case of tests/digest_cases.py, the
+    reference's ProjectLayer.forward (project_whole.py:119-168) on the case's
+    input; stored are the SHA-256 digests of each frame's full fp32 cube and
+    of its 8 x-slabs (oracle.fvp_oracle.cube_digests), the input's SHA-256,
+    and the float64 sum of each frame's cube (numpy order)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    sys.path.insert(0, REPO)
+    import digest_cases as dc
+    from oracle import fvp_oracle as O
+
+    d = {}
+    for key, (wname, src, frames) in dc.CASES.items():
+        w = WORKLOADS[wname]
+        hm, _ = dc.inputs(key)
+        cams, seq = w.cameras()
+        rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+        layer = pw.ProjectLayer(make_cfg(w, device="cpu"))
+        with torch.no_grad():
+            cube = layer(torch.from_numpy(hm), {"seq": [seq] * frames}, cams, rt).numpy()
+        d[f"{key}_digests"] = O.cube_digests(cube)
+        d[f"{key}_input_sha256"] = dc.input_sha(hm)
+        d[f"{key}_sum64"] = cube.astype(np.float64).sum(axis=(1, 2, 3, 4))
+        d[f"{key}_zeros"] = np.array([int(np.count_nonzero(cube == 0)), int(np.count_nonzero(np.signbit(cube)))])
+        sg = np.ascontiguousarray(layer.sample_grid[seq][:, 0].numpy(), "<f4")  # [V,N,2]: the per-sequence cache
+        d[f"grid_{wname}_sha256"] = np.stack([dc.input_sha(sg[v]) for v in range(sg.shape[0])])
+        print(f"digest {key}: {frames} x {cube.shape[1:]}  sum {d[f'{key}_sum64']}", flush=True)
+    np.savez_compressed(os.path.join(OUT, "cube_digests.npz"), **d)
+    print("wrote cube_digests", len(d), "arrays")
+
+
 def main():
     only = None
     if len(sys.argv) > 2 and sys.argv[1] == "--only":
@@ -188,6 +219,8 @@ def main():
         whole_case("whole_c4", "c4", batch=1, uniform_batch=1, stride=97)
     if only is None or "c5" in only:  # configs[4]: 31 ring cameras, fp16-rounded heatmaps, 160x160x64
         whole_case("whole_c5", "c5", batch=1, stride=997, store_heatmaps=False)
+    if only is None or "digests" in only:  # whole-cube SHA-256 pins of every config
+        digest_cases(torch, pw, geometry, WORKLOADS, make_cfg)
     if only is None or "e2e" in only:
         e2e_case(torch, geometry, synthetic, WORKLOADS, make_cfg)
     if only is None or "backbone" in only:

@@ -189,8 +189,12 @@ def cpu_baseline(w, sample_grid_cpu, threads_req):
             continue
         fps, frames, runs = cpu_baseline_run(w, sample_grid_cpu, th)
         lines[tag] = {"threads": th, "frames_per_s": round(fps, 2), "runs": runs}
-    main_line = lines["all_cores"]
+    # the reported value is the fastest measured thread count (the baseline most
+    # favourable to the CPU); on the pool the cgroup quota (cgroup_cpu_max) caps
+    # the process at 16 CPUs, where 16 threads ran slower than 8
+    main_line = max(lines.values(), key=lambda v: v["frames_per_s"])
     return {"value": main_line["frames_per_s"], "unit": "frames/s", "cores": main_line["threads"], "kind": "port",
+            "value_all_cores": lines["all_cores"]["frames_per_s"], "all_cores_threads": lines["all_cores"]["threads"],
             "host_physical_cores": phys, "host_logical_cpus_available": avail, "cgroup_cpu_max": limit,
             "value_8_threads": lines["8_threads"]["frames_per_s"],
             "value_pool_share": lines["pool_share"]["frames_per_s"], "pool_share_threads": share,

@@ -123,6 +123,7 @@ __device__ __forceinline__ void static_for(std::integer_sequence<int, K...>, F &
 }
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float h_lo(unsigned u) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu));

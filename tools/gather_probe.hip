@@ -1,0 +1,314 @@
+// Replay probe of the C2 voxelize gather.
+//
+// voxelize_kernel<LPV=4, fp32 channels-last, packed grid, NF=1> restated with
+// a MODE switch that keeps its exact block decomposition (cols, 16-row bands,
+// XCD remap), its per-lane grid loads, tap setup and DPP broadcasts, and its
+// per-lane tap offsets, and removes or alters one part at a time:
+//   FULL          the kernel as shipped (sanity: matches fvp_voxelize_cl)
+//   TAPS          grid + setup + the 4 tap loads per voxel-camera; the loaded
+//                 bits are XOR-folded (no FMA, no stage, no cube / xy stores)
+//   TAPS_L1       TAPS with every tap offset folded into one 16 KB window (all
+//                 taps valid and L1-resident): the texture path's floor for
+//                 this instruction stream
+//   TAPS_SKIP_OOB TAPS, but a voxel-camera whose 4 taps are all off-image
+//                 issues no loads (exec-masked lanes)
+//   TAPS_ALL_OOB  TAPS with every offset off-image (range check -> 0): what an
+//                 off-image lane costs the texture path
+//   NO_TAPS       FULL without the tap loads (zeros): grid, setup, FMA,
+//                 stage, cube and xy stores
+//   TAPS_2ROW     TAPS with 2 of the 4 loads (the y0 row only)
+//   CAM_OUTER     a candidate: camera-outer loop order (cam_outer_kernel below)
+//   NOSTORE       FULL without the cube / xy stores (the stage is still written)
+//   FULL2         FULL with a vector epilogue: float4 non-temporal cube stores
+//                 from LDS, float4 LDS reads for the z-max (Z % 4 == 0)
+//   STORES_ONLY   no main loop: the epilogue's LDS reads and cube / xy stores
+// Test tooling only (tools/gather_probe.py); not part of libfvp.
+#include "../faster-voxelpose_amd/csrc/fvp_layout.h"
+
+using namespace fvp;
+
+enum { FULL = 0, TAPS = 1, TAPS_L1 = 2, TAPS_SKIP_OOB = 3, TAPS_ALL_OOB = 4, NO_TAPS = 5, TAPS_2ROW = 6,
+       NOSTORE = 8, FULL2 = 9, STORES_ONLY = 10 };
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__global__ __launch_bounds__(256, 8) void probe_kernel(const float *__restrict__ tab, const float *__restrict__ grids,
+                                                       float *__restrict__ cube, float *__restrict__ xy,
+                                                       float *__restrict__ sink, int V, int J, int H, int W, int X,
+                                                       int Y, int Z, int cols, int col_blocks, int SP, int band) {
+    constexpr int LPV = 4, JP = 16, VPP = 64, CPG = 8;
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = L / col_blocks;
+    const int XY = X * Y;
+    int cb = L - b * col_blocks;
+    if (band > 0) {
+        const int gpr = Y / cols;
+        const int per_band = band * gpr;
+        const int bi = cb / per_band, r = cb - bi * per_band;
+        const int rows = min(band, X - bi * band);
+        const int gc = r / rows, xr = r - gc * rows;
+        cb = (bi * band + xr) * gpr + gc;
+    }
+    const int c0 = cb * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(grids, (unsigned)(N * GV * 8));
+    const unsigned unit = 64u;
+    const unsigned img = (unsigned)(H * W) * unit;
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)b * V * img;
+    unsigned fold = 0;
+    constexpr bool STAGED = MODE == FULL || MODE == NO_TAPS || MODE == NOSTORE || MODE == FULL2 || MODE == STORES_ONLY;
+    for (int i0 = 0; i0 < (MODE == STORES_ONLY ? 0 : T); i0 += VPP) {
+        const int i = i0 + threadIdx.x / LPV;
+        const bool valid = i < T;
+        const int ii = min(i, T - 1);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int v0 = 0; v0 < V; v0 += CPG) {
+            const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)(((n0 + ii) * GV + v0 + 2 * q) * 8),
+                                                                     0, 0);
+            float g[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = valid ? __builtin_bit_cast(float, (unsigned)graw[k]) : -2.0f;
+            const Taps4<false> t0 = setup_taps<false>(g[0], g[1], sxs, sys, W, H, unit);
+            const Taps4<false> t1 = setup_taps<false>(g[2], g[3], sxs, sys, W, H, unit);
+            static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = k >> 1;
+                const int v = v0 + k;
+                if (v >= V) return;
+                const Taps4<false> &src = (k & 1) ? t1 : t0;
+                unsigned o[4];
+                unsigned all = kOOB;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    o[m] = group_bcast<LPV, S>(src.o[m]);
+                    all &= o[m];
+                }
+                if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+                float w[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(src.w[m]);
+                if constexpr (MODE == TAPS_L1) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) o[m] &= 0x3FC0u;
+                }
+                if constexpr (MODE == TAPS_ALL_OOB) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) o[m] = kOOB | (o[m] & 0x3FC0u) | (unsigned)(m << 6);  // distinct (no CSE)
+                }
+                const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+                if constexpr (MODE == NO_TAPS) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) acc[m] = acc[m] + 0.0f * w[m];
+                } else if constexpr (MODE == TAPS_2ROW) {
+                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                    const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                    fold ^= a[0] ^ a[1] ^ a[2] ^ a[3] ^ bq[0] ^ bq[1] ^ bq[2] ^ bq[3];
+                } else {
+                    if (MODE == TAPS_SKIP_OOB && (all & kOOB)) return;  // (lanes of a group agree)
+                    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                    const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                    const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
+                    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+                    if constexpr (STAGED) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
+                            const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
+                            const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
+                            const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
+                            acc[m] = acc[m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
+                                                             __builtin_fmaf(fb, w[1], fa * w[0])));
+                        }
+                    } else {
+                        fold ^= a[0] ^ a[1] ^ a[2] ^ a[3] ^ bq[0] ^ bq[1] ^ bq[2] ^ bq[3] ^ c[0] ^ c[1] ^ c[2] ^ c[3] ^
+                                d[0] ^ d[1] ^ d[2] ^ d[3];
+                    }
+                }
+            });
+        }
+        if constexpr (STAGED) {
+            if (valid) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf(acc[m] / fV, 0.0f, 1.0f);
+            }
+        }
+    }
+    if constexpr (MODE == NOSTORE) {
+        __syncthreads();
+        if (stage[threadIdx.x] == 12345.0f) sink[blockIdx.x * 256 + threadIdx.x] = 1.0f;
+    } else if constexpr (MODE == FULL2 || MODE == STORES_ONLY) {
+        __syncthreads();
+        const int T4 = T >> 2;  // (host: T, SP, Z multiples of 4)
+        for (int e = threadIdx.x; e < J * T4; e += 256) {
+            const int j = e / T4, r = e - j * T4;
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + j * SP + 4 * r);
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + ((size_t)b * J + j) * N + n0) + r);
+        }
+        for (int e = threadIdx.x; e < J * ncols; e += 256) {
+            const int j = e / ncols, cc = e - (e / ncols) * ncols;
+            const f32x4 *s4 = reinterpret_cast<const f32x4 *>(stage + j * SP + cc * Z);
+            float m = -INFINITY;
+#pragma unroll 5
+            for (int z = 0; z < (Z >> 2); ++z) {
+                const f32x4 v = s4[z];
+                m = nanmax(nanmax(m, v[0]), nanmax(nanmax(v[1], v[2]), v[3]));
+            }
+            __builtin_nontemporal_store(m, xy + ((size_t)b * J + j) * XY + c0 + cc);
+        }
+    } else if constexpr (MODE == FULL || MODE == NO_TAPS) {
+        __syncthreads();
+        for (int j = 0; j < J; ++j) {
+            float *__restrict__ dst = cube + ((size_t)b * J + j) * N + n0;
+            for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(stage[j * SP + e], dst + e);
+        }
+        for (int e = threadIdx.x; e < J * ncols; e += 256) {
+            const int j = e / ncols, cc = e - (e / ncols) * ncols;
+            const float *s = stage + j * SP + cc * Z;
+            float m = -INFINITY;
+            for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+            __builtin_nontemporal_store(m, xy + ((size_t)b * J + j) * XY + c0 + cc);
+        }
+    } else {
+        if (fold == 0x7f7f7f7fu) sink[blockIdx.x * 256 + threadIdx.x] = 1.0f;  // keeps the loads alive
+    }
+}
+
+
+// CAM_OUTER: the same block (cols whole columns, 16-row bands, XCD remap) with
+// the loop order turned: camera outer, the block's PASSES voxel passes inner,
+// PASSES x 4 accumulators per lane carried across the cameras.  Each voxel
+// still sums its cameras in order (bit-identical).  Per (camera, pass) each
+// lane loads its voxel's 8-B coordinate (the 4 lanes of a group share the
+// address) and sets up the taps itself.  Aim: the blocks resident on an XCD
+// work through the cameras together, so the L2 holds about one camera image
+// of a frame (2 MB at C2) instead of all five, and a wave keeps PASSES x 4
+// tap loads in flight.
+template <int PASSES>
+__global__ __launch_bounds__(256, 4) void cam_outer_kernel(const float *__restrict__ tab, const float *__restrict__ grids,
+                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
+                                                           int J, int H, int W, int X, int Y, int Z, int cols,
+                                                           int col_blocks, int SP, int band) {
+    constexpr int LPV = 4, VPP = 64;
+    extern __shared__ __attribute__((aligned(16))) float stage[];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int b = L / col_blocks;
+    const int XY = X * Y;
+    int cb = L - b * col_blocks;
+    if (band > 0) {
+        const int gpr = Y / cols;
+        const int per_band = band * gpr;
+        const int bi = cb / per_band, r = cb - bi * per_band;
+        const int rows = min(band, X - bi * band);
+        const int gc = r / rows, xr = r - gc * rows;
+        cb = (bi * band + xr) * gpr + gc;
+    }
+    const int c0 = cb * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(grids, (unsigned)(N * GV * 8));
+    const unsigned unit = 64u;
+    const unsigned img = (unsigned)(H * W) * unit;
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)b * V * img;
+    float acc[PASSES][4];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[p][m] = 0.0f;
+    for (int v = 0; v < V; ++v) {
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+#pragma unroll
+        for (int p = 0; p < PASSES; ++p) {
+            const int i = p * VPP + threadIdx.x / LPV;
+            const bool valid = i < T;
+            const int ii = min(i, T - 1);
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 graw = __builtin_amdgcn_raw_buffer_load_b64(grs, (unsigned)(((n0 + ii) * GV + v) * 8), 0, 0);
+            const float gx = valid ? __builtin_bit_cast(float, (unsigned)graw[0]) : -2.0f;
+            const float gy = valid ? __builtin_bit_cast(float, (unsigned)graw[1]) : -2.0f;
+            const Taps4<false> t = setup_taps<false>(gx, gy, sxs, sys, W, H, unit);
+            const unsigned all = t.o[0] & t.o[1] & t.o[2] & t.o[3];
+            if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) continue;
+            const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, t.o[0] + qo, 0, 0);
+            const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, t.o[1] + qo, 0, 0);
+            const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, t.o[2] + qo, 0, 0);
+            const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, t.o[3] + qo, 0, 0);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
+                const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
+                const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
+                const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
+                acc[p][m] = acc[p][m] + __builtin_fmaf(fd, t.w[3], __builtin_fmaf(fc, t.w[2],
+                                                       __builtin_fmaf(fb, t.w[1], fa * t.w[0])));
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+        const int i = p * VPP + threadIdx.x / LPV;
+        if (i < T) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + i] = clampf((acc[p][m] + 0.0f) / fV, 0.0f, 1.0f);
+        }
+    }
+    __syncthreads();
+    for (int j = 0; j < J; ++j) {
+        float *__restrict__ dst = cube + ((size_t)b * J + j) * N + n0;
+        for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(stage[j * SP + e], dst + e);
+    }
+    for (int e = threadIdx.x; e < J * ncols; e += 256) {
+        const int j = e / ncols, cc = e - (e / ncols) * ncols;
+        const float *s = stage + j * SP + cc * Z;
+        float m = -INFINITY;
+        for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+        __builtin_nontemporal_store(m, xy + ((size_t)b * J + j) * XY + c0 + cc);
+    }
+}
+
+extern "C" int gather_probe(int mode, const float *tab, const float *grids, float *cube, float *xy, float *sink, int B,
+                            int V, int J, int H, int W, int X, int Y, int Z, int cols, int band, void *stream) {
+    const int col_blocks = (X * Y + cols - 1) / cols;
+    const int T = cols * Z;
+    const int SP = ((size_t)16 * 4 * (T + 1) > 20480 && (size_t)16 * 4 * T <= 20480) ? T : T + 1;
+    const size_t lds = (size_t)4 * 4 * 4 * SP;
+    const dim3 grid((unsigned)(B * col_blocks)), blk(256);
+    hipStream_t s = (hipStream_t)stream;
+#define GO(M) hipLaunchKernelGGL((probe_kernel<M>), grid, blk, lds, s, tab, grids, cube, xy, sink, V, J, H, W, X, Y, Z, \
+                                 cols, col_blocks, SP, band)
+    switch (mode) {
+        case FULL: GO(FULL); break;
+        case TAPS: GO(TAPS); break;
+        case TAPS_L1: GO(TAPS_L1); break;
+        case TAPS_SKIP_OOB: GO(TAPS_SKIP_OOB); break;
+        case TAPS_ALL_OOB: GO(TAPS_ALL_OOB); break;
+        case NO_TAPS: GO(NO_TAPS); break;
+        case TAPS_2ROW: GO(TAPS_2ROW); break;
+        case NOSTORE: GO(NOSTORE); break;
+        case FULL2: if (T % 4 || SP % 4 || Z % 4) return -3; GO(FULL2); break;
+        case STORES_ONLY: if (T % 4 || SP % 4 || Z % 4) return -3; GO(STORES_ONLY); break;
+        case 7:  // CAM_OUTER, 5 passes of 64 voxels (cols * Z <= 320)
+            if (T > 320) return -2;
+            hipLaunchKernelGGL((cam_outer_kernel<5>), grid, blk, lds, s, tab, grids, cube, xy, V, J, H, W, X, Y, Z, cols,
+                               col_blocks, SP, band);
+            break;
+        default: return -1;
+    }
+#undef GO
+    return (int)hipGetLastError();
+}

@@ -17,8 +17,11 @@ step() {  # name timeout cmd...
 }
 for s in ${STEPS:-tests bench prof pmc}; do
   case $s in
-    tests) step tests 600 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -rf ;;
+    tests) step tests 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -rf ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    probe) step probe 300 python tools/gather_probe.py ${PROBE_ARGS:-} ;;
+    probe_prof) step probe_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${R}_probe_prof -o run -- \
+            python3 tools/gather_probe.py --iters 20 ${PROBE_ARGS:-} ;;
     prof) step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${R}_prof -o run -- \
             python3 bench.py --traffic off --cpu-baseline off ${BENCH_ARGS:-} ;;
     pmc) PMC_GROUPS="FETCH_SIZE

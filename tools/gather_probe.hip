@@ -312,3 +312,186 @@ extern "C" int gather_probe(int mode, const float *tab, const float *grids, floa
 #undef GO
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// LDS prototype (planar fp32 input, packed grid, V <= 16, NF = 1): no layout
+// pass.  Block = (frame, joint group of 4, tile of TX x TY whole columns).
+// Per camera in view order: every slot's tap setup, the block's footprint
+// box over its in-image taps (LDS min/max), then per band of rows: the box's
+// rows of the 4 joint planes staged into LDS as [pixel][4] (dwordx4 loads
+// along x, register transpose, swizzled ds_write_b128), and each voxel whose
+// top tap row falls in the band reads its 4 taps with ds_read_b128.  Each
+// voxel sums its cameras in order (bit-identical to the product gather).
+constexpr int kLdsTB = 512;
+constexpr int kBufPx = 2048;  // pixels per band buffer (16 B each)
+
+__device__ __forceinline__ int lds_slot(int p) {  // conflict-free b128 writes of 4-pixel runs
+    return (p & ~3) | ((p & 3) ^ ((p >> 3) & 3));
+}
+
+template <int SLOTS>
+__global__ __launch_bounds__(kLdsTB, 2) void lds_gather_kernel(const float *__restrict__ hm, const float *__restrict__ grids,
+                                                                 float *__restrict__ cube, float *__restrict__ xy, int V,
+                                                                 int J, int H, int W, int X, int Y, int Z, int TX, int TY) {
+    __shared__ f32x4 buf[kBufPx];
+    __shared__ int bbox[4];
+    const int tiles_y = Y / TY, tiles = (X / TX) * tiles_y;
+    const int JG = (J + 3) / 4;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = L % tiles, rest = L / tiles;
+    const int g = rest % JG, b = rest / JG;
+    const int xt = (tile / tiles_y) * TX, yt = (tile % tiles_y) * TY;
+    const int T = TX * TY * Z;
+    const int HW = H * W;
+    const int GV = V + (V & 1);
+    const long long N = (long long)X * Y * Z;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(grids, (unsigned)(N * GV * 8));
+    long long nvox[SLOTS];
+    bool sval[SLOTS];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+        const int i = s * kLdsTB + (int)threadIdx.x;
+        sval[s] = i < T;
+        const int ii = min(i, T - 1);
+        const int c = ii / Z, z = ii - c * Z;
+        nvox[s] = ((long long)(xt + c / TY) * Y + (yt + c % TY)) * Z + z;
+    }
+    float acc[SLOTS][4];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[s][m] = 0.0f;
+    for (int v = 0; v < V; ++v) {
+        // the view's 4 joint planes of this group (planes past J read 0: buffer range)
+        const float *planes = hm + (((size_t)b * V + v) * J + 4 * g) * HW;
+        const __amdgpu_buffer_rsrc_t prs = uniform_rsrc(planes, (unsigned)((J - 4 * g) * HW * 4));
+        int x0[SLOTS], y0[SLOTS];
+        float w[SLOTS][4];
+        unsigned msk[SLOTS];  // bit m: tap m in the image (nw, ne, sw, se)
+        int bx0 = 1 << 30, bx1 = -1, by0 = 1 << 30, by1 = -1;
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s) {
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 gr = __builtin_amdgcn_raw_buffer_load_b64(grs, (unsigned)((nvox[s] * GV + v) * 8), 0, 0);
+            const float gx = sval[s] ? __builtin_bit_cast(float, (unsigned)gr[0]) : -2.0f;
+            const float gy = sval[s] ? __builtin_bit_cast(float, (unsigned)gr[1]) : -2.0f;
+            // setup_taps arithmetic (fvp_layout.h), pixel units
+            const float ix = (gx + 1.0f) * sxs, iy = (gy + 1.0f) * sys;
+            const float x0f = floorf(ix), y0f = floorf(iy);
+            const float wx = ix - x0f, ex = 1.0f - wx;
+            const float ny = iy - y0f, syw = 1.0f - ny;
+            w[s][0] = syw * ex; w[s][1] = syw * wx; w[s][2] = ny * ex; w[s][3] = ny * wx;
+            int xx, yy;
+            tap_origin(ix, iy, W, H, xx, yy);
+            x0[s] = xx; y0[s] = yy;
+            const bool vx0 = (unsigned)xx < (unsigned)W, vx1 = (unsigned)(xx + 1) < (unsigned)W;
+            const bool vy0 = (unsigned)yy < (unsigned)H, vy1 = (unsigned)(yy + 1) < (unsigned)H;
+            msk[s] = (unsigned)(vy0 & vx0) | ((unsigned)(vy0 & vx1) << 1) | ((unsigned)(vy1 & vx0) << 2) |
+                     ((unsigned)(vy1 & vx1) << 3);
+            if (msk[s]) {
+                bx0 = min(bx0, vx0 ? xx : xx + 1); bx1 = max(bx1, vx1 ? xx + 1 : xx);
+                by0 = min(by0, vy0 ? yy : yy + 1); by1 = max(by1, vy1 ? yy + 1 : yy);
+            }
+        }
+        // block footprint box
+        if (threadIdx.x == 0) { bbox[0] = 1 << 30; bbox[1] = -1; bbox[2] = 1 << 30; bbox[3] = -1; }
+        __syncthreads();
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            bx0 = min(bx0, __shfl_xor(bx0, o)); bx1 = max(bx1, __shfl_xor(bx1, o));
+            by0 = min(by0, __shfl_xor(by0, o)); by1 = max(by1, __shfl_xor(by1, o));
+        }
+        if ((threadIdx.x & 63) == 0 && bx1 >= 0) {
+            atomicMin(&bbox[0], bx0); atomicMax(&bbox[1], bx1); atomicMin(&bbox[2], by0); atomicMax(&bbox[3], by1);
+        }
+        __syncthreads();
+        const int Bx0 = bbox[0] & ~3, Bx1 = bbox[1], By0 = bbox[2], By1 = bbox[3];
+        __syncthreads();  // (bbox is rewritten for the next camera)
+        if (Bx1 < 0) continue;  // no tap of this camera in the image: every voxel adds 0
+        const int bw = ((Bx1 - Bx0 + 1) + 3) & ~3;
+        const int R = kBufPx / bw - 1;  // band rows of top taps (>= 7: bw <= W + 3)
+        for (int r0 = By0; r0 < max(By1, By0 + 1); r0 += R) {
+            const int rl = min(r0 + R, By1);  // staged rows r0..rl
+            const int quads = (rl - r0 + 1) * (bw >> 2);
+            for (int qd = threadIdx.x; qd < quads; qd += kLdsTB) {
+                const int row = qd / (bw >> 2), cq = qd - row * (bw >> 2);
+                const unsigned off = (unsigned)(((r0 + row) * W + Bx0 + 4 * cq) * 4);
+                u32x4 p[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) p[j] = __builtin_amdgcn_raw_buffer_load_b128(prs, off + (unsigned)(j * HW * 4), 0, 0);
+                const int pix = row * bw + 4 * cq;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    f32x4 px;
+                    px[0] = __builtin_bit_cast(float, (unsigned)p[0][k]);
+                    px[1] = __builtin_bit_cast(float, (unsigned)p[1][k]);
+                    px[2] = __builtin_bit_cast(float, (unsigned)p[2][k]);
+                    px[3] = __builtin_bit_cast(float, (unsigned)p[3][k]);
+                    buf[lds_slot(pix + k)] = px;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < SLOTS; ++s) {
+                const int yb = max(y0[s], By0);  // (a top row above the box is off-image)
+                if (!msk[s] || yb < r0 || (yb >= r0 + R && r0 + R <= By1)) continue;
+                const int pb = (y0[s] - r0) * bw + (x0[s] - Bx0);
+                f32x4 t[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int pm = pb + (m >> 1) * bw + (m & 1);
+                    t[m] = (msk[s] >> m) & 1 ? buf[lds_slot(pm)] : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    acc[s][m] = acc[s][m] + __builtin_fmaf(t[3][m], w[s][3], __builtin_fmaf(t[2][m], w[s][2],
+                                                            __builtin_fmaf(t[1][m], w[s][1], t[0][m] * w[s][0])));
+            }
+            __syncthreads();
+            if (r0 + R > By1) break;
+        }
+    }
+    // epilogue: cube (runs of Z along each column) and the z-max via LDS
+    const float fV = (float)V;
+    float *stage = reinterpret_cast<float *>(buf);  // [4][T] (T <= 2048)
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+        const int i = s * kLdsTB + (int)threadIdx.x;
+        if (!sval[s]) continue;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float val = clampf((acc[s][m] + 0.0f) / fV, 0.0f, 1.0f);
+            const int j = 4 * g + m;
+            if (j < J) __builtin_nontemporal_store(val, cube + ((size_t)b * J + j) * N + nvox[s]);
+            stage[m * T + i] = val;
+        }
+    }
+    __syncthreads();
+    const int ncol = TX * TY;
+    for (int e = threadIdx.x; e < 4 * ncol; e += kLdsTB) {
+        const int m = e / ncol, c = e - m * ncol;
+        const int j = 4 * g + m;
+        if (j >= J) continue;
+        float mx = -INFINITY;
+        for (int z = 0; z < Z; ++z) mx = nanmax(mx, stage[m * T + c * Z + z]);
+        __builtin_nontemporal_store(mx, xy + ((size_t)b * J + j) * X * Y + (size_t)(xt + c / TY) * Y + (yt + c % TY));
+    }
+}
+
+extern "C" int lds_gather_probe(const float *hm, const float *grids, float *cube, float *xy, int B, int V, int J, int H,
+                                int W, int X, int Y, int Z, int TX, int TY, void *stream) {
+    const int T = TX * TY * Z;
+    if (X % TX || Y % TY || T > 2048 || 4 * T > 4 * kBufPx || V > 16) return -1;
+    const int slots = (T + kLdsTB - 1) / kLdsTB;
+    const dim3 grid((unsigned)(B * ((J + 3) / 4) * (X / TX) * (Y / TY))), blk(kLdsTB);
+    hipStream_t s = (hipStream_t)stream;
+    switch (slots) {
+        case 1: hipLaunchKernelGGL(lds_gather_kernel<1>, grid, blk, 0, s, hm, grids, cube, xy, V, J, H, W, X, Y, Z, TX, TY); break;
+        case 2: hipLaunchKernelGGL(lds_gather_kernel<2>, grid, blk, 0, s, hm, grids, cube, xy, V, J, H, W, X, Y, Z, TX, TY); break;
+        case 3: hipLaunchKernelGGL(lds_gather_kernel<3>, grid, blk, 0, s, hm, grids, cube, xy, V, J, H, W, X, Y, Z, TX, TY); break;
+        case 4: hipLaunchKernelGGL(lds_gather_kernel<4>, grid, blk, 0, s, hm, grids, cube, xy, V, J, H, W, X, Y, Z, TX, TY); break;
+        default: return -2;
+    }
+    return (int)hipGetLastError();
+}

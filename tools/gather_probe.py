@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--modes", default=",".join(MODES))
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--lds-tiles", default="8x8,4x8,8x4,4x4,8x10,10x8", help="LDS prototype tiles (TXxTY columns)")
     args = ap.parse_args()
     path = build()
     if args.build_only:
@@ -61,6 +62,7 @@ def main():
 
     lib = ctypes.CDLL(path)
     lib.gather_probe.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 5 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
+    lib.lds_gather_probe.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
     dev = torch.device("cuda:0")
     w = WORKLOADS[args.workload]
     cams, seq = w.cameras()
@@ -108,6 +110,26 @@ def main():
     taps = B * X * Y * Z * V
     print(json.dumps({"mode": "product fvp_voxelize_cl", "us": round(us, 2), "frames": B, "workload": w.name}),
           flush=True)
+    # the headline op on the same frames: planar heatmaps, layout pass + gather
+    us = timed(lambda: ops.voxelize(hm, grids, None, X, Y, Z, True, True))
+    print(json.dumps({"mode": "product fvp_voxelize (planar: layout + gather)", "us": round(us, 2), "frames": B}),
+          flush=True)
+    for tile in [t for t in args.lds_tiles.split(",") if t]:
+        TX, TY = map(int, tile.split("x"))
+
+        def lds():
+            rc = lib.lds_gather_probe(hm.data_ptr(), grids.data_ptr(), cube.data_ptr(), xy.data_ptr(), B, V, J, Hd,
+                                      Wd, X, Y, Z, TX, TY, stream.cuda_stream)
+            assert rc == 0, (tile, rc)
+        cube.zero_()
+        xy.zero_()
+        lds()
+        torch.cuda.synchronize()
+        same = torch.equal(cube, ref_cube) and torch.equal(xy, ref_xy)
+        ndiff = int((cube != ref_cube).sum())
+        us = timed(lds)
+        print(json.dumps({"mode": f"LDS planar {tile}", "us": round(us, 2), "frames": B, "bit_exact": same,
+                          "cube_values_differing": ndiff}), flush=True)
     for name in args.modes.split(","):
         if name in EXACT:
             cube.zero_()

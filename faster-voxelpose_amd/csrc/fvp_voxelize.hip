@@ -358,7 +358,6 @@ struct GatherCfg {
 
 template <int LPV, bool OTF>
 static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg &c) {
-    // on the fly: smaller blocks (128 voxels) -- the coordinate VALU per pass is larger (C5: -2 %)
     // Column groups that tile the x-rows exactly (largest divisor of Y, if it
     // keeps at least half the columns), so the blocks can be walked in bands of
     // 16 x-rows: the blocks resident on an XCD at a time then cover a compact
@@ -374,7 +373,9 @@ static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg 
         return c;
     };
     auto blocks = [&](int c) { return (long long)frames / NF * ((X * Y + c - 1) / c); };
-    int cols = snap(OTF ? (Z >= 128 ? 1 : 128 / Z) : cols_per_block(Z));
+    // on the fly: 256-voxel blocks (C5: 4 columns of 64; 128-voxel blocks
+    // measured 2-4 % slower, 64 -> 8 % slower, 512 -> 40 % slower, round 3)
+    int cols = snap(OTF ? (Z >= 256 ? 1 : 256 / Z) : cols_per_block(Z));
     // latency (few frames): one pass of 256/LPV voxels per block, so a single
     // frame spreads over enough blocks to fill the CUs -- or two passes when
     // one-pass blocks would overflow one round of 8 blocks per CU (the counts

@@ -70,13 +70,16 @@ class FvpOptions:
       exceed recompute_cube_bytes (a memory saving: the TD-bound gather hides
       the cube writes, so below that the one-launch NMS + column gather is as
       fast or faster).  Default from the environment variable
-      FVP_RECOMPUTE_COLUMNS (0 / 1) when set."""
+      FVP_RECOMPUTE_COLUMNS (0 / 1) when set.
+    c2c_graphs: with cnn, the launch-bound 1-D C2CNet replays from a
+      hipGraph per column-batch shape (fvp.cnn.GraphedCNN)."""
     cnn: bool = False
     cnn_dtype: torch.dtype = torch.float32
     backbone: bool = False
     backbone_dtype: torch.dtype = torch.float32
     recompute_columns: bool | None = dataclasses.field(default_factory=_env_recompute)
     recompute_cube_bytes: int = 512 << 20
+    c2c_graphs: bool = True
 
 
 DEFAULT_OPTIONS = FvpOptions()
@@ -200,7 +203,7 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     match_bbox = proposal.gather_bbox(bbox_preds, flat)
     c2c = self.c2c_net
     if opts.cnn and not c2c.training:
-        c2c = fvp_cnn.cached(c2c, opts.cnn_dtype)
+        c2c = fvp_cnn.cached(c2c, opts.cnn_dtype, graphs=opts.c2c_graphs)
     hm1d = c2c(torch.flatten(columns, 0, 1)).view(batch_size, self.max_people, -1)
     pl = self.proposal_layer
     if pl.training and ("roots_3d" in meta and "num_person" in meta):  # GT matching (training)

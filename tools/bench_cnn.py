@@ -88,8 +88,11 @@ def main():
                                      lambda: (cn.output_hm(cn.encoder_decoder(cn.front_layers(x_hdn))),), x_hdn)):
             fl = flops(f_p2p if name.startswith("p2p") else (lambda t: f_cn.from_xy(t)), x)
             t_f, t_t, t_b = timeit(fv), timeit(tv), timeit(bv)
+            from fvp.graphs import CapturedStep
+            t_g = timeit(CapturedStep(fv).replay)  # the same launches replayed from one hipGraph
             out[name] = {"images": int(x.shape[0]), "shape": list(x.shape[1:]), "gflop": round(fl / 1e9, 3),
                          "fvp_ms": round(t_f, 4), "torch_ms": round(t_t, 4),
+                         "fvp_graph_ms": round(t_g, 4), "fvp_graph_tflops": round(fl / (t_g * 1e-3) / 1e12, 2),
                          "fvp_tflops": round(fl / (t_f * 1e-3) / 1e12, 2),
                          "mfma_frac_of_f32_peak": round(fl / (t_f * 1e-3) / 1e12 / MFMA_F32_PEAK_TF, 4),
                          "speedup_vs_torch": round(t_t / t_f, 3),
@@ -106,8 +109,11 @@ def main():
         f_c2c, f_wn = cnn.FvpCNN(c2c), cnn.FvpWeightNet(wn)
         fl = flops(lambda t: f_c2c(t), x_col)
         t_f, t_t = timeit(lambda: f_c2c(x_col)), timeit(lambda: c2c(x_col))
+        from fvp.graphs import CapturedStep
+        t_g = timeit(CapturedStep(lambda: f_c2c(x_col)).replay)
         out["c2cnet_hdn"] = {"columns": int(x_col.shape[0]), "shape": list(x_col.shape[1:]),
                              "gflop": round(fl / 1e9, 4), "fvp_ms": round(t_f, 4), "torch_ms": round(t_t, 4),
+                             "fvp_graph_ms": round(t_g, 4),
                              "speedup_vs_torch": round(t_t / t_f, 3)}
         t_f, t_t = timeit(lambda: f_wn(x_feat)), timeit(lambda: wn(x_feat))
         nbytes = x_feat.numel() * 4

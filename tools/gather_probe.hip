@@ -22,13 +22,15 @@
 //   FULL2         FULL with a vector epilogue: float4 non-temporal cube stores
 //                 from LDS, float4 LDS reads for the z-max (Z % 4 == 0)
 //   STORES_ONLY   no main loop: the epilogue's LDS reads and cube / xy stores
+//   TAPS_L2       TAPS with in-image offsets folded into 512 KB per camera
+//                 image (the frame's 5 images, 2.5 MB, fit the XCD's 4 MB L2)
 // Test tooling only (tools/gather_probe.py); not part of libfvp.
 #include "../faster-voxelpose_amd/csrc/fvp_layout.h"
 
 using namespace fvp;
 
 enum { FULL = 0, TAPS = 1, TAPS_L1 = 2, TAPS_SKIP_OOB = 3, TAPS_ALL_OOB = 4, NO_TAPS = 5, TAPS_2ROW = 6,
-       NOSTORE = 8, FULL2 = 9, STORES_ONLY = 10 };
+       NOSTORE = 8, FULL2 = 9, STORES_ONLY = 10, TAPS_L2 = 11 };
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int MODE>
@@ -99,6 +101,10 @@ __global__ __launch_bounds__(256, 8) void probe_kernel(const float *__restrict__
                 if constexpr (MODE == TAPS_L1) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m) o[m] &= 0x3FC0u;
+                }
+                if constexpr (MODE == TAPS_L2) {  // 512 KB per camera image: the frame's 5 fit one XCD's L2
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) o[m] = (o[m] & kOOB) ? o[m] : (o[m] & 0x7FFC0u);
                 }
                 if constexpr (MODE == TAPS_ALL_OOB) {
 #pragma unroll
@@ -302,6 +308,7 @@ extern "C" int gather_probe(int mode, const float *tab, const float *grids, floa
         case NOSTORE: GO(NOSTORE); break;
         case FULL2: if (T % 4 || SP % 4 || Z % 4) return -3; GO(FULL2); break;
         case STORES_ONLY: if (T % 4 || SP % 4 || Z % 4) return -3; GO(STORES_ONLY); break;
+        case TAPS_L2: GO(TAPS_L2); break;
         case 7:  // CAM_OUTER, 5 passes of 64 voxels (cols * Z <= 320)
             if (T > 320) return -2;
             hipLaunchKernelGGL((cam_outer_kernel<5>), grid, blk, lds, s, tab, grids, cube, xy, V, J, H, W, X, Y, Z, cols,

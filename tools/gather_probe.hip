@@ -502,3 +502,52 @@ extern "C" int lds_gather_probe(const float *hm, const float *grids, float *cube
     }
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Layout-pass candidates (planar [b][V][J][H*W] fp32 -> [b][V][H*W][16], J <= 16).
+// LAYOUT_T (shipped heatmaps_to_cl_kernel<4>): thread = (pixel, joint quad),
+// 4 plane loads whose adjacent lanes hit 4 different planes, one coalesced
+// float4 store.  LAYOUT_C: a wave loads 64 consecutive pixels of ONE plane per
+// instruction (coalesced 256 B), the 4x4 quad goes through LDS so the store
+// is a coalesced 1 KiB run; LAYOUT_S: the same loads, the float4 stored
+// straight from registers (16 B per lane at a 64-B stride).
+template <bool VIA_LDS>
+__global__ __launch_bounds__(256) void layout_c_kernel(const float *__restrict__ hm, f32x4 *__restrict__ cl, int J,
+                                                       int HW, long long total_px) {
+    __shared__ f32x4 t4[256];
+    const int px = threadIdx.x & 63, qd = threadIdx.x >> 6;
+    const long long p0 = (long long)blockIdx.x * 64;  // first pixel of the block (never straddles a view: HW % 64 == 0)
+    const long long bv = p0 / HW;
+    const int pix = (int)(p0 - bv * HW) + px;
+    const float *src = hm + (size_t)bv * J * HW + pix;
+    f32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * qd + k;
+        o[k] = j < J ? src[(size_t)j * HW] : 0.0f;
+    }
+    if constexpr (VIA_LDS) {
+        t4[px * 4 + qd] = o;
+        __syncthreads();
+        cl[p0 * 4 + threadIdx.x] = t4[threadIdx.x];
+    } else {
+        cl[(p0 + px) * 4 + qd] = o;
+    }
+}
+
+extern "C" int layout_probe(int mode, const float *hm, float *cl, int B, int V, int J, int H, int W, void *stream) {
+    const long long px = (long long)B * V * H * W;
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == 0) {  // the thread-per-(pixel, quad) kernel (round 2's layout pass)
+        hipLaunchKernelGGL((heatmaps_to_cl_kernel<4, float, 1>), dim3((unsigned)((px * 4 + 255) / 256)), dim3(256), 0, s,
+                           hm, reinterpret_cast<float4 *>(cl), J, J, H * W, V, px);
+    } else {
+        if ((H * W) % 64 || J > 16) return -1;
+        const dim3 grid((unsigned)(px / 64));
+        if (mode == 1)
+            hipLaunchKernelGGL(layout_c_kernel<true>, grid, dim3(256), 0, s, hm, reinterpret_cast<f32x4 *>(cl), J, H * W, px);
+        else
+            hipLaunchKernelGGL(layout_c_kernel<false>, grid, dim3(256), 0, s, hm, reinterpret_cast<f32x4 *>(cl), J, H * W, px);
+    }
+    return (int)hipGetLastError();
+}

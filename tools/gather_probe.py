@@ -63,6 +63,7 @@ def main():
     lib = ctypes.CDLL(path)
     lib.gather_probe.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 5 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
     lib.lds_gather_probe.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 10 + [ctypes.c_void_p]
+    lib.layout_probe.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p]
     dev = torch.device("cuda:0")
     w = WORKLOADS[args.workload]
     cams, seq = w.cameras()
@@ -110,6 +111,21 @@ def main():
     taps = B * X * Y * Z * V
     print(json.dumps({"mode": "product fvp_voxelize_cl", "us": round(us, 2), "frames": B, "workload": w.name}),
           flush=True)
+    # layout-pass candidates (tools/gather_probe.hip layout_probe): same output bytes
+    outs = {}
+    for lm, lname in ((0, "LAYOUT_T shipped"), (1, "LAYOUT_C via LDS"), (2, "LAYOUT_S strided store")):
+        dst = torch.full((B, V, Hd * Wd, 16), 7.0, device=dev)
+
+        def lay():
+            rc = lib.layout_probe(lm, hm.data_ptr(), dst.data_ptr(), B, V, J, Hd, Wd, stream.cuda_stream)
+            assert rc == 0, rc
+        lay()
+        torch.cuda.synchronize()
+        outs[lm] = dst.clone()
+        us = timed(lay)
+        print(json.dumps({"mode": lname, "us": round(us, 2), "frames": B,
+                          "same_as_shipped": bool(torch.equal(outs[lm], outs[0]))}), flush=True)
+    del outs
     # the headline op on the same frames: planar heatmaps, layout pass + gather
     us = timed(lambda: ops.voxelize(hm, grids, None, X, Y, Z, True, True))
     print(json.dumps({"mode": "product fvp_voxelize (planar: layout + gather)", "us": round(us, 2), "frames": B}),

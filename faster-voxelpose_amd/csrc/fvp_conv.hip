@@ -97,25 +97,26 @@ __device__ __forceinline__ void load_chunk(const ConvArgs &a, const float *__res
     constexpr int AV = AE >= 256 ? AE / 256 : 1;   // per thread
     constexpr int BV = TL::KC * TL::BN / 4 / 256;  // float4 per thread (B), may be 0
     const int t = threadIdx.x;
+    constexpr int Q = TL::KC / 4;                  // float4 per pixel row of a chunk
     if (a.Cpi >= TL::KC) {  // one tap per chunk (Cpi % KC == 0)
         const int cpc = a.Cpi / TL::KC;  // chunks per tap
         const int tap = chunk / cpc, c = chunk - tap * cpc;
         const int ky = tap / a.KW, kx = tap - ky * a.KW;
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
-            const int e = u * 256 + t;  // -> (pixel e/4, 4 channels)
+            const int e = u * 256 + t;  // -> (pixel e/Q, 4 channels)
             const int y = pr[u].y + ky, x = pr[u].x + kx;
             av[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (e < AE && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W)
                 av[u] = *reinterpret_cast<const float4 *>(pr[u].p + ((size_t)y * a.W + x) * a.Cpi + c * TL::KC +
-                                                         (e & 3) * 4);
+                                                         (e % Q) * 4);
         }
-    } else {  // Cpi in {4, 8, 12}: each float4 is 4 channels of its own tap; k past the taps reads 0
+    } else {  // Cpi < KC (4 / 8 / 12 at KC = 16): each float4 is 4 channels of its own tap; k past the taps reads 0
         const int ntaps = a.KH * a.KW;
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
             const int e = u * 256 + t;
-            const int k = chunk * TL::KC + (e & 3) * 4;
+            const int k = chunk * TL::KC + (e % Q) * 4;
             const int tap = k / a.Cpi, ci = k - tap * a.Cpi;
             const int ky = tap / a.KW, kx = tap - ky * a.KW;
             const int y = pr[u].y + ky, x = pr[u].x + kx;
@@ -302,7 +303,7 @@ __device__ __forceinline__ void conv_tile(int &mt, int &nt) {
     mt = (int)(id / gridDim.y);
 }
 
-template <class TL>
+template <class TL, int PF = 1>
 __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
     constexpr int BM = TL::BM, BN = TL::BN, KC = TL::KC, AP = TL::AP, MS = TL::MS;
     constexpr int AE = BM * KC / 4;
@@ -336,14 +337,15 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
 
     PixRef pr[AV];
 #pragma unroll
-    for (int u = 0; u < AV; ++u) pix_ref(a, m0 + ((u * 256 + t) >> 2), M, py, px, pr[u]);
-    float4 av[AV], bv[BVN];
-    auto stage = [&](int buf) {  // registers -> LDS buffer buf
+    for (int u = 0; u < AV; ++u) pix_ref(a, m0 + (u * 256 + t) / (KC / 4), M, py, px, pr[u]);
+    using AReg = float4[AV];
+    using BReg = float4[BVN];
+    auto stage = [&](int buf, const AReg &av, const BReg &bv) {  // registers -> LDS buffer buf
 #pragma unroll
         for (int u = 0; u < AV; ++u) {
             const int e = u * 256 + t;
             if (e >= AE) break;
-            float *ap = &As[buf][(e >> 2) * AP + (e & 3) * 4];
+            float *ap = &As[buf][(e / (KC / 4)) * AP + (e % (KC / 4)) * 4];
             ap[0] = av[u].x; ap[1] = av[u].y; ap[2] = av[u].z; ap[3] = av[u].w;
         }
         if constexpr (KC * BN / 4 >= 256) {
@@ -356,17 +358,7 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
             *reinterpret_cast<float4 *>(&Bs[buf][(t / (BN / 4)) * BN + (t % (BN / 4)) * 4]) = bv[0];
         }
     };
-    load_chunk<TL>(a, w, n0, cb, pr, av, bv);
-    stage(cb & 1);
-    __syncthreads();
-    // One barrier per chunk: chunk ch+1's global loads are issued first, the
-    // MFMAs of chunk ch next, and the loaded registers go to the other buffer
-    // after the last MFMA has issued (it was last read before the previous
-    // barrier), so the LDS stores and the barrier overlap the MFMA tail.
-    for (int ch = cb; ch < ce; ++ch) {
-        const int buf = ch & 1;
-        const bool more = ch + 1 < ce;
-        if (more) load_chunk<TL>(a, w, n0, ch + 1, pr, av, bv);
+    auto mfma = [&](int buf) {
 #pragma unroll
         for (int kk = 0; kk < KC / TL::KSTEP; ++kk) {
             float fa[TL::TM], fb[TL::TN];
@@ -390,8 +382,41 @@ __global__ __launch_bounds__(256, 4) void conv_mfma_kernel(ConvArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
                 }
         }
-        if (more) stage(buf ^ 1);
+    };
+    float4 av[AV], bv[BVN];
+    load_chunk<TL>(a, w, n0, cb, pr, av, bv);
+    stage(cb & 1, av, bv);
+    if constexpr (PF == 1) {
         __syncthreads();
+        // One barrier per chunk: chunk ch+1's global loads are issued first, the
+        // MFMAs of chunk ch next, and the loaded registers go to the other buffer
+        // after the last MFMA has issued (it was last read before the previous
+        // barrier), so the LDS stores and the barrier overlap the MFMA tail.
+        for (int ch = cb; ch < ce; ++ch) {
+            const bool more = ch + 1 < ce;
+            if (more) load_chunk<TL>(a, w, n0, ch + 1, pr, av, bv);
+            mfma(ch & 1);
+            if (more) stage((ch & 1) ^ 1, av, bv);
+            __syncthreads();
+        }
+    } else {
+        // Two chunks in flight: chunk ch+2 is loaded into the register set that
+        // chunk ch came through while chunk ch+1's registers (loaded one
+        // iteration earlier) go to LDS -- a global round trip per two chunks of
+        // MFMA work instead of one (the short-K-walk small tiles).
+        float4 av2[AV], bv2[BVN];
+        if (cb + 1 < ce) load_chunk<TL>(a, w, n0, cb + 1, pr, av2, bv2);
+        __syncthreads();
+        auto step = [&](int ch, AReg &la, BReg &lb, const AReg &sa, const BReg &sb) {
+            if (ch + 2 < ce) load_chunk<TL>(a, w, n0, ch + 2, pr, la, lb);
+            mfma(ch & 1);
+            if (ch + 1 < ce) stage((ch & 1) ^ 1, sa, sb);
+            __syncthreads();
+        };
+        for (int ch = cb; ch < ce; ch += 2) {
+            step(ch, av, bv, av2, bv2);
+            if (ch + 1 < ce) step(ch + 1, av2, bv2, av, bv);
+        }
     }
 
     if (a.part) {  // split-K: raw partial sums, combined in z order by conv_splitk_reduce
@@ -596,7 +621,9 @@ using TileN32s = Tile<64, 32, 16, 4>;   //             4 waves x (16 px x 32 ch)
 using TileN64 = Tile<128, 64, 32, 2>;   // wider: 2x2 waves x (64 px x 32 ch), 2 accumulators
 using TileN64m = Tile<64, 64, 32, 2>;   //        2x2 waves x (32 px x 32 ch)
 using TileN64s = Tile<32, 64, 16, 2>;   //        2x2 waves x (16 px x 32 ch)
-// (larger wave tiles -- 64x64 per wave -- and 32-wide K chunks measured slower)
+using TileN32sK = Tile<64, 32, 16, 4, 32>;  // TileN32s with 32-deep K chunks
+// (larger wave tiles -- 64x64 per wave -- were slower; 32-deep K chunks win only
+// on the 64 x 32 tile of the small CenterNet launches, see conv_launch)
 
 }  // namespace fvp
 
@@ -1563,7 +1590,22 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
                        dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                      \
                             (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN), (unsigned)(G * p.ks)),            \
                        dim3(256), 0, st, a)
-    switch (p.tile) {
+#define FVP_CONV2(TL)                                                                                             \
+    hipLaunchKernelGGL((fvp::conv_mfma_kernel<fvp::TL, 2>),                                                       \
+                       dim3((unsigned)((M + fvp::TL::BM - 1) / fvp::TL::BM),                                      \
+                            (unsigned)((Ntot + fvp::TL::BN - 1) / fvp::TL::BN), (unsigned)(G * p.ks)),            \
+                       dim3(256), 0, st, a)
+    // Measured per layer on CenterNet at 8 frames (rocprofv3 kernel traces,
+    // profiles/round3/centernet_trace): 32-deep K chunks on the 64 x 32 tile
+    // (3x3 32->32 at 80x80: 24-26 -> 21-24 us) and two chunks in flight on the
+    // 64 x 16 tile (7x7 16->16 front: 46 -> 42.5 us); the same changes on the
+    // 32 x 64 tile, a padded B pitch and an LDS-free wave-per-tile kernel were
+    // neutral or slower.
+    if (p.tile == 4 && Cpi % 32 == 0) {  // (a 32-deep chunk = 32 channels of one tap)
+        FVP_CONV(TileN32sK);
+    } else if (p.tile == 2) {
+        FVP_CONV2(TileN16s);
+    } else switch (p.tile) {
         case 1: FVP_CONV(TileN16); break;
         case 2: FVP_CONV(TileN16s); break;
         case 3: FVP_CONV(TileN32); break;
@@ -1573,6 +1615,7 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
         default: FVP_CONV(TileN64s); break;
     }
 #undef FVP_CONV
+#undef FVP_CONV2
     if (p.ks > 1) {
         const long long tot = G * M * Ntot;
         hipLaunchKernelGGL(fvp::conv_splitk_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, a, (int)M,

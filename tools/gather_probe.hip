@@ -24,13 +24,16 @@
 //   STORES_ONLY   no main loop: the epilogue's LDS reads and cube / xy stores
 //   TAPS_L2       TAPS with in-image offsets folded into 512 KB per camera
 //                 image (the frame's 5 images, 2.5 MB, fit the XCD's 4 MB L2)
+//   TAPS_HALF     TAPS with every odd voxel slot's lanes exec-masked off: does
+//                 the texture path charge per active quad or per instruction?
+//   TAPS_L1_HALF  TAPS_L1 likewise (no cache misses in the way)
 // Test tooling only (tools/gather_probe.py); not part of libfvp.
 #include "../faster-voxelpose_amd/csrc/fvp_layout.h"
 
 using namespace fvp;
 
 enum { FULL = 0, TAPS = 1, TAPS_L1 = 2, TAPS_SKIP_OOB = 3, TAPS_ALL_OOB = 4, NO_TAPS = 5, TAPS_2ROW = 6,
-       NOSTORE = 8, FULL2 = 9, STORES_ONLY = 10, TAPS_L2 = 11 };
+       NOSTORE = 8, FULL2 = 9, STORES_ONLY = 10, TAPS_L2 = 11, TAPS_HALF = 12, TAPS_L1_HALF = 13 };
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int MODE>
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(256, 8) void probe_kernel(const float *__restrict__
                 float w[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(src.w[m]);
-                if constexpr (MODE == TAPS_L1) {
+                if constexpr (MODE == TAPS_L1 || MODE == TAPS_L1_HALF) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m) o[m] &= 0x3FC0u;
                 }
@@ -120,6 +123,7 @@ __global__ __launch_bounds__(256, 8) void probe_kernel(const float *__restrict__
                     fold ^= a[0] ^ a[1] ^ a[2] ^ a[3] ^ bq[0] ^ bq[1] ^ bq[2] ^ bq[3];
                 } else {
                     if (MODE == TAPS_SKIP_OOB && (all & kOOB)) return;  // (lanes of a group agree)
+                    if ((MODE == TAPS_HALF || MODE == TAPS_L1_HALF) && ((threadIdx.x >> 2) & 1)) return;
                     const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
                     const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
                     const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
@@ -309,6 +313,8 @@ extern "C" int gather_probe(int mode, const float *tab, const float *grids, floa
         case FULL2: if (T % 4 || SP % 4 || Z % 4) return -3; GO(FULL2); break;
         case STORES_ONLY: if (T % 4 || SP % 4 || Z % 4) return -3; GO(STORES_ONLY); break;
         case TAPS_L2: GO(TAPS_L2); break;
+        case TAPS_HALF: GO(TAPS_HALF); break;
+        case TAPS_L1_HALF: GO(TAPS_L1_HALF); break;
         case 7:  // CAM_OUTER, 5 passes of 64 voxels (cols * Z <= 320)
             if (T > 320) return -2;
             hipLaunchKernelGGL((cam_outer_kernel<5>), grid, blk, lds, s, tab, grids, cube, xy, V, J, H, W, X, Y, Z, cols,

@@ -20,7 +20,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "faster-voxelpose_amd")]
 
 MODES = {"FULL": 0, "TAPS": 1, "TAPS_L1": 2, "TAPS_SKIP_OOB": 3, "TAPS_ALL_OOB": 4, "NO_TAPS": 5, "TAPS_2ROW": 6,
-         "CAM_OUTER": 7, "NOSTORE": 8, "FULL2": 9, "STORES_ONLY": 10, "TAPS_L2": 11}
+         "CAM_OUTER": 7, "NOSTORE": 8, "FULL2": 9, "STORES_ONLY": 10, "TAPS_L2": 11,
+         "TAPS_HALF": 12, "TAPS_L1_HALF": 13}
 EXACT = ("FULL", "CAM_OUTER", "FULL2")  # modes that must reproduce the product's cube and xy
 
 

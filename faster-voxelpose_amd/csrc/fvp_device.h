@@ -88,7 +88,26 @@ __device__ __forceinline__ void project_point(const Cam &c, float x, float y, fl
     py = c.f[1] * v + c.c[1];
 }
 
+// a / b for a divisor fixed per launch, rb = 1.0f / b (correctly rounded; the
+// callers' loop-invariant division, hoisted out of their loops): q = a*rb,
+// the exact remainder a - q*b by one fma, one correction step.  Equal to the
+// correctly rounded a / b whenever the quotient is a normal float
+// (Markstein's theorem for rb = RN(1/b); checked exhaustively over all 2^32
+// fp32 a for b in {3, 7, 127, 151, 199, 239, 512, 608, 800, 960},
+// tests/test_div_const.py): only subnormal quotients (|a| < ~1e-36 here) and a
+// = -0 (gives +0) can differ.  Three VALU ops against ~10 for an IEEE
+// division (v_div_scale / v_rcp / v_div_fmas / v_div_fixup).
+__device__ __forceinline__ float div_const(float a, float b, float rb) {
+    const float q = a * rb;
+    return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
+}
+
 // project_whole.py:96-117 after project_pose: pixel -> normalised sample coords.
+// The four divisions by launch constants use div_const: where it could differ
+// from an IEEE division (a subnormal or -0 quotient) the value next goes
+// through `* 2 - 1` (directly, or after a second division that keeps it below
+// 2^-100), which rounds it to -1 either way, so gx / gy are bit-identical to
+// the reference's (and the sample-grid digests of C1-C5 pin it).
 __device__ __forceinline__ void pixel_to_sample(float px, float py, const float *__restrict__ t, float ori_max,
                                                 float img_w, float img_h, float hm_w, float hm_h,
                                                 float &gx, float &gy) {
@@ -97,10 +116,11 @@ __device__ __forceinline__ void pixel_to_sample(float px, float py, const float 
     // transforms.py:59-63: torch.mm(t, [x, y, 1]^T)
     const float ax = __builtin_fmaf(t[2], 1.0f, __builtin_fmaf(t[1], py, t[0] * px));
     const float ay = __builtin_fmaf(t[5], 1.0f, __builtin_fmaf(t[4], py, t[3] * px));
-    const float hx = (ax * hm_w) / img_w;
-    const float hy = (ay * hm_h) / img_h;
-    gx = clampf((hx / (hm_w - 1.0f)) * 2.0f - 1.0f, -1.1f, 1.1f);
-    gy = clampf((hy / (hm_h - 1.0f)) * 2.0f - 1.0f, -1.1f, 1.1f);
+    const float sw = hm_w - 1.0f, sh = hm_h - 1.0f;
+    const float hx = div_const(ax * hm_w, img_w, 1.0f / img_w);
+    const float hy = div_const(ay * hm_h, img_h, 1.0f / img_h);
+    gx = clampf(div_const(hx, sw, 1.0f / sw) * 2.0f - 1.0f, -1.1f, 1.1f);
+    gy = clampf(div_const(hy, sh, 1.0f / sh) * 2.0f - 1.0f, -1.1f, 1.1f);
 }
 
 // Bilinear tap set of F.grid_sample(align_corners=True, padding zeros) at a

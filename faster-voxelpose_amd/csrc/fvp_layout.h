@@ -130,6 +130,22 @@ __device__ __forceinline__ float h_lo(unsigned u) {
 }
 __device__ __forceinline__ float h_hi(unsigned u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)); }
 
+// fmaf(h, b, c) with h the fp16 in half HI of u, as one v_fma_mix_f32: the
+// fp16 -> fp32 conversion is exact and the fma rounds once, so this equals
+// fmaf(HI ? h_hi(u) : h_lo(u), b, c) bit for bit -- without the separate
+// v_cvt_f32_f16 (the compiler packs the fp32 fmas instead and keeps the
+// conversions).  With c = -0.0f it is the product h * b exactly (x + -0 = x,
+// signed zeros included).
+template <int HI>
+__device__ __forceinline__ float fma_h(unsigned u, float b, float c) {
+    float d;
+    if constexpr (HI)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(u), "v"(b), "v"(c));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(u), "v"(b), "v"(c));
+    return d;
+}
+
 // Bilinear setup of one voxel-camera (aten grid_sampler_2d, align_corners=True,
 // zeros padding): weights nw, ne, sw, se and the byte offsets of the taps
 // (kOOB when outside).  CL: 4 pixel offsets.  PAIR: 2 row-entry offsets.

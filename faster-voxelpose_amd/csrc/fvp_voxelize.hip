@@ -188,17 +188,14 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                     }
 #pragma unroll
                     for (int f = 0; f < NF; ++f)
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
+                        static_for(std::make_integer_sequence<int, 4>{}, [&](auto mc) {
+                            constexpr int m = decltype(mc)::value, HI = m & 1;
                             const unsigned ua = r0[f][m >> 1], ub = r0[f][2 + (m >> 1)];
                             const unsigned uc = r1[f][m >> 1], ud = r1[f][2 + (m >> 1)];
-                            const float fa = (m & 1) ? h_hi(ua) : h_lo(ua);
-                            const float fb = (m & 1) ? h_hi(ub) : h_lo(ub);
-                            const float fc = (m & 1) ? h_hi(uc) : h_lo(uc);
-                            const float fd = (m & 1) ? h_hi(ud) : h_lo(ud);
-                            acc[f][m] = acc[f][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
-                                                                   __builtin_fmaf(fb, w[1], fa * w[0])));
-                        }
+                            // fd*w3 + (fc*w2 + (fb*w1 + fa*w0)), the fp16 taps converted inside the fmas
+                            const float t = fma_h<HI>(ua, w[0], -0.0f);
+                            acc[f][m] = acc[f][m] + fma_h<HI>(ud, w[3], fma_h<HI>(uc, w[2], fma_h<HI>(ub, w[1], t)));
+                        });
                 } else {
                     u32x4 a[NF], bq[NF], c[NF], d[NF];
 #pragma unroll
@@ -324,12 +321,17 @@ constexpr int kBandRows = 16;
 
 static int cols_per_block(int Z) { return Z >= 320 ? 1 : 320 / Z; }
 
-// LDS row pitch of the stage: one float of padding against bank conflicts,
-// unless dropping it lets 8 blocks (32 waves, full occupancy) share a CU's 160 KB.
+// LDS row pitch of the stage: padding against bank conflicts (a pitch of 0
+// mod 32 dwords puts a voxel's 4 lanes on one bank), unless dropping it lets 8
+// blocks (32 waves, full occupancy) share a CU's 160 KB.  When the block's
+// voxel count is a multiple of 4 the pad is 4 floats, keeping the rows 16-B
+// aligned for the vector epilogue (C4 / C5 / the one-frame launches, T = 256
+// and 100: 2-way stage-write conflicts, as with the pad of 1).
 static int stage_pitch(int LPV, int cols, int Z) {
     const int T = cols * Z;
-    const size_t padded = (size_t)16 * LPV * (T + 1), tight = (size_t)16 * LPV * T;
-    return (padded > 20480 && tight <= 20480) ? T : T + 1;
+    const int pad = T % 4 ? 1 : 4;
+    const size_t padded = (size_t)16 * LPV * (T + pad), tight = (size_t)16 * LPV * T;
+    return (padded > 20480 && tight <= 20480) ? T : T + pad;
 }
 
 static bool use_pairs(int J, bool half) { return half && J <= 16; }

@@ -557,3 +557,227 @@ extern "C" int layout_probe(int mode, const float *hm, float *cl, int B, int V, 
     }
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// C5 replay: voxelize_cams_kernel<LPV 4, fp16 pixel-pair
+// table, on-the-fly projection, 16-camera cascade, 2 frames per entry>
+// restated with the same launch (256-voxel blocks of 4 columns, 16-row bands,
+// XCD remap) and MODE switches:
+//   FULL (0)        the kernel (must reproduce fvp_voxelize_cams bit for bit)
+//   TAPS (1)        projection + tap setup + the 2 x 2 pair loads, XOR-folded
+//   TAPS_ALL_OOB(4) TAPS with every offset off-image: the instruction floor
+//   NO_TAPS (5)     FULL with zeros for the taps (projection, FMA, stores)
+//   NOSTORE (8)     FULL without the cube / xy stores
+//   TAPS_HALF (12)  TAPS with every odd voxel's lanes exec-masked off
+//   PROJ (14)       the projection and tap setup alone (offsets folded)
+enum { PROJ = 14 };
+
+template <int MODE>
+__global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ tab, const float *__restrict__ cams_,
+                                                       const float *__restrict__ resize_t, fvp_grid_spec gs,
+                                                       fvp_image_spec im, float *__restrict__ cube,
+                                                       float *__restrict__ xy, float *__restrict__ sink, int V, int J,
+                                                       int H, int W, int X, int Y, int Z, int cols, int col_blocks,
+                                                       int SP, int band) {
+    constexpr int LPV = 4, NF = 2, JP = 16, VPP = 64, CPG = 8;
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [NF][JP][SP] + camera records
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int bl = L / col_blocks;
+    const int b = bl * NF;
+    const int XY = X * Y;
+    int cb = L - bl * col_blocks;
+    if (band > 0) {
+        const int gpr = Y / cols;
+        const int per_band = band * gpr;
+        const int bi = cb / per_band, r = cb - bi * per_band;
+        const int rows = min(band, X - bi * band);
+        const int gc = r / rows, xr = r - gc * rows;
+        cb = (bi * band + xr) * gpr + gc;
+    }
+    const int c0 = cb * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    float *lcam = stage + ((NF * JP * SP + 3) & ~3);
+    for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256) lcam[e] = e < V * FVP_CAM_STRIDE ? cams_[e] : 0.0f;
+    float rt[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rt[k] = resize_t[k];
+    __syncthreads();
+    const unsigned pix = 64u, unit = pix * NF;
+    const unsigned img = (unsigned)(H * (W + 1)) * unit;
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
+    unsigned fold = 0;
+    for (int i0 = 0; i0 < T; i0 += VPP) {
+        const int i = i0 + threadIdx.x / LPV;
+        const bool valid = i < T;
+        const int ii = min(i, T - 1);
+        float acc[NF][4], blk[NF][4];
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[f][m] = blk[f][m] = 0.0f;
+        const long long n = n0 + ii;
+        const int iz = (int)(n % Z);
+        const long long r = n / Z;
+        const float wx_ = axis_coord(gs.start[0], gs.end[0], X, (int)(r / Y), gs.center[0]);
+        const float wy_ = axis_coord(gs.start[1], gs.end[1], Y, (int)(r % Y), gs.center[1]);
+        const float wz_ = axis_coord(gs.start[2], gs.end[2], Z, iz, gs.center[2]);
+        for (int v0 = 0; v0 < V; v0 += CPG) {
+            float g[4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
+                float px, py;
+                project_point(c, wx_, wy_, wz_, px, py);
+                pixel_to_sample(px, py, rt, im.ori_max, im.img_w, im.img_h, (float)im.hm_w, (float)im.hm_h, g[2 * h],
+                                g[2 * h + 1]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
+            const Taps4<true> t0 = setup_taps<true>(g[0], g[1], sxs, sys, W, H, unit);
+            const Taps4<true> t1 = setup_taps<true>(g[2], g[3], sxs, sys, W, H, unit);
+            if constexpr (MODE == PROJ) {
+                fold ^= t0.o[0] ^ t0.o[1] ^ t1.o[0] ^ t1.o[1] ^ __builtin_bit_cast(unsigned, t0.w[0] + t1.w[3]);
+                continue;
+            }
+            static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = k >> 1;
+                const int v = v0 + k;
+                if (v >= V) return;
+                if ((v & 15) == 0 && v > 0) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            blk[f][m] = blk[f][m] + acc[f][m];
+                            acc[f][m] = 0.0f;
+                        }
+                }
+                const Taps4<true> &src = (k & 1) ? t1 : t0;
+                unsigned o[2];
+                unsigned all = kOOB;
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    o[m] = group_bcast<LPV, S>(src.o[m]);
+                    all &= o[m];
+                }
+                if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+                float w[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(src.w[m]);
+                if constexpr (MODE == TAPS_ALL_OOB) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) o[m] = kOOB | (o[m] & 0x3FC0u) | (unsigned)(m << 6);
+                }
+                const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+                if constexpr (MODE == TAPS_HALF) {
+                    if ((threadIdx.x >> 2) & 1) return;
+                }
+                u32x4 r0[NF], r1[NF];
+                if constexpr (MODE == NO_TAPS) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) r0[f] = r1[f] = u32x4{0u, 0u, 0u, 0u};
+                } else {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) {
+                        r0[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + f * pix + qo, 0, 0);
+                        r1[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + f * pix + qo, 0, 0);
+                    }
+                }
+                if constexpr (MODE == TAPS || MODE == TAPS_ALL_OOB || MODE == TAPS_HALF) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) fold ^= r0[f][0] ^ r0[f][1] ^ r0[f][2] ^ r0[f][3] ^ r1[f][0] ^
+                                                         r1[f][1] ^ r1[f][2] ^ r1[f][3];
+                } else {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+                        static_for(std::make_integer_sequence<int, 4>{}, [&](auto mc) {
+                            constexpr int m = decltype(mc)::value, HI = m & 1;
+                            const unsigned ua = r0[f][m >> 1], ub = r0[f][2 + (m >> 1)];
+                            const unsigned uc = r1[f][m >> 1], ud = r1[f][2 + (m >> 1)];
+                            const float t = fma_h<HI>(ua, w[0], -0.0f);
+                            acc[f][m] = acc[f][m] + fma_h<HI>(ud, w[3], fma_h<HI>(uc, w[2], fma_h<HI>(ub, w[1], t)));
+                        });
+                }
+            });
+        }
+        if constexpr (MODE == FULL || MODE == NO_TAPS || MODE == NOSTORE) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc[f][m] = acc[f][m] + blk[f][m];
+            if (valid) {
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        stage[(f * JP + 4 * q + m) * SP + i] = clampf(acc[f][m] / fV, 0.0f, 1.0f);
+            }
+        }
+    }
+    if constexpr (MODE == FULL || MODE == NO_TAPS) {
+        __syncthreads();
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {  // the product's vector epilogue (T, SP, Z multiples of 4)
+            const float *fst = stage + f * JP * SP;
+            const size_t bf = (size_t)(b + f);
+            const int T4 = T >> 2;
+            for (int e = threadIdx.x; e < J * T4; e += 256) {
+                const int j = e / T4, r4 = e - (e / T4) * T4;
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(fst + j * SP + 4 * r4);
+                __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * J + j) * N + n0) + r4);
+            }
+            for (int e = threadIdx.x; e < J * ncols; e += 256) {
+                const int j = e / ncols, cc = e - (e / ncols) * ncols;
+                const f32x4 *s4 = reinterpret_cast<const f32x4 *>(fst + j * SP + cc * Z);
+                float m = -INFINITY;
+#pragma unroll 4
+                for (int z = 0; z < (Z >> 2); ++z) {
+                    const f32x4 v = s4[z];
+                    m = nanmax(nanmax(m, v[0]), nanmax(nanmax(v[1], v[2]), v[3]));
+                }
+                __builtin_nontemporal_store(m, xy + (bf * J + j) * XY + c0 + cc);
+            }
+        }
+    } else if constexpr (MODE == NOSTORE) {
+        __syncthreads();
+        if (stage[threadIdx.x] == 12345.0f) sink[blockIdx.x * 256 + threadIdx.x] = 1.0f;
+    } else {
+        if (fold == 0x7f7f7f7fu) sink[blockIdx.x * 256 + threadIdx.x] = 1.0f;
+    }
+}
+
+extern "C" int gather_probe_c5(int mode, const void *tab, const float *cams, const float *resize_t,
+                               const fvp_grid_spec *gs, const fvp_image_spec *im, float *cube, float *xy, float *sink,
+                               int B, int V, int J, int H, int W, int X, int Y, int Z, int cols, int band,
+                               void *stream) {
+    if (B % 2 || V > 32 || J > 16 || (cols * Z) % 4 || Z % 4 || (X * Y) % cols) return -4;
+    const int col_blocks = (X * Y + cols - 1) / cols;
+    const int T = cols * Z;
+    const int SP = ((size_t)16 * 4 * (T + 4) > 20480 && (size_t)16 * 4 * T <= 20480) ? T : T + 4;  // (product)
+    const size_t lds = (((size_t)2 * 16 * SP + 3) & ~(size_t)3) * 4 + (size_t)(V + (V & 1)) * FVP_CAM_STRIDE * 4;
+    const dim3 grid((unsigned)(B / 2 * col_blocks)), blk(256);
+    hipStream_t s = (hipStream_t)stream;
+#define GO5(M) hipLaunchKernelGGL((probe_c5_kernel<M>), grid, blk, lds, s, tab, cams, resize_t, *gs, *im, cube, xy, \
+                                  sink, V, J, H, W, X, Y, Z, cols, col_blocks, SP, band)
+    switch (mode) {
+        case FULL: GO5(FULL); break;
+        case TAPS: GO5(TAPS); break;
+        case TAPS_ALL_OOB: GO5(TAPS_ALL_OOB); break;
+        case NO_TAPS: GO5(NO_TAPS); break;
+        case NOSTORE: GO5(NOSTORE); break;
+        case TAPS_HALF: GO5(TAPS_HALF); break;
+        case PROJ: GO5(PROJ); break;
+        default: return -1;
+    }
+#undef GO5
+    return (int)hipGetLastError();
+}

@@ -570,7 +570,10 @@ extern "C" int layout_probe(int mode, const float *hm, float *cl, int B, int V, 
 //   NOSTORE (8)     FULL without the cube / xy stores
 //   TAPS_HALF (12)  TAPS with every odd voxel's lanes exec-masked off
 //   PROJ (14)       the projection and tap setup alone (offsets folded)
-enum { PROJ = 14 };
+//   STORE_PLAIN(16) FULL with ordinary (not non-temporal) cube / xy stores
+//   STORE_SMALL(17) FULL with the cube stores folded into a 4 MB window
+//                   (L2-resident: the stores' issue cost without HBM writes)
+enum { PROJ = 14, STORE_PLAIN = 16, STORE_SMALL = 17 };
 
 template <int MODE>
 __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ tab, const float *__restrict__ cams_,
@@ -709,7 +712,7 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
                 }
             });
         }
-        if constexpr (MODE == FULL || MODE == NO_TAPS || MODE == NOSTORE) {
+        if constexpr (MODE == FULL || MODE == NO_TAPS || MODE == NOSTORE || MODE == STORE_PLAIN || MODE == STORE_SMALL) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
             }
         }
     }
-    if constexpr (MODE == FULL || MODE == NO_TAPS) {
+    if constexpr (MODE == FULL || MODE == NO_TAPS || MODE == STORE_PLAIN || MODE == STORE_SMALL) {
         __syncthreads();
 #pragma unroll
         for (int f = 0; f < NF; ++f) {  // the product's vector epilogue (T, SP, Z multiples of 4)
@@ -733,7 +736,10 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
             for (int e = threadIdx.x; e < J * T4; e += 256) {
                 const int j = e / T4, r4 = e - (e / T4) * T4;
                 const f32x4 v = *reinterpret_cast<const f32x4 *>(fst + j * SP + 4 * r4);
-                __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * J + j) * N + n0) + r4);
+                f32x4 *dst = reinterpret_cast<f32x4 *>(cube + (bf * J + j) * N + n0) + r4;
+                if constexpr (MODE == STORE_SMALL) dst = reinterpret_cast<f32x4 *>(cube) + (((bf * J + j) * N + n0) / 4 + r4) % (1 << 18);
+                if constexpr (MODE == STORE_PLAIN) *dst = v;
+                else __builtin_nontemporal_store(v, dst);
             }
             for (int e = threadIdx.x; e < J * ncols; e += 256) {
                 const int j = e / ncols, cc = e - (e / ncols) * ncols;
@@ -744,7 +750,8 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
                     const f32x4 v = s4[z];
                     m = nanmax(nanmax(m, v[0]), nanmax(nanmax(v[1], v[2]), v[3]));
                 }
-                __builtin_nontemporal_store(m, xy + (bf * J + j) * XY + c0 + cc);
+                if constexpr (MODE == STORE_PLAIN) xy[(bf * J + j) * XY + c0 + cc] = m;
+                else __builtin_nontemporal_store(m, xy + (bf * J + j) * XY + c0 + cc);
             }
         }
     } else if constexpr (MODE == NOSTORE) {
@@ -776,6 +783,8 @@ extern "C" int gather_probe_c5(int mode, const void *tab, const float *cams, con
         case NOSTORE: GO5(NOSTORE); break;
         case TAPS_HALF: GO5(TAPS_HALF); break;
         case PROJ: GO5(PROJ); break;
+        case STORE_PLAIN: GO5(STORE_PLAIN); break;
+        case STORE_SMALL: GO5(STORE_SMALL); break;
         default: return -1;
     }
 #undef GO5

@@ -479,6 +479,46 @@ def main():
             torch.cuda.synchronize()
             lat.append((time.perf_counter() - t1) * 1e3)
         extra["latency_b1_graph_ms"] = float(np.median(lat))
+        # the same step at the C ABI (include/fvp.h) as a C / C++ host binds it:
+        # fvp_voxelize (layout + gather) and fvp_nms_topk_columns on preallocated
+        # buffers, then a stream sync -- no op wrappers, no allocation per call
+        if hm1.dim() == 5 and not layer._project_on_the_fly(V):
+            from fvp import _lib
+            grids1, _ = layer._grids_for_batch(hm1, meta1, cams, rt)
+            L = _lib.load()
+            half = hm1.dtype == torch.float16
+            nws = (L.fvp_voxelize_f16_workspace_bytes if half else L.fvp_voxelize_workspace_bytes)(1, V, J, Hd, Wd)
+            ws1 = torch.empty((nws + 3) // 4, device=dev)
+            cube1 = torch.empty((1, J, X, Y, Z), device=dev)
+            xy1 = torch.empty((1, J, X, Y), device=dev)
+            vals1 = torch.empty((1, K), device=dev)
+            flat1 = torch.empty((1, K), dtype=torch.int64, device=dev)
+            kxy1 = torch.empty((1, K, 2), dtype=torch.int64, device=dev)
+            cols1 = torch.empty((1, K, J, Z), device=dev)
+            st1 = torch.cuda.current_stream(dev)
+            f_vox = L.fvp_voxelize_f16 if half else L.fvp_voxelize
+            a_vox = (hm1.data_ptr(), 1, V, J, Hd, Wd, grids1.data_ptr(), None, X, Y, Z, cube1.data_ptr(),
+                     xy1.data_ptr(), ws1.data_ptr(), nws, st1.cuda_stream)
+            a_nms = (xy1.data_ptr() + root * X * Y * 4, 1, X, Y, J * X * Y, K, vals1.data_ptr(), flat1.data_ptr(),
+                     kxy1.data_ptr(), cube1.data_ptr(), J, Z, cols1.data_ptr(), st1.cuda_stream)
+
+            def step_abi():
+                _lib.check(f_vox(*a_vox), "fvp_voxelize")
+                _lib.check(L.fvp_nms_topk_columns(*a_nms), "fvp_nms_topk_columns")
+
+            for _ in range(3):
+                step_abi()
+            torch.cuda.synchronize()
+            if not torch.equal(cols1, step1()):
+                raise SystemExit("bench: the C-ABI one-frame step differs from the op path")
+            torch.cuda.synchronize()
+            lat = []
+            for _ in range(20):
+                t1 = time.perf_counter()
+                step_abi()
+                st1.synchronize()
+                lat.append((time.perf_counter() - t1) * 1e3)
+            extra["latency_b1_abi_ms"] = float(np.median(lat))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
@@ -531,6 +571,7 @@ def main():
             },
             "latency_b1_ms": round(extra["latency_b1_ms"], 3) if "latency_b1_ms" in extra else None,
             "latency_b1_graph_ms": round(extra["latency_b1_graph_ms"], 3) if "latency_b1_graph_ms" in extra else None,
+            "latency_b1_abi_ms": round(extra["latency_b1_abi_ms"], 4) if "latency_b1_abi_ms" in extra else None,
             "cpu_baseline": cpu,
             "execution": "hipGraph replay of the GPU-local step" if args.graph == "on" else "eager",
             "cache_build": cache_ms,

@@ -76,6 +76,39 @@ def main():
     out["graph_stream_sync_ms"] = timed(cap.replay, stream.synchronize)
     out["graph_event_sync_ms"] = timed(cap.replay, ev_sync)
     out["graph_event_spin_ms"] = timed(cap.replay, ev_spin)
+    # the same step through the C ABI directly (what a C/C++ host would bind,
+    # INTEGRATION.md): two calls per frame -- fvp_voxelize (layout + gather)
+    # and fvp_nms_topk_columns -- on preallocated buffers, then the stream sync
+    from fvp import _lib
+    X, Y, Z = w.voxels_per_axis
+    B, V, J, H, W = hm1.shape
+    grids, _ = layer._grids_for_batch(hm1, meta1, cams, rt)
+    L = _lib.load()
+    ws_bytes = L.fvp_voxelize_workspace_bytes(B, V, J, H, W)
+    ws = torch.empty((ws_bytes + 3) // 4, device=dev)
+    cube = torch.empty((B, J, X, Y, Z), device=dev)
+    xy = torch.empty((B, J, X, Y), device=dev)
+    vals = torch.empty((B, K), device=dev)
+    flat = torch.empty((B, K), dtype=torch.int64, device=dev)
+    kxy = torch.empty((B, K, 2), dtype=torch.int64, device=dev)
+    cols = torch.empty((B, K, J, Z), device=dev)
+    st = stream.cuda_stream
+    a_vox = (hm1.data_ptr(), B, V, J, H, W, grids.data_ptr(), None, X, Y, Z, cube.data_ptr(), xy.data_ptr(),
+             ws.data_ptr(), ws_bytes, st)
+    a_nms = (xy.data_ptr() + root * X * Y * 4, B, X, Y, J * X * Y, K, vals.data_ptr(), flat.data_ptr(),
+             kxy.data_ptr(), cube.data_ptr(), J, Z, cols.data_ptr(), st)
+    f_vox, f_nms = L.fvp_voxelize, L.fvp_nms_topk_columns
+
+    def abi_step():
+        f_vox(*a_vox)
+        f_nms(*a_nms)
+
+    abi_step()
+    torch.cuda.synchronize()
+    ref = step1()
+    torch.cuda.synchronize()
+    out["abi_matches_op_path"] = bool(torch.equal(cols, ref))
+    out["abi_direct_stream_sync_ms"] = timed(abi_step, stream.synchronize)
     out["note"] = "(median, p90) host wall ms per step, inputs resident on the GPU"
     print(json.dumps(out))
 

@@ -573,7 +573,10 @@ extern "C" int layout_probe(int mode, const float *hm, float *cl, int B, int V, 
 //   STORE_PLAIN(16) FULL with ordinary (not non-temporal) cube / xy stores
 //   STORE_SMALL(17) FULL with the cube stores folded into a 4 MB window
 //                   (L2-resident: the stores' issue cost without HBM writes)
-enum { PROJ = 14, STORE_PLAIN = 16, STORE_SMALL = 17 };
+//   FULL_PASS (18)  FULL with each 64-voxel pass (= one column at Z = 64)
+//                   stored right after it is computed instead of a block-end
+//                   epilogue: the stores drain under the next pass's taps
+enum { PROJ = 14, STORE_PLAIN = 16, STORE_SMALL = 17, FULL_PASS = 18 };
 
 template <int MODE>
 __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ tab, const float *__restrict__ cams_,
@@ -712,7 +715,8 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
                 }
             });
         }
-        if constexpr (MODE == FULL || MODE == NO_TAPS || MODE == NOSTORE || MODE == STORE_PLAIN || MODE == STORE_SMALL) {
+        if constexpr (MODE == FULL || MODE == NO_TAPS || MODE == NOSTORE || MODE == STORE_PLAIN || MODE == STORE_SMALL ||
+                      MODE == FULL_PASS) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
@@ -723,6 +727,27 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
 #pragma unroll
                     for (int m = 0; m < 4; ++m)
                         stage[(f * JP + 4 * q + m) * SP + i] = clampf(acc[f][m] / fV, 0.0f, 1.0f);
+            }
+        }
+        if constexpr (MODE == FULL_PASS) {  // (host: Z == VPP, so the pass is column i0 / Z)
+            __syncthreads();
+            const int cc = i0 / Z;
+            for (int e = threadIdx.x; e < NF * J * (VPP / 4); e += 256) {
+                const int fj = e / (VPP / 4), r4 = e - fj * (VPP / 4);
+                const int f = fj / J, j = fj - f * J;
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + (f * JP + j) * SP + i0 + 4 * r4);
+                __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + ((size_t)(b + f) * J + j) * N + n0 + i0) + r4);
+            }
+            if (threadIdx.x < NF * J) {
+                const int f = threadIdx.x / J, j = threadIdx.x - f * J;
+                const f32x4 *s4 = reinterpret_cast<const f32x4 *>(stage + (f * JP + j) * SP + i0);
+                float mx = -INFINITY;
+#pragma unroll 4
+                for (int z = 0; z < (VPP >> 2); ++z) {
+                    const f32x4 v = s4[z];
+                    mx = nanmax(nanmax(mx, v[0]), nanmax(nanmax(v[1], v[2]), v[3]));
+                }
+                __builtin_nontemporal_store(mx, xy + ((size_t)(b + f) * J + j) * XY + c0 + cc);
             }
         }
     }
@@ -785,6 +810,7 @@ extern "C" int gather_probe_c5(int mode, const void *tab, const float *cams, con
         case PROJ: GO5(PROJ); break;
         case STORE_PLAIN: GO5(STORE_PLAIN); break;
         case STORE_SMALL: GO5(STORE_SMALL); break;
+        case FULL_PASS: if (Z != 64) return -5; GO5(FULL_PASS); break;
         default: return -1;
     }
 #undef GO5

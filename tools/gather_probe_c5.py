@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "faster-voxelpose_amd"), os.path.join(REPO, "tools")]
 
 MODES = {"FULL": 0, "TAPS": 1, "TAPS_ALL_OOB": 4, "NO_TAPS": 5, "NOSTORE": 8, "TAPS_HALF": 12, "PROJ": 14,
-         "STORE_PLAIN": 16, "STORE_SMALL": 17}
+         "STORE_PLAIN": 16, "STORE_SMALL": 17, "FULL_PASS": 18}
 
 
 def main():
@@ -96,7 +96,7 @@ def main():
                       "frames": B, "workload": "c5"}), flush=True)
     taps = B * X * Y * Z * V
     for name in args.modes.split(","):
-        if name in ("FULL", "STORE_PLAIN"):
+        if name in ("FULL", "STORE_PLAIN", "FULL_PASS"):
             cube.zero_()
             probe(MODES[name])
             torch.cuda.synchronize()

@@ -482,7 +482,7 @@ def main():
         # the same step at the C ABI (include/fvp.h) as a C / C++ host binds it:
         # fvp_voxelize (layout + gather) and fvp_nms_topk_columns on preallocated
         # buffers, then a stream sync -- no op wrappers, no allocation per call
-        if hm1.dim() == 5 and not layer._project_on_the_fly(V):
+        if isinstance(hm1, torch.Tensor) and hm1.dim() == 5 and not layer._project_on_the_fly(V):
             from fvp import _lib
             grids1, _ = layer._grids_for_batch(hm1, meta1, cams, rt)
             L = _lib.load()

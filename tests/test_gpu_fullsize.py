@@ -185,6 +185,8 @@ def test_fused_hdn_forward_matches_reference_hdn(gpu_device, cnn):
     rv, _, rfl = O.nms2d(d["hm2d"], w.max_people)
     gv, _, gfl = O.nms2d(hm2d, w.max_people)
     n_idx = _match_ranked(gv, gfl, rv, rfl, tol2, "2-D proposal indices")
+    print(f"HDN ({cnn} CNNs): {n_idx} of {rfl.size} proposal ranks compared by index, {rfl.size - n_idx} skipped "
+          f"(reference values within 2x{tol2:.2e} of a neighbour); {int((gfl == rfl).sum())} indices identical")
     assert n_idx >= 10, f"only {n_idx} proposals compared by index"
     X = w.voxels_per_axis[0]
     mm = lambda fl, a: (np.float32(fl // X if a == 0 else fl % X) * np.float32(w.space_size[a] / (w.voxels_per_axis[a] - 1))  # noqa: E731

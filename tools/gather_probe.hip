@@ -541,6 +541,34 @@ __global__ __launch_bounds__(256) void layout_c_kernel(const float *__restrict__
     }
 }
 
+// the shipped layout pass's arithmetic as a grid-stride loop over `blocks`
+// blocks (few CU slots, a bounded streaming rate: can it run under a gather?)
+__global__ __launch_bounds__(256) void layout_stride_kernel(const float *__restrict__ hm, float4 *__restrict__ cl, int J,
+                                                            int HW, long long total_px) {
+    for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x; gid < total_px * 4; gid += (long long)gridDim.x * 256) {
+        const long long pxg = gid >> 2;
+        const int q = (int)(gid & 3);
+        const long long bv = pxg / HW;
+        const int pix = (int)(pxg - bv * HW);
+        const float *__restrict__ src = hm + (size_t)bv * J * HW + pix;
+        const int j = 4 * q;
+        float4 o;
+        o.x = (j + 0 < J) ? src[(size_t)(j + 0) * HW] : 0.f;
+        o.y = (j + 1 < J) ? src[(size_t)(j + 1) * HW] : 0.f;
+        o.z = (j + 2 < J) ? src[(size_t)(j + 2) * HW] : 0.f;
+        o.w = (j + 3 < J) ? src[(size_t)(j + 3) * HW] : 0.f;
+        cl[gid] = o;
+    }
+}
+
+extern "C" int layout_stride_probe(const float *hm, float *cl, int B, int V, int J, int H, int W, int blocks,
+                                   void *stream) {
+    const long long px = (long long)B * V * H * W;
+    hipLaunchKernelGGL(layout_stride_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, hm,
+                       reinterpret_cast<float4 *>(cl), J, H * W, px);
+    return (int)hipGetLastError();
+}
+
 extern "C" int layout_probe(int mode, const float *hm, float *cl, int B, int V, int J, int H, int W, void *stream) {
     const long long px = (long long)B * V * H * W;
     hipStream_t s = (hipStream_t)stream;

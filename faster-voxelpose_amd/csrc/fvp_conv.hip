@@ -1605,9 +1605,8 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
         FVP_CONV(TileN32sK);
     } else if (p.tile == 2) {
         FVP_CONV2(TileN16s);
-    } else switch (p.tile) {
+    } else switch (p.tile) {  // (tile 2 took the branch above)
         case 1: FVP_CONV(TileN16); break;
-        case 2: FVP_CONV(TileN16s); break;
         case 3: FVP_CONV(TileN32); break;
         case 4: FVP_CONV(TileN32s); break;
         case 5: FVP_CONV(TileN64); break;

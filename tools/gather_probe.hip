@@ -295,7 +295,8 @@ extern "C" int gather_probe(int mode, const float *tab, const float *grids, floa
                             int V, int J, int H, int W, int X, int Y, int Z, int cols, int band, void *stream) {
     const int col_blocks = (X * Y + cols - 1) / cols;
     const int T = cols * Z;
-    const int SP = ((size_t)16 * 4 * (T + 1) > 20480 && (size_t)16 * 4 * T <= 20480) ? T : T + 1;
+    const int pad = T % 4 ? 1 : 4;  // the product's stage_pitch (fvp_voxelize.hip)
+    const int SP = ((size_t)16 * 4 * (T + pad) > 20480 && (size_t)16 * 4 * T <= 20480) ? T : T + pad;
     const size_t lds = (size_t)4 * 4 * 4 * SP;
     const dim3 grid((unsigned)(B * col_blocks)), blk(256);
     hipStream_t s = (hipStream_t)stream;

@@ -85,7 +85,7 @@ def main():
     xy = torch.empty((B, J, X, Y), device=dev)
     sink = torch.zeros(64 << 20, device=dev)
     stream = torch.cuda.current_stream(dev)
-    cols, band = 16, 16  # the product's launch at C2 / C3 (fvp_voxelize.hip gather_cfg)
+    cols, band = 16, 16  # the launch at C2 / C3 when the probe was written (the product now takes 8: gather_cfg)
 
     def timed(fn):
         for _ in range(3):

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--layout-blocks", default="0", help="0 = the shipped launch; n = grid-stride over n blocks")
+    ap.add_argument("--cols", default="16", help="gather columns per block (the product: 16 at C2)")
+    ap.add_argument("--schedules", default="sequential,overlapped")
     args = ap.parse_args()
     import gather_probe
     path = gather_probe.build()
@@ -59,6 +61,7 @@ def main():
     sink = torch.zeros(64 << 20, device=dev)
 
     lay_blocks = [0]
+    cols = [16]
 
     def layout(k, C, buf, stream):
         src = hm.data_ptr() + k * C * frame_elems * 4
@@ -70,11 +73,12 @@ def main():
 
     def gather(C, buf, cube, xy, stream):
         rc = lib.gather_probe(9, buf.data_ptr(), grids.data_ptr(), cube.data_ptr(), xy.data_ptr(), sink.data_ptr(),
-                              C, V, J, Hd, Wd, X, Y, Z, 16, 16, stream.cuda_stream)
+                              C, V, J, Hd, Wd, X, Y, Z, cols[0], 16, stream.cuda_stream)
         assert rc == 0, rc
 
-    for C, lb in [(int(c), int(b)) for c in args.chunks.split(",") for b in args.layout_blocks.split(",")]:
-        lay_blocks[0] = lb
+    for C, lb, nc in [(int(c), int(b), int(k)) for c in args.chunks.split(",") for b in args.layout_blocks.split(",")
+                      for k in args.cols.split(",")]:
+        lay_blocks[0], cols[0] = lb, nc
         n = F // C
         bufs = [torch.empty((C, V, Hd * Wd, 16), device=dev) for _ in range(2)]
         cube = torch.empty((F, J, X, Y, Z), device=dev)
@@ -108,8 +112,8 @@ def main():
             s_main.wait_stream(s_lay)
 
         ref = None
-        for name, fn in (("sequential", sequential), ("overlapped", overlapped), ("sequential", sequential),
-                         ("overlapped", overlapped)):
+        scheds = [(n_, {"sequential": sequential, "overlapped": overlapped}[n_]) for n_ in args.schedules.split(",")]
+        for name, fn in scheds + scheds:
             fn()
             torch.cuda.synchronize()
             if ref is None:
@@ -123,7 +127,7 @@ def main():
             e1.record(s_main)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
-            print(json.dumps({"chunk_frames": C, "layout_blocks": lb or "shipped", "schedule": name, "ms_per_256_frames": round(ms * 256 / F, 4),
+            print(json.dumps({"chunk_frames": C, "cols": nc, "layout_blocks": lb or "shipped", "schedule": name, "ms_per_256_frames": round(ms * 256 / F, 4),
                               "frames_per_s": round(F / (ms * 1e-3), 1)}), flush=True)
         del bufs, cube, xy, ref
 

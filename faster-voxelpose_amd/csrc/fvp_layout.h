@@ -4,6 +4,7 @@
 // range check.
 #pragma once
 
+#include <cstdlib>
 #include <utility>
 
 #include "fvp_device.h"
@@ -91,7 +92,80 @@ __global__ __launch_bounds__(256) void heatmaps_to_pairs_kernel(const T *__restr
     }
 }
 
+// The same table, one block per (frame group, view, row): the NF frames' J
+// joint rows are read with coalesced 4-B loads (a wave covers 256 B of one
+// row) into LDS as [NF][16][W+4] halves (pixel x at x+2, zeros at x = -1, W
+// and for joints >= J), then the row's (W+1) x NF entries go out as one
+// contiguous run of 16-B stores.  The per-entry kernel above reads 2-B values
+// per lane (8 loads per 16-B store) and writes 64-B pieces NF*64 B apart.
+// Needs W even (4-B aligned rows); LDS NF*16*(W/2+2)*4 B.
+template <int NF>
+__global__ __launch_bounds__(256) void pairs_rows_kernel(const _Float16 *__restrict__ hm, uint4 *__restrict__ tab,
+                                                         int J, int H, int W, int V) {
+    extern __shared__ unsigned s32[];
+    const int P2 = W / 2 + 2;  // words per staged joint row
+    const int row = blockIdx.x;  // (g * V + v) * H + y
+    const int gv = row / H, y = row - gv * H;
+    const int g = gv / V, v = gv - g * V;
+    const size_t HW = (size_t)H * W;
+    for (int t = threadIdx.x; t < NF * 16 * P2; t += 256) {  // the zero borders and padding joints
+        const int jr = t / P2, w = t - jr * P2;
+        if ((jr & 15) >= J || w == 0 || w == P2 - 1) s32[t] = 0u;
+    }
+    // all U loads of a lane issued before their LDS writes (clamped, always
+    // legal addresses): a row is one dependent HBM round trip per block
+    constexpr int U = 16;
+    const int HWc = W / 2, total = NF * J * HWc;
+    for (int t0 = threadIdx.x; t0 < total; t0 += 256 * U) {
+        unsigned val[U];
+        int at[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = min(t0 + u * 256, total - 1);
+            const int fj = t / HWc, c = t - fj * HWc;
+            const int f = fj / J, j = fj - f * J;
+            val[u] = reinterpret_cast<const unsigned *>(hm + (((size_t)(g * NF + f) * V + v) * J + j) * HW +
+                                                        (size_t)y * W)[c];
+            at[u] = (f * 16 + j) * P2 + 1 + c;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + u * 256 < total) s32[at[u]] = val[u];
+    }
+    __syncthreads();
+    const unsigned short *s16 = reinterpret_cast<const unsigned short *>(s32);
+    const int W1 = W + 1;
+    uint4 *__restrict__ dst = tab + (size_t)row * W1 * NF * 4;
+    for (int t = threadIdx.x; t < W1 * NF * 4; t += 256) {  // t = (e * NF + f) * 4 + q
+        const int q = t & 3, ef = t >> 2;
+        const int e = ef / NF, f = ef - e * NF;
+        const unsigned short *r = s16 + (f * 16 + 4 * q) * (2 * P2) + e + 1;  // pixel e-1, then pixel e
+        unsigned h[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = r[k * 2 * P2];
+            h[4 + k] = r[k * 2 * P2 + 1];
+        }
+        dst[t] = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16));
+    }
+}
+
 inline size_t pair_frame_bytes(int V, int H, int W) { return (size_t)V * H * (W + 1) * 64; }
+
+// Launch the pair-table layout for nb frames (a multiple of NF).
+template <int NF>
+inline void launch_pairs(const _Float16 *hm, int nb, int V, int J, int H, int W, uint4 *tab, hipStream_t s) {
+    const size_t lds = (size_t)NF * 16 * (W / 2 + 2) * 4;
+    const char *ab = getenv("FVP_PAIRS_LAYOUT");  // "entry": the per-entry kernel (A/B)
+    if (W % 2 == 0 && lds <= 64 * 1024 && !(ab && ab[0] == 'e')) {
+        hipLaunchKernelGGL((pairs_rows_kernel<NF>), dim3((unsigned)((long long)nb / NF * V * H)), dim3(256), lds, s, hm,
+                           tab, J, H, W, V);
+    } else {
+        const long long total = (long long)nb * V * H * (W + 1) * 4;
+        hipLaunchKernelGGL((heatmaps_to_pairs_kernel<_Float16, NF>), dim3((unsigned)((total + 255) / 256)), dim3(256),
+                           0, s, hm, tab, J, H, W, V, total);
+    }
+}
 
 // -- lane-group helpers -----------------------------------------------------------
 // Broadcast lane S of each LPV-lane voxel group to the whole group (DPP quad

@@ -32,6 +32,7 @@
 // tap and the camera sum order are the reference's (fvp_device.h: torch's
 // CPU mean over the views folds complete blocks of 16 cameras, CASC = V > 16),
 // so the result is bit-exact.
+#include <cstdlib>
 #include <type_traits>
 
 #include "fvp_layout.h"
@@ -285,7 +286,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
 // Cached-grid gather: <= 64 VGPRs so 8 waves/SIMD fit (32 waves/CU with the
 // 20 KB stage); the on-the-fly variant keeps its registers (no spills).
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
-__global__ __launch_bounds__(256, NF == 1 ? 8 : 5) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
+__global__ __launch_bounds__(256, NF == 1 ? 8 : NF == 2 ? 5 : 4) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int Jst, int H, int W, int X, int Y, int Z,
@@ -341,17 +342,30 @@ static int stage_pitch(int LPV, int cols, int Z) {
 
 static bool use_pairs(int J, bool half) { return half && J <= 16; }
 
+// Frames per fp16 pair-table entry: 4 (two 128-B lines per entry), so each
+// tap setup -- at C5 the on-the-fly projection of 31 cameras -- serves four
+// frames.  Same box, C5 (profiles/round3/c5/pair_frames_ab.txt): B = 8 2.83 k
+// -> 3.25 k frames/s, B = 32 3.11 k -> 3.43 k against 2 per entry.
+// FVP_PAIR_FRAMES=2 restores two (read per call: the A/B and the tests).
+static int pair_frames() {
+    const char *e = getenv("FVP_PAIR_FRAMES");
+    return (e && atoi(e) == 2) ? 2 : 4;
+}
+
 static size_t frame_bytes(int V, int J, int H, int W, bool half) {
     return use_pairs(J, half) ? pair_frame_bytes(V, H, W) : cl_frame_bytes(V, J, H, W);
 }
 
 // Frames per chunk: keep a chunk's re-laid-out copy inside the 256 MB Infinity
-// Cache (measured best: ~80 MB for the fp32 layout, C2: 8 frames; 2 frames
-// (~122 MB) of the fp16 pair table at C5).
+// Cache (measured best: ~80 MB for the fp32 layout, C2: 8 frames; ~128 MB of
+// the fp16 pair table, but at least one group of pair_frames() frames when
+// that fits the cache: 4 frames = 245 MB at C5).
 static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     const size_t per = frame_bytes(V, J, H, W, half);
-    const size_t budget = use_pairs(J, half) ? (128ull << 20) : (80ull << 20);
+    const bool pairs = use_pairs(J, half);
+    const size_t budget = pairs ? (128ull << 20) : (80ull << 20);
     long long c = (long long)(budget / (per ? per : 1));
+    if (pairs && c < pair_frames() && (size_t)pair_frames() * per <= (256ull << 20)) c = pair_frames();
     if (c < 1) c = 1;
     if (c > B) c = B;
     return (int)c;
@@ -381,8 +395,10 @@ static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg 
     };
     auto blocks = [&](int c) { return (long long)frames / NF * ((X * Y + c - 1) / c); };
     // on the fly: 256-voxel blocks (C5: 4 columns of 64; 128-voxel blocks
-    // measured 2-4 % slower, 64 -> 8 % slower, 512 -> 40 % slower, round 3)
-    int cols = snap(OTF ? (Z >= 256 ? 1 : 256 / Z) : cols_per_block(Z));
+    // measured 2-4 % slower, 64 -> 8 % slower, 512 -> 40 % slower, round 3);
+    // 4 frames per entry: 128 (the stage holds NF frames)
+    const int otf_vox = NF >= 4 ? 128 : 256;
+    int cols = snap(OTF ? (Z >= otf_vox ? 1 : otf_vox / Z) : cols_per_block(Z));
     // latency (few frames): one pass of 256/LPV voxels per block, so a single
     // frame spreads over enough blocks to fill the CUs -- or two passes when
     // one-pass blocks would overflow one round of 8 blocks per CU (the counts
@@ -445,10 +461,8 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
         const int nb = min(chunk, last - f0);
         const T *hsrc = hm + (size_t)f0 * frame_elems;
         if constexpr (PAIR) {  // (J <= 16: never sliced)
-            const long long total = (long long)nb * j.V * j.H * (j.W + 1) * 4;
-            hipLaunchKernelGGL((heatmaps_to_pairs_kernel<_Float16, NF>), dim3((unsigned)((total + 255) / 256)),
-                               dim3(256), 0, s, reinterpret_cast<const _Float16 *>(hsrc), reinterpret_cast<uint4 *>(ws),
-                               j.J, j.H, j.W, j.V, total);
+            launch_pairs<NF>(reinterpret_cast<const _Float16 *>(hsrc), nb, j.V, j.J, j.H, j.W,
+                             reinterpret_cast<uint4 *>(ws), s);
         } else {
             launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
         }
@@ -485,17 +499,27 @@ static int run_direct(const float *hm_cl, int cp, int B, const VoxJob &j, const 
 // with one line and one tap setup: C5 3.97 -> 3.12 ms per 8 frames (the
 // gather waits on L1 misses; measured).  The fp32 channels-last table keeps
 // one frame per entry (NF = 2 measured 4 % slower at C2: the L2 working set
-// doubles).  Frames of a pair must share one sampling grid, so batches that
-// mix sequences (grid_index given) and an odd last frame run at NF = 1.
+// doubles).  Four frames per entry (pair_frames) amortise the tap setup
+// further; the batch runs as groups of 4, then a pair, then a single frame.
+// Frames of a group must share one sampling grid, so batches that mix
+// sequences (grid_index given) run at NF = 1.
 template <int LPV, bool PAIR, bool OTF, bool CASC, typename T>
 static int run_frames(const T *hm, int B, const VoxJob &j, const CoordSource &src, void *ws, hipStream_t s) {
     if constexpr (PAIR) {
-        if (!j.grid_index && chunk_frames(B, j.V, j.J, j.H, j.W, sizeof(T) == 2) >= 2) {  // workspace holds >= 2 frames
-            const int even = B & ~1;
-            const int st = run_chunks<LPV, PAIR, OTF, CASC, 2, T>(hm, 0, even, j, src, ws, s);
-            if (st != FVP_OK || even == B) return st;
-            return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, even, B, j, src, ws, s);
+        const int cf = chunk_frames(B, j.V, j.J, j.H, j.W, sizeof(T) == 2);
+        int done = 0;
+        if (!j.grid_index && pair_frames() == 4 && cf >= 4) {  // workspace holds >= 4 frames
+            done = B & ~3;
+            const int st = run_chunks<LPV, PAIR, OTF, CASC, 4, T>(hm, 0, done, j, src, ws, s);
+            if (st != FVP_OK || done == B) return st;
         }
+        if (!j.grid_index && cf >= 2 && B - done >= 2) {  // workspace holds >= 2 frames
+            const int even = done + ((B - done) & ~1);
+            const int st = run_chunks<LPV, PAIR, OTF, CASC, 2, T>(hm, done, even, j, src, ws, s);
+            if (st != FVP_OK || even == B) return st;
+            done = even;
+        }
+        if (done > 0) return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, done, B, j, src, ws, s);
     }
     return run_chunks<LPV, PAIR, OTF, CASC, 1, T>(hm, 0, B, j, src, ws, s);
 }

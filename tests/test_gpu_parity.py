@@ -432,12 +432,15 @@ def test_fp16_heatmaps_computed_in_fp32(gpu_device):
     _assert_same(cube[1].cpu().numpy(), ref, "fp16 frame")
 
 
-@pytest.mark.parametrize("B", [2, 3, 5])
+@pytest.mark.parametrize("B", [2, 3, 5, 7])
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
-def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf):
-    """The fp16 pair table holds two frames per 128-B entry (NF = 2): every
-    frame of an even or odd batch equals its own single-frame launch and the
-    fp32 layout's result; 31 ring cameras (the 16-camera cascade) on a small grid."""
+@pytest.mark.parametrize("nf", ["2", "4"], ids=["nf2", "nf4"])
+def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf, nf, monkeypatch):
+    """The fp16 pair table holds two (or, FVP_PAIR_FRAMES=4, four) frames per
+    entry: every frame of a batch (7 = one group of 4, a pair, a single)
+    equals its own single-frame launch and the fp32 layout's result; 31 ring
+    cameras (the 16-camera cascade) on a small grid."""
+    monkeypatch.setenv("FVP_PAIR_FRAMES", nf)
     from fvp import geometry, synthetic
     from fvp.config import make_cfg
     from fvp.project_whole import ProjectLayer

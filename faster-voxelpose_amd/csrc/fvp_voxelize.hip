@@ -347,12 +347,15 @@ __global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict
 
 constexpr int kBandRows = 16;
 
-// Cached-grid blocks of ~160 voxels (C2 / C3: 8 columns of 20, C4: 4 of 32).
-// Measured on the same box against 320 / 200 / 100 (profiles/round3/block_voxels):
-// C2 +2-3 %, C4 +2-5 % over 320 -- twice the blocks per chunk (6,400 at C2)
-// leave a shorter last round on 2,048 block slots, and since the stage pitch
-// keeps 16-B rows (stage_pitch) the smaller blocks keep the vector epilogue.
-static int cols_per_block(int Z) { return Z >= 160 ? 1 : 160 / Z; }
+// Cached-grid blocks of ~160 voxels at Z < 32 (C2 / C3: 8 columns of 20) and
+// 256 from Z = 32 (C4: 8 of 32).  Measured on the same box against 320 / 200 /
+// 100 (profiles/round3/block_voxels): C2 +2-3 %, C4 +2-5 % over 320 -- twice
+// the blocks per chunk (6,400 at C2) leave a shorter last round on 2,048 block
+// slots, and since the stage pitch keeps 16-B rows (stage_pitch) the smaller
+// blocks keep the vector epilogue.  With layer-major slots C4 is 3-4 % faster
+// at 8 columns than at 4 (a wave = 8 columns x 2 layers; 16: -13 %), C2 stays
+// best at 8 (4: -11 %, 16: -3 %) (profiles/round3/slot_order/cols_sweep.txt).
+static int cols_per_block(int Z) { return Z >= 256 ? 1 : Z >= 32 ? 256 / Z : 160 / Z; }
 
 // LDS row pitch of the stage: padding against bank conflicts (a pitch of 0
 // mod 32 dwords puts a voxel's 4 lanes on one bank), unless dropping it lets 8

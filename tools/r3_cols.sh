@@ -11,3 +11,5 @@ for rep in 1 2; do
     line $L "$w cols$cols rep$rep"
   done
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_c2 -o run -- python3 bench.py --workload c2 --steps 10 --warmup 2 --traffic off --cpu-baseline off > gpurun_out/${T}_prof_c2.log 2>&1 || { tail -20 gpurun_out/${T}_prof_c2.log; exit 1; }
+f=$(find gpurun_out/${T}_prof_c2 -name '*kernel_stats.csv' | head -1); cut -d, -f1-4 "$f" | cut -c1-160 | head -12

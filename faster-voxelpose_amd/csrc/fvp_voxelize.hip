@@ -335,159 +335,6 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
                                             col_blocks, SP, band, pixb, order, tx);
 }
 
-// -- camera-outer gather -----------------------------------------------------------
-// The cached-grid gather re-fetches each line of a frame's table ~2.5x into the
-// XCD's L2: pixels are shared along camera rays, which cross the whole space,
-// so voxels that share a line are far apart in any block walk (an LRU model of
-// one XCD's 4 MB L2 over the real C2 geometry: 194 k misses per frame whatever
-// the walk or the number of resident blocks).  Here one launch keeps every
-// voxel of the chunk resident at once (one round: bpf blocks per frame, 4 per
-// CU, PMAX passes of 64 voxels each with its accumulators in registers), and
-// each block walks the cameras in the outer loop, so the blocks of an XCD --
-// started together -- work on about one camera image (2 MB at C2) at a time:
-// the model gives 113 k misses, ~the compulsory ones.  Coordinates come from
-// the per-camera grid [V][N][2] (cgrid); lane q of a voxel group loads the
-// group's voxel of pass 4k+q and sets it up, the group takes the set-ups of
-// passes 4k..4k+3 over by lane broadcasts.  Each voxel still sums its cameras in
-// view order with the same expressions (bit-identical); V <= 16 only.
-template <int PMAX>
-__global__ __launch_bounds__(256, 4) void voxelize_co_kernel(const void *__restrict__ tab,
-                                                             const float *__restrict__ cgrid, int frame0,
-                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
-                                                             int J, int Jst, int H, int W, int X, int Y, int Z,
-                                                             int cpb, int bpf, unsigned pixb) {
-    constexpr int LPV = 4;
-    extern __shared__ __attribute__((aligned(16))) float st[];  // [4][T]: one joint quad of the results
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int bl = L / bpf, cb = L - bl * bpf;
-    const int b = frame0 + bl;
-    const int XY = X * Y;
-    const int c0 = cb * cpb;
-    const int ncols = min(cpb, XY - c0);
-    const int T = ncols * Z;
-    const int P = (T + 63) / 64;
-    const long long N = (long long)XY * Z;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int g = lane >> 2, q = lane & 3;
-    const unsigned qo = (unsigned)q * 16u;
-    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
-    const float fV = (float)V;
-    const unsigned img = (unsigned)(H * W) * pixb;
-    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
-    // slot s (layer-major: column s mod ncols, layer s / ncols) -> its voxel's stage index and cube index
-    auto voxel = [&](int s, int &ii) -> long long {
-        const int zl = s / ncols, cl = s - zl * ncols;
-        ii = cl * Z + zl;
-        return (long long)(c0 + cl) * Z + zl;
-    };
-    float acc[PMAX][4];
-#pragma unroll
-    for (int p = 0; p < PMAX; ++p)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc[p][m] = 0.0f;
-    for (int v = 0; v < V; ++v) {
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
-        const float2 *__restrict__ gv = reinterpret_cast<const float2 *>(cgrid) + (size_t)v * N;
-        static_for(std::make_integer_sequence<int, PMAX / 4>{}, [&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            if (4 * k >= P) return;
-            Taps4<false> t;
-            {  // pass 4k+q of this group's slot
-                const int s = (4 * k + q) * 64 + wv * 16 + g;
-                int ii;
-                const float2 c = gv[voxel(min(s, T - 1), ii)];
-                t = setup_taps<false>(s < T ? c.x : -2.0f, s < T ? c.y : -2.0f, sxs, sys, W, H, pixb);
-            }
-            static_for(std::make_integer_sequence<int, 4>{}, [&](auto jc) {
-                constexpr int S = decltype(jc)::value;
-                constexpr int p = 4 * k + S;
-                if (p >= P) return;
-                unsigned o[4];
-                unsigned all = kOOB;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    o[m] = group_bcast<LPV, S>(t.o[m]);
-                    all &= o[m];
-                }
-                if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
-                float w[4];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, S>(t.w[m]);
-                const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
-                const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
-                const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
-                const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
-                    const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
-                    const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
-                    const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
-                    acc[p][m] = acc[p][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
-                                                           __builtin_fmaf(fb, w[1], fa * w[0])));
-                }
-            });
-        });
-    }
-    // Epilogue, one joint quad at a time through a [4][T] stage: the block's
-    // columns are consecutive, so each joint's cube run is one contiguous range.
-    const size_t bf = (size_t)b;
-    const bool vec = ((T | Z | (int)(N & 3) | (c0 * Z)) & 3) == 0;
-    for (int jq = 0; jq < 4 && 4 * jq < J; ++jq) {
-        if (q == jq) {
-#pragma unroll
-            for (int p = 0; p < PMAX; ++p) {
-                const int s = p * 64 + wv * 16 + g;
-                if (p < P && s < T) {
-                    int ii;
-                    voxel(s, ii);
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) st[m * T + ii] = clampf((acc[p][m] + 0.0f) / fV, 0.0f, 1.0f);
-                }
-            }
-        }
-        __syncthreads();
-        const int nj = min(4, J - 4 * jq);
-        if (cube) {
-            if (vec) {
-                const int T4 = T >> 2;
-                for (int e = threadIdx.x; e < nj * T4; e += 256) {
-                    const int m = e / T4, r = e - m * T4;
-                    const f32x4 val = *reinterpret_cast<const f32x4 *>(st + m * T + 4 * r);
-                    __builtin_nontemporal_store(
-                        val, reinterpret_cast<f32x4 *>(cube + (bf * Jst + 4 * jq + m) * N + (long long)c0 * Z) + r);
-                }
-            } else {
-                for (int e = threadIdx.x; e < nj * T; e += 256) {
-                    const int m = e / T, r = e - m * T;
-                    __builtin_nontemporal_store(st[m * T + r], cube + (bf * Jst + 4 * jq + m) * N + (long long)c0 * Z + r);
-                }
-            }
-        }
-        if (xy) {
-            for (int e = threadIdx.x; e < nj * ncols; e += 256) {
-                const int m = e / ncols, cc = e - m * ncols;
-                const float *s = st + m * T + cc * Z;
-                float mx = -INFINITY;
-                for (int z = 0; z < Z; ++z) mx = nanmax(mx, s[z]);
-                __builtin_nontemporal_store(mx, xy + (bf * Jst + 4 * jq + m) * XY + c0 + cc);
-            }
-        }
-        __syncthreads();
-    }
-}
-
-constexpr int kCoPasses = 16;  // passes of 64 voxels per camera-outer block (accumulators in registers)
-
-// packed [N][GV][2] -> per-camera [V][N][2] (the camera-outer gather's coordinates)
-__global__ __launch_bounds__(256) void unpack_grid_kernel(const float2 *__restrict__ packed, float2 *__restrict__ out,
-                                                          int V, int GV, long long N) {
-    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (t >= N * V) return;
-    const long long v = t / N, n = t - v * N;
-    out[t] = packed[n * GV + v];
-}
-
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
 __global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict__ g, float2 *__restrict__ out, int V,
                                                         int GV, long long N) {
@@ -658,29 +505,6 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
     GatherCfg c;
     if (gather_cfg<LPV, OTF>(min(chunk, B), NF, j.V, j.X, j.Y, j.Z, c) != FVP_OK) return FVP_ERR_SHAPE;
     const size_t frame_elems = (size_t)j.V * j.Jst * j.H * j.W;
-    // camera-outer gather (voxelize_co_kernel): one sequence, fp32 table, V <= 16,
-    // the chunk's voxels resident in one round of 4 blocks per CU
-    float *cgrid = nullptr;
-    int bpf = 0, cpb = 0;
-    if constexpr (!PAIR && !OTF && !CASC && NF == 1 && LPV == 4) {
-        const char *e = getenv("FVP_CAM_OUTER");
-        const int XY = j.X * j.Y, cmin = min(chunk, B);
-        bpf = max(1, (4 * 256) / cmin);
-        cpb = (XY + bpf - 1) / bpf;
-        bpf = (XY + cpb - 1) / cpb;
-        if (!(e && e[0] == '0') && !j.grid_index && cmin >= 4 && cpb * j.Z <= kCoPasses * 64) {
-            const long long N = (long long)XY * j.Z;
-            if (hipMallocAsync(reinterpret_cast<void **>(&cgrid), (size_t)N * j.V * 8, s) == hipSuccess) {
-                const long long tot = N * j.V;
-                hipLaunchKernelGGL(unpack_grid_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
-                                   reinterpret_cast<const float2 *>(src.grids), reinterpret_cast<float2 *>(cgrid), j.V,
-                                   FVP_GRID_SLOTS(j.V), N);
-            } else {
-                cgrid = nullptr;
-                (void)hipGetLastError();
-            }
-        }
-    }
     for (int f0 = first; f0 < last; f0 += chunk) {
         const int nb = min(chunk, last - f0);
         const T *hsrc = hm + (size_t)f0 * frame_elems;
@@ -690,16 +514,9 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
         } else {
             launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
         }
-        if (cgrid) {
-            hipLaunchKernelGGL((voxelize_co_kernel<kCoPasses>), dim3((unsigned)(nb * bpf)), dim3(256),
-                               (size_t)4 * cpb * j.Z * sizeof(float), s, ws, cgrid, f0, j.cube, j.xy, j.V, j.J, j.Jst,
-                               j.H, j.W, j.X, j.Y, j.Z, cpb, bpf, 4u * 4u * LPV);
-        } else {
-            launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X,
-                                                   j.Y, j.Z, j.cube, j.xy, 4u * 4u * LPV, s);
-        }
+        launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
+                                               j.Z, j.cube, j.xy, 4u * 4u * LPV, s);
     }
-    if (cgrid) (void)hipFreeAsync(cgrid, s);
     return (int)hipGetLastError();
 }
 

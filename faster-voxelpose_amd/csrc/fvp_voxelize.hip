@@ -427,7 +427,8 @@ static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg 
     // on the fly: 256-voxel blocks (C5: 4 columns of 64; 128-voxel blocks
     // measured 2-4 % slower, 64 -> 8 % slower, 512 -> 40 % slower, round 3);
     // 4 frames per entry: 128 (the stage holds NF frames)
-    const int otf_vox = NF >= 4 ? 128 : 256;
+    int otf_vox = NF >= 4 ? 128 : 256;
+    if (const char *ov = getenv("FVP_OTF_VOXELS"); ov && OTF) otf_vox = max(64, atoi(ov));  // (A/B)
     int cols = snap(OTF ? (Z >= otf_vox ? 1 : otf_vox / Z) : cols_per_block(Z));
     if (const char *ce = getenv("FVP_GATHER_COLS"); ce && !OTF) cols = max(1, atoi(ce));  // (A/B)
     // latency (few frames): one pass of 256/LPV voxels per block, so a single

@@ -57,7 +57,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
                                                        int Jst, int H, int W, int X, int Y, int Z, int cols,
-                                                       int col_blocks, int SP, int band, unsigned pixb, int order, int tx) {
+                                                       int col_blocks, int SP, int band, unsigned pixb) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
@@ -68,32 +68,21 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     const int b = frame0 + bl * NF;  // first frame of the group within the batch (outputs, grid_index)
     const int XY = X * Y;
     int cb = L - bl * col_blocks;
-    // The block's columns: tx == 1: cols consecutive (x, y) columns from c0
-    // (an x-row segment); tx > 1 (host: band > 0): a tile of tx x-rows by
-    // ty = cols / tx columns at (x0, y0), the last tile row clipped at X.
-    const int ty = cols / tx;
-    int x0 = 0, y0 = 0, c0 = 0, ncols;
     if (band > 0) {
-        // bands of `band` x-rows walked tile-column-major: consecutive blocks
+        // bands of `band` x-rows walked column-group-major: consecutive blocks
         // (those resident together on an XCD) cover a compact x-y patch
-        const int gpr = Y / ty;  // tiles per tile row (host: Y % ty == 0, band % tx == 0)
-        const int tb = band / tx, trows = (X + tx - 1) / tx;
-        const int per_band = tb * gpr;
+        const int gpr = Y / cols;  // column groups per x-row (host: Y % cols == 0)
+        const int per_band = band * gpr;
         const int bi = cb / per_band, r = cb - bi * per_band;
-        const int rows = min(tb, trows - bi * tb);
+        const int rows = min(band, X - bi * band);
         const int gc = r / rows, xr = r - gc * rows;
-        x0 = (bi * tb + xr) * tx;
-        y0 = gc * ty;
-        ncols = min(tx, X - x0) * ty;
-        c0 = x0 * Y + y0;
-    } else {
-        c0 = cb * cols;
-        ncols = min(cols, XY - c0);
+        cb = (bi * band + xr) * gpr + gc;
     }
-    // (x, y) column index of the block's column c
-    auto col_of = [&](int c) { return tx == 1 ? c0 + c : (x0 + c / ty) * Y + y0 + (c - (c / ty) * ty); };
+    const int c0 = cb * cols;  // the block's columns: c0 .. c0 + ncols - 1 (an x-row segment when banded)
+    const int ncols = min(cols, XY - c0);
     const int T = ncols * Z;
     const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
     const int q = threadIdx.x % LPV;
     const int GV = V + (V & 1);
     const unsigned qo = (unsigned)q * 16u;
@@ -122,18 +111,13 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     for (int i0 = 0; i0 < T; i0 += VPP) {
         const int i = i0 + threadIdx.x / LPV;
         const bool valid = i < T;
-        // the slot's voxel: column cl, layer zl; ii = its stage index (column-major)
+        // the slot's voxel, layer-major (a wave holds 16/ncols z-layers of all
+        // the block's columns): column cl, layer zl; ii = its stage index
+        // (column-major, as the cube), gn = its index in the cube
         const int sl = min(i, T - 1);
-        int cl, zl;
-        if (order) {  // layer-major slots: a wave holds 16/ncols z-layers of all the block's columns
-            zl = sl / ncols;
-            cl = sl - zl * ncols;
-        } else {
-            cl = sl / Z;
-            zl = sl - cl * Z;
-        }
+        const int zl = sl / ncols, cl = sl - zl * ncols;
         const int ii = cl * Z + zl;
-        const long long gn = (long long)col_of(cl) * Z + zl;  // the voxel's index in the cube
+        const long long gn = (long long)(c0 + cl) * Z + zl;
         float acc[NF][4], blk[NF][4];  // blk (CASC): completed 16-camera blocks (view_sum order)
 #pragma unroll
         for (int f = 0; f < NF; ++f)
@@ -142,7 +126,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         float wx_ = 0.f, wy_ = 0.f, wz_ = 0.f;  // OTF: voxel centre (compute_grid, project_whole.py:43-79)
         if constexpr (OTF) {
             const int iz = zl;
-            const long long r = col_of(cl);
+            const long long r = c0 + cl;
             wx_ = axis_coord(src_.gs.start[0], src_.gs.end[0], X, (int)(r / Y), src_.gs.center[0]);
             wy_ = axis_coord(src_.gs.start[1], src_.gs.end[1], Y, (int)(r % Y), src_.gs.center[1]);
             wz_ = axis_coord(src_.gs.start[2], src_.gs.end[2], Z, iz, src_.gs.center[2]);
@@ -271,17 +255,12 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 for (int e = threadIdx.x; e < J * T4; e += 256) {
                     const int j = e / T4, r = e - (e / T4) * T4;
                     const f32x4 v = *reinterpret_cast<const f32x4 *>(fst + j * SP + 4 * r);
-                    const int c = (4 * r) / Z;  // (Z % 4 == 0: a float4 stays in its column)
-                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * Jst + j) * N +
-                                                                             (long long)col_of(c) * Z + (4 * r - c * Z)));
+                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * Jst + j) * N + n0) + r);
                 }
             } else {
                 for (int j = 0; j < J; ++j) {
-                    float *__restrict__ dst = cube + (bf * Jst + j) * N;
-                    for (int e = threadIdx.x; e < T; e += 256) {
-                        const int c = e / Z;
-                        __builtin_nontemporal_store(fst[j * SP + e], dst + (long long)col_of(c) * Z + (e - c * Z));
-                    }
+                    float *__restrict__ dst = cube + (bf * Jst + j) * N + n0;
+                    for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
                 }
             }
         }
@@ -300,7 +279,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 } else {
                     for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
                 }
-                __builtin_nontemporal_store(m, xy + (bf * Jst + j) * XY + col_of(cc));
+                __builtin_nontemporal_store(m, xy + (bf * Jst + j) * XY + c0 + cc);
             }
         }
     }
@@ -316,11 +295,10 @@ __global__ __launch_bounds__(256, NF == 1 ? 8 : NF == 2 ? 5 : 4) void voxelize_k
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int Jst, int H, int W, int X, int Y, int Z,
-                                                          int cols, int col_blocks, int SP, int band, unsigned pixb,
-                                                          int order, int tx) {
+                                                          int cols, int col_blocks, int SP, int band, unsigned pixb) {
     static_assert(!OTF, "grid kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
-                                            col_blocks, SP, band, pixb, order, tx);
+                                            col_blocks, SP, band, pixb);
 }
 
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
@@ -329,10 +307,10 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
                                                             int J, int Jst, int H, int W, int X, int Y, int Z,
                                                             int cols, int col_blocks, int SP, int band,
-                                                            unsigned pixb, int order, int tx) {
+                                                            unsigned pixb) {
     static_assert(OTF, "on-the-fly kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
-                                            col_blocks, SP, band, pixb, order, tx);
+                                            col_blocks, SP, band, pixb);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -403,7 +381,7 @@ static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
 
 // Gather launch shape for `frames` frames per launch (NF per table entry).
 struct GatherCfg {
-    int cols, band, col_blocks, SP, order, tx;
+    int cols, band, col_blocks, SP;
     size_t lds;
 };
 
@@ -427,10 +405,8 @@ static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg 
     // on the fly: 256-voxel blocks (C5: 4 columns of 64; 128-voxel blocks
     // measured 2-4 % slower, 64 -> 8 % slower, 512 -> 40 % slower, round 3);
     // 4 frames per entry: 128 (the stage holds NF frames)
-    int otf_vox = NF >= 4 ? 128 : 256;
-    if (const char *ov = getenv("FVP_OTF_VOXELS"); ov && OTF) otf_vox = max(64, atoi(ov));  // (A/B)
+    const int otf_vox = NF >= 4 ? 128 : 256;  // (4 frames: 256 -17 %, 64 -9 %; profiles/round3/c5/otf_voxels.txt)
     int cols = snap(OTF ? (Z >= otf_vox ? 1 : otf_vox / Z) : cols_per_block(Z));
-    if (const char *ce = getenv("FVP_GATHER_COLS"); ce && !OTF) cols = max(1, atoi(ce));  // (A/B)
     // latency (few frames): one pass of 256/LPV voxels per block, so a single
     // frame spreads over enough blocks to fill the CUs -- or two passes when
     // one-pass blocks would overflow one round of 8 blocks per CU (the counts
@@ -443,25 +419,8 @@ static int gather_cfg(int frames, int NF, int V, int X, int Y, int Z, GatherCfg 
         if (blocks(cols) > 8 * 256) cols = snap(max(1, 2 * (256 / LPV) / Z));
     }
     c.cols = cols;
-    // Slot order within a block: layer-major (a wave's 16 voxels = z-layers of
-    // all the block's columns, so neighbouring columns' taps share 128-B lines:
-    // C2 0.75 -> 0.59 distinct lines per in-image tap and camera, by a CPU count
-    // over the real geometry) unless FVP_GATHER_ORDER=col (z fastest; A/B).
-    const char *ord = getenv("FVP_GATHER_ORDER");
-    c.order = (ord && ord[0] == 'c') ? 0 : 1;
-    // Column tiles of tx x-rows by cols/tx columns (walked in the same bands),
-    // FVP_GATHER_TILE_X=2 (A/B): neighbours in x share taps as neighbours in y
-    // do, so a 2 x 4 tile with layer-major slots touches fewer lines per wave
-    // than a 1 x 8 strip (CPU count: C2 0.59 -> 0.49 lines per tap and camera,
-    // C4 0.39 -> 0.35 at 2 x 2), but measured slower on the same box (C2 95.3 k
-    // -> 92.8 k frames/s, C4 32.8 k -> 31.6 k; profiles/round3/slot_order):
-    // the default stays 1 x cols strips.
-    const char *tenv = getenv("FVP_GATHER_TILE_X");
-    int tx = tenv ? max(1, atoi(tenv)) : 1;
-    if (!(big && X > kBandRows && kBandRows % tx == 0 && cols % tx == 0 && Y % (cols / tx) == 0)) tx = 1;
-    c.tx = tx;
-    c.band = (big && Y % (cols / tx) == 0 && X > kBandRows) ? kBandRows : 0;
-    c.col_blocks = tx > 1 ? ((X + tx - 1) / tx) * (Y / (cols / tx)) : (X * Y + cols - 1) / cols;
+    c.band = (big && Y % cols == 0 && X > kBandRows) ? kBandRows : 0;
+    c.col_blocks = (X * Y + cols - 1) / cols;
     c.SP = stage_pitch(LPV, cols, Z);
     c.lds = (size_t)NF * 4 * LPV * c.SP * sizeof(float);
     if (OTF) c.lds = ((c.lds / 4 + 3) & ~(size_t)3) * 4 + (size_t)FVP_GRID_SLOTS(V) * FVP_CAM_STRIDE * sizeof(float);
@@ -476,11 +435,11 @@ static void launch_gather(const void *tab, int f0, int nb, const GatherCfg &c, c
     if constexpr (OTF)
         hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
-                           pixb, c.order, c.tx);
+                           pixb);
     else
         hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
-                           pixb, c.order, c.tx);
+                           pixb);
 }
 
 // One voxelize call's shapes.  Heatmaps with more than kJointSlice joints run

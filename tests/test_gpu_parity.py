@@ -467,6 +467,31 @@ def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf, nf, monkeypatch):
     _assert_same(cube[B - 1].cpu().numpy(), ref, "fp16 ring frame")
 
 
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
+def test_fp16_pair_layouts_agree(gpu_device, otf, monkeypatch):
+    """pairs_rows_kernel (a block per row, through LDS) and the per-entry layout
+    kernel (FVP_PAIRS_LAYOUT=entry; also what odd heatmap widths use) build the
+    same pair table: identical cubes and xy planes for 7 frames (entries of 4,
+    2 and 1 frames), 31 ring cameras on a small grid."""
+    from fvp import geometry, synthetic
+    from fvp.config import make_cfg
+    from fvp.project_whole import ProjectLayer
+    from fvp.workloads import WORKLOADS
+    import dataclasses
+
+    w = dataclasses.replace(WORKLOADS["c5"], voxels_per_axis=(24, 20, 12))
+    layer = ProjectLayer(make_cfg(w, str(gpu_device)))
+    layer.verbose = False
+    layer.on_the_fly = otf
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = synthetic.uniform_heatmaps(w, 7, seed=23).half().to(gpu_device)
+    cube, xy = layer.forward_fused(hm, {"seq": [seq] * 7}, cams, rt)
+    monkeypatch.setenv("FVP_PAIRS_LAYOUT", "entry")
+    c_e, x_e = layer.forward_fused(hm, {"seq": [seq] * 7}, cams, rt)
+    assert torch.equal(cube, c_e) and torch.equal(xy, x_e)
+
+
 def test_nms_on_channel_slice_without_copy(gpu_device):
     from fvp.proposal import nms2D
 

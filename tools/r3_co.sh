@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Ran at commit 3524f68: the camera-outer kernel was reverted after this A/B.)
 # Camera-outer gather (voxelize_co_kernel) A/B: FVP_CAM_OUTER=0 (block gather) vs default.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; mkdir -p gpurun_out

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Ran at commit 10edbe4 or earlier: the FVP_GATHER_ORDER / FVP_GATHER_TILE_X / FVP_GATHER_COLS /
+# FVP_OTF_VOXELS knobs were removed once the A/B settled; check that commit out to reproduce.)
 # Columns per cached-grid block with layer-major slots (FVP_GATHER_COLS sweep), C2 / C3 / C4.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; mkdir -p gpurun_out

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Ran at commit 10edbe4 or earlier: the FVP_GATHER_ORDER / FVP_GATHER_TILE_X / FVP_GATHER_COLS /
+# FVP_OTF_VOXELS knobs were removed once the A/B settled; check that commit out to reproduce.)
 # Gather slot order A/B (FVP_GATHER_ORDER=col = z fastest, default = layer-major):
 # the voxelize parity tests (every config bit-exact), then bench lines per order,
 # interleaved, two repeats; and the C5 layout kernel A/B under rocprofv3.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Ran at commit 10edbe4 or earlier: the FVP_GATHER_ORDER / FVP_GATHER_TILE_X / FVP_GATHER_COLS /
+# FVP_OTF_VOXELS knobs were removed once the A/B settled; check that commit out to reproduce.)
 # C5 (on the fly, 4 frames per entry): voxels per block 128 (default) vs 256 vs 64, layer-major slots.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; mkdir -p gpurun_out

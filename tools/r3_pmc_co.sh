@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Ran at commit 3524f68: the camera-outer kernel was reverted after this A/B.)
 # PMC of the C2 gather: block gather (FVP_CAM_OUTER=0) vs camera-outer.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; mkdir -p gpurun_out

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Ran at commit 10edbe4 or earlier: the FVP_GATHER_ORDER / FVP_GATHER_TILE_X / FVP_GATHER_COLS /
+# FVP_OTF_VOXELS knobs were removed once the A/B settled; check that commit out to reproduce.)
 # Column-tile A/B (FVP_GATHER_TILE_X=1: 1 x cols x-row strips; 2: 2 x cols/2 tiles),
 # both with layer-major slots; C4 also at 8 columns (FVP_GATHER_COLS=8).  Full GPU
 # test suite first (the default tiling), then interleaved bench lines, two repeats.

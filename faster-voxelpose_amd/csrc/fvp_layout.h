@@ -97,7 +97,8 @@ __global__ __launch_bounds__(256) void heatmaps_to_pairs_kernel(const T *__restr
 // row) into LDS as [NF][16][W+4] halves (pixel x at x+2, zeros at x = -1, W
 // and for joints >= J), then the row's (W+1) x NF entries go out as one
 // contiguous run of 16-B stores.  The per-entry kernel above reads 2-B values
-// per lane (8 loads per 16-B store) and writes 64-B pieces NF*64 B apart.
+// per lane (8 loads per 16-B store) and writes 64-B pieces NF*64 B apart:
+// C5, 4 frames per entry, 132 -> 97.5 us per launch (profiles/round3/c5/pairs_layout.txt).
 // Needs W even (4-B aligned rows); LDS NF*16*(W/2+2)*4 B.
 template <int NF>
 __global__ __launch_bounds__(256) void pairs_rows_kernel(const _Float16 *__restrict__ hm, uint4 *__restrict__ tab,
@@ -157,7 +158,9 @@ template <int NF>
 inline void launch_pairs(const _Float16 *hm, int nb, int V, int J, int H, int W, uint4 *tab, hipStream_t s) {
     const size_t lds = (size_t)NF * 16 * (W / 2 + 2) * 4;
     const char *ab = getenv("FVP_PAIRS_LAYOUT");  // "entry": the per-entry kernel (A/B)
-    if (W % 2 == 0 && lds <= 64 * 1024 && !(ab && ab[0] == 'e')) {
+    // (one frame per entry: the per-entry kernel, 20.8 vs 40.8 us at C5 B = 1 --
+    // a 15 KB row per block leaves its load / store phases exposed)
+    if (NF > 1 && W % 2 == 0 && lds <= 64 * 1024 && !(ab && ab[0] == 'e')) {
         hipLaunchKernelGGL((pairs_rows_kernel<NF>), dim3((unsigned)((long long)nb / NF * V * H)), dim3(256), lds, s, hm,
                            tab, J, H, W, V);
     } else {

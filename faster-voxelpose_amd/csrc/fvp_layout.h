@@ -160,7 +160,8 @@ inline void launch_pairs(const _Float16 *hm, int nb, int V, int J, int H, int W,
     const char *ab = getenv("FVP_PAIRS_LAYOUT");  // "entry": the per-entry kernel (A/B)
     // (one frame per entry: the per-entry kernel, 20.8 vs 40.8 us at C5 B = 1 --
     // a 15 KB row per block leaves its load / store phases exposed)
-    if (NF > 1 && W % 2 == 0 && lds <= 64 * 1024 && !(ab && ab[0] == 'e')) {
+    const bool aligned = ((unsigned long long)hm & 3ull) == 0;  // 4-B row loads (a C-ABI caller may pass any fp16 pointer)
+    if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024 && !(ab && ab[0] == 'e')) {
         hipLaunchKernelGGL((pairs_rows_kernel<NF>), dim3((unsigned)((long long)nb / NF * V * H)), dim3(256), lds, s, hm,
                            tab, J, H, W, V);
     } else {

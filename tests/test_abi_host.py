@@ -47,8 +47,14 @@ def test_argument_validation_without_gpu():
     assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, 1, 100, None) == 1003
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 4 * 5 * 128 * 240 * 32 * 4  # one 32-joint slice
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 1025, 128, 240) == 0
-    # fp16, J <= 16: pixel-pair table [V][H][W+1] x 64 B, 2 frames of C5 per chunk
-    assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 2 * 31 * 128 * 241 * 64
+    # fp16, J <= 16: pixel-pair table [V][H][W+1] x 64 B, one group of 4 C5 frames per chunk
+    # (FVP_PAIR_FRAMES=2: the two-frame grouping, 2 frames)
+    assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 4 * 31 * 128 * 241 * 64
+    os.environ["FVP_PAIR_FRAMES"] = "2"
+    try:
+        assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 2 * 31 * 128 * 241 * 64
+    finally:
+        del os.environ["FVP_PAIR_FRAMES"]
     # fp16, J > 16: the fp32 channels-last copy
     assert lib.fvp_voxelize_f16_workspace_bytes(1, 5, 17, 128, 240) == 5 * 128 * 240 * 32 * 4
     assert lib.fvp_pack_grid(None, 5, 100, None, None) == 1001

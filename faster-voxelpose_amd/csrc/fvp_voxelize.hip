@@ -365,13 +365,16 @@ static size_t frame_bytes(int V, int J, int H, int W, bool half) {
 }
 
 // Frames per chunk: keep a chunk's re-laid-out copy inside the 256 MB Infinity
-// Cache (measured best: ~80 MB for the fp32 layout, C2: 8 frames; ~128 MB of
-// the fp16 pair table, but at least one group of pair_frames() frames when
-// that fits the cache: 4 frames = 245 MB at C5).
+// Cache.  fp32 layout: ~120 MB (C2 / C3 / C4: 12 frames) -- with layer-major
+// slots 12 frames beat 8 by 5.5 % at C2, 3.5 % at C3, 1-3 % at C4, while 16+
+// lose (C2: 4 / 8 / 10 / 12 / 16 / 20 / 32 frames = 83 / 96 / 98 / 101 / 96 /
+// 80 / 81 k frames/s; profiles/round3/slot_order/chunk_sweep.txt; 8 was best
+// with column-major slots).  fp16 pair table: ~128 MB, but at least one group
+// of pair_frames() frames when that fits the cache: 4 frames = 245 MB at C5.
 static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     const size_t per = frame_bytes(V, J, H, W, half);
     const bool pairs = use_pairs(J, half);
-    const size_t budget = pairs ? (128ull << 20) : (80ull << 20);
+    const size_t budget = pairs ? (128ull << 20) : (120ull << 20);
     long long c = (long long)(budget / (per ? per : 1));
     if (pairs && c < pair_frames() && (size_t)pair_frames() * per <= (256ull << 20)) c = pair_frames();
     if (c < 1) c = 1;

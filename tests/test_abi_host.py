@@ -43,7 +43,7 @@ def test_argument_validation_without_gpu():
     assert lib.fvp_voxelize(1, 1, 5, 1025, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1002  # J > 1024
     assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, None, 0, None) == 1003  # no workspace
     need = lib.fvp_voxelize_workspace_bytes(256, 5, 15, 128, 240)
-    assert need == 8 * 5 * 128 * 240 * 16 * 4  # channels-last chunk of 8 frames (J padded to 16)
+    assert need == 12 * 5 * 128 * 240 * 16 * 4  # channels-last chunk of 12 frames (J padded to 16)
     assert lib.fvp_voxelize(1, 1, 5, 15, 128, 240, 1, None, 80, 80, 20, 1, None, 1, 100, None) == 1003
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 4 * 5 * 128 * 240 * 32 * 4  # one 32-joint slice
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 1025, 128, 240) == 0

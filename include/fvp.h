@@ -118,8 +118,10 @@ int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W,
                  void *workspace, size_t workspace_bytes, void *stream);
 /* Same with fp16 heatmaps (IEEE binary16), computed in fp32 (exact upcast).
  * For J <= 16 the chunk is re-laid out as an fp16 pixel-pair table (each
- * 64-B entry holds pixels x and x+1 of a row), so a voxel-camera is 2 loads;
- * the workspace size differs from the fp32 one. */
+ * 64-B entry holds pixels x and x+1 of a row), so a voxel-camera is 2 loads
+ * per frame, with up to 4 frames interleaved per entry; the workspace size
+ * differs from the fp32 one and is read per call (the environment variable
+ * FVP_PAIR_FRAMES=2 selects the two-frame grouping). */
 size_t fvp_voxelize_f16_workspace_bytes(int B, int V, int J, int H, int W);
 int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W,
                      const float *packed_grids, const int32_t *grid_index,

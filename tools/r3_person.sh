@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Ran on a temporary build with person_cl_kernel<..., RW=4> and its FVP_PERSON_ROWS knob; both were removed.)
 # Person planes: 4-row x 16-z blocks (default) vs one-row 64-z blocks (FVP_PERSON_ROWS=1).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; mkdir -p gpurun_out

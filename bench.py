@@ -31,7 +31,9 @@ sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
 
 METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_pairs_kernel", "voxelize_kernel", "voxelize_cams_kernel")  # the fvp_voxelize op
+# the fvp_voxelize op: layout pass (fp32 channels-last, fp16 pair table per entry or per row) + gather
+VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_pairs_kernel", "pairs_rows_kernel", "voxelize_kernel",
+               "voxelize_cams_kernel")
 
 
 def parse():
@@ -209,6 +211,88 @@ def note(msg):
 
 
 # ---------------------------------------------------------------------------
+# The step's sharding and its GPU-local / collective parts, importable so that
+# tests/test_bench_step_gloo.py runs this exact code at world 2 and 3 over gloo
+# with the CPU oracle as the compute (the driver's SCALE run executes it over
+# RCCL with the HIP ops).
+def shard_plan(world, rank, batch, X, slabs=False, strong=False):
+    """(frames per rank, the rank's first frame of the job, x0, x1) of one step.
+
+    weak (default): every rank takes `batch` frames, rank r frames
+    [r*batch, (r+1)*batch) of the job; --strong: `batch` is the job's frames,
+    split evenly; --slabs: every rank holds the same `batch` frames and
+    voxelises x-rows [x0, x1) of each (SURVEY.md §8(e) large-frame mode)."""
+    from fvp import parallel
+
+    B = batch
+    if strong and not slabs:  # fixed total frames: each rank takes its shard
+        if B % world:
+            raise ValueError(f"--strong: {B} frames do not split evenly over {world} ranks")
+        B //= world
+    first = 0 if slabs else parallel.shard_frames(world * B, world, rank)[0]
+    x0, x1 = parallel.shard_slab(X, world, rank) if slabs else (0, X)
+    return B, first, x0, x1
+
+
+class HipCompute:
+    """The step's compute on the HIP ops (fvp.project_whole / fvp.proposal)."""
+
+    def __init__(self, layer, cams, rt):
+        self.layer, self.cams, self.rt = layer, cams, rt
+
+    def voxelize(self, hm, meta, x0=None, x1=None):
+        if x0 is None:
+            return self.layer.forward_fused(hm, meta, self.cams, self.rt, want_cube=True, want_xy=True)
+        return self.layer.forward_slab(hm, meta, self.cams, self.rt, x0, x1, want_cube=True, want_xy=True)
+
+    @staticmethod
+    def nms2D(prob, K):
+        from fvp.proposal import nms2D
+        return nms2D(prob, K)
+
+    @staticmethod
+    def nms2D_columns(prob, K, cube):
+        from fvp.proposal import nms2D_columns
+        return nms2D_columns(prob, K, cube)
+
+    @staticmethod
+    def gather_columns(cube, flat):
+        from fvp.proposal import gather_columns
+        return gather_columns(cube, flat)
+
+
+def step_functions(compute, hm, meta, x0, x1, X, world, grouped, slabs, root, K):
+    """vox() -> (cube, xy); post(cube, xy) -> (vals, flat, cols); collect(vals, flat)
+    -> every rank's proposals or None.  One step = vox, post, collect."""
+    from fvp import parallel
+
+    def vox():
+        return compute.voxelize(hm, meta, x0, x1) if slabs else compute.voxelize(hm, meta)
+
+    def post(cube, xy):
+        if slabs and world > 1:  # xy slabs -> full planes; owned columns -> one all-reduce
+            xy = parallel.gather_xy_slabs(xy, X)
+            vals, idx, flat = compute.nms2D(xy[:, root:root + 1], K)
+            return vals, flat, parallel.columns_from_slab(cube, flat, x0, gather=compute.gather_columns)
+        vals, idx, flat, cols = compute.nms2D_columns(xy[:, root:root + 1], K, cube)  # one launch
+        return vals, flat, cols
+
+    def collect(vals, flat):
+        if grouped and not slabs:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
+            return parallel.gather_proposals(vals, flat)
+        return None
+
+    return vox, post, collect
+
+
+def run_step(run_vox, run_post, collect, after_vox=None):
+    cube, xy = run_vox()
+    if after_vox is not None:
+        after_vox()
+    vals, flat, cols = run_post(cube, xy)
+    return vals, flat, cols, collect(vals, flat)
+
+
 def main():
     # stdout carries only the JSON line: native libraries (RCCL prints a version
     # banner when a communicator comes up) write to fd 1 directly, so fd 1 points
@@ -229,9 +313,9 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from fvp import geometry, parallel, synthetic
+    from fvp import geometry, synthetic
     from fvp.project_whole import ProjectLayer
-    from fvp.proposal import nms2D, nms2D_columns
+    from fvp.proposal import nms2D_columns
     from fvp.workloads import WORKLOADS
 
     # FVP_BENCH_BACKEND=gloo: plumbing rehearsal of N ranks that may share a
@@ -263,11 +347,11 @@ def main():
     n_devices = min(world, ndev) if rehearsal else world  # distinct GPUs doing the work
 
     w = WORKLOADS[args.workload]
-    B = args.batch or DEFAULT_BATCH.get(args.workload, 64)
-    if args.strong and not args.slabs:  # fixed total frames: each rank takes its shard
-        if B % world:
-            raise SystemExit(f"--strong: {B} frames do not split evenly over {world} ranks")
-        B //= world
+    try:
+        B, first, x0, x1 = shard_plan(world, rank, args.batch or DEFAULT_BATCH.get(args.workload, 64),
+                                      w.voxels_per_axis[0], args.slabs, args.strong)
+    except ValueError as e:
+        raise SystemExit(str(e))
     cams, seq = w.cameras()
     V = len(cams[seq])
     J = w.num_joints
@@ -281,10 +365,7 @@ def main():
     layer.on_the_fly = {"auto": None, "on": True, "off": False}[args.on_the_fly]
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
     # large-frame mode: all ranks hold the same frames (x-slabs); otherwise own frames
-    # weak scaling: rank r owns frames shard_frames(world*B, world, r) of the job
-    first = 0 if args.slabs else parallel.shard_frames(world * B, world, rank)[0]
     hm_host = synthetic.gaussian_heatmaps(w, B, first_frame=first)
-    x0, x1 = parallel.shard_slab(X, world, rank) if args.slabs else (0, X)
     hm = torch.from_numpy(hm_host).to(dev)
     if w.dtype == "float16":  # C5: fp16 heatmaps (computed in fp32 by the kernels)
         hm = hm.half()
@@ -329,18 +410,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ev = []
 
-    def vox():
-        if args.slabs:
-            return layer.forward_slab(hm, meta, cams, rt, x0, x1, want_cube=True, want_xy=True)
-        return layer.forward_fused(hm, meta, cams, rt, want_cube=True, want_xy=True)
-
-    def post(cube, xy):
-        if args.slabs and world > 1:  # xy slabs -> full planes; owned columns -> one all-reduce
-            xy = parallel.gather_xy_slabs(xy, X)
-            vals, idx, flat = nms2D(xy[:, root:root + 1], K)
-            return vals, flat, parallel.columns_from_slab(cube, flat, x0)
-        vals, idx, flat, cols = nms2D_columns(xy[:, root:root + 1], K, cube)  # one launch
-        return vals, flat, cols
+    vox, post, collect = step_functions(HipCompute(layer, cams, rt), hm, meta, x0, x1, X, world, grouped,
+                                        args.slabs, root, K)
 
     if args.graph == "on" and args.slabs and world > 1:
         raise SystemExit("--graph on captures GPU-local work only; the slab collectives sit inside post()")
@@ -358,14 +429,8 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        cube, xy = run_vox()
-        if record:
-            e1.record(stream)
             ev.append((e0, e1))
-        vals, flat, cols = run_post(cube, xy)
-        if grouped and not args.slabs:  # the one collective: compact proposals of every rank's frames (RCCL over xGMI)
-            parallel.gather_proposals(vals, flat)
-        return cols
+        return run_step(run_vox, run_post, collect, after_vox=(lambda: e1.record(stream)) if record else None)[2]
 
     note(f"warmup {args.warmup} + {args.steps} timed steps of {B} frames")
     for _ in range(args.warmup):

@@ -4,7 +4,6 @@
 // range check.
 #pragma once
 
-#include <cstdlib>
 #include <utility>
 
 #include "fvp_device.h"
@@ -157,11 +156,11 @@ inline size_t pair_frame_bytes(int V, int H, int W) { return (size_t)V * H * (W 
 template <int NF>
 inline void launch_pairs(const _Float16 *hm, int nb, int V, int J, int H, int W, uint4 *tab, hipStream_t s) {
     const size_t lds = (size_t)NF * 16 * (W / 2 + 2) * 4;
-    const char *ab = getenv("FVP_PAIRS_LAYOUT");  // "entry": the per-entry kernel (A/B)
     // (one frame per entry: the per-entry kernel, 20.8 vs 40.8 us at C5 B = 1 --
-    // a 15 KB row per block leaves its load / store phases exposed)
+    // a 15 KB row per block leaves its load / store phases exposed; it also
+    // serves odd widths and fp16 pointers that are not 4-B aligned)
     const bool aligned = ((unsigned long long)hm & 3ull) == 0;  // 4-B row loads (a C-ABI caller may pass any fp16 pointer)
-    if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024 && !(ab && ab[0] == 'e')) {
+    if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024) {
         hipLaunchKernelGGL((pairs_rows_kernel<NF>), dim3((unsigned)((long long)nb / NF * V * H)), dim3(256), lds, s, hm,
                            tab, J, H, W, V);
     } else {

@@ -32,7 +32,6 @@
 // tap and the camera sum order are the reference's (fvp_device.h: torch's
 // CPU mean over the views folds complete blocks of 16 cameras, CASC = V > 16),
 // so the result is bit-exact.
-#include <cstdlib>
 #include <type_traits>
 
 #include "fvp_layout.h"
@@ -48,8 +47,9 @@ struct CoordSource {
     const float *grids;     // packed grids [S][N][GV][2]            (!OTF)
     const float *cams;      // camera records [S][V][FVP_CAM_STRIDE] (OTF)
     const float *resize_t;  // [2][3]                                (OTF)
-    fvp_grid_spec gs;
+    fvp_grid_spec gs;       // (OTF) the whole grid: x-row i of a launch is row x_off + i of gs
     fvp_image_spec im;
+    int x_off;              // (OTF) first x-row of an x-slab launch (0: the whole grid)
 };
 
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
@@ -57,7 +57,8 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
                                                        int Jst, int H, int W, int X, int Y, int Z, int cols,
-                                                       int col_blocks, int SP, int band, unsigned pixb) {
+                                                       int col_blocks, int SP, int band, unsigned pixb,
+                                                       bool cube16) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
@@ -127,7 +128,8 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         if constexpr (OTF) {
             const int iz = zl;
             const long long r = c0 + cl;
-            wx_ = axis_coord(src_.gs.start[0], src_.gs.end[0], X, (int)(r / Y), src_.gs.center[0]);
+            wx_ = axis_coord(src_.gs.start[0], src_.gs.end[0], src_.gs.bins[0], src_.x_off + (int)(r / Y),
+                             src_.gs.center[0]);
             wy_ = axis_coord(src_.gs.start[1], src_.gs.end[1], Y, (int)(r % Y), src_.gs.center[1]);
             wz_ = axis_coord(src_.gs.start[2], src_.gs.end[2], Z, iz, src_.gs.center[2]);
         }
@@ -240,11 +242,12 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
     }
     __syncthreads();
     // Epilogue.  When every run is 16-B aligned (T, SP, Z, N multiples of 4: the
-    // C2 / C3 / C4 launches) the cube goes out as float4 non-temporal stores and
+    // C2 / C3 / C4 launches; cube16: the caller's cube pointer is 16-B aligned,
+    // checked on the host) the cube goes out as float4 non-temporal stores and
     // the z-max reads 4 voxels per LDS load: a sixth of the store instructions
     // and independent LDS reads instead of a 20-long dependent chain
     // (tools/gather_probe.py FULL2: C2 8 frames 62.1 -> 59.8 us).
-    const bool vec = ((T | SP | Z | (int)(N & 3)) & 3) == 0;
+    const bool vec = ((T | SP | Z | (int)(N & 3)) & 3) == 0 && cube16;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
         const float *fst = stage + f * JP * SP;
@@ -295,10 +298,11 @@ __global__ __launch_bounds__(256, NF == 1 ? 8 : NF == 2 ? 5 : 4) void voxelize_k
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int Jst, int H, int W, int X, int Y, int Z,
-                                                          int cols, int col_blocks, int SP, int band, unsigned pixb) {
+                                                          int cols, int col_blocks, int SP, int band, unsigned pixb,
+                                                          bool cube16) {
     static_assert(!OTF, "grid kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
-                                            col_blocks, SP, band, pixb);
+                                            col_blocks, SP, band, pixb, cube16);
 }
 
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
@@ -307,10 +311,10 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
                                                             float *__restrict__ cube, float *__restrict__ xy, int V,
                                                             int J, int Jst, int H, int W, int X, int Y, int Z,
                                                             int cols, int col_blocks, int SP, int band,
-                                                            unsigned pixb) {
+                                                            unsigned pixb, bool cube16) {
     static_assert(OTF, "on-the-fly kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
-                                            col_blocks, SP, band, pixb);
+                                            col_blocks, SP, band, pixb, cube16);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -353,12 +357,10 @@ static bool use_pairs(int J, bool half) { return half && J <= 16; }
 // Frames per fp16 pair-table entry: 4 (two 128-B lines per entry), so each
 // tap setup -- at C5 the on-the-fly projection of 31 cameras -- serves four
 // frames.  Same box, C5 (profiles/round3/c5/pair_frames_ab.txt): B = 8 2.83 k
-// -> 3.25 k frames/s, B = 32 3.11 k -> 3.43 k against 2 per entry.
-// FVP_PAIR_FRAMES=2 restores two (read per call: the A/B and the tests).
-static int pair_frames() {
-    const char *e = getenv("FVP_PAIR_FRAMES");
-    return (e && atoi(e) == 2) ? 2 : 4;
-}
+// -> 3.25 k frames/s, B = 32 3.11 k -> 3.43 k against 2 per entry.  A batch's
+// remainder runs as a pair and / or a single frame (run_frames), so every
+// grouping is exercised by batches of 2, 3, 5 and 7 frames.
+constexpr int kPairFrames = 4;
 
 static size_t frame_bytes(int V, int J, int H, int W, bool half) {
     return use_pairs(J, half) ? pair_frame_bytes(V, H, W) : cl_frame_bytes(V, J, H, W);
@@ -370,13 +372,13 @@ static size_t frame_bytes(int V, int J, int H, int W, bool half) {
 // lose (C2: 4 / 8 / 10 / 12 / 16 / 20 / 32 frames = 83 / 96 / 98 / 101 / 96 /
 // 80 / 81 k frames/s; profiles/round3/slot_order/chunk_sweep.txt; 8 was best
 // with column-major slots).  fp16 pair table: ~128 MB, but at least one group
-// of pair_frames() frames when that fits the cache: 4 frames = 245 MB at C5.
+// of kPairFrames frames when that fits the cache: 4 frames = 245 MB at C5.
 static int chunk_frames(int B, int V, int J, int H, int W, bool half) {
     const size_t per = frame_bytes(V, J, H, W, half);
     const bool pairs = use_pairs(J, half);
     const size_t budget = pairs ? (128ull << 20) : (120ull << 20);
     long long c = (long long)(budget / (per ? per : 1));
-    if (pairs && c < pair_frames() && (size_t)pair_frames() * per <= (256ull << 20)) c = pair_frames();
+    if (pairs && c < kPairFrames && (size_t)kPairFrames * per <= (256ull << 20)) c = kPairFrames;
     if (c < 1) c = 1;
     if (c > B) c = B;
     return (int)c;
@@ -435,14 +437,15 @@ static void launch_gather(const void *tab, int f0, int nb, const GatherCfg &c, c
                           const int32_t *grid_index, int V, int J, int Jst, int H, int W, int X, int Y, int Z,
                           float *cube, float *xy, unsigned pixb, hipStream_t s) {
     const dim3 grid((unsigned)(nb / NF * c.col_blocks));
+    const bool cube16 = ((unsigned long long)cube & 15ull) == 0;  // float4 epilogue stores
     if constexpr (OTF)
         hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
-                           pixb);
+                           pixb, cube16);
     else
         hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
-                           pixb);
+                           pixb, cube16);
 }
 
 // One voxelize call's shapes.  Heatmaps with more than kJointSlice joints run
@@ -510,7 +513,7 @@ static int run_direct(const float *hm_cl, int cp, int B, const VoxJob &j, const 
 // with one line and one tap setup: C5 3.97 -> 3.12 ms per 8 frames (the
 // gather waits on L1 misses; measured).  The fp32 channels-last table keeps
 // one frame per entry (NF = 2 measured 4 % slower at C2: the L2 working set
-// doubles).  Four frames per entry (pair_frames) amortise the tap setup
+// doubles).  Four frames per entry (kPairFrames) amortise the tap setup
 // further; the batch runs as groups of 4, then a pair, then a single frame.
 // Frames of a group must share one sampling grid, so batches that mix
 // sequences (grid_index given) run at NF = 1.
@@ -519,9 +522,9 @@ static int run_frames(const T *hm, int B, const VoxJob &j, const CoordSource &sr
     if constexpr (PAIR) {
         const int cf = chunk_frames(B, j.V, j.J, j.H, j.W, sizeof(T) == 2);
         int done = 0;
-        if (!j.grid_index && pair_frames() == 4 && cf >= 4) {  // workspace holds >= 4 frames
-            done = B & ~3;
-            const int st = run_chunks<LPV, PAIR, OTF, CASC, 4, T>(hm, 0, done, j, src, ws, s);
+        if (!j.grid_index && cf >= kPairFrames) {  // workspace holds >= 4 frames
+            done = B / kPairFrames * kPairFrames;
+            const int st = run_chunks<LPV, PAIR, OTF, CASC, kPairFrames, T>(hm, 0, done, j, src, ws, s);
             if (st != FVP_OK || done == B) return st;
         }
         if (!j.grid_index && cf >= 2 && B - done >= 2) {  // workspace holds >= 2 frames
@@ -742,10 +745,6 @@ extern "C" int fvp_voxel_columns(const void *heatmaps, int half, long long view_
     return (int)hipGetLastError();
 }
 
-namespace fvp {
-
-}  // namespace fvp
-
 extern "C" int fvp_pack_grid(const float *sample_grid, int V, long long N, float *packed, void *stream) {
     if (!sample_grid || !packed) return FVP_ERR_NULL;
     if (V <= 0 || N <= 0) return FVP_ERR_SHAPE;
@@ -789,27 +788,55 @@ extern "C" int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H
                                               (hipStream_t)stream);
 }
 
-extern "C" int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H, int W,
-                                 const float *cams, const int32_t *grid_index, const float *resize_t,
-                                 const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
-                                 void *workspace, size_t workspace_bytes, void *stream) {
+namespace fvp {
+
+// The on-the-fly entry points, for the whole grid or for x-rows [x0, x1) of it
+// (the large-frame mode): every voxel's coordinates come from
+// its global indices, so a slab is bit-identical to the same rows of the
+// whole-grid launch, and no rank builds or reads a sample grid.
+static int voxelize_cams_rows(const void *heatmaps, bool half, const float *hm_cl, int cp, int B, int V, int J, int H,
+                              int W, const float *cams, const int32_t *grid_index, const float *resize_t,
+                              const fvp_grid_spec *grid, const fvp_image_spec *img, int x0, int x1, float *cube,
+                              float *xy, void *workspace, size_t workspace_bytes, hipStream_t s) {
     if (!cams || !resize_t || !grid || !img) return FVP_ERR_NULL;
-    const int X = grid->bins[0], Y = grid->bins[1], Z = grid->bins[2];
-    const int st = fvp::check_args(heatmaps, B, V, J, H, W, cams, X, Y, Z);
+    const int Y = grid->bins[1], Z = grid->bins[2];
+    if (x0 < 0 || x1 > grid->bins[0] || x0 >= x1) return FVP_ERR_SHAPE;
+    const int X = x1 - x0;  // the launch's x-rows
+    const int st = check_args(hm_cl ? (const void *)hm_cl : heatmaps, B, V, J, H, W, cams, X, Y, Z);
     if (st != FVP_OK) return st;
     if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
     if (!cube && !xy) return FVP_OK;
-    fvp::CoordSource src{};
+    CoordSource src{};
     src.cams = cams;
     src.resize_t = resize_t;
     src.gs = *grid;
     src.im = *img;
+    src.x_off = x0;
+    if (hm_cl) return voxelize_cl_any<true>(hm_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, s);
     if (half)
-        return fvp::voxelize_any<true, _Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, src,
-                                                 grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes,
-                                                 (hipStream_t)stream);
-    return fvp::voxelize_any<true, float>(reinterpret_cast<const float *>(heatmaps), B, V, J, H, W, src, grid_index,
-                                          X, Y, Z, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
+        return voxelize_any<true, _Float16>(reinterpret_cast<const _Float16 *>(heatmaps), B, V, J, H, W, src,
+                                            grid_index, X, Y, Z, cube, xy, workspace, workspace_bytes, s);
+    return voxelize_any<true, float>(reinterpret_cast<const float *>(heatmaps), B, V, J, H, W, src, grid_index, X, Y,
+                                     Z, cube, xy, workspace, workspace_bytes, s);
+}
+
+}  // namespace fvp
+
+extern "C" int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H, int W,
+                                 const float *cams, const int32_t *grid_index, const float *resize_t,
+                                 const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
+                                 void *workspace, size_t workspace_bytes, void *stream) {
+    if (!grid) return FVP_ERR_NULL;
+    return fvp::voxelize_cams_rows(heatmaps, half != 0, nullptr, 0, B, V, J, H, W, cams, grid_index, resize_t, grid,
+                                   img, 0, grid->bins[0], cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+extern "C" int fvp_voxelize_cams_slab(const void *heatmaps, int half, int B, int V, int J, int H, int W,
+                                      const float *cams, const int32_t *grid_index, const float *resize_t,
+                                      const fvp_grid_spec *grid, const fvp_image_spec *img, int x_begin, int x_end,
+                                      float *cube, float *xy, void *workspace, size_t workspace_bytes, void *stream) {
+    return fvp::voxelize_cams_rows(heatmaps, half != 0, nullptr, 0, B, V, J, H, W, cams, grid_index, resize_t, grid,
+                                   img, x_begin, x_end, cube, xy, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" int fvp_voxelize_cl(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
@@ -828,17 +855,17 @@ extern "C" int fvp_voxelize_cl_cams(const float *heatmaps_cl, int cp, int B, int
                                     const float *cams, const int32_t *grid_index, const float *resize_t,
                                     const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
                                     void *stream) {
-    if (!cams || !resize_t || !grid || !img) return FVP_ERR_NULL;
-    const int X = grid->bins[0], Y = grid->bins[1], Z = grid->bins[2];
-    const int st = fvp::check_args(heatmaps_cl, B, V, J, H, W, cams, X, Y, Z);
-    if (st != FVP_OK) return st;
-    if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
-    if (!cube && !xy) return FVP_OK;
-    fvp::CoordSource src{};
-    src.cams = cams;
-    src.resize_t = resize_t;
-    src.gs = *grid;
-    src.im = *img;
-    return fvp::voxelize_cl_any<true>(heatmaps_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy,
-                                      (hipStream_t)stream);
+    if (!heatmaps_cl) return FVP_ERR_NULL;
+    if (!grid) return FVP_ERR_NULL;
+    return fvp::voxelize_cams_rows(nullptr, false, heatmaps_cl, cp, B, V, J, H, W, cams, grid_index, resize_t, grid,
+                                   img, 0, grid->bins[0], cube, xy, nullptr, 0, (hipStream_t)stream);
+}
+
+extern "C" int fvp_voxelize_cl_cams_slab(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
+                                         const float *cams, const int32_t *grid_index, const float *resize_t,
+                                         const fvp_grid_spec *grid, const fvp_image_spec *img, int x_begin,
+                                         int x_end, float *cube, float *xy, void *stream) {
+    if (!heatmaps_cl) return FVP_ERR_NULL;
+    return fvp::voxelize_cams_rows(nullptr, false, heatmaps_cl, cp, B, V, J, H, W, cams, grid_index, resize_t, grid,
+                                   img, x_begin, x_end, cube, xy, nullptr, 0, (hipStream_t)stream);
 }

@@ -48,10 +48,16 @@ SIGNATURES = {
     "fvp_voxelize_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                           ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p, c_void_p, c_void_p,
                           ctypes.c_size_t, c_void_p],
+    "fvp_voxelize_cams_slab": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                               ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_int, c_int, c_void_p, c_void_p,
+                               c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_voxelize_cl": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                         c_void_p, c_void_p, c_void_p],
     "fvp_voxelize_cl_cams": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                              ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_void_p, c_void_p, c_void_p],
+    "fvp_voxelize_cl_cams_slab": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                  ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec), c_int, c_int, c_void_p,
+                                  c_void_p, c_void_p],
     "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_nms_topk_columns": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_int, c_int, c_void_p, c_void_p],
@@ -101,7 +107,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _LIB = None
 
 

@@ -527,35 +527,42 @@ class FvpWeightNet:
 
 
 class GraphedCNN:
-    """An FvpCNN whose calls replay from hipGraphs, one per input shape (up to
-    ``max_shapes``, most recent kept): the input is copied into the captured
+    """An FvpCNN whose calls replay from hipGraphs, one per input shape (the
+    first ``max_shapes`` shapes seen): the input is copied into the captured
     buffer and the outputs are cloned out.  For launch-bound networks: the
     1-D C2CNet on B*K columns of length Z is ~20 kernels of a few us each
-    (C3 B=8: 0.35 -> 0.21 ms, profiles/round3).  Inside another capture, or
-    for shapes beyond the cache, the network runs eagerly."""
+    (C3 B=8: 0.35 -> 0.21 ms, profiles/round3).  Inside another capture, and
+    for shapes beyond the cache (counted in ``eager_calls``, so a workload
+    that cycles through more shapes shows up instead of re-capturing on every
+    call), the network runs eagerly.  Capture and replay run with the input's
+    device current: the fvp ops launch on that device's stream, so a net on a
+    device that is not the current one still records into its graph."""
 
     def __init__(self, net: "FvpCNN", max_shapes: int = 4):
         self.net, self.max_shapes = net, max_shapes
         self._graphs = {}  # (method, shape, dtype, device) -> (static input, CapturedStep)
+        self.eager_calls = 0
 
     def _run(self, method: str, x: torch.Tensor):
         fn = getattr(self.net, method)
         if torch.cuda.is_current_stream_capturing() or not x.is_cuda:
             return fn(x)
         key = (method, tuple(x.shape), x.dtype, x.device)
-        hit = self._graphs.pop(key, None)
-        if hit is None:
-            from .graphs import CapturedStep
+        hit = self._graphs.get(key)
+        if hit is None and len(self._graphs) >= self.max_shapes:
+            self.eager_calls += 1
+            return fn(x)
+        with torch.cuda.device(x.device):
+            if hit is None:
+                from .graphs import CapturedStep
 
-            static = x.detach().clone()
-            hit = (static, CapturedStep(lambda: fn(static)))
-            if len(self._graphs) >= self.max_shapes:
-                self._graphs.pop(next(iter(self._graphs)))
-        self._graphs[key] = hit  # most recent last
-        static, cap = hit
-        static.copy_(x)
-        out = cap.replay()
-        return tuple(o.clone() for o in out) if isinstance(out, tuple) else out.clone()
+                static = x.detach().clone()
+                hit = (static, CapturedStep(lambda: fn(static)))
+                self._graphs[key] = hit
+            static, cap = hit
+            static.copy_(x)
+            out = cap.replay()
+            return tuple(o.clone() for o in out) if isinstance(out, tuple) else out.clone()
 
     def __call__(self, x: torch.Tensor):
         return self._run("__call__", x)

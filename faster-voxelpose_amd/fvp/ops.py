@@ -133,9 +133,11 @@ def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Opt
 def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Optional[torch.Tensor],
                   resize_t: torch.Tensor, start: list[float], end: list[float], center: list[float], bins: list[int],
                   ori_max: float, img_w: float, img_h: float, want_cube: bool,
-                  want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
+                  want_xy: bool, x_begin: int = 0, x_end: int = -1) -> tuple[torch.Tensor, torch.Tensor]:
     """voxelize with the sampling coordinates projected on the fly from packed camera
-    records cams [S,V,FVP_CAM_STRIDE] (no cached grid; for grids too large to stay cached)."""
+    records cams [S,V,FVP_CAM_STRIDE] (no cached grid; for grids too large to stay cached).
+    x_begin / x_end (-1: bins[0]): only the voxels of x-rows [x_begin, x_end) of the
+    grid -- an x-slab of the large-frame mode -- as cube [B,J,x_end-x_begin,Y,Z]."""
     if heatmaps.device.type != "cuda":
         raise _lib.FvpError(f"fvp: heatmaps must be on a HIP device, got {heatmaps.device}")
     half = heatmaps.dtype == torch.float16
@@ -147,7 +149,7 @@ def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Option
         cm = cm.unsqueeze(0)
     if cm.shape[1] != V:
         raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
-    X, Y, Z = bins
+    x0, x1, X, Y, Z = _x_rows(bins, x_begin, x_end)
     gi = _grid_index(grid_index, B, cm.shape[0], hm.device)
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
@@ -160,15 +162,29 @@ def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Option
     ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=hm.device)
     g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
     im = ImageSpec(ori_max, img_w, img_h, W, H)
-    _lib.call("fvp_voxelize_cams", _ptr(hm), int(half), B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im,
-              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _ptr(ws), ws_bytes, _stream(hm))
+    outs = (_ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _ptr(ws), ws_bytes, _stream(hm))
+    if X == bins[0]:
+        _lib.call("fvp_voxelize_cams", _ptr(hm), int(half), B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im, *outs)
+    else:
+        _lib.call("fvp_voxelize_cams_slab", _ptr(hm), int(half), B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im,
+                  x0, x1, *outs)
     return cube, xy
 
 
+def _x_rows(bins, x_begin: int, x_end: int):
+    """(x0, x1, rows, Y, Z) of an x-row range of a grid (x_end = -1: to the end)."""
+    X, Y, Z = (int(b) for b in bins)
+    x1 = X if x_end < 0 else int(x_end)
+    if not 0 <= x_begin < x1 <= X:
+        raise ValueError(f"x-slab [{x_begin}, {x1}) outside [0, {X})")
+    return int(x_begin), x1, x1 - int(x_begin), Y, Z
+
+
 @voxelize_cams.register_fake
-def _(heatmaps, cams, grid_index, resize_t, start, end, center, bins, ori_max, img_w, img_h, want_cube, want_xy):
+def _(heatmaps, cams, grid_index, resize_t, start, end, center, bins, ori_max, img_w, img_h, want_cube, want_xy,
+      x_begin=0, x_end=-1):
     B, V, J = heatmaps.shape[:3]
-    X, Y, Z = bins
+    _, _, X, Y, Z = _x_rows(bins, x_begin, x_end)
     return (heatmaps.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
             heatmaps.new_empty((B, J, X, Y) if want_xy else (0,)))
 
@@ -235,8 +251,8 @@ def _(heatmaps_cl, J, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
 def voxelize_cl_cams(heatmaps_cl: torch.Tensor, J: int, cams: torch.Tensor, grid_index: Optional[torch.Tensor],
                      resize_t: torch.Tensor, start: list[float], end: list[float], center: list[float],
                      bins: list[int], ori_max: float, img_w: float, img_h: float, want_cube: bool,
-                     want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
-    """voxelize_cams on channels-last heatmaps [B,V,H,W,Cp]."""
+                     want_xy: bool, x_begin: int = 0, x_end: int = -1) -> tuple[torch.Tensor, torch.Tensor]:
+    """voxelize_cams on channels-last heatmaps [B,V,H,W,Cp] (x_begin / x_end as there)."""
     hm = _cl_input(heatmaps_cl, J)
     cm = _dev_f32(cams, "cams")
     rt = _dev_f32(resize_t, "resize_transform")
@@ -245,7 +261,7 @@ def voxelize_cl_cams(heatmaps_cl: torch.Tensor, J: int, cams: torch.Tensor, grid
         cm = cm.unsqueeze(0)
     if cm.shape[1] != V:
         raise _lib.FvpError(f"fvp: {cm.shape[1]} camera records for {V} heatmap views")
-    X, Y, Z = bins
+    x0, x1, X, Y, Z = _x_rows(bins, x_begin, x_end)
     gi = _grid_index(grid_index, B, cm.shape[0], hm.device)
     cube = torch.empty((B, J, X, Y, Z) if want_cube else (0,), dtype=torch.float32, device=hm.device)
     xy = torch.empty((B, J, X, Y) if want_xy else (0,), dtype=torch.float32, device=hm.device)
@@ -253,16 +269,20 @@ def voxelize_cl_cams(heatmaps_cl: torch.Tensor, J: int, cams: torch.Tensor, grid
         return cube, xy
     g = GridSpec(_f3(start), _f3(end), _f3(center), _i3(bins))
     im = ImageSpec(ori_max, img_w, img_h, W, H)
-    _lib.call("fvp_voxelize_cl_cams", _ptr(hm), cp, B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im,
-              _ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _stream(hm))
+    outs = (_ptr(cube) if want_cube else None, _ptr(xy) if want_xy else None, _stream(hm))
+    if X == bins[0]:
+        _lib.call("fvp_voxelize_cl_cams", _ptr(hm), cp, B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im, *outs)
+    else:
+        _lib.call("fvp_voxelize_cl_cams_slab", _ptr(hm), cp, B, V, J, H, W, _ptr(cm), _ptr(gi), _ptr(rt), g, im,
+                  x0, x1, *outs)
     return cube, xy
 
 
 @voxelize_cl_cams.register_fake
 def _(heatmaps_cl, J, cams, grid_index, resize_t, start, end, center, bins, ori_max, img_w, img_h, want_cube,
-      want_xy):
+      want_xy, x_begin=0, x_end=-1):
     B = heatmaps_cl.shape[0]
-    X, Y, Z = bins
+    _, _, X, Y, Z = _x_rows(bins, x_begin, x_end)
     return (heatmaps_cl.new_empty((B, J, X, Y, Z) if want_cube else (0,)),
             heatmaps_cl.new_empty((B, J, X, Y) if want_xy else (0,)))
 

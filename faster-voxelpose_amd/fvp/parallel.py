@@ -72,17 +72,23 @@ def gather_xy_slabs(xy_slab: torch.Tensor, X: int, group=None) -> torch.Tensor:
     return rows.permute(1, 2, 0, 3).contiguous()
 
 
-def columns_from_slab(cube_slab: torch.Tensor, flat: torch.Tensor, x0: int, group=None, gather=None) -> torch.Tensor:
-    """feature_1d [B,K,J,Z] (human_detection_net.py:199-200) for proposals at
-    global flat index x*Y + y, from x-slabs [B,J,Xs,Y,Z] starting at row x0:
-    each rank gathers the columns it owns (zeros elsewhere), one SUM all-reduce
-    (exact: one non-zero term per element)."""
+def owned_columns(cube_slab: torch.Tensor, flat: torch.Tensor, x0: int, gather=None) -> torch.Tensor:
+    """This rank's share of feature_1d [B,K,J,Z] (human_detection_net.py:199-200)
+    for proposals at global flat index x*Y + y, from x-slabs [B,J,Xs,Y,Z]
+    starting at row x0: the columns whose x-row lies in the slab, zeros
+    elsewhere (every column is owned by exactly one slab)."""
     if gather is None:
         from .proposal import gather_columns as gather
     Xs, Y = cube_slab.shape[2], cube_slab.shape[3]
     local = flat - x0 * Y
     own = (local >= 0) & (local < Xs * Y)
     cols = gather(cube_slab, torch.where(own, local, torch.zeros_like(local)))
-    cols = torch.where(own[:, :, None, None], cols, torch.zeros((), dtype=cols.dtype, device=cols.device))
+    return torch.where(own[:, :, None, None], cols, torch.zeros((), dtype=cols.dtype, device=cols.device))
+
+
+def columns_from_slab(cube_slab: torch.Tensor, flat: torch.Tensor, x0: int, group=None, gather=None) -> torch.Tensor:
+    """feature_1d [B,K,J,Z] on every rank from each rank's owned_columns: one
+    SUM all-reduce (exact: one non-zero term per element)."""
+    cols = owned_columns(cube_slab, flat, x0, gather)
     dist.all_reduce(cols, op=dist.ReduceOp.SUM, group=group)
     return cols

@@ -223,25 +223,37 @@ class ProjectLayer(nn.Module):
         """Voxels with x in [x_begin, x_end) only: (cube[B,J,x_end-x_begin,Y,Z], xy[B,J,x_end-x_begin,Y]).
 
         The large-frame mode of SURVEY.md §8(e): each rank of a group owns an
-        x-slab of every frame (fvp.parallel.shard_slab).  The packed grid is
-        voxel-major with x slowest, so a slab is a contiguous slice of it and
-        the kernel runs unchanged on X' = x_end - x_begin rows; every voxel and
-        every (x, y) column lies wholly in one slab, so the slabs are
-        bit-identical to the same rows of forward_fused.  Always reads the
-        cached grid (a rank touches only its slab: 1/k of the grid)."""
+        x-slab of every frame (fvp.parallel.shard_slab); every voxel and every
+        (x, y) column lies wholly in one slab, so the slabs are bit-identical
+        to the same rows of forward_fused.  The coordinates come from where
+        forward_fused would take them: for a grid that would not stay cached
+        (C5: 406 MB per sequence) they are projected on the fly from the
+        camera records for the slab's rows only (fvp_voxelize_cams_slab), so
+        no rank builds or reads a sample grid; otherwise the packed grid is
+        voxel-major with x slowest, a slab is a contiguous slice of it, and
+        the kernel runs unchanged on the slab's rows."""
         ops.forward_only(heatmaps)
         X, Y, Z = _as_list3(self.voxels_per_axis, int)
         if not 0 <= x_begin < x_end <= X:
             raise ValueError(f"x-slab [{x_begin}, {x_end}) outside [0, {X})")
         if heatmaps.shape[0] == 0:
             return self._empty(heatmaps, x_end - x_begin, want_cube, want_xy)
+        cl = channels_last_of(heatmaps)
+        if self._project_on_the_fly(heatmaps.shape[1]):
+            cams, index = self._cams_for_batch(heatmaps, meta, cameras)
+            start, end, center, nb = self.grid_spec()
+            rt = resize_transform.to(device=heatmaps.device, dtype=torch.float32)
+            geo = (start, end, center, nb, float(max(self.ori_image_size[0], self.ori_image_size[1])),
+                   float(self.image_size[0]), float(self.image_size[1]), want_cube, want_xy, x_begin, x_end)
+            if cl is not None:
+                return ops.voxelize_cl_cams(cl.t, cl.J, cams, index, rt, *geo)
+            return ops.voxelize_cams(heatmaps, cams, index, rt, *geo)
         grids, index = self._grids_for_batch(heatmaps, meta, cameras, resize_transform)
         n0, n1 = x_begin * Y * Z, x_end * Y * Z
         if grids.dim() == 3:
             slab = grids[n0:n1]
         else:  # mixed sequences: the stacked slab rows (kept across calls)
             slab = self._stacked_grids(list(dict.fromkeys(list(meta["seq"])[: heatmaps.shape[0]])), n0, n1)
-        cl = channels_last_of(heatmaps)
         if cl is not None:
             return ops.voxelize_cl(cl.t, cl.J, slab, index, x_end - x_begin, Y, Z, want_cube, want_xy)
         return ops.voxelize(heatmaps, slab, index, x_end - x_begin, Y, Z, want_cube, want_xy)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 11
+#define FVP_ABI_VERSION 12
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -119,9 +119,9 @@ int fvp_voxelize(const float *heatmaps, int B, int V, int J, int H, int W,
 /* Same with fp16 heatmaps (IEEE binary16), computed in fp32 (exact upcast).
  * For J <= 16 the chunk is re-laid out as an fp16 pixel-pair table (each
  * 64-B entry holds pixels x and x+1 of a row), so a voxel-camera is 2 loads
- * per frame, with up to 4 frames interleaved per entry; the workspace size
- * differs from the fp32 one and is read per call (the environment variable
- * FVP_PAIR_FRAMES=2 selects the two-frame grouping). */
+ * per frame, with 4 frames interleaved per entry (a batch's remainder in
+ * entries of 2 and 1); the workspace size differs from the fp32 one and depends
+ * on the arguments only. */
 size_t fvp_voxelize_f16_workspace_bytes(int B, int V, int J, int H, int W);
 int fvp_voxelize_f16(const void *heatmaps, int B, int V, int J, int H, int W,
                      const float *packed_grids, const int32_t *grid_index,
@@ -141,6 +141,18 @@ int fvp_voxelize_cams(const void *heatmaps, int half, int B, int V, int J, int H
                       const fvp_grid_spec *grid, const fvp_image_spec *img, float *cube, float *xy,
                       void *workspace, size_t workspace_bytes, void *stream);
 
+/* fvp_voxelize_cams for the voxels of x-rows [x_begin, x_end) of the grid only
+ * (0 <= x_begin < x_end <= grid->bins[0]): cube [B][J][x_end-x_begin][Y][Z],
+ * xy [B][J][x_end-x_begin][Y].  Every voxel's coordinates come from its global
+ * indices, so the slab equals the same rows of the whole-grid call bit for bit,
+ * without any sample grid -- the large-frame mode of SURVEY.md §8(e), where each
+ * rank of a group voxelises one x-slab of every frame (the per-sequence cache
+ * of project_whole.py:151-156 is never built). */
+int fvp_voxelize_cams_slab(const void *heatmaps, int half, int B, int V, int J, int H, int W,
+                           const float *cams, const int32_t *grid_index, const float *resize_t,
+                           const fvp_grid_spec *grid, const fvp_image_spec *img, int x_begin, int x_end,
+                           float *cube, float *xy, void *workspace, size_t workspace_bytes, void *stream);
+
 /* fvp_voxelize / fvp_voxelize_cams on heatmaps that are already channels-last,
  * [B][V][H][W][cp] fp32 with cp >= 4*ceil(J/4) rounded to {4, 8, 16, 32} and
  * cp % 4 == 0 (joints j < J in channels 0..J-1, the rest ignored) -- the NHWC
@@ -154,6 +166,10 @@ int fvp_voxelize_cl(const float *heatmaps_cl, int cp, int B, int V, int J, int H
 int fvp_voxelize_cl_cams(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W, const float *cams,
                          const int32_t *grid_index, const float *resize_t, const fvp_grid_spec *grid,
                          const fvp_image_spec *img, float *cube, float *xy, void *stream);
+int fvp_voxelize_cl_cams_slab(const float *heatmaps_cl, int cp, int B, int V, int J, int H, int W,
+                              const float *cams, const int32_t *grid_index, const float *resize_t,
+                              const fvp_grid_spec *grid, const fvp_image_spec *img, int x_begin, int x_end,
+                              float *cube, float *xy, void *stream);
 
 /* Peak NMS + top-K on a [B,1,X,Y] map: 3x3 max-pool keep mask, top-K of the
  * masked map (value descending, flat index ascending on ties), and

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 12
     assert lib.fvp_status_string(0) == b"success"
 
 
@@ -48,11 +48,11 @@ def test_argument_validation_without_gpu():
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 40, 128, 240) == 4 * 5 * 128 * 240 * 32 * 4  # one 32-joint slice
     assert lib.fvp_voxelize_workspace_bytes(4, 5, 1025, 128, 240) == 0
     # fp16, J <= 16: pixel-pair table [V][H][W+1] x 64 B, one group of 4 C5 frames per chunk
-    # (FVP_PAIR_FRAMES=2: the two-frame grouping, 2 frames)
+    # (the size depends on the arguments only: no process environment is read)
     assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 4 * 31 * 128 * 241 * 64
-    os.environ["FVP_PAIR_FRAMES"] = "2"
+    os.environ["FVP_PAIR_FRAMES"] = "2"  # the round-3 A/B knob: gone
     try:
-        assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 2 * 31 * 128 * 241 * 64
+        assert lib.fvp_voxelize_f16_workspace_bytes(8, 31, 15, 128, 240) == 4 * 31 * 128 * 241 * 64
     finally:
         del os.environ["FVP_PAIR_FRAMES"]
     # fp16, J > 16: the fp32 channels-last copy

@@ -84,3 +84,51 @@ def test_sample_grid_digest(gpu_device, wname):
     ref = golden("cube_digests.npz")[f"grid_{wname}_sha256"]
     bad = [v for v in range(sg.shape[0]) if not np.array_equal(dc.input_sha(np.ascontiguousarray(sg[v], "<f4")), ref[v])]
     assert not bad, f"{wname}: sample grid of cameras {bad} differs from the reference's"
+
+
+@pytest.mark.parametrize("key", ["c5_g4", "c5_u"])
+def test_c5_x_slabs_on_the_fly_match_reference(gpu_device, key):
+    """Large-frame mode at full C5 geometry (31 ring cameras,
+    fp16 heatmaps, the 16-camera cascade, 4 frames per pair-table entry): each
+    of k = 8 ranks' x-slab of 20 rows, projected on the fly from the camera
+    records (fvp_voxelize_cams_slab: no rank builds the 406 MB sample grid),
+    hashes to the reference's own per-slab digest of the same rows; the xy
+    slabs assemble the whole xy plane, and the columns each slab owns sum to
+    the whole cube's columns at the top-K proposals."""
+    import hashlib
+
+    from fvp import geometry, parallel
+    from fvp.proposal import gather_columns, nms2D
+
+    wname, _, frames = dc.CASES[key]
+    hm, half = dc.inputs(key)
+    assert half and np.array_equal(dc.input_sha(hm), golden("cube_digests.npz")[f"{key}_input_sha256"])
+    ref = golden("cube_digests.npz")[f"{key}_digests"]
+    w, layer, cams, seq = _layer(wname, gpu_device, None)  # automatic choice: on the fly at C5
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    x = torch.from_numpy(hm).half().to(gpu_device)
+    meta = {"seq": [seq] * frames}
+    X, Y, Z = w.voxels_per_axis
+    k = ref.shape[1] - 1
+    assert layer._project_on_the_fly(x.shape[1]) and k == 8
+    xy_rows, slabs = [], []
+    for r in range(k):
+        x0, x1 = parallel.shard_slab(X, k, r)
+        cs, xs = layer.forward_slab(x, meta, cams, rt, x0, x1)
+        assert cs.shape == (frames, w.num_joints, x1 - x0, Y, Z)
+        c = cs.cpu().numpy()
+        for b in range(frames):
+            got = np.frombuffer(hashlib.sha256(np.ascontiguousarray(c[b], "<f4").tobytes()).digest(), np.uint8)
+            assert np.array_equal(got, ref[b, 1 + r]), f"{key}: frame {b} x-slab {r} [{x0},{x1}) differs"
+        assert torch.equal(xs, cs.amax(dim=4))
+        xy_rows.append(xs)
+        slabs.append((x0, cs))
+    assert not layer.sample_grid, "the slab path built a sample grid"
+    xy = torch.cat(xy_rows, dim=2)
+    _, _, flat = nms2D(xy[:, 2:3].contiguous(), w.max_people)
+    cols = sum(parallel.owned_columns(cs, flat, x0) for x0, cs in slabs)
+    cube, xy_full = layer.forward_fused(x, meta, cams, rt)
+    assert torch.equal(xy, xy_full)
+    assert torch.equal(cols, gather_columns(cube, flat))
+    print(f"{key}: {frames} frame(s) x {k} on-the-fly x-slabs identical to the reference's slab digests; "
+          f"columns from the slabs == whole-cube columns")

@@ -107,23 +107,21 @@ def test_c5_full_size_vs_reference(gpu_device, otf):
                  f"C5 {'otf' if otf else 'grid'}")
 
 
-@pytest.mark.parametrize("nf", ["4", "2"], ids=["nf4", "nf2"])
-def test_c5_full_size_frame_groups(gpu_device, nf, monkeypatch):
+def test_c5_full_size_frame_groups(gpu_device):
     """C5 at full size with 7 frames: one group of 4 frames per pair-table
     entry (the default), then a pair, then a single frame -- every frame's cube
     and xy plane equal its own one-frame launch (the single-frame path is
     pinned by the C5 digests and whole_c5.npz)."""
     from fvp import geometry, synthetic
 
-    monkeypatch.setenv("FVP_PAIR_FRAMES", nf)
     w, layer, cams, seq = _layer("c5", gpu_device, True)
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 7, first_frame=5).astype(np.float16)).to(gpu_device)
     cube, xy = layer.forward_fused(hm, {"seq": [seq] * 7}, cams, rt)
     for b in range(7):
         c1, x1 = layer.forward_fused(hm[b:b + 1], {"seq": [seq]}, cams, rt)
-        assert torch.equal(cube[b:b + 1], c1) and torch.equal(xy[b:b + 1], x1), f"frame {b} (FVP_PAIR_FRAMES={nf})"
-    print(f"C5 7 frames (FVP_PAIR_FRAMES={nf}): every frame equals its one-frame launch")
+        assert torch.equal(cube[b:b + 1], c1) and torch.equal(xy[b:b + 1], x1), f"frame {b}"
+    print("C5 7 frames (entries of 4, 2, 1 frames): every frame equals its one-frame launch")
 
 
 # ---------------------------------------------------------------------------

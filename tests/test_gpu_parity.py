@@ -432,15 +432,14 @@ def test_fp16_heatmaps_computed_in_fp32(gpu_device):
     _assert_same(cube[1].cpu().numpy(), ref, "fp16 frame")
 
 
-@pytest.mark.parametrize("B", [2, 3, 5, 7])
+@pytest.mark.parametrize("B", [2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
-@pytest.mark.parametrize("nf", ["2", "4"], ids=["nf2", "nf4"])
-def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf, nf, monkeypatch):
-    """The fp16 pair table holds two (or, FVP_PAIR_FRAMES=4, four) frames per
-    entry: every frame of a batch (7 = one group of 4, a pair, a single)
-    equals its own single-frame launch and the fp32 layout's result; 31 ring
-    cameras (the 16-camera cascade) on a small grid."""
-    monkeypatch.setenv("FVP_PAIR_FRAMES", nf)
+def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf):
+    """The fp16 pair table holds four frames per entry, a batch's remainder
+    two and / or one: every frame of a batch (2 = a pair, 3 = a pair and a
+    single, 4 / 5 = a group of 4 (and a single), 6 = a group and a pair, 7 =
+    all three) equals its own single-frame launch and the fp32 layout's
+    result; 31 ring cameras (the 16-camera cascade) on a small grid."""
     from fvp import geometry, synthetic
     from fvp.config import make_cfg
     from fvp.project_whole import ProjectLayer
@@ -468,11 +467,12 @@ def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf, nf, monkeypatch):
 
 
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
-def test_fp16_pair_layouts_agree(gpu_device, otf, monkeypatch):
-    """pairs_rows_kernel (a block per row, through LDS) and the per-entry layout
-    kernel (FVP_PAIRS_LAYOUT=entry; also what odd heatmap widths use) build the
-    same pair table: identical cubes and xy planes for 7 frames (entries of 4,
-    2 and 1 frames), 31 ring cameras on a small grid."""
+def test_fp16_pair_layouts_agree(gpu_device, otf):
+    """pairs_rows_kernel (a block per row, through LDS, 4-B row loads) and the
+    per-entry layout kernel (what fp16 heatmaps at a 2-B-aligned address and odd
+    heatmap widths use) build the same pair table: identical cubes and xy
+    planes for 7 frames (entries of 4, 2 and 1 frames), 31 ring cameras on a
+    small grid."""
     from fvp import geometry, synthetic
     from fvp.config import make_cfg
     from fvp.project_whole import ProjectLayer
@@ -487,8 +487,11 @@ def test_fp16_pair_layouts_agree(gpu_device, otf, monkeypatch):
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
     hm = synthetic.uniform_heatmaps(w, 7, seed=23).half().to(gpu_device)
     cube, xy = layer.forward_fused(hm, {"seq": [seq] * 7}, cams, rt)
-    monkeypatch.setenv("FVP_PAIRS_LAYOUT", "entry")
-    c_e, x_e = layer.forward_fused(hm, {"seq": [seq] * 7}, cams, rt)
+    buf = torch.empty(hm.numel() + 1, dtype=torch.float16, device=gpu_device)
+    hm_odd = buf[1:].view(hm.shape)  # contiguous, 2 B past a 4-B boundary: the per-entry kernel
+    hm_odd.copy_(hm)
+    assert hm_odd.is_contiguous() and hm_odd.data_ptr() % 4 == 2
+    c_e, x_e = layer.forward_fused(hm_odd, {"seq": [seq] * 7}, cams, rt)
     assert torch.equal(cube, c_e) and torch.equal(xy, x_e)
 
 
@@ -813,15 +816,19 @@ def test_person_planes_on_the_fly_equals_fine_grid(gpu_device):
     assert torch.equal(p1, p2) and torch.equal(o1, o2) and torch.equal(f1, f2)
 
 
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
 @pytest.mark.parametrize("wname,nslab,half", [("c2", 2, False), ("c4", 3, False), ("c2", 3, True)])
-def test_x_slabs_equal_full_grid(gpu_device, wname, nslab, half):
+def test_x_slabs_equal_full_grid(gpu_device, wname, nslab, half, otf):
     """Large-frame mode: forward_slab on each rank's x-slab
     (fvp.parallel.shard_slab, uneven at 3 slabs) is bit-identical to the same
-    rows of the whole-grid launch, for mixed-sequence batches too."""
+    rows of the whole-grid launch, for mixed-sequence batches too, from the
+    cached grid's rows and projected on the fly for the slab's rows only
+    (channels-last input as well)."""
     from fvp import geometry, parallel, synthetic
+    from fvp.heatmaps import ChannelsLastHeatmaps
 
     w, layer, cams, seq = _whole(wname, gpu_device)
-    layer.on_the_fly = False
+    layer.on_the_fly = otf
     X = w.voxels_per_axis[0]
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 3)).to(gpu_device)
@@ -835,6 +842,14 @@ def test_x_slabs_equal_full_grid(gpu_device, wname, nslab, half):
             x0, x1 = parallel.shard_slab(X, nslab, r)
             cs, xs = layer.forward_slab(hm, meta, cams2, rt, x0, x1)
             assert torch.equal(cs, cube[:, :, x0:x1]) and torch.equal(xs, xy[:, :, x0:x1])
+            if not half:
+                B, V, J, H, W = hm.shape
+                cl = torch.zeros((B, V, H, W, 16), device=gpu_device)
+                cl[..., :J] = hm.permute(0, 1, 3, 4, 2)
+                cs, xs = layer.forward_slab(ChannelsLastHeatmaps(cl, J), meta, cams2, rt, x0, x1)
+                assert torch.equal(cs, cube[:, :, x0:x1]) and torch.equal(xs, xy[:, :, x0:x1])
+    if otf:
+        assert not layer.sample_grid, "the on-the-fly slab path built a sample grid"
     with pytest.raises(ValueError):
         layer.forward_slab(hm, meta, cams2, rt, 4, 4)
 
@@ -1002,3 +1017,37 @@ def test_nms_large_maps_vs_oracle(gpu_device, side):
     ov, oxy, ofl = O.nms2d(p.numpy(), 10)
     assert np.array_equal(v.cpu().numpy(), ov) and np.array_equal(fl.cpu().numpy(), ofl)
     assert np.array_equal(xy.cpu().numpy(), oxy)
+
+
+@pytest.mark.parametrize("wname", ["c2", "c4"])
+def test_cube_pointer_not_16b_aligned(gpu_device, wname):
+    """The C ABI takes any float* for the cube: the gather's float4 epilogue
+    runs only when the caller's pointer is 16-B aligned (checked on the host),
+    so a cube 4 B past a 16-B boundary gets the scalar stores -- same values
+    (fvp_voxelize.hip vec epilogue)."""
+    from fvp import _lib, geometry, synthetic
+
+    w, layer, cams, seq = _whole(wname, gpu_device)
+    layer.on_the_fly = False
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, 2)).to(gpu_device)
+    meta = {"seq": [seq] * 2}
+    cube, xy = layer.forward_fused(hm, meta, cams, rt)
+    grids, _ = layer._grids_for_batch(hm, meta, cams, rt)
+    B, V, J, H, W = hm.shape
+    X, Y, Z = w.voxels_per_axis
+    L = _lib.load()
+    nws = L.fvp_voxelize_workspace_bytes(B, V, J, H, W)
+    ws = torch.empty((nws + 3) // 4, device=gpu_device)
+    buf = torch.full((cube.numel() + 4,), -7.0, device=gpu_device)
+    xy2 = torch.empty_like(xy)
+    st = torch.cuda.current_stream(gpu_device).cuda_stream
+    for off in (1, 2, 3):
+        buf.fill_(-7.0)
+        assert (buf.data_ptr() + 4 * off) % 16 != 0
+        _lib.check(L.fvp_voxelize(hm.data_ptr(), B, V, J, H, W, grids.data_ptr(), None, X, Y, Z,
+                                  buf.data_ptr() + 4 * off, xy2.data_ptr(), ws.data_ptr(), nws, st), "fvp_voxelize")
+        torch.cuda.synchronize()
+        assert torch.equal(buf[off:off + cube.numel()].view(cube.shape), cube), off
+        assert bool((buf[:off] == -7.0).all()) and bool((buf[off + cube.numel():] == -7.0).all()), off
+        assert torch.equal(xy2, xy)

@@ -90,37 +90,68 @@ __device__ __forceinline__ void project_point(const Cam &c, float x, float y, fl
 
 // a / b for a divisor fixed per launch, rb = 1.0f / b (correctly rounded; the
 // callers' loop-invariant division, hoisted out of their loops): q = a*rb,
-// the exact remainder a - q*b by one fma, one correction step.  Equal to the
-// correctly rounded a / b whenever the quotient is a normal float
-// (Markstein's theorem for rb = RN(1/b); checked exhaustively over all 2^32
-// fp32 a for b in {3, 7, 127, 151, 199, 239, 512, 608, 800, 960},
-// tests/test_div_const.py): only subnormal quotients (|a| < ~1e-36 here) and a
-// = -0 (gives +0) can differ.  Three VALU ops against ~10 for an IEEE
-// division (v_div_scale / v_rcp / v_div_fmas / v_div_fixup).
+// the exact remainder a - q*b by one fma, one correction step.  Three VALU
+// ops against ~10 for an IEEE division (v_div_scale / v_rcp / v_div_fmas /
+// v_div_fixup).  Equal to the correctly rounded a / b for every integer
+// divisor b in [1, 65535] whenever the quotient is a normal float: checked
+// for every odd b in that range over all 2^23 mantissas of a in [1, 2)
+// (tools/div_const_sweep.c; the three operations and a / b scale exactly by
+// powers of two in a and in b while everything stays normal, and are odd in
+// a), and over whole fp32 exponent ranges for the BASELINE divisors
+// (tests/test_div_const.py).  Only subnormal quotients (|a| < ~1e-36 here)
+// and a = -0 (gives +0) can differ.  Markstein's theorem alone does not
+// cover it (RN(a * RN(1/b)) can be 1.5 ulp off), so the fast path is taken
+// only for divisors the sweep covers (ImageConsts::exact, set on the host);
+// any other divisor takes the IEEE division.
 __device__ __forceinline__ float div_const(float a, float b, float rb) {
     const float q = a * rb;
     return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
 }
 
+// The launch constants of pixel_to_sample: fvp_image_spec plus which of the
+// four divisors div_const serves exactly (bit 0 img_w, 1 img_h, 2 hm_w - 1,
+// 3 hm_h - 1; image_consts() on the host).
+struct ImageConsts {
+    float ori_max, img_w, img_h, hm_w, hm_h;
+    unsigned exact;
+};
+
+// Host: an integer divisor in [1, 65535] (the range tools/div_const_sweep.c covers).
+inline bool div_const_covered(float b) {
+    return b >= 1.0f && b <= 65535.0f && (float)(int)b == b;
+}
+
+inline ImageConsts image_consts(const fvp_image_spec &im) {
+    ImageConsts c{im.ori_max, im.img_w, im.img_h, (float)im.hm_w, (float)im.hm_h, 0u};
+    c.exact = (div_const_covered(im.img_w) ? 1u : 0u) | (div_const_covered(im.img_h) ? 2u : 0u) |
+              (div_const_covered((float)im.hm_w - 1.0f) ? 4u : 0u) |
+              (div_const_covered((float)im.hm_h - 1.0f) ? 8u : 0u);
+    return c;
+}
+
+__device__ __forceinline__ float div_launch(float a, float b, bool exact) {
+    return exact ? div_const(a, b, 1.0f / b) : a / b;
+}
+
 // project_whole.py:96-117 after project_pose: pixel -> normalised sample coords.
-// The four divisions by launch constants use div_const: where it could differ
-// from an IEEE division (a subnormal or -0 quotient) the value next goes
-// through `* 2 - 1` (directly, or after a second division that keeps it below
-// 2^-100), which rounds it to -1 either way, so gx / gy are bit-identical to
-// the reference's (and the sample-grid digests of C1-C5 pin it).
-__device__ __forceinline__ void pixel_to_sample(float px, float py, const float *__restrict__ t, float ori_max,
-                                                float img_w, float img_h, float hm_w, float hm_h,
-                                                float &gx, float &gy) {
-    px = clampf(px, -1.0f, ori_max);
-    py = clampf(py, -1.0f, ori_max);
+// The four divisions by launch constants use div_const where it is exact
+// (ImageConsts::exact): where it could differ from an IEEE division (a
+// subnormal or -0 quotient) the value next goes through `* 2 - 1` (directly,
+// or after a second division that keeps it below 2^-100), which rounds it to
+// -1 either way, so gx / gy are bit-identical to the reference's (and the
+// sample-grid digests of C1-C5 pin it).
+__device__ __forceinline__ void pixel_to_sample(float px, float py, const float *__restrict__ t,
+                                                const ImageConsts &c, float &gx, float &gy) {
+    px = clampf(px, -1.0f, c.ori_max);
+    py = clampf(py, -1.0f, c.ori_max);
     // transforms.py:59-63: torch.mm(t, [x, y, 1]^T)
     const float ax = __builtin_fmaf(t[2], 1.0f, __builtin_fmaf(t[1], py, t[0] * px));
     const float ay = __builtin_fmaf(t[5], 1.0f, __builtin_fmaf(t[4], py, t[3] * px));
-    const float sw = hm_w - 1.0f, sh = hm_h - 1.0f;
-    const float hx = div_const(ax * hm_w, img_w, 1.0f / img_w);
-    const float hy = div_const(ay * hm_h, img_h, 1.0f / img_h);
-    gx = clampf(div_const(hx, sw, 1.0f / sw) * 2.0f - 1.0f, -1.1f, 1.1f);
-    gy = clampf(div_const(hy, sh, 1.0f / sh) * 2.0f - 1.0f, -1.1f, 1.1f);
+    const float sw = c.hm_w - 1.0f, sh = c.hm_h - 1.0f;
+    const float hx = div_launch(ax * c.hm_w, c.img_w, c.exact & 1u);
+    const float hy = div_launch(ay * c.hm_h, c.img_h, c.exact & 2u);
+    gx = clampf(div_launch(hx, sw, c.exact & 4u) * 2.0f - 1.0f, -1.1f, 1.1f);
+    gy = clampf(div_launch(hy, sh, c.exact & 8u) * 2.0f - 1.0f, -1.1f, 1.1f);
 }
 
 // Bilinear tap set of F.grid_sample(align_corners=True, padding zeros) at a

@@ -10,7 +10,7 @@
 namespace fvp {
 
 __global__ __launch_bounds__(256) void project_grid_kernel(
-    const float *__restrict__ cams, const float *__restrict__ resize_t, fvp_grid_spec g, fvp_image_spec im,
+    const float *__restrict__ cams, const float *__restrict__ resize_t, fvp_grid_spec g, ImageConsts im,
     float2 *__restrict__ out, int V, long long N) {
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const int v = blockIdx.y;
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void project_grid_kernel(
     const Cam c = load_cam(cams + (size_t)v * FVP_CAM_STRIDE);
     float px, py, gx, gy;
     project_point(c, x, y, z, px, py);
-    pixel_to_sample(px, py, resize_t, im.ori_max, im.img_w, im.img_h, (float)im.hm_w, (float)im.hm_h, gx, gy);
+    pixel_to_sample(px, py, resize_t, im, gx, gy);
     out[(size_t)v * N + gid] = make_float2(gx, gy);
 }
 
@@ -43,6 +43,6 @@ extern "C" int fvp_project_grid(const float *cams, int V, const float *resize_t,
     if (blocks > 0x7fffffffLL) return FVP_ERR_SHAPE;
     dim3 gdim((unsigned)blocks, (unsigned)V);
     hipLaunchKernelGGL(fvp::project_grid_kernel, gdim, dim3(256), 0, (hipStream_t)stream, cams, resize_t, *grid,
-                       *img, reinterpret_cast<float2 *>(sample_grid), V, N);
+                       fvp::image_consts(*img), reinterpret_cast<float2 *>(sample_grid), V, N);
     return (int)hipGetLastError();
 }

@@ -15,6 +15,10 @@
 // over x, xz a register + LDS max over y, xy a wave reduction over z.
 #include "fvp_layout.h"
 
+#ifndef FVP_AB_GRID_AUX
+#define FVP_AB_GRID_AUX 0
+#endif
+
 namespace fvp {
 
 struct Window {
@@ -135,7 +139,7 @@ struct PersonCoords {
     const float *cams;      // [V][FVP_CAM_STRIDE]   (OTF)
     const float *resize_t;  // [2][3]                (OTF)
     fvp_grid_spec fine;     // fine whole-space grid (OTF)
-    fvp_image_spec im;      //                       (OTF)
+    ImageConsts im;         //                       (OTF)
 };
 
 template <int LPV, int YG, bool OTF, bool CASC>
@@ -244,13 +248,12 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                             const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
                             float px, py;
                             project_point(c, wxc, wyc, wzc, px, py);
-                            pixel_to_sample(px, py, rt, pc.im.ori_max, pc.im.img_w, pc.im.img_h, (float)pc.im.hm_w,
-                                            (float)pc.im.hm_h, g[2 * h], g[2 * h + 1]);
+                            pixel_to_sample(px, py, rt, pc.im, g[2 * h], g[2 * h + 1]);
                         }
                     } else {
                         // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
                         const u32x4 graw =
-                            __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
+                            __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, FVP_AB_GRID_AUX);
 #pragma unroll
                         for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
                     }
@@ -362,9 +365,12 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     }
 }
 
+#ifndef FVP_AB_XSPLIT_BIG
+#define FVP_AB_XSPLIT_BIG 1
+#endif
 static int person_xsplit(int P, int SY) {
     const long long rows = (long long)P * SY;
-    return rows >= 4096 ? 1 : rows >= 1024 ? 2 : 4;
+    return rows >= 4096 ? FVP_AB_XSPLIT_BIG : rows >= 1024 ? 2 : 4;
 }
 
 template <int LPV, bool OTF, bool CASC>
@@ -504,7 +510,7 @@ extern "C" int fvp_person_planes_cams(const float *heatmaps, int B, int V, int J
     if (img->hm_w != W || img->hm_h != H) return FVP_ERR_SHAPE;
     for (int a = 0; a < 3; ++a)
         if (fine_grid_spec->bins[a] != spec->fine[a]) return FVP_ERR_SHAPE;
-    const fvp::PersonCoords pc{cams, resize_t, *fine_grid_spec, *img};
+    const fvp::PersonCoords pc{cams, resize_t, *fine_grid_spec, fvp::image_consts(*img)};
     return fvp::person_planes_any(heatmaps, 0, B, V, J, H, W, nullptr, &pc, spec, proposals, frame_of, P, cubes,
                                   planes, offset, workspace, workspace_bytes, stream);
 }

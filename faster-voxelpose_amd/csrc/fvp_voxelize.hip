@@ -48,7 +48,7 @@ struct CoordSource {
     const float *cams;      // camera records [S][V][FVP_CAM_STRIDE] (OTF)
     const float *resize_t;  // [2][3]                                (OTF)
     fvp_grid_spec gs;       // (OTF) the whole grid: x-row i of a launch is row x_off + i of gs
-    fvp_image_spec im;
+    ImageConsts im;
     int x_off;              // (OTF) first x-row of an x-slab launch (0: the whole grid)
 };
 
@@ -142,8 +142,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                     const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
                     float px, py;
                     project_point(c, wx_, wy_, wz_, px, py);
-                    pixel_to_sample(px, py, rt, src_.im.ori_max, src_.im.img_w, src_.im.img_h, (float)src_.im.hm_w,
-                                    (float)src_.im.hm_h, g[2 * h], g[2 * h + 1]);
+                    pixel_to_sample(px, py, rt, src_.im, g[2 * h], g[2 * h + 1]);
                 }
             } else {
                 // slots v0+2q, v0+2q+1 (past the row: the next voxel's or 0)
@@ -666,8 +665,7 @@ __global__ __launch_bounds__(256) void voxel_columns_kernel(const T *__restrict_
                 const Cam c = load_cam(src.cams + ((size_t)gsel * V + v) * FVP_CAM_STRIDE);
                 float px, py;
                 project_point(c, wx_, wy_, wz_, px, py);
-                pixel_to_sample(px, py, rt, src.im.ori_max, src.im.img_w, src.im.img_h, (float)src.im.hm_w,
-                                (float)src.im.hm_h, gx, gy);
+                pixel_to_sample(px, py, rt, src.im, gx, gy);
             } else {
                 const float2 gp = *reinterpret_cast<const float2 *>(src.grids + (((size_t)gsel * N + n) * GV + v) * 2);
                 gx = gp.x;
@@ -718,7 +716,7 @@ extern "C" int fvp_voxel_columns(const void *heatmaps, int half, long long view_
         src.cams = cams;
         src.resize_t = resize_t;
         src.gs = *grid;
-        src.im = *img;
+        src.im = fvp::image_consts(*img);
     } else {
         src.grids = packed_grids;
     }
@@ -810,7 +808,7 @@ static int voxelize_cams_rows(const void *heatmaps, bool half, const float *hm_c
     src.cams = cams;
     src.resize_t = resize_t;
     src.gs = *grid;
-    src.im = *img;
+    src.im = fvp::image_consts(*img);
     src.x_off = x0;
     if (hm_cl) return voxelize_cl_any<true>(hm_cl, cp, B, V, J, H, W, src, grid_index, X, Y, Z, cube, xy, s);
     if (half)

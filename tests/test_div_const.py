@@ -72,3 +72,24 @@ def test_div_const_matches_ieee_division():
         print(r.stdout)
         assert r.returncode == 0, r.stdout
         assert r.stdout.count("bad=0 ") == len(DIVISORS)
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
+def test_div_const_integer_divisor_sweep():
+    """tools/div_const_sweep.c over the odd divisors 3..4095 (every mantissa of
+    a in [1, 2); with the power-of-two scaling this covers every integer
+    divisor up to 4095 -- every image / heatmap size of the reference's
+    configs).  The whole range 3..65535 that ImageConsts::exact admits was run
+    once (profiles/round4/div_const_sweep_65535.txt, 2.7e11 quotients, no
+    difference); any other divisor takes the IEEE division on the device."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "sweep")
+        subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-fno-fast-math", "-mfma",
+                        os.path.join(repo, "tools", "div_const_sweep.c"), "-o", exe, "-lm"], check=True)
+        env = dict(os.environ, OMP_NUM_THREADS=str(min(8, os.cpu_count() or 1)))
+        r = subprocess.run([exe, "3", "4095"], capture_output=True, text=True, timeout=600, env=env)
+        print(r.stdout)
+        assert r.returncode == 0 and "0 divisors with a difference" in r.stdout, r.stdout
+    with open(os.path.join(repo, "profiles", "round4", "div_const_sweep_65535.txt")) as f:
+        assert "odd divisors 3..65535:" in f.read()

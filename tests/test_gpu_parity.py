@@ -1051,3 +1051,34 @@ def test_cube_pointer_not_16b_aligned(gpu_device, wname):
         assert torch.equal(buf[off:off + cube.numel()].view(cube.shape), cube), off
         assert bool((buf[:off] == -7.0).all()) and bool((buf[off + cube.numel():] == -7.0).all()), off
         assert torch.equal(xy2, xy)
+
+
+@pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
+@pytest.mark.parametrize("image_size,hm_size", [((800.5, 608.0), (240, 128)), ((960.0, 512.0), (65537, 2)),
+                                                ((70000.0, 512.0), (240, 128))])
+def test_divisors_outside_div_const_sweep_take_ieee_division(gpu_device, otf, image_size, hm_size):
+    """pixel_to_sample's four divisions (IMAGE_SIZE w / h, HEATMAP_SIZE - 1)
+    take the reciprocal form div_const only for integer divisors in
+    [1, 65535], the range tools/div_const_sweep.c proves exact; a fractional
+    image size, a heatmap 65537 wide and an image 70000 wide take the IEEE
+    division -- the sample grid equals the oracle's (numpy fp32 division)
+    bit for bit, and so does the on-the-fly projection's cube."""
+    from fvp import geometry, synthetic
+    from fvp.project_whole import ProjectLayer
+
+    bins = (6, 5, 4)
+    w = _custom_workload(voxels_per_axis=bins, num_joints=3, heatmap_size=hm_size, image_size=image_size)
+    layer = ProjectLayer(w.cfg(str(gpu_device)))
+    layer.verbose = False
+    layer.on_the_fly = otf
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+    grid = O.compute_grid(w.space_size, w.space_center, bins)
+    sg = np.stack([O.project_grid(grid, c, w.ori_image_size, w.image_size, hm_size, rt.numpy())
+                   for c in geometry.camera_list(cams, seq)])
+    got = layer.build_sample_grid(cams, seq, rt.to(gpu_device), gpu_device)[:, 0].cpu().numpy()
+    _assert_same(got, sg, "sample grid")
+    if hm_size[0] * hm_size[1] <= 1 << 20:
+        hm = synthetic.uniform_heatmaps(w, 1, seed=3)
+        cube, _ = layer.forward_fused(hm.to(gpu_device), {"seq": [seq]}, cams, rt.to(gpu_device))
+        _assert_same(cube[0].cpu().numpy(), O.voxelize(hm[0].numpy(), sg).reshape(3, *bins), "cube")

@@ -671,8 +671,8 @@ __global__ __launch_bounds__(256) void probe_c5_kernel(const void *__restrict__ 
                 const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
                 float px, py;
                 project_point(c, wx_, wy_, wz_, px, py);
-                pixel_to_sample(px, py, rt, im.ori_max, im.img_w, im.img_h, (float)im.hm_w, (float)im.hm_h, g[2 * h],
-                                g[2 * h + 1]);
+                pixel_to_sample(px, py, rt, ImageConsts{im.ori_max, im.img_w, im.img_h, (float)im.hm_w, (float)im.hm_h, 15u},
+                                g[2 * h], g[2 * h + 1]);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;

@@ -36,6 +36,10 @@
 
 #include "fvp_layout.h"
 
+#ifndef FVP_AB_VGRID_AUX
+#define FVP_AB_VGRID_AUX 0
+#endif
+
 namespace fvp {
 
 // -- gather pass ----------------------------------------------------------------
@@ -147,7 +151,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
             } else {
                 // slots v0+2q, v0+2q+1 (past the row: the next voxel's or 0)
                 const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(
-                    grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
+                    grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, FVP_AB_VGRID_AUX);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
             }
@@ -231,7 +235,41 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         for (int f = 0; f < NF; ++f)
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc[f][m] = acc[f][m] + (CASC ? blk[f][m] : 0.0f);
-        if (valid) {
+#ifndef FVP_AB_MEANDIV
+#define FVP_AB_MEANDIV 0
+#endif
+        if constexpr (FVP_AB_MEANDIV) {
+            // the mean's division by V through div_const when the whole wave's sums
+            // are finite and 0 or at least 2^-100 (normal quotients: exact for an
+            // integer V, tools/div_const_sweep.c); otherwise the IEEE division
+            bool ok = true;
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float a = fabsf(acc[f][m]);
+                    ok &= (a == 0.0f) | ((a >= 0x1p-100f) & (a <= 0x1p100f));
+                }
+            const float rV = 1.0f / fV;
+            if (!__builtin_amdgcn_ballot_w64(!ok)) {  // wave-uniform branch
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) acc[f][m] = div_const(acc[f][m], fV, rV);
+            } else {
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) acc[f][m] = acc[f][m] / fV;
+            }
+            if (valid) {
+#pragma unroll
+                for (int f = 0; f < NF; ++f)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        stage[(f * JP + 4 * q + m) * SP + ii] = clampf(acc[f][m], 0.0f, 1.0f);
+            }
+        } else if (valid) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll

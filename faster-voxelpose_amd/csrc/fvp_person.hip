@@ -142,7 +142,11 @@ struct PersonCoords {
     ImageConsts im;         //                       (OTF)
 };
 
-template <int LPV, int YG, bool OTF, bool CASC>
+// MODE (replay probe, tools/person_probe.hip; the product launches 0): 1 = no
+// plane reductions / stores (the sums folded into `offset`), 2 = zeros instead
+// of the tap loads, 3 = every tap offset off-image (range-checked loads, no
+// memory access), 4 = grid loads and tap setup only (no tap loads, no planes).
+template <int LPV, int YG, bool OTF, bool CASC, int MODE = 0>
 __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
                                                              const float *__restrict__ props,
@@ -287,11 +291,23 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                         float wt[4];
 #pragma unroll
                         for (int m = 0; m < 4; ++m) wt[m] = group_bcast<LPV, S>(src.w[m]);
+                        if constexpr (MODE == 4) {
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) acc[m] = acc[m] + wt[m] + __builtin_bit_cast(float, o[m]);
+                            return;
+                        }
+                        if constexpr (MODE == 3) {
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) o[m] = kOOB;
+                        }
                         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_cl + (size_t)v * img, img);
-                        const u32x4 ta = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
-                        const u32x4 tb = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
-                        const u32x4 tc = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
-                        const u32x4 td = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+                        u32x4 ta = {0u, 0u, 0u, 0u}, tb = ta, tc = ta, td = ta;
+                        if constexpr (MODE != 2) {
+                            ta = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                            tb = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                            tc = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
+                            td = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
+                        }
 #pragma unroll
                         for (int m = 0; m < 4; ++m) {
                             const float fa = __builtin_bit_cast(float, (unsigned)ta[m]);
@@ -313,6 +329,11 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                 // clamp(0,1) of the mean; +0.0f turns a -0 into +0 (unsigned max order below)
                 o[k] = valid ? clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f : 0.0f;
                 if (!zok || y >= SY) o[k] = -INFINITY;  // lanes/rows beyond the cube take no part
+            }
+            if constexpr (MODE == 1 || MODE == 4) {  // probe: keep the sums live, no planes
+                if (offset && zok && y < SY && (acc[0] + acc[1] + acc[2] + acc[3]) == -1.0f)
+                    offset[(size_t)p * 3] = o[0];
+                continue;
             }
             if (cubes && zok && y < SY) {
 #pragma unroll

@@ -56,6 +56,59 @@ struct CoordSource {
     int x_off;              // (OTF) first x-row of an x-slab launch (0: the whole grid)
 };
 
+// Epilogue of a gather block: the stage [NF][JP][SP] (clamped means, column-
+// major within the block's columns) -> the cube runs and the xy max over z.
+template <int NF, int JP>
+__device__ __forceinline__ void store_stage(const float *__restrict__ stage, int SP, int T, int Z, long long N,
+                                            long long n0, int c0, int ncols, int XY, int J, int Jst, int b,
+                                            float *__restrict__ cube, float *__restrict__ xy, bool cube16) {
+    // Epilogue.  When every run is 16-B aligned (T, SP, Z, N multiples of 4: the
+    // C2 / C3 / C4 launches; cube16: the caller's cube pointer is 16-B aligned,
+    // checked on the host) the cube goes out as float4 non-temporal stores and
+    // the z-max reads 4 voxels per LDS load: a sixth of the store instructions
+    // and independent LDS reads instead of a 20-long dependent chain
+    // (tools/gather_probe.py FULL2: C2 8 frames 62.1 -> 59.8 us).
+    const bool vec = ((T | SP | Z | (int)(N & 3)) & 3) == 0 && cube16;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const float *fst = stage + f * JP * SP;
+        const size_t bf = (size_t)(b + f);
+        if (cube) {
+            if (vec) {
+                const int T4 = T >> 2;
+                for (int e = threadIdx.x; e < J * T4; e += 256) {
+                    const int j = e / T4, r = e - (e / T4) * T4;
+                    const f32x4 v = *reinterpret_cast<const f32x4 *>(fst + j * SP + 4 * r);
+                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * Jst + j) * N + n0) + r);
+                }
+            } else {
+                for (int j = 0; j < J; ++j) {
+                    float *__restrict__ dst = cube + (bf * Jst + j) * N + n0;
+                    for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
+                }
+            }
+        }
+        if (xy) {
+            for (int e = threadIdx.x; e < J * ncols; e += 256) {
+                const int j = e / ncols, cc = e - (e / ncols) * ncols;
+                const float *s = fst + j * SP + cc * Z;
+                float m = -INFINITY;
+                if (vec) {
+                    const f32x4 *s4 = reinterpret_cast<const f32x4 *>(s);
+#pragma unroll 4
+                    for (int z = 0; z < (Z >> 2); ++z) {
+                        const f32x4 v = s4[z];  // (torch.max's order is immaterial: max is exact, NaN wins)
+                        m = nanmax(nanmax(m, v[0]), nanmax(nanmax(v[1], v[2]), v[3]));
+                    }
+                } else {
+                    for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
+                }
+                __builtin_nontemporal_store(m, xy + (bf * Jst + j) * XY + c0 + cc);
+            }
+        }
+    }
+}
+
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
@@ -278,51 +331,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         }
     }
     __syncthreads();
-    // Epilogue.  When every run is 16-B aligned (T, SP, Z, N multiples of 4: the
-    // C2 / C3 / C4 launches; cube16: the caller's cube pointer is 16-B aligned,
-    // checked on the host) the cube goes out as float4 non-temporal stores and
-    // the z-max reads 4 voxels per LDS load: a sixth of the store instructions
-    // and independent LDS reads instead of a 20-long dependent chain
-    // (tools/gather_probe.py FULL2: C2 8 frames 62.1 -> 59.8 us).
-    const bool vec = ((T | SP | Z | (int)(N & 3)) & 3) == 0 && cube16;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-        const float *fst = stage + f * JP * SP;
-        const size_t bf = (size_t)(b + f);
-        if (cube) {
-            if (vec) {
-                const int T4 = T >> 2;
-                for (int e = threadIdx.x; e < J * T4; e += 256) {
-                    const int j = e / T4, r = e - (e / T4) * T4;
-                    const f32x4 v = *reinterpret_cast<const f32x4 *>(fst + j * SP + 4 * r);
-                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * Jst + j) * N + n0) + r);
-                }
-            } else {
-                for (int j = 0; j < J; ++j) {
-                    float *__restrict__ dst = cube + (bf * Jst + j) * N + n0;
-                    for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
-                }
-            }
-        }
-        if (xy) {
-            for (int e = threadIdx.x; e < J * ncols; e += 256) {
-                const int j = e / ncols, cc = e - (e / ncols) * ncols;
-                const float *s = fst + j * SP + cc * Z;
-                float m = -INFINITY;
-                if (vec) {
-                    const f32x4 *s4 = reinterpret_cast<const f32x4 *>(s);
-#pragma unroll 4
-                    for (int z = 0; z < (Z >> 2); ++z) {
-                        const f32x4 v = s4[z];  // (torch.max's order is immaterial: max is exact, NaN wins)
-                        m = nanmax(nanmax(m, v[0]), nanmax(nanmax(v[1], v[2]), v[3]));
-                    }
-                } else {
-                    for (int z = 0; z < Z; ++z) m = nanmax(m, s[z]);
-                }
-                __builtin_nontemporal_store(m, xy + (bf * Jst + j) * XY + c0 + cc);
-            }
-        }
-    }
+    store_stage<NF, JP>(stage, SP, T, Z, N, n0, c0, ncols, XY, J, Jst, b, cube, xy, cube16);
 }
 
 // The cube and xy plane are written with non-temporal stores: they are not
@@ -352,6 +361,166 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
     static_assert(OTF, "on-the-fly kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
                                             col_blocks, SP, band, pixb, cube16);
+}
+
+// Camera-outer gather for the on-the-fly fp16 pair table (C5: 31 cameras).
+// voxelize_cams_kernel walks a block's voxels pass by pass with all cameras
+// inside, so the blocks resident on an XCD touch every camera's footprint at
+// once (31 cameras x a 16 x 16-column patch ~ 19 MB of pair entries against a
+// 4 MB L2: each table line is fetched many times).  Here a block's two passes
+// of 64 voxels (128 voxels: 2 columns x 64 z at C5) keep their sums in
+// registers while the cameras advance two at a time; one launch runs one round
+// of blocks that are resident together (`block0`: the round's first block), so
+// the blocks of an XCD start in step and move through the cameras together,
+// and the XCD's working set is a few cameras' footprints.  Per voxel the
+// cameras are summed in the same order (sequentially, with the 16-camera block
+// fold), so the cube is the voxelize_cams_kernel's bit for bit.  Lane q
+// projects camera c0v + (q >> 1) for pass q & 1; the group picks the four
+// setups up by DPP in the order (c, pass 0), (c, pass 1), (c + 1, pass 0),
+// (c + 1, pass 1).
+#ifndef FVP_AB_CO_MINB
+#define FVP_AB_CO_MINB 1
+#endif
+template <bool CASC, int NF>
+__global__ __launch_bounds__(256, FVP_AB_CO_MINB) void voxelize_co_kernel(const void *__restrict__ tab, CoordSource src_, int frame0,
+                                                          float *__restrict__ cube, float *__restrict__ xy, int V,
+                                                          int J, int Jst, int H, int W, int X, int Y, int Z,
+                                                          int cols, int col_blocks, int SP, int band, int block0,
+                                                          int nblocks, bool cube16) {
+    constexpr int LPV = 4, JP = 16, VPP = 64;
+    extern __shared__ __attribute__((aligned(16))) float stage[];  // [NF][JP][SP] + camera records
+    const int L = block0 + xcd_remap(blockIdx.x, gridDim.x);
+    if (L >= nblocks) return;  // (whole block: no barrier is left behind)
+    const int bl = L / col_blocks;
+    const int b = frame0 + bl * NF;
+    const int XY = X * Y;
+    int cb = L - bl * col_blocks;
+    if (band > 0) {  // as voxelize_body
+        const int gpr = Y / cols;
+        const int per_band = band * gpr;
+        const int bi = cb / per_band, r = cb - bi * per_band;
+        const int rows = min(band, X - bi * band);
+        const int gc = r / rows, xr = r - gc * rows;
+        cb = (bi * band + xr) * gpr + gc;
+    }
+    const int c0 = cb * cols;
+    const int ncols = min(cols, XY - c0);
+    const int T = ncols * Z;  // <= 2 * VPP (host)
+    const long long N = (long long)XY * Z;
+    const long long n0 = (long long)c0 * Z;
+    const int q = threadIdx.x % LPV;
+    const int GV = V + (V & 1);
+    const unsigned qo = (unsigned)q * 16u;
+    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
+    const float fV = (float)V;
+    float *lcam = stage + ((NF * JP * SP + 3) & ~3);
+    float rt[6];
+    for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256) lcam[e] = e < V * FVP_CAM_STRIDE ? src_.cams[e] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rt[k] = src_.resize_t[k];
+    __syncthreads();
+    constexpr unsigned pix = 64u, unit = pix * NF;
+    const unsigned img = (unsigned)(H * (W + 1)) * unit;
+    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
+    // the group's voxel in each pass (layer-major slots, as voxelize_body)
+    int ii[2];
+    bool valid[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int i = p * VPP + (int)threadIdx.x / LPV;
+        valid[p] = i < T;
+        const int sl = min(i, T - 1);
+        const int zl = sl / ncols, cl = sl - zl * ncols;
+        ii[p] = cl * Z + zl;
+    }
+    // the voxel this lane projects: pass q & 1 (compute_grid, project_whole.py:43-79)
+    const int pp = q & 1;
+    float wx_, wy_, wz_;
+    {
+        const int zl = ii[pp] % Z, cl = ii[pp] / Z;
+        const long long r = c0 + cl;
+        wx_ = axis_coord(src_.gs.start[0], src_.gs.end[0], src_.gs.bins[0], src_.x_off + (int)(r / Y),
+                         src_.gs.center[0]);
+        wy_ = axis_coord(src_.gs.start[1], src_.gs.end[1], Y, (int)(r % Y), src_.gs.center[1]);
+        wz_ = axis_coord(src_.gs.start[2], src_.gs.end[2], Z, zl, src_.gs.center[2]);
+    }
+    const bool pvalid = valid[pp];
+    float acc[2][NF][4], blk[2][NF][4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[p][f][m] = blk[p][f][m] = 0.0f;
+    for (int cv0 = 0; cv0 < V; cv0 += 2) {
+        float g[2];
+        {
+            const Cam c = load_cam(lcam + min(cv0 + (q >> 1), GV - 1) * FVP_CAM_STRIDE);
+            float px, py;
+            project_point(c, wx_, wy_, wz_, px, py);
+            pixel_to_sample(px, py, rt, src_.im, g[0], g[1]);
+        }
+        g[0] = pvalid ? g[0] : -2.0f;
+        g[1] = pvalid ? g[1] : -2.0f;
+        const Taps4<true> t = setup_taps<true>(g[0], g[1], sxs, sys, W, H, unit);
+        static_for(std::make_integer_sequence<int, 4>{}, [&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int P = k & 1;  // pass
+            const int v = cv0 + (k >> 1);
+            if (v >= V) return;
+            if constexpr (CASC) {
+                if ((v & 15) == 0 && v > 0) {  // a block of 16 cameras is complete (fvp_device.h)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            blk[P][f][m] = blk[P][f][m] + acc[P][f][m];
+                            acc[P][f][m] = 0.0f;
+                        }
+                }
+            }
+            unsigned o[2];
+            unsigned all = kOOB;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                o[m] = group_bcast<LPV, k>(t.o[m]);
+                all &= o[m];
+            }
+            if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+            float w[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, k>(t.w[m]);
+            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
+            u32x4 r0[NF], r1[NF];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                r0[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + f * pix + qo, 0, 0);
+                r1[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + f * pix + qo, 0, 0);
+            }
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                static_for(std::make_integer_sequence<int, 4>{}, [&](auto mc) {
+                    constexpr int m = decltype(mc)::value, HI = m & 1;
+                    const unsigned ua = r0[f][m >> 1], ub = r0[f][2 + (m >> 1)];
+                    const unsigned uc = r1[f][m >> 1], ud = r1[f][2 + (m >> 1)];
+                    const float tt = fma_h<HI>(ua, w[0], -0.0f);
+                    acc[P][f][m] = acc[P][f][m] + fma_h<HI>(ud, w[3], fma_h<HI>(uc, w[2], fma_h<HI>(ub, w[1], tt)));
+                });
+        });
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        if (valid[p]) {
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    stage[(f * JP + 4 * q + m) * SP + ii[p]] =
+                        clampf((acc[p][f][m] + (CASC ? blk[p][f][m] : 0.0f)) / fV, 0.0f, 1.0f);
+        }
+    }
+    __syncthreads();
+    store_stage<NF, JP>(stage, SP, T, Z, N, n0, c0, ncols, XY, J, Jst, b, cube, xy, cube16);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -497,6 +666,42 @@ struct VoxJob {
     float *cube, *xy;
 };
 
+// The camera-outer gather (voxelize_co_kernel) for nb frames of one chunk, in
+// rounds of `rounds_x` x the blocks that are resident at once; false when the
+// shape does not suit it (blocks over 128 voxels, LDS), the caller then runs
+// voxelize_cams_kernel.
+template <bool CASC, int NF>
+static bool launch_co(const void *tab, int f0, int nb, const CoordSource &src, const VoxJob &j, int rounds_x,
+                      hipStream_t s) {
+    GatherCfg c;
+    c.cols = max(1, 128 / j.Z);
+    while (c.cols > 1 && j.Y % c.cols != 0) --c.cols;
+    if (c.cols * j.Z > 128) return false;
+    const bool big = (long long)j.X * j.Y >= 4096;
+    c.band = (big && j.Y % c.cols == 0 && j.X > kBandRows) ? kBandRows : 0;
+    c.col_blocks = (j.X * j.Y + c.cols - 1) / c.cols;
+    c.SP = stage_pitch(4, c.cols, j.Z);
+    c.lds = ((size_t)NF * 16 * c.SP + 3) / 4 * 4 * sizeof(float) + (size_t)FVP_GRID_SLOTS(j.V) * FVP_CAM_STRIDE * 4;
+    if (c.lds > 160 * 1024) return false;
+    static int resident = 0;  // blocks resident at once on this device (occupancy x CUs), queried once
+    if (!resident) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, voxelize_co_kernel<CASC, NF>, 256, c.lds) != hipSuccess)
+            return false;
+        resident = max(1, cus * max(1, per));
+    }
+    const int nblocks = nb / NF * c.col_blocks;
+    const int round = resident * max(1, rounds_x);
+    const bool cube16 = ((unsigned long long)j.cube & 15ull) == 0;
+    for (int b0 = 0; b0 < nblocks; b0 += round)
+        hipLaunchKernelGGL((voxelize_co_kernel<CASC, NF>), dim3((unsigned)min(round, nblocks - b0)), dim3(256), c.lds,
+                           s, tab, src, f0, j.cube, j.xy, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y, j.Z, c.cols,
+                           c.col_blocks, c.SP, c.band, b0, nblocks, cube16);
+    return true;
+}
+
 // Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
 // layout pass into the workspace, then the gather, NF frames per table entry.
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, typename T>
@@ -516,6 +721,12 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
                              reinterpret_cast<uint4 *>(ws), s);
         } else {
             launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
+        }
+#ifndef FVP_AB_CO
+#define FVP_AB_CO 0
+#endif
+        if constexpr (PAIR && OTF && NF >= 2 && FVP_AB_CO > 0) {
+            if (!j.grid_index && launch_co<CASC, NF>(ws, f0, nb, src, j, FVP_AB_CO, s)) continue;
         }
         launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
                                                j.Z, j.cube, j.xy, 4u * 4u * LPV, s);

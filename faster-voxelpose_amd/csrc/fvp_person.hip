@@ -208,11 +208,15 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     const int gz = w.ctl[2] + zl;
     const bool zin = zok && gz >= w.start[2] && gz < w.end[2];
 
-    float yzacc[YG][4];
+    // plane maxima on the float bits: every voxel value is +0 .. 1 or NaN (the
+    // mean is clamped and +0.0f turns a -0 into +0), so unsigned order is float
+    // order with NaN on top (torch.max: NaN wins) -- one v_max_u32 per step
+    // instead of a NaN-aware float max (compares + select); +0 is neutral
+    unsigned yzacc[YG][4];
 #pragma unroll
     for (int r = 0; r < YG; ++r)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) yzacc[r][k] = 0.0f;
+        for (int k = 0; k < 4; ++k) yzacc[r][k] = 0u;
 
     // block-uniform: does any of this block's rows meet the window in y?
     bool rows_in = false;
@@ -221,14 +225,50 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
         const int gy = w.ctl[1] + yg0 + r;
         rows_in |= yg0 + r < SY && gy >= w.start[1] && gy < w.end[1];
     }
-    const int x_lo = xpart * SX / xsplit, x_hi = (xpart + 1) * SX / xsplit;
+    int x_lo = xpart * SX / xsplit, x_hi = (xpart + 1) * SX / xsplit;
+    if (!cubes) {
+        // planes only: the x-planes outside the window are all 0, which changes none
+        // of the maxima (pre-zeroed xy / xz planes, yzacc >= 0) -- walk the window only
+        if (w.skip || !rows_in) {
+            x_hi = x_lo;
+        } else {
+            x_lo = max(x_lo, w.start[0] - w.ctl[0]);
+            x_hi = min(x_hi, w.end[0] - w.ctl[0]);
+        }
+    }
+#ifndef FVP_AB_PERSON_PF
+#define FVP_AB_PERSON_PF 0
+#endif
+    // packed-grid coordinates of the x-plane PF ahead, loaded after the current
+    // plane's taps are consumed (one row per block, V <= 8: one grid load per voxel)
+    constexpr int PF = (OTF || YG != 1) ? 0 : FVP_AB_PERSON_PF;
+    const bool pf = PF > 0 && V <= CPG;
+    const int gy0 = w.ctl[1] + yg0;
+    const bool row_ok = zin && yg0 < SY && gy0 >= w.start[1] && gy0 < w.end[1];
+    auto grid_at = [&](int xx) -> u32x4 {
+        const bool ok = row_ok && xx < x_hi;
+        const long long gn = ok ? ((long long)(w.ctl[0] + xx) * s.fine[1] + gy0) * s.fine[2] + gz : 0;
+        return __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + 2 * q) * 8), 0, 0);
+    };
+    u32x4 gring[PF > 0 ? PF : 1];
+    if constexpr (PF > 0) {
+        if (pf) {
+#pragma unroll
+            for (int d = 0; d < PF; ++d) gring[d] = grid_at(x_lo + d);
+        }
+    }
     for (int x = x_lo; x < x_hi; ++x) {
         const int gx = w.ctl[0] + x;
         const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
-        // planes only, nothing of this x-plane in the window: every voxel is 0,
-        // which changes none of the maxima (pre-zeroed xy / xz planes, yzacc >= 0)
-        if (!cubes && !(xin && rows_in)) continue;
-        float xzacc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (!cubes && !(xin && rows_in)) continue;  // (not taken: the walk is the window)
+        u32x4 gpre = gring[0];
+        if constexpr (PF > 0) {
+            if (pf) {
+#pragma unroll
+                for (int d = 0; d + 1 < PF; ++d) gring[d] = gring[d + 1];
+            }
+        }
+        unsigned xzacc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int r = 0; r < YG; ++r) {
             const int y = yg0 + r;
@@ -256,7 +296,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                         }
                     } else {
                         // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
-                        const u32x4 graw =
+                        const u32x4 graw = (PF > 0 && pf) ? gpre :
                             __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, FVP_AB_GRID_AUX);
 #pragma unroll
                         for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
@@ -320,15 +360,22 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                     });
                 }
             }
+            if constexpr (PF > 0) {  // the x-plane PF ahead, issued after this plane's taps were consumed
+                if (pf) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    gring[PF - 1] = grid_at(x + PF);
+                }
+            }
             // the sum's final levels (fvp_device.h): remainder + blocks, or + 0 (a -0 sum becomes +0)
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc[m] = acc[m] + (CASC ? blk[m] : 0.0f);
             float o[4];
+            unsigned ou[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 // clamp(0,1) of the mean; +0.0f turns a -0 into +0 (unsigned max order below)
                 o[k] = valid ? clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f : 0.0f;
-                if (!zok || y >= SY) o[k] = -INFINITY;  // lanes/rows beyond the cube take no part
+                ou[k] = (zok && y < SY) ? __builtin_bit_cast(unsigned, o[k]) : 0u;  // beyond the cube: neutral
             }
             if constexpr (MODE == 1 || MODE == 4) {  // probe: keep the sums live, no planes
                 if (offset && zok && y < SY && (acc[0] + acc[1] + acc[2] + acc[3]) == -1.0f)
@@ -343,16 +390,14 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
             if (planes) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    yzacc[r][k] = nanmax(yzacc[r][k], o[k]);
-                    xzacc[k] = nanmax(xzacc[k], o[k]);
-                    float m = o[k];
+                    yzacc[r][k] = max(yzacc[r][k], ou[k]);
+                    xzacc[k] = max(xzacc[k], ou[k]);
+                    unsigned m = ou[k];
 #pragma unroll
-                    for (int off = LPV; off < 64; off <<= 1) m = nanmax(m, __shfl_xor(m, off));
-                    // this wave's z-range maximum into the pre-zeroed xy plane (values are
-                    // in [0,1] or NaN, so unsigned order == float order; -inf: no z lane here)
-                    const unsigned u = __builtin_bit_cast(unsigned, m);
-                    if (lane < LPV && 4 * q + k < J && y < SY && u != 0u && m != -INFINITY)
-                        atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + k) * SX + x) * SY + y, u);
+                    for (int off = LPV; off < 64; off <<= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
+                    // this wave's z-range maximum into the pre-zeroed xy plane (+0 cannot raise it)
+                    if (lane < LPV && 4 * q + k < J && y < SY && m != 0u)
+                        atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + k) * SX + x) * SY + y, m);
                 }
             }
         }
@@ -361,7 +406,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     // +0 cannot raise the pre-zeroed plane: skip those atomics (most of the 64^3 cube)
-                    const unsigned u = __builtin_bit_cast(unsigned, xzacc[k]);
+                    const unsigned u = xzacc[k];
                     if (4 * q + k < J && u != 0u)
                         atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl, u);
                 }
@@ -377,8 +422,8 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                 for (int k = 0; k < 4; ++k) {
                     if (4 * q + k >= J) continue;
                     float *dst = yz_pl + ((size_t)(4 * q + k) * SY + y) * SZ + zl;
-                    const unsigned u = __builtin_bit_cast(unsigned, yzacc[r][k]);
-                    if (xsplit == 1) *dst = yzacc[r][k];
+                    const unsigned u = yzacc[r][k];
+                    if (xsplit == 1) *dst = __builtin_bit_cast(float, u);
                     else if (u != 0u) atomicMax(reinterpret_cast<unsigned *>(dst), u);  // pre-zeroed plane
                 }
             }

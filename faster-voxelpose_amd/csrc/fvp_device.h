@@ -26,6 +26,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef FVP_AB_DIVPAIR
+#define FVP_AB_DIVPAIR 0
+#endif
+
 namespace fvp {
 
 constexpr int kWave = 64;
@@ -70,6 +74,40 @@ __device__ __forceinline__ float nanmax(float a, float b) {
     return (b > a || b != b) ? b : a;
 }
 
+// a0 / b and a1 / b, correctly rounded, for the two quotients of one divisor in
+// project_point (y = xcam[:2] / (xcam[2] + 1e-5), cameras.py:44).  The IEEE
+// division the compiler emits (-fhip-fp32-correctly-rounded-divide-sqrt) is
+// v_div_scale x2, v_rcp, fma(-d, r, 1), fma(e, r, r), n * r, then two
+// remainder steps fma(-d, q, n) / fma(e, r, q), v_div_fmas and v_div_fixup.
+// When |a0|, |a1| and |b| lie in [2^-40, 2^40] none of its scaling or fixup
+// cases can trigger (v_div_scale scales only for an exponent gap >= 96, a
+// denormal divisor, reciprocal or quotient, or a numerator below 2^-103;
+// v_div_fixup acts only on NaN / inf / zero operands and out-of-range
+// quotients), so that sequence is exactly the unscaled core below -- whose
+// reciprocal refinement depends on b alone and is shared by both numerators:
+// 3 + 2 x 5 VALU ops (plus the range test) against 2 x ~12.  Outside the range
+// (zero numerators, divisors near 0) the lanes take the IEEE division itself.
+// Bit-identity is also checked on the host for reciprocal seeds 1 ulp either
+// side of RN(1/b) (tests/test_div_const.py::test_div_pair_*) and by the C1-C5
+// sample-grid and on-the-fly cube digests.
+__device__ __forceinline__ void div_pair(float a0, float a1, float b, float &q0, float &q1) {
+    const float r0 = __builtin_amdgcn_rcpf(b);
+    const float r = __builtin_fmaf(__builtin_fmaf(-b, r0, 1.0f), r0, r0);
+    const float lo = fminf(fminf(fabsf(a0), fabsf(a1)), fabsf(b));
+    const float hi = fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fabsf(b));
+    if (lo >= 0x1p-40f && hi <= 0x1p40f) {
+        float q = a0 * r;
+        q = __builtin_fmaf(__builtin_fmaf(-b, q, a0), r, q);
+        q0 = __builtin_fmaf(__builtin_fmaf(-b, q, a0), r, q);
+        q = a1 * r;
+        q = __builtin_fmaf(__builtin_fmaf(-b, q, a1), r, q);
+        q1 = __builtin_fmaf(__builtin_fmaf(-b, q, a1), r, q);
+    } else {
+        q0 = a0 / b;
+        q1 = a1 / b;
+    }
+}
+
 // lib/utils/cameras.py:30-56 project_point for one world point -> pixel.
 __device__ __forceinline__ void project_point(const Cam &c, float x, float y, float z, float &px, float &py) {
     const float dx = x - c.T[0], dy = y - c.T[1], dz = z - c.T[2];
@@ -77,8 +115,13 @@ __device__ __forceinline__ void project_point(const Cam &c, float x, float y, fl
     const float xc1 = __builtin_fmaf(c.R[5], dz, __builtin_fmaf(c.R[4], dy, c.R[3] * dx));
     const float xc2 = __builtin_fmaf(c.R[8], dz, __builtin_fmaf(c.R[7], dy, c.R[6] * dx));
     const float den = xc2 + 1e-5f;
-    const float y0 = xc0 / den;
-    const float y1 = xc1 / den;
+    float y0, y1;
+#if FVP_AB_DIVPAIR
+    div_pair(xc0, xc1, den, y0, y1);
+#else
+    y0 = xc0 / den;
+    y1 = xc1 / den;
+#endif
     const float r = y0 * y0 + y1 * y1;
     float d = (1.0f + c.k[0] * r) + (c.k[1] * r) * r;
     d = d + ((c.k[2] * r) * r) * r;

@@ -93,3 +93,80 @@ def test_div_const_integer_divisor_sweep():
         assert r.returncode == 0 and "0 divisors with a difference" in r.stdout, r.stdout
     with open(os.path.join(repo, "profiles", "round4", "div_const_sweep_65535.txt")) as f:
         assert "odd divisors 3..65535:" in f.read()
+
+
+DIV_PAIR_SRC = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+static inline float bits_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t f_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+/* fvp_device.h div_pair, one numerator, from a reciprocal seed r0 (v_rcp_f32 is
+   within 1 ulp of 1/b; its exact value is the hardware's, so every seed in
+   {RN(1/b) - 1 ulp, RN(1/b), RN(1/b) + 1 ulp} is tried) */
+static inline float div_pair1(float a, float b, float r0) {
+    const float r = fmaf(fmaf(-b, r0, 1.0f), r0, r0);
+    float q = a * r;
+    q = fmaf(fmaf(-b, q, a), r, q);
+    return fmaf(fmaf(-b, q, a), r, q);
+}
+static inline uint64_t mix(uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; return x ^ (x >> 33); }
+int main(int argc, char **argv) {
+    const int per_b = argc > 1 ? atoi(argv[1]) : 8;
+    const uint32_t bstep = argc > 2 ? (uint32_t)atoi(argv[2]) : 1;
+    long long checked = 0, bad = 0;
+    /* every (bstep-th) mantissa of b in [1, 2): the quotient, the reciprocal and the
+       remainders scale exactly by powers of two in a and b while everything stays
+       normal (|a|, |b| in [2^-40, 2^40] on the device), so mantissas decide */
+#pragma omp parallel for schedule(static) reduction(+ : checked, bad)
+    for (uint32_t mb = 0; mb < (1u << 23); mb += bstep) {
+        const float b = bits_f(0x3f800000u | mb);
+        const float rn = 1.0f / b;
+        const float seeds[3] = {bits_f(f_bits(rn) - 1), rn, bits_f(f_bits(rn) + 1)};
+        for (int k = 0; k < per_b; ++k) {
+            const uint64_t h = mix(((uint64_t)mb << 20) ^ (uint64_t)k);
+            float as[6];
+            /* a random numerator in [1, 2) and [2, 4), and the numerators whose
+               quotient lies next to a rounding midpoint (the hard cases):
+               a = RN(b * (q + ulp(q)/2)) and its neighbours */
+            as[0] = bits_f(0x3f800000u | (uint32_t)(h & 0x7fffff));
+            as[1] = bits_f(0x40000000u | (uint32_t)((h >> 23) & 0x7fffff));
+            const float q = bits_f(0x3f000000u | (uint32_t)((h >> 40) & 0x7fffff));  /* [0.5, 1) */
+            const double mid = (double)q + ldexp(1.0, -25);
+            const float a0 = (float)(mid * (double)b);
+            as[2] = a0; as[3] = bits_f(f_bits(a0) + 1); as[4] = bits_f(f_bits(a0) - 1);
+            as[5] = -as[0];
+            for (int i = 0; i < 6; ++i) {
+                const float ref = as[i] / b;
+                for (int s = 0; s < 3; ++s) {
+                    ++checked;
+                    bad += f_bits(div_pair1(as[i], b, seeds[s])) != f_bits(ref);
+                }
+            }
+        }
+    }
+    printf("div_pair: %lld quotients checked, %lld differ\n", checked, bad);
+    return bad != 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
+def test_div_pair_matches_ieee_division():
+    """fvp_device.h div_pair (project_point's two quotients by one divisor): the
+    unscaled core of the IEEE division sequence, from reciprocal seeds 1 ulp
+    either side of RN(1/b), against a / b -- every mantissa of b in [1, 2) with
+    random numerators in two binades and the numerators whose quotients sit next
+    to rounding midpoints."""
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "divp.c"), os.path.join(d, "divp")
+        with open(c, "w") as f:
+            f.write(DIV_PAIR_SRC)
+        subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-fno-fast-math", "-mfma", c, "-o", exe,
+                        "-lm"], check=True)
+        env = dict(os.environ, OMP_NUM_THREADS=str(min(8, os.cpu_count() or 1)))
+        r = subprocess.run([exe, "4", "1"], capture_output=True, text=True, timeout=600, env=env)
+        print(r.stdout)
+        assert r.returncode == 0 and " 0 differ" in r.stdout, r.stdout

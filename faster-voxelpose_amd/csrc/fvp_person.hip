@@ -18,6 +18,9 @@
 #ifndef FVP_AB_GRID_AUX
 #define FVP_AB_GRID_AUX 0
 #endif
+#ifndef FVP_AB_PERSON_PIPE
+#define FVP_AB_PERSON_PIPE 0
+#endif
 
 namespace fvp {
 
@@ -156,6 +159,7 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                                                              int H, int W, int xmap, int xsplit, int zsplit,
                                                              unsigned pix_bytes) {
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
+    constexpr bool PIPE = FVP_AB_PERSON_PIPE != 0 && !OTF;
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
     const int ngroups = (SY + YG - 1) / YG;
@@ -305,6 +309,67 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                     for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
                     const Taps4<false> t0 = setup_taps<false>(g[0], g[1], sxs, sys, W, H, pix_bytes);
                     const Taps4<false> t1 = setup_taps<false>(g[2], g[3], sxs, sys, W, H, pix_bytes);
+                    if constexpr (PIPE) {
+                        // two-stage camera pipeline: camera k+1's four tap loads are issued
+                        // before camera k's are consumed (8 loads in flight per wave instead
+                        // of 4); no per-camera wave skip (an all-off-image camera's loads are
+                        // range-checked no-ops)
+                        u32x4 tb[2][4];
+                        float wb[2][4];
+                        auto issue = [&](auto kc2) {
+                            constexpr int k = decltype(kc2)::value;
+                            constexpr int S = k >> 1;
+                            const Taps4<false> &src = (k & 1) ? t1 : t0;
+                            unsigned o[4];
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                o[m] = group_bcast<LPV, S>(src.o[m]);
+                                wb[k & 1][m] = group_bcast<LPV, S>(src.w[m]);
+                                if constexpr (MODE == 3) o[m] = kOOB;
+                            }
+                            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_cl + (size_t)(v0 + k) * img, img);
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                if constexpr (MODE == 4) tb[k & 1][m] = u32x4{o[m], 0u, 0u, 0u};
+                                else if constexpr (MODE == 2) tb[k & 1][m] = u32x4{0u, 0u, 0u, 0u};
+                                else tb[k & 1][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[m] + qo, 0, 0);
+                            }
+                        };
+                        issue(std::integral_constant<int, 0>{});
+                        static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                            constexpr int k = decltype(kc)::value;
+                            const int v = v0 + k;
+                            if (v >= V) return;
+                            if constexpr (k + 1 < CPG) {
+                                if (v + 1 < V) issue(std::integral_constant<int, k + 1>{});
+                            }
+                            if constexpr (CASC) {
+                                if ((v & 15) == 0 && v > 0) {
+#pragma unroll
+                                    for (int m = 0; m < 4; ++m) {
+                                        blk[m] = blk[m] + acc[m];
+                                        acc[m] = 0.0f;
+                                    }
+                                }
+                            }
+                            const u32x4 *t = tb[k & 1];
+                            const float *wt = wb[k & 1];
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                if constexpr (MODE == 4) {
+                                    acc[m] = acc[m] + wt[m] + __builtin_bit_cast(float, (unsigned)t[m][0]);
+                                    continue;
+                                }
+                                const float fa = __builtin_bit_cast(float, (unsigned)t[0][m]);
+                                const float fb = __builtin_bit_cast(float, (unsigned)t[1][m]);
+                                const float fc = __builtin_bit_cast(float, (unsigned)t[2][m]);
+                                const float fd = __builtin_bit_cast(float, (unsigned)t[3][m]);
+                                acc[m] = acc[m] + __builtin_fmaf(fd, wt[3], __builtin_fmaf(fc, wt[2],
+                                                                 __builtin_fmaf(fb, wt[1], fa * wt[0])));
+                            }
+                        });
+                        continue;
+                    }
                     static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
                         constexpr int k = decltype(kc)::value;
                         constexpr int S = k >> 1;
@@ -454,8 +519,13 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // (the yz maxima then go through atomics into a pre-zeroed plane).
     // Cubes deeper than 64 run as 64-deep z chunks, one block each (the xy and xz
     // maxima already combine across blocks through atomics; yz is per (y, z)).
+#ifndef FVP_AB_PERSON_YG
+#define FVP_AB_PERSON_YG 1
+#endif
+    constexpr int YG = FVP_AB_PERSON_YG;
     const int xmap = 1, xsplit = person_xsplit(P, SY), zsplit = (s.bins[2] + 63) / 64;
-    hipLaunchKernelGGL((person_cl_kernel<LPV, 1, OTF, CASC>), dim3((unsigned)((long long)P * SY * xsplit * zsplit)),
+    hipLaunchKernelGGL((person_cl_kernel<LPV, YG, OTF, CASC>),
+                       dim3((unsigned)((long long)P * ((SY + YG - 1) / YG) * xsplit * zsplit)),
                        dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H,
                        W, xmap, xsplit, zsplit, pix_bytes);
 }

@@ -117,6 +117,10 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        int col_blocks, int SP, int band, unsigned pixb,
                                                        bool cube16) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
+#ifndef FVP_AB_VPIPE
+#define FVP_AB_VPIPE 0
+#endif
+    constexpr bool VPIPE = FVP_AB_VPIPE != 0 && !PAIR && NF == 1;
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
     constexpr int CPG = 2 * LPV;    // cameras per grid load (2 per lane)
@@ -212,6 +216,55 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
             for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
             const Taps4<PAIR> t0 = setup_taps<PAIR>(g[0], g[1], sxs, sys, W, H, unit);
             const Taps4<PAIR> t1 = setup_taps<PAIR>(g[2], g[3], sxs, sys, W, H, unit);
+            if constexpr (VPIPE) {
+                // two-stage camera pipeline (fp32 table, one frame per entry): camera
+                // k+1's four tap loads are issued before camera k's are consumed; no
+                // per-camera wave skip (off-image loads are range-checked no-ops)
+                u32x4 tb[2][4];
+                float wb[2][4];
+                auto issue = [&](auto kc2) {
+                    constexpr int k = decltype(kc2)::value;
+                    constexpr int S = k >> 1;
+                    const Taps4<PAIR> &src = (k & 1) ? t1 : t0;
+                    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)(v0 + k) * img, img);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const unsigned o = group_bcast<LPV, S>(src.o[m]);
+                        wb[k & 1][m] = group_bcast<LPV, S>(src.w[m]);
+                        tb[k & 1][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + qo, 0, 0);
+                    }
+                };
+                issue(std::integral_constant<int, 0>{});
+                static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    const int v = v0 + k;
+                    if (v >= V) return;
+                    if constexpr (k + 1 < CPG) {
+                        if (v + 1 < V) issue(std::integral_constant<int, k + 1>{});
+                    }
+                    if constexpr (CASC) {
+                        if ((v & 15) == 0 && v > 0) {
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                blk[0][m] = blk[0][m] + acc[0][m];
+                                acc[0][m] = 0.0f;
+                            }
+                        }
+                    }
+                    const u32x4 *t = tb[k & 1];
+                    const float *w = wb[k & 1];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const float fa = __builtin_bit_cast(float, (unsigned)t[0][m]);
+                        const float fb = __builtin_bit_cast(float, (unsigned)t[1][m]);
+                        const float fc = __builtin_bit_cast(float, (unsigned)t[2][m]);
+                        const float fd = __builtin_bit_cast(float, (unsigned)t[3][m]);
+                        acc[0][m] = acc[0][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
+                                                                __builtin_fmaf(fb, w[1], fa * w[0])));
+                    }
+                });
+                continue;
+            }
             static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = k >> 1;  // lane of the group that set this camera up

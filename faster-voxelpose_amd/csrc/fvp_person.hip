@@ -149,7 +149,7 @@ struct PersonCoords {
 // plane reductions / stores (the sums folded into `offset`), 2 = zeros instead
 // of the tap loads, 3 = every tap offset off-image (range-checked loads, no
 // memory access), 4 = grid loads and tap setup only (no tap loads, no planes).
-template <int LPV, int YG, bool OTF, bool CASC, int MODE = 0>
+template <int LPV, int YG, bool OTF, bool CASC, int MODE = 0, int VC = 0>
 __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
                                                              const float *__restrict__ props,
@@ -159,7 +159,10 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                                                              int H, int W, int xmap, int xsplit, int zsplit,
                                                              unsigned pix_bytes) {
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
-    constexpr bool PIPE = FVP_AB_PERSON_PIPE != 0 && !OTF;
+    // PIPE: the two-stage camera pipeline, for launches whose camera count VC is a
+    // compile-time constant (a uniform branch around the next camera's loads would
+    // make the wait at the join cover them too)
+    constexpr bool PIPE = VC > 0 && !OTF && !CASC;
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
     const int ngroups = (SY + YG - 1) / YG;
@@ -338,20 +341,8 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                         issue(std::integral_constant<int, 0>{});
                         static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
                             constexpr int k = decltype(kc)::value;
-                            const int v = v0 + k;
-                            if (v >= V) return;
-                            if constexpr (k + 1 < CPG) {
-                                if (v + 1 < V) issue(std::integral_constant<int, k + 1>{});
-                            }
-                            if constexpr (CASC) {
-                                if ((v & 15) == 0 && v > 0) {
-#pragma unroll
-                                    for (int m = 0; m < 4; ++m) {
-                                        blk[m] = blk[m] + acc[m];
-                                        acc[m] = 0.0f;
-                                    }
-                                }
-                            }
+                            if constexpr (k >= VC) return;
+                            if constexpr (k + 1 < VC) issue(std::integral_constant<int, k + 1>{});
                             const u32x4 *t = tb[k & 1];
                             const float *wt = wb[k & 1];
 #pragma unroll
@@ -524,6 +515,15 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
 #endif
     constexpr int YG = FVP_AB_PERSON_YG;
     const int xmap = 1, xsplit = person_xsplit(P, SY), zsplit = (s.bins[2] + 63) / 64;
+    if constexpr (!OTF && !CASC && 2 * LPV >= 5) {
+        if (FVP_AB_PERSON_PIPE && V == 5) {
+            hipLaunchKernelGGL((person_cl_kernel<LPV, YG, OTF, CASC, 0, 5>),
+                               dim3((unsigned)((long long)P * ((SY + YG - 1) / YG) * xsplit * zsplit)), dim3(64 * LPV),
+                               0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H, W,
+                               xmap, xsplit, zsplit, pix_bytes);
+            return;
+        }
+    }
     hipLaunchKernelGGL((person_cl_kernel<LPV, YG, OTF, CASC>),
                        dim3((unsigned)((long long)P * ((SY + YG - 1) / YG) * xsplit * zsplit)),
                        dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H,

@@ -39,6 +39,12 @@
 #ifndef FVP_AB_VGRID_AUX
 #define FVP_AB_VGRID_AUX 0
 #endif
+#ifndef FVP_AB_VPIPE
+#define FVP_AB_VPIPE 0
+#endif
+#ifndef FVP_AB_VPIPE_MINB
+#define FVP_AB_VPIPE_MINB 8
+#endif
 
 namespace fvp {
 
@@ -109,7 +115,7 @@ __device__ __forceinline__ void store_stage(const float *__restrict__ stage, int
     }
 }
 
-template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, int VC = 0>
 __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
@@ -117,10 +123,10 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        int col_blocks, int SP, int band, unsigned pixb,
                                                        bool cube16) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
-#ifndef FVP_AB_VPIPE
-#define FVP_AB_VPIPE 0
-#endif
-    constexpr bool VPIPE = FVP_AB_VPIPE != 0 && !PAIR && NF == 1;
+    // VPIPE: the two-stage camera pipeline, for launches whose camera count VC is a
+    // compile-time constant (no conditional loads: a uniform branch around the next
+    // camera's loads would make the wait at the join cover them too)
+    constexpr bool VPIPE = VC > 0 && !PAIR && NF == 1;
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
     constexpr int CPG = 2 * LPV;    // cameras per grid load (2 per lane)
@@ -238,10 +244,8 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                 static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
                     constexpr int k = decltype(kc)::value;
                     const int v = v0 + k;
-                    if (v >= V) return;
-                    if constexpr (k + 1 < CPG) {
-                        if (v + 1 < V) issue(std::integral_constant<int, k + 1>{});
-                    }
+                    if constexpr (k < VC) {
+                        if constexpr (k + 1 < VC) issue(std::integral_constant<int, k + 1>{});
                     if constexpr (CASC) {
                         if ((v & 15) == 0 && v > 0) {
 #pragma unroll
@@ -261,6 +265,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                         const float fd = __builtin_bit_cast(float, (unsigned)t[3][m]);
                         acc[0][m] = acc[0][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
                                                                 __builtin_fmaf(fb, w[1], fa * w[0])));
+                    }
                     }
                 });
                 continue;
@@ -392,15 +397,15 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
 // (C2 -4 %, C4 -8 % gather time, measured).
 // Cached-grid gather: <= 64 VGPRs so 8 waves/SIMD fit (32 waves/CU with the
 // 20 KB stage); the on-the-fly variant keeps its registers (no spills).
-template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
-__global__ __launch_bounds__(256, NF == 1 ? 8 : NF == 2 ? 5 : 4) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, int VC = 0>
+__global__ __launch_bounds__(256, NF == 1 ? (VC ? FVP_AB_VPIPE_MINB : 8) : NF == 2 ? 5 : 4) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int Jst, int H, int W, int X, int Y, int Z,
                                                           int cols, int col_blocks, int SP, int band, unsigned pixb,
                                                           bool cube16) {
     static_assert(!OTF, "grid kernel");
-    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
+    voxelize_body<LPV, PAIR, OTF, CASC, NF, VC>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
                                             col_blocks, SP, band, pixb, cube16);
 }
 
@@ -701,10 +706,19 @@ static void launch_gather(const void *tab, int f0, int nb, const GatherCfg &c, c
         hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
                            pixb, cube16);
-    else
+    else {
+        if constexpr (!PAIR && NF == 1 && !CASC && 2 * LPV >= 5) {
+            if (FVP_AB_VPIPE && V == 5) {
+                hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF, 5>), grid, dim3(256), c.lds, s, tab,
+                                   src, grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP,
+                                   c.band, pixb, cube16);
+                return;
+            }
+        }
         hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
                            pixb, cube16);
+    }
 }
 
 // One voxelize call's shapes.  Heatmaps with more than kJointSlice joints run

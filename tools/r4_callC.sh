@@ -13,4 +13,5 @@ FVP_LIB=$PWD/ab_libs/jpipe.so timeout -k 10 300 python -u -m pytest tests/test_g
   tests/test_integration.py -m gpu -x -q --timeout 120 --timeout-method thread -k "person or jln or e2e or individual" \
   > gpurun_out/r4c_jpipe_tests.log 2>&1 || { tail -30 gpurun_out/r4c_jpipe_tests.log; exit 1; }
 echo "jpipe tests: $(tail -1 gpurun_out/r4c_jpipe_tests.log)"
+LIBS="ab_libs/vbase.so ab_libs/vpipe.so ab_libs/vpipe8.so ab_libs/vpipe5.so" WL="c2:256" REPS=2 TAG=vpipe bash tools/r4_ab_c5.sh || exit 1
 echo callC done

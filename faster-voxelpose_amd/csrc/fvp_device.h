@@ -27,7 +27,7 @@
 #pragma clang fp contract(off)
 
 #ifndef FVP_AB_DIVPAIR
-#define FVP_AB_DIVPAIR 0
+#define FVP_AB_DIVPAIR 1
 #endif
 
 namespace fvp {

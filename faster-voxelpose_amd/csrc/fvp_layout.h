@@ -246,6 +246,30 @@ __device__ __forceinline__ unsigned group_bcast(unsigned x) {
     }
 }
 
+// Unsigned maximum over the lanes of the wave that hold the same group slot
+// (lane mod LPV), all in VALU: DPP row rotations by LPV, 2 LPV, .. 8 within each
+// 16-lane row, then v_permlane16_swap / v_permlane32_swap (gfx950) across the
+// rows.  Every lane ends with its slot's maximum.  (A __shfl_xor chain compiles
+// to ds_bpermute, an LDS round trip and an lgkmcnt(0) wait per step.)
+template <int LPV>
+__device__ __forceinline__ unsigned slot_umax(unsigned m) {
+    static_assert(LPV == 1 || LPV == 2 || LPV == 4 || LPV == 8, "voxel groups of 1, 2, 4 or 8 lanes");
+    // row_ror:s = DPP control 0x120 + s
+    auto ror = [](unsigned v, auto sc) {
+        return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + decltype(sc)::value, 0xf, 0xf, false);
+    };
+    unsigned r;
+    if constexpr (LPV <= 1) { r = ror(m, std::integral_constant<int, 1>{}); m = m > r ? m : r; }
+    if constexpr (LPV <= 2) { r = ror(m, std::integral_constant<int, 2>{}); m = m > r ? m : r; }
+    if constexpr (LPV <= 4) { r = ror(m, std::integral_constant<int, 4>{}); m = m > r ? m : r; }
+    r = ror(m, std::integral_constant<int, 8>{});
+    m = m > r ? m : r;
+    const auto h = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+    m = h[0] > h[1] ? h[0] : h[1];
+    const auto w = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+    return w[0] > w[1] ? w[0] : w[1];
+}
+
 template <int LPV, int S>
 __device__ __forceinline__ float group_bcast(float x) {
     return __builtin_bit_cast(float, group_bcast<LPV, S>(__builtin_bit_cast(unsigned, x)));

@@ -21,6 +21,9 @@
 #ifndef FVP_AB_PERSON_PIPE
 #define FVP_AB_PERSON_PIPE 0
 #endif
+#ifndef FVP_AB_PERSON_MINB
+#define FVP_AB_PERSON_MINB 1
+#endif
 
 namespace fvp {
 
@@ -150,7 +153,7 @@ struct PersonCoords {
 // of the tap loads, 3 = every tap offset off-image (range-checked loads, no
 // memory access), 4 = grid loads and tap setup only (no tap loads, no planes).
 template <int LPV, int YG, bool OTF, bool CASC, int MODE = 0, int VC = 0>
-__global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
+__global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
                                                              const float *__restrict__ props,
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
@@ -448,13 +451,17 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                 for (int k = 0; k < 4; ++k) {
                     yzacc[r][k] = max(yzacc[r][k], ou[k]);
                     xzacc[k] = max(xzacc[k], ou[k]);
-                    unsigned m = ou[k];
-#pragma unroll
-                    for (int off = LPV; off < 64; off <<= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
-                    // this wave's z-range maximum into the pre-zeroed xy plane (+0 cannot raise it)
-                    if (lane < LPV && 4 * q + k < J && y < SY && m != 0u)
-                        atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + k) * SX + x) * SY + y, m);
                 }
+                // this wave's z-range maxima (all lanes: their slot's), four independent
+                // VALU chains; then lane L < 4 LPV sends joint 4 (L % LPV) + L / LPV into the
+                // pre-zeroed xy plane with one atomic instruction (+0 cannot raise it)
+                unsigned zm[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) zm[k] = slot_umax<LPV>(ou[k]);
+                const int kk = lane / LPV;  // q == lane % LPV
+                const unsigned mv = kk == 0 ? zm[0] : kk == 1 ? zm[1] : kk == 2 ? zm[2] : zm[3];
+                if (lane < 4 * LPV && 4 * q + kk < J && y < SY && mv != 0u)
+                    atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + kk) * SX + x) * SY + y, mv);
             }
         }
         if (planes) {

@@ -24,6 +24,9 @@
 #ifndef FVP_AB_PERSON_MINB
 #define FVP_AB_PERSON_MINB 1
 #endif
+#ifndef FVP_AB_XZ_LATE
+#define FVP_AB_XZ_LATE 0
+#endif
 
 namespace fvp {
 
@@ -151,7 +154,8 @@ struct PersonCoords {
 // MODE (replay probe, tools/person_probe.hip; the product launches 0): 1 = no
 // plane reductions / stores (the sums folded into `offset`), 2 = zeros instead
 // of the tap loads, 3 = every tap offset off-image (range-checked loads, no
-// memory access), 4 = grid loads and tap setup only (no tap loads, no planes).
+// memory access), 4 = grid loads and tap setup only (no tap loads, no planes),
+// 5 / 6 = no xz / xy plane atomics.
 template <int LPV, int YG, bool OTF, bool CASC, int MODE = 0, int VC = 0>
 __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
@@ -167,6 +171,9 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
     // make the wait at the join cover them too)
     constexpr bool PIPE = VC > 0 && !OTF && !CASC;
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
+    // xy maxima deferred to the block's end (DXY): [wave][x][joint slot] per-wave z maxima
+    constexpr bool DXY = LPV <= 4 && YG == 1;
+    __shared__ unsigned lxy[DXY ? LPV * 64 * 4 * LPV : 1];
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
     const int ngroups = (SY + YG - 1) / YG;
     // XCD-aware: each XCD runs whole proposals, so the row groups of one
@@ -235,6 +242,15 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
         const int gy = w.ctl[1] + yg0 + r;
         rows_in |= yg0 + r < SY && gy >= w.start[1] && gy < w.end[1];
     }
+    // the block owns its row's xy cells when nothing else writes them (one x part,
+    // one z chunk): the per-wave z maxima go to LDS and out as plain stores at the
+    // end -- an atomic per wave and x step costs ~0.6 us per proposal (probe mode 6)
+    // because non-returning atomics count in vmcnt and the next taps wait on them
+    const bool defer = DXY && planes && xsplit == 1 && zsplit == 1 && SX <= 64;
+    const int wave = (int)threadIdx.x >> 6;
+    if (defer) {
+        for (int e = lane; e < 64 * 4 * LPV; e += 64) lxy[wave * 64 * 4 * LPV + e] = 0u;
+    }
     int x_lo = xpart * SX / xsplit, x_hi = (xpart + 1) * SX / xsplit;
     if (!cubes) {
         // planes only: the x-planes outside the window are all 0, which changes none
@@ -267,6 +283,25 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
             for (int d = 0; d < PF; ++d) gring[d] = grid_at(x_lo + d);
         }
     }
+    // LATE: the xz atomics of x step i are issued during step i + 1, after its second
+    // camera's tap loads (vmcnt counts non-returning atomics and waits in issue order:
+    // issued at the end of a step, the next step's first wait would cover their whole
+    // L2 round trip; issued after camera 1's loads, only camera 2's wait can)
+    constexpr bool LATE = FVP_AB_XZ_LATE != 0;
+    unsigned xz_pend[4] = {0u, 0u, 0u, 0u};
+    int xz_px = -1;  // the pending step's x (block-uniform), -1: none
+    auto flush_xz = [&]() {
+        if (xz_px >= 0) {
+            if (zok) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (MODE != 5 && 4 * q + k < J && xz_pend[k] != 0u)
+                        atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + xz_px) * SZ + zl,
+                                  xz_pend[k]);
+            }
+            xz_px = -1;
+        }
+    };
     for (int x = x_lo; x < x_hi; ++x) {
         const int gx = w.ctl[0] + x;
         const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
@@ -407,6 +442,9 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
                             tc = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
                             td = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
                         }
+                        if constexpr (LATE && k == 1) {
+                            if (v0 == 0) flush_xz();
+                        }
 #pragma unroll
                         for (int m = 0; m < 4; ++m) {
                             const float fa = __builtin_bit_cast(float, (unsigned)ta[m]);
@@ -460,22 +498,31 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
                 for (int k = 0; k < 4; ++k) zm[k] = slot_umax<LPV>(ou[k]);
                 const int kk = lane / LPV;  // q == lane % LPV
                 const unsigned mv = kk == 0 ? zm[0] : kk == 1 ? zm[1] : kk == 2 ? zm[2] : zm[3];
-                if (lane < 4 * LPV && 4 * q + kk < J && y < SY && mv != 0u)
+                if (defer) {
+                    if (lane < 4 * LPV) lxy[(wave * 64 + x) * (4 * LPV) + 4 * q + kk] = mv;
+                } else if (MODE != 6 && lane < 4 * LPV && 4 * q + kk < J && y < SY && mv != 0u) {
                     atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + kk) * SX + x) * SY + y, mv);
+                }
             }
         }
-        if (planes) {
+        if (planes && LATE) {
+            flush_xz();  // (not yet issued: this step's first camera was skipped)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xz_pend[k] = xzacc[k];
+            xz_px = x;
+        } else if (planes) {
             if (zok) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     // +0 cannot raise the pre-zeroed plane: skip those atomics (most of the 64^3 cube)
                     const unsigned u = xzacc[k];
-                    if (4 * q + k < J && u != 0u)
+                    if (MODE != 5 && 4 * q + k < J && u != 0u)
                         atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl, u);
                 }
             }
         }
     }
+    flush_xz();
     if (planes && zok) {
 #pragma unroll
         for (int r = 0; r < YG; ++r) {
@@ -490,6 +537,17 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
                     else if (u != 0u) atomicMax(reinterpret_cast<unsigned *>(dst), u);  // pre-zeroed plane
                 }
             }
+        }
+    }
+    if (defer) {  // xy[j][x][y] = max over the block's waves (z ranges); the plane is pre-zeroed
+        __syncthreads();
+        const int n = (x_hi - x_lo) * J;
+        for (int e = threadIdx.x; e < n; e += 64 * LPV) {
+            const int xi = x_lo + e / J, j = e - (e / J) * J;
+            unsigned m = 0u;
+#pragma unroll
+            for (int wv = 0; wv < LPV; ++wv) m = max(m, lxy[(wv * 64 + xi) * (4 * LPV) + j]);
+            if (MODE != 6 && m != 0u) xy_pl[((size_t)j * SX + xi) * SY + yg0] = __builtin_bit_cast(float, m);
         }
     }
 }

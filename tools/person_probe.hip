@@ -7,6 +7,8 @@
 //   2 NOTAPS    zeros instead of the tap loads
 //   3 ALL_OOB   every tap offset off-image (range-checked loads)
 //   4 SETUP     grid loads + tap setup only
+//   5 NO_XZ_ATOMICS  FULL without the xz-plane atomics
+//   6 NO_XY_ATOMICS  FULL without the xy-plane atomics
 // Test tooling only (tools/person_probe.py); not part of libfvp.
 #include "../faster-voxelpose_amd/csrc/fvp_person.hip"
 
@@ -36,6 +38,8 @@ extern "C" int person_probe(int mode, const float *cl, int cp, const float *fgri
         case 2: go<2>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         case 3: go<3>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         case 4: go<4>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
+        case 5: go<5>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
+        case 6: go<6>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         default: return FVP_ERR_SHAPE;
     }
     return (int)hipGetLastError();

@@ -10,4 +10,6 @@ for v in jmb6 jmb7; do
     > gpurun_out/r4f_${v}_tests.log 2>&1 || { tail -30 gpurun_out/r4f_${v}_tests.log; exit 1; }
   echo "$v tests: $(tail -1 gpurun_out/r4f_${v}_tests.log)"
 done
+timeout -k 10 300 python3 tools/person_probe.py --iters 20 > gpurun_out/r4f_person_probe.jsonl 2>&1 || { tail -20 gpurun_out/r4f_person_probe.jsonl; exit 1; }
+cat gpurun_out/r4f_person_probe.jsonl
 echo callF done

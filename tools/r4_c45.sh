@@ -23,7 +23,9 @@ pmc() {  # tag args...
   TAG=r4_c45/pmc_$tag BENCH_EXTRA="$*" PMC_GROUPS="FETCH_SIZE
 WRITE_SIZE
 TCC_HIT_sum TCC_MISS_sum
-TD_TD_BUSY_sum TD_TC_STALL_sum TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE GRBM_COUNT
+TD_TD_BUSY_sum TD_TC_STALL_sum
+TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum
+GRBM_GUI_ACTIVE GRBM_COUNT
 SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_VALU" \
     bash tools/pmc.sh > $OUT/pmc_$tag.txt 2>&1 || { tail -5 $OUT/pmc_$tag.txt; exit 1; }
   echo "pmc $tag ok"
@@ -34,6 +36,7 @@ SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_
   line c4_b64 --workload c4 --batch 64
   CPU=off line c4_b32 --workload c4 --batch 32
 }
+[ -n "${SKIP_STATS:-}" ] && { echo done; exit 0; }
 stats c5_b8 --workload c5 --batch 8
 stats c4_b64 --workload c4 --batch 64
 pmc c5_b8 --workload c5 --batch 8

@@ -26,10 +26,6 @@
 
 #pragma clang fp contract(off)
 
-#ifndef FVP_AB_DIVPAIR
-#define FVP_AB_DIVPAIR 1
-#endif
-
 namespace fvp {
 
 constexpr int kWave = 64;
@@ -116,12 +112,7 @@ __device__ __forceinline__ void project_point(const Cam &c, float x, float y, fl
     const float xc2 = __builtin_fmaf(c.R[8], dz, __builtin_fmaf(c.R[7], dy, c.R[6] * dx));
     const float den = xc2 + 1e-5f;
     float y0, y1;
-#if FVP_AB_DIVPAIR
     div_pair(xc0, xc1, den, y0, y1);
-#else
-    y0 = xc0 / den;
-    y1 = xc1 / den;
-#endif
     const float r = y0 * y0 + y1 * y1;
     float d = (1.0f + c.k[0] * r) + (c.k[1] * r) * r;
     d = d + ((c.k[2] * r) * r) * r;

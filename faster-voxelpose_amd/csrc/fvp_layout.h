@@ -150,56 +150,6 @@ __global__ __launch_bounds__(256) void pairs_rows_kernel(const _Float16 *__restr
     }
 }
 
-// The same table without LDS: one thread per (row, frame f, joint quad q, entry
-// pair ep) builds entries e = 2ep and 2ep + 1 (pixels e-1, e, e+1) from eight
-// 4-B loads -- words (e-2, e-1) and (e, e+1) of joints 4q..4q+3 -- and six
-// v_perm_b32, then two 16-B stores.  Lanes run along ep, so each wave-load
-// reads 256 contiguous bytes of one joint row (a neighbouring lane's words are
-// read twice, from L1); the stores land 16 B of every 256-B entry group, whose
-// other 240 B come from the neighbouring (f, q) waves.  Needs W even and a 4-B
-// aligned heatmap pointer (rows then start on 4 B).
-template <int NF>
-__global__ __launch_bounds__(256) void pairs_vec_kernel(const _Float16 *__restrict__ hm, uint4 *__restrict__ tab,
-                                                        int J, int H, int W, int V, int EP, long long total) {
-    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (t >= total) return;
-    const int ep = (int)(t % EP);
-    long long r = t / EP;
-    const int q = (int)(r & 3);
-    r >>= 2;
-    const int f = (int)(r % NF);
-    const long long row = r / NF;  // (g * V + v) * H + y
-    const long long gv = row / H;
-    const int y = (int)(row - gv * H);
-    const long long g = gv / V;
-    const int v = (int)(gv - g * V);
-    const size_t HW = (size_t)H * W;
-    const int W2 = W / 2, e = 2 * ep;
-    const unsigned *__restrict__ src = reinterpret_cast<const unsigned *>(
-        hm + (((size_t)(g * NF + f) * V + v) * J) * HW + (size_t)y * W);
-    unsigned w0[4], w1[4];  // joint 4q+k: pixels (e-2, e-1) and (e, e+1)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 4 * q + k;
-        const unsigned *__restrict__ rowp = src + (size_t)j * (HW / 2);
-        const bool jok = j < J;
-        w0[k] = (jok && ep > 0) ? rowp[ep - 1] : 0u;
-        w1[k] = (jok && ep < W2) ? rowp[ep] : 0u;
-    }
-    // v_perm_b32 selectors: high halves of (a, b) -> [a.hi | b.hi], low halves -> [a.lo | b.lo]
-    // (__builtin_amdgcn_perm(hi_src, lo_src, sel): bytes 0-3 of lo_src, 4-7 of hi_src)
-    const unsigned HI = 0x07060302u, LO = 0x05040100u;
-    const uint4 ent0 = make_uint4(__builtin_amdgcn_perm(w0[1], w0[0], HI), __builtin_amdgcn_perm(w0[3], w0[2], HI),
-                                  __builtin_amdgcn_perm(w1[1], w1[0], LO), __builtin_amdgcn_perm(w1[3], w1[2], LO));
-    uint4 *__restrict__ dst = tab + ((size_t)row * (W + 1) * NF + f) * 4 + q;
-    dst[(size_t)e * NF * 4] = ent0;  // entry e: pixels e-1, e
-    if (e + 1 <= W) {
-        const uint4 ent1 = make_uint4(ent0.z, ent0.w, __builtin_amdgcn_perm(w1[1], w1[0], HI),
-                                      __builtin_amdgcn_perm(w1[3], w1[2], HI));
-        dst[(size_t)(e + 1) * NF * 4] = ent1;  // entry e+1: pixels e, e+1
-    }
-}
-
 inline size_t pair_frame_bytes(int V, int H, int W) { return (size_t)V * H * (W + 1) * 64; }
 
 // Launch the pair-table layout for nb frames (a multiple of NF).
@@ -210,15 +160,7 @@ inline void launch_pairs(const _Float16 *hm, int nb, int V, int J, int H, int W,
     // a 15 KB row per block leaves its load / store phases exposed; it also
     // serves odd widths and fp16 pointers that are not 4-B aligned)
     const bool aligned = ((unsigned long long)hm & 3ull) == 0;  // 4-B row loads (a C-ABI caller may pass any fp16 pointer)
-#ifndef FVP_AB_PAIRS
-#define FVP_AB_PAIRS 0
-#endif
-    if (FVP_AB_PAIRS == 1 && aligned && W % 2 == 0) {
-        const int EP = (W + 2) / 2;  // entry pairs per row: entries 0 .. W
-        const long long total = (long long)nb / NF * V * H * NF * 4 * EP;
-        hipLaunchKernelGGL((pairs_vec_kernel<NF>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, hm, tab, J,
-                           H, W, V, EP, total);
-    } else if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024) {
+    if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024) {
         hipLaunchKernelGGL((pairs_rows_kernel<NF>), dim3((unsigned)((long long)nb / NF * V * H)), dim3(256), lds, s, hm,
                            tab, J, H, W, V);
     } else {

@@ -15,19 +15,6 @@
 // over x, xz a register + LDS max over y, xy a wave reduction over z.
 #include "fvp_layout.h"
 
-#ifndef FVP_AB_GRID_AUX
-#define FVP_AB_GRID_AUX 0
-#endif
-#ifndef FVP_AB_PERSON_PIPE
-#define FVP_AB_PERSON_PIPE 0
-#endif
-#ifndef FVP_AB_PERSON_MINB
-#define FVP_AB_PERSON_MINB 1
-#endif
-#ifndef FVP_AB_XZ_LATE
-#define FVP_AB_XZ_LATE 0
-#endif
-
 namespace fvp {
 
 struct Window {
@@ -132,14 +119,16 @@ __global__ __launch_bounds__(256) void max_planes_generic_kernel(const float *__
 }
 
 // Channels-last per-person kernel (batched over frames, optional fused planes).
-// Block = (proposal p, group of YG y-rows); threads = 64 z-lanes x LPV joint
-// quads.  The block walks x = 0..S-1 and, for each x, its YG rows:
-//   xy[x][y] = max_z   -> wave shuffles over z + one atomicMax per wave into the
-//                         pre-zeroed plane (no barriers in the x walk)
-//   yz[y][z] = max_x   -> registers (the block owns its y rows), stored at the end
-//   xz[x][z] = max_y   -> max over the block's rows, then one atomicMax per
-//                         (x, z, joint) into the pre-zeroed plane (values are
-//                         clamped to [0,1] or NaN, so unsigned order == float order)
+// Block = (proposal p, one y-row, x part, 64-deep z chunk); threads = 64 z-lanes
+// x LPV joint quads.  The block walks the x-planes of its row:
+//   xy[x][y] = max_z   -> per-wave z maxima in VALU (slot_umax), then either kept
+//                         in LDS and stored once per (x, joint) at the block's end
+//                         (xy_direct: the block owns the row's xy cells) or one
+//                         atomicMax per wave into the pre-zeroed plane
+//   yz[y][z] = max_x   -> registers (the block owns its row), stored at the end
+//                         (atomics into a pre-zeroed plane when x is split)
+//   xz[x][z] = max_y   -> one atomicMax per (x, z, joint) into the pre-zeroed plane
+// (values are clamped to [0,1] or NaN, so unsigned order == float order.)
 // Outside-window voxels are 0 exactly as in the reference cube.
 // Sampling coordinates of the fine grid: the packed per-sequence grid
 // (OTF = false) or projected on the fly from the camera records with the fp32
@@ -155,45 +144,40 @@ struct PersonCoords {
 // plane reductions / stores (the sums folded into `offset`), 2 = zeros instead
 // of the tap loads, 3 = every tap offset off-image (range-checked loads, no
 // memory access), 4 = grid loads and tap setup only (no tap loads, no planes),
-// 5 / 6 = no xz / xy plane atomics.
-template <int LPV, int YG, bool OTF, bool CASC, int MODE = 0, int VC = 0>
-__global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel(const float *__restrict__ cl,
+// 5 / 6 = no xz / xy plane atomics or stores.
+template <int LPV, bool OTF, bool CASC, int MODE = 0>
+__global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
                                                              const float *__restrict__ props,
                                                              const int32_t *__restrict__ frame_of, fvp_person_spec s,
                                                              float *__restrict__ cubes, float *__restrict__ planes,
                                                              float *__restrict__ offset, int P, int V, int J, int Jst,
                                                              int H, int W, int xmap, int xsplit, int zsplit,
-                                                             unsigned pix_bytes) {
+                                                             unsigned pix_bytes, int xy_direct) {
     constexpr int CPG = 2 * LPV;  // cameras per packed-grid load (2 per lane)
-    // PIPE: the two-stage camera pipeline, for launches whose camera count VC is a
-    // compile-time constant (a uniform branch around the next camera's loads would
-    // make the wait at the join cover them too)
-    constexpr bool PIPE = VC > 0 && !OTF && !CASC;
     __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
-    // xy maxima deferred to the block's end (DXY): [wave][x][joint slot] per-wave z maxima
-    constexpr bool DXY = LPV <= 4 && YG == 1;
+    // xy_direct: [wave][x][joint slot] per-wave z maxima, stored at the block's end
+    constexpr bool DXY = LPV <= 4;
     __shared__ unsigned lxy[DXY ? LPV * 64 * 4 * LPV : 1];
     const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
-    const int ngroups = (SY + YG - 1) / YG;
-    // XCD-aware: each XCD runs whole proposals, so the row groups of one
-    // proposal (walking x together) share that XCD's L2 footprint (L2 hit 35 %
-    // with round-robin placement)
+    // XCD-aware: each XCD runs whole proposals, so the rows of one proposal
+    // (walking x together) share that XCD's L2 footprint (L2 hit 35 % with
+    // round-robin placement)
     const int L = xmap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    // block -> (proposal, row group, x part): a proposal's blocks stay contiguous
-    const int parts = xsplit * zsplit;  // x parts x 64-deep z chunks per row group
-    const int p = L / (ngroups * parts);
-    const int rem = L - p * ngroups * parts;
-    const int yg0 = (rem / parts) * YG;
-    const int part = rem - (rem / parts) * parts;
+    // block -> (proposal, row, x part, z chunk): a proposal's blocks stay contiguous
+    const int parts = xsplit * zsplit;
+    const int p = L / (SY * parts);
+    const int rem = L - p * SY * parts;
+    const int y = rem / parts;
+    const int part = rem - y * parts;
     const int xpart = part % xsplit, zc = part / xsplit;
     const Window w = person_window(props + (size_t)p * 7, s);
-    if (offset && yg0 == 0 && part == 0 && threadIdx.x < 3) {
+    if (offset && y == 0 && part == 0 && threadIdx.x < 3) {
         const int a = threadIdx.x;
         offset[(size_t)p * 3 + a] =
             ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
     }
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
     const int zl = zc * 64 + (int)threadIdx.x / LPV, q = threadIdx.x % LPV;
     const int b = frame_of ? frame_of[p] : 0;
     const unsigned HW = (unsigned)(H * W);
@@ -224,375 +208,225 @@ __global__ __launch_bounds__(64 * LPV, FVP_AB_PERSON_MINB) void person_cl_kernel
     const bool zok = zl < SZ;
     const int gz = w.ctl[2] + zl;
     const bool zin = zok && gz >= w.start[2] && gz < w.end[2];
+    const int gy = w.ctl[1] + y;
+    const bool row_in = gy >= w.start[1] && gy < w.end[1];  // block-uniform
 
     // plane maxima on the float bits: every voxel value is +0 .. 1 or NaN (the
     // mean is clamped and +0.0f turns a -0 into +0), so unsigned order is float
     // order with NaN on top (torch.max: NaN wins) -- one v_max_u32 per step
     // instead of a NaN-aware float max (compares + select); +0 is neutral
-    unsigned yzacc[YG][4];
-#pragma unroll
-    for (int r = 0; r < YG; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) yzacc[r][k] = 0u;
+    unsigned yzacc[4] = {0u, 0u, 0u, 0u};
 
-    // block-uniform: does any of this block's rows meet the window in y?
-    bool rows_in = false;
-#pragma unroll
-    for (int r = 0; r < YG; ++r) {
-        const int gy = w.ctl[1] + yg0 + r;
-        rows_in |= yg0 + r < SY && gy >= w.start[1] && gy < w.end[1];
-    }
-    // the block owns its row's xy cells when nothing else writes them (one x part,
-    // one z chunk): the per-wave z maxima go to LDS and out as plain stores at the
-    // end -- an atomic per wave and x step costs ~0.6 us per proposal (probe mode 6)
-    // because non-returning atomics count in vmcnt and the next taps wait on them
-    const bool defer = DXY && planes && xsplit == 1 && zsplit == 1 && SX <= 64;
-    const int wave = (int)threadIdx.x >> 6;
+    // xy_direct (host: one x part, one z chunk, S <= 64, LPV <= 4 for every joint
+    // slice): the block owns its row's xy cells, so the per-wave z maxima go to LDS
+    // and leave as plain stores at the block's end -- no atomics (one per wave and x
+    // step cost ~0.6 us per proposal, probe mode 6: non-returning atomics count in
+    // vmcnt and the next taps wait on them)
+    const bool defer = DXY && planes && xy_direct;
     if (defer) {
         for (int e = lane; e < 64 * 4 * LPV; e += 64) lxy[wave * 64 * 4 * LPV + e] = 0u;
     }
     int x_lo = xpart * SX / xsplit, x_hi = (xpart + 1) * SX / xsplit;
     if (!cubes) {
         // planes only: the x-planes outside the window are all 0, which changes none
-        // of the maxima (pre-zeroed xy / xz planes, yzacc >= 0) -- walk the window only
-        if (w.skip || !rows_in) {
+        // of the maxima (pre-zeroed xy / xz planes, yzacc >= 0)
+        // -- walk the window only
+        if (w.skip || !row_in) {
             x_hi = x_lo;
         } else {
             x_lo = max(x_lo, w.start[0] - w.ctl[0]);
             x_hi = min(x_hi, w.end[0] - w.ctl[0]);
         }
     }
-#ifndef FVP_AB_PERSON_PF
-#define FVP_AB_PERSON_PF 0
-#endif
-    // packed-grid coordinates of the x-plane PF ahead, loaded after the current
-    // plane's taps are consumed (one row per block, V <= 8: one grid load per voxel)
-    constexpr int PF = (OTF || YG != 1) ? 0 : FVP_AB_PERSON_PF;
-    const bool pf = PF > 0 && V <= CPG;
-    const int gy0 = w.ctl[1] + yg0;
-    const bool row_ok = zin && yg0 < SY && gy0 >= w.start[1] && gy0 < w.end[1];
-    auto grid_at = [&](int xx) -> u32x4 {
-        const bool ok = row_ok && xx < x_hi;
-        const long long gn = ok ? ((long long)(w.ctl[0] + xx) * s.fine[1] + gy0) * s.fine[2] + gz : 0;
-        return __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + 2 * q) * 8), 0, 0);
-    };
-    u32x4 gring[PF > 0 ? PF : 1];
-    if constexpr (PF > 0) {
-        if (pf) {
-#pragma unroll
-            for (int d = 0; d < PF; ++d) gring[d] = grid_at(x_lo + d);
-        }
-    }
-    // LATE: the xz atomics of x step i are issued during step i + 1, after its second
-    // camera's tap loads (vmcnt counts non-returning atomics and waits in issue order:
-    // issued at the end of a step, the next step's first wait would cover their whole
-    // L2 round trip; issued after camera 1's loads, only camera 2's wait can)
-    constexpr bool LATE = FVP_AB_XZ_LATE != 0;
-    unsigned xz_pend[4] = {0u, 0u, 0u, 0u};
-    int xz_px = -1;  // the pending step's x (block-uniform), -1: none
-    auto flush_xz = [&]() {
-        if (xz_px >= 0) {
-            if (zok) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (MODE != 5 && 4 * q + k < J && xz_pend[k] != 0u)
-                        atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + xz_px) * SZ + zl,
-                                  xz_pend[k]);
-            }
-            xz_px = -1;
-        }
-    };
     for (int x = x_lo; x < x_hi; ++x) {
         const int gx = w.ctl[0] + x;
         const bool xin = !w.skip && gx >= w.start[0] && gx < w.end[0];
-        if (!cubes && !(xin && rows_in)) continue;  // (not taken: the walk is the window)
-        u32x4 gpre = gring[0];
-        if constexpr (PF > 0) {
-            if (pf) {
-#pragma unroll
-                for (int d = 0; d + 1 < PF; ++d) gring[d] = gring[d + 1];
+        const bool valid = xin && zin && row_in;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        float blk[4] = {0.f, 0.f, 0.f, 0.f};  // CASC: completed 16-camera blocks (fvp_device.h)
+        if (__builtin_amdgcn_ballot_w64(valid)) {
+            const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
+            float wxc = 0.f, wyc = 0.f, wzc = 0.f;  // OTF: fine voxel centre (compute_grid at fine resolution)
+            if constexpr (OTF) {
+                wxc = axis_coord(pc.fine.start[0], pc.fine.end[0], s.fine[0], valid ? gx : 0, pc.fine.center[0]);
+                wyc = axis_coord(pc.fine.start[1], pc.fine.end[1], s.fine[1], valid ? gy : 0, pc.fine.center[1]);
+                wzc = axis_coord(pc.fine.start[2], pc.fine.end[2], s.fine[2], valid ? gz : 0, pc.fine.center[2]);
             }
-        }
-        unsigned xzacc[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int r = 0; r < YG; ++r) {
-            const int y = yg0 + r;
-            const int gy = w.ctl[1] + y;
-            const bool valid = xin && zin && y < SY && gy >= w.start[1] && gy < w.end[1];
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
-            float blk[4] = {0.f, 0.f, 0.f, 0.f};  // CASC: completed 16-camera blocks (fvp_device.h)
-            if (__builtin_amdgcn_ballot_w64(valid)) {
-                const long long gn = valid ? ((long long)gx * s.fine[1] + gy) * s.fine[2] + gz : 0;
-                float wxc = 0.f, wyc = 0.f, wzc = 0.f;  // OTF: fine voxel centre (compute_grid at fine resolution)
+            for (int v0 = 0; v0 < V; v0 += CPG) {
+                float g[4];
                 if constexpr (OTF) {
-                    wxc = axis_coord(pc.fine.start[0], pc.fine.end[0], s.fine[0], valid ? gx : 0, pc.fine.center[0]);
-                    wyc = axis_coord(pc.fine.start[1], pc.fine.end[1], s.fine[1], valid ? gy : 0, pc.fine.center[1]);
-                    wzc = axis_coord(pc.fine.start[2], pc.fine.end[2], s.fine[2], valid ? gz : 0, pc.fine.center[2]);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
+                        float px, py;
+                        project_point(c, wxc, wyc, wzc, px, py);
+                        pixel_to_sample(px, py, rt, pc.im, g[2 * h], g[2 * h + 1]);
+                    }
+                } else {
+                    // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
+                    const u32x4 graw =
+                        __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
                 }
-                for (int v0 = 0; v0 < V; v0 += CPG) {
-                    float g[4];
-                    if constexpr (OTF) {
 #pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const Cam c = load_cam(lcam + min(v0 + 2 * q + h, GV - 1) * FVP_CAM_STRIDE);
-                            float px, py;
-                            project_point(c, wxc, wyc, wzc, px, py);
-                            pixel_to_sample(px, py, rt, pc.im, g[2 * h], g[2 * h + 1]);
+                for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
+                const Taps4<false> t0 = setup_taps<false>(g[0], g[1], sxs, sys, W, H, pix_bytes);
+                const Taps4<false> t1 = setup_taps<false>(g[2], g[3], sxs, sys, W, H, pix_bytes);
+                static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int S = k >> 1;
+                    const int v = v0 + k;
+                    if (v >= V) return;
+                    if constexpr (CASC) {
+                        if ((v & 15) == 0 && v > 0) {
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                blk[m] = blk[m] + acc[m];
+                                acc[m] = 0.0f;
+                            }
                         }
-                    } else {
-                        // slots v0+2q, v0+2q+1 of fine voxel gn (packed grid, fvp_pack_grid)
-                        const u32x4 graw = (PF > 0 && pf) ? gpre :
-                            __builtin_amdgcn_raw_buffer_load_b128(grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, FVP_AB_GRID_AUX);
+                    }
+                    const Taps4<false> &src = (k & 1) ? t1 : t0;
+                    unsigned o[4];
+                    unsigned all = kOOB;
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
+                    for (int m = 0; m < 4; ++m) {
+                        o[m] = group_bcast<LPV, S>(src.o[m]);
+                        all &= o[m];
+                    }
+                    if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
+                    float wt[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) wt[m] = group_bcast<LPV, S>(src.w[m]);
+                    if constexpr (MODE == 4) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) acc[m] = acc[m] + wt[m] + __builtin_bit_cast(float, o[m]);
+                        return;
+                    }
+                    if constexpr (MODE == 3) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) o[m] = kOOB;
+                    }
+                    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_cl + (size_t)v * img, img);
+                    u32x4 ta = {0u, 0u, 0u, 0u}, tb = ta, tc = ta, td = ta;
+                    if constexpr (MODE != 2) {
+                        ta = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
+                        tb = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
+                        tc = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
+                        td = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
                     }
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
-                    const Taps4<false> t0 = setup_taps<false>(g[0], g[1], sxs, sys, W, H, pix_bytes);
-                    const Taps4<false> t1 = setup_taps<false>(g[2], g[3], sxs, sys, W, H, pix_bytes);
-                    if constexpr (PIPE) {
-                        // two-stage camera pipeline: camera k+1's four tap loads are issued
-                        // before camera k's are consumed (8 loads in flight per wave instead
-                        // of 4); no per-camera wave skip (an all-off-image camera's loads are
-                        // range-checked no-ops)
-                        u32x4 tb[2][4];
-                        float wb[2][4];
-                        auto issue = [&](auto kc2) {
-                            constexpr int k = decltype(kc2)::value;
-                            constexpr int S = k >> 1;
-                            const Taps4<false> &src = (k & 1) ? t1 : t0;
-                            unsigned o[4];
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) {
-                                o[m] = group_bcast<LPV, S>(src.o[m]);
-                                wb[k & 1][m] = group_bcast<LPV, S>(src.w[m]);
-                                if constexpr (MODE == 3) o[m] = kOOB;
-                            }
-                            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_cl + (size_t)(v0 + k) * img, img);
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) {
-                                if constexpr (MODE == 4) tb[k & 1][m] = u32x4{o[m], 0u, 0u, 0u};
-                                else if constexpr (MODE == 2) tb[k & 1][m] = u32x4{0u, 0u, 0u, 0u};
-                                else tb[k & 1][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[m] + qo, 0, 0);
-                            }
-                        };
-                        issue(std::integral_constant<int, 0>{});
-                        static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
-                            constexpr int k = decltype(kc)::value;
-                            if constexpr (k >= VC) return;
-                            if constexpr (k + 1 < VC) issue(std::integral_constant<int, k + 1>{});
-                            const u32x4 *t = tb[k & 1];
-                            const float *wt = wb[k & 1];
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) {
-                                if constexpr (MODE == 4) {
-                                    acc[m] = acc[m] + wt[m] + __builtin_bit_cast(float, (unsigned)t[m][0]);
-                                    continue;
-                                }
-                                const float fa = __builtin_bit_cast(float, (unsigned)t[0][m]);
-                                const float fb = __builtin_bit_cast(float, (unsigned)t[1][m]);
-                                const float fc = __builtin_bit_cast(float, (unsigned)t[2][m]);
-                                const float fd = __builtin_bit_cast(float, (unsigned)t[3][m]);
-                                acc[m] = acc[m] + __builtin_fmaf(fd, wt[3], __builtin_fmaf(fc, wt[2],
-                                                                 __builtin_fmaf(fb, wt[1], fa * wt[0])));
-                            }
-                        });
-                        continue;
+                    for (int m = 0; m < 4; ++m) {
+                        const float fa = __builtin_bit_cast(float, (unsigned)ta[m]);
+                        const float fb = __builtin_bit_cast(float, (unsigned)tb[m]);
+                        const float fc = __builtin_bit_cast(float, (unsigned)tc[m]);
+                        const float fd = __builtin_bit_cast(float, (unsigned)td[m]);
+                        acc[m] = acc[m] + __builtin_fmaf(fd, wt[3], __builtin_fmaf(fc, wt[2],
+                                                                                  __builtin_fmaf(fb, wt[1], fa * wt[0])));
                     }
-                    static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
-                        constexpr int k = decltype(kc)::value;
-                        constexpr int S = k >> 1;
-                        const int v = v0 + k;
-                        if (v >= V) return;
-                        if constexpr (CASC) {
-                            if ((v & 15) == 0 && v > 0) {
-#pragma unroll
-                                for (int m = 0; m < 4; ++m) {
-                                    blk[m] = blk[m] + acc[m];
-                                    acc[m] = 0.0f;
-                                }
-                            }
-                        }
-                        const Taps4<false> &src = (k & 1) ? t1 : t0;
-                        unsigned o[4];
-                        unsigned all = kOOB;
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            o[m] = group_bcast<LPV, S>(src.o[m]);
-                            all &= o[m];
-                        }
-                        if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
-                        float wt[4];
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) wt[m] = group_bcast<LPV, S>(src.w[m]);
-                        if constexpr (MODE == 4) {
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) acc[m] = acc[m] + wt[m] + __builtin_bit_cast(float, o[m]);
-                            return;
-                        }
-                        if constexpr (MODE == 3) {
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) o[m] = kOOB;
-                        }
-                        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_cl + (size_t)v * img, img);
-                        u32x4 ta = {0u, 0u, 0u, 0u}, tb = ta, tc = ta, td = ta;
-                        if constexpr (MODE != 2) {
-                            ta = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
-                            tb = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
-                            tc = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
-                            td = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
-                        }
-                        if constexpr (LATE && k == 1) {
-                            if (v0 == 0) flush_xz();
-                        }
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            const float fa = __builtin_bit_cast(float, (unsigned)ta[m]);
-                            const float fb = __builtin_bit_cast(float, (unsigned)tb[m]);
-                            const float fc = __builtin_bit_cast(float, (unsigned)tc[m]);
-                            const float fd = __builtin_bit_cast(float, (unsigned)td[m]);
-                            acc[m] = acc[m] + __builtin_fmaf(fd, wt[3], __builtin_fmaf(fc, wt[2],
-                                                                                      __builtin_fmaf(fb, wt[1], fa * wt[0])));
-                        }
-                    });
-                }
-            }
-            if constexpr (PF > 0) {  // the x-plane PF ahead, issued after this plane's taps were consumed
-                if (pf) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    gring[PF - 1] = grid_at(x + PF);
-                }
-            }
-            // the sum's final levels (fvp_device.h): remainder + blocks, or + 0 (a -0 sum becomes +0)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) acc[m] = acc[m] + (CASC ? blk[m] : 0.0f);
-            float o[4];
-            unsigned ou[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                // clamp(0,1) of the mean; +0.0f turns a -0 into +0 (unsigned max order below)
-                o[k] = valid ? clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f : 0.0f;
-                ou[k] = (zok && y < SY) ? __builtin_bit_cast(unsigned, o[k]) : 0u;  // beyond the cube: neutral
-            }
-            if constexpr (MODE == 1 || MODE == 4) {  // probe: keep the sums live, no planes
-                if (offset && zok && y < SY && (acc[0] + acc[1] + acc[2] + acc[3]) == -1.0f)
-                    offset[(size_t)p * 3] = o[0];
-                continue;
-            }
-            if (cubes && zok && y < SY) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (4 * q + k < J) cubes[((size_t)p * Jst + 4 * q + k) * S3 + ((size_t)x * SY + y) * SZ + zl] = o[k];
-            }
-            if (planes) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    yzacc[r][k] = max(yzacc[r][k], ou[k]);
-                    xzacc[k] = max(xzacc[k], ou[k]);
-                }
-                // this wave's z-range maxima (all lanes: their slot's), four independent
-                // VALU chains; then lane L < 4 LPV sends joint 4 (L % LPV) + L / LPV into the
-                // pre-zeroed xy plane with one atomic instruction (+0 cannot raise it)
-                unsigned zm[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) zm[k] = slot_umax<LPV>(ou[k]);
-                const int kk = lane / LPV;  // q == lane % LPV
-                const unsigned mv = kk == 0 ? zm[0] : kk == 1 ? zm[1] : kk == 2 ? zm[2] : zm[3];
-                if (defer) {
-                    if (lane < 4 * LPV) lxy[(wave * 64 + x) * (4 * LPV) + 4 * q + kk] = mv;
-                } else if (MODE != 6 && lane < 4 * LPV && 4 * q + kk < J && y < SY && mv != 0u) {
-                    atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + kk) * SX + x) * SY + y, mv);
-                }
+                });
             }
         }
-        if (planes && LATE) {
-            flush_xz();  // (not yet issued: this step's first camera was skipped)
+        // the sum's final levels (fvp_device.h): remainder + blocks, or + 0 (a -0 sum becomes +0)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) xz_pend[k] = xzacc[k];
-            xz_px = x;
-        } else if (planes) {
+        for (int m = 0; m < 4; ++m) acc[m] = acc[m] + (CASC ? blk[m] : 0.0f);
+        float o[4];
+        unsigned ou[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // clamp(0,1) of the mean; +0.0f turns a -0 into +0 (unsigned max order below)
+            o[k] = valid ? clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f : 0.0f;
+            ou[k] = zok ? __builtin_bit_cast(unsigned, o[k]) : 0u;  // beyond the cube: neutral
+        }
+        if constexpr (MODE == 1 || MODE == 4) {  // probe: keep the sums live, no planes
+            if (offset && zok && (acc[0] + acc[1] + acc[2] + acc[3]) == -1.0f) offset[(size_t)p * 3] = o[0];
+            continue;
+        }
+        if (cubes && zok) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (4 * q + k < J) cubes[((size_t)p * Jst + 4 * q + k) * S3 + ((size_t)x * SY + y) * SZ + zl] = o[k];
+        }
+        if (planes) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) yzacc[k] = max(yzacc[k], ou[k]);
+            // this wave's z-range maxima (all lanes: their slot's), four independent
+            // VALU chains; lane L < 4 LPV then holds joint 4 (L % LPV) + L / LPV
+            unsigned zm[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) zm[k] = slot_umax<LPV>(ou[k]);
+            const int kk = lane / LPV;  // q == lane % LPV
+            const unsigned mv = kk == 0 ? zm[0] : kk == 1 ? zm[1] : kk == 2 ? zm[2] : zm[3];
+            if (defer) {
+                if (lane < 4 * LPV) lxy[(wave * 64 + x) * (4 * LPV) + 4 * q + kk] = mv;
+            } else if (MODE != 6 && lane < 4 * LPV && 4 * q + kk < J && mv != 0u) {
+                // into the pre-zeroed plane (+0 cannot raise it)
+                atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)(4 * q + kk) * SX + x) * SY + y, mv);
+            }
             if (zok) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     // +0 cannot raise the pre-zeroed plane: skip those atomics (most of the 64^3 cube)
-                    const unsigned u = xzacc[k];
+                    const unsigned u = ou[k];
                     if (MODE != 5 && 4 * q + k < J && u != 0u)
                         atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl, u);
                 }
             }
         }
     }
-    flush_xz();
     if (planes && zok) {
 #pragma unroll
-        for (int r = 0; r < YG; ++r) {
-            const int y = yg0 + r;
-            if (y < SY) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (4 * q + k >= J) continue;
-                    float *dst = yz_pl + ((size_t)(4 * q + k) * SY + y) * SZ + zl;
-                    const unsigned u = yzacc[r][k];
-                    if (xsplit == 1) *dst = __builtin_bit_cast(float, u);
-                    else if (u != 0u) atomicMax(reinterpret_cast<unsigned *>(dst), u);  // pre-zeroed plane
-                }
-            }
+        for (int k = 0; k < 4; ++k) {
+            if (4 * q + k >= J) continue;
+            float *dst = yz_pl + ((size_t)(4 * q + k) * SY + y) * SZ + zl;
+            const unsigned u = yzacc[k];
+            if (xsplit == 1) *dst = __builtin_bit_cast(float, u);
+            else if (u != 0u) atomicMax(reinterpret_cast<unsigned *>(dst), u);  // pre-zeroed plane
         }
     }
     if (defer) {  // xy[j][x][y] = max over the block's waves (z ranges); the plane is pre-zeroed
         __syncthreads();
+        // (only the walked x range and values above +0: a row's cells are SY floats
+        // apart, and storing the zeros as well -- instead of the memset -- measured
+        // slower: 5.45 -> 5.73 us per proposal)
         const int n = (x_hi - x_lo) * J;
         for (int e = threadIdx.x; e < n; e += 64 * LPV) {
             const int xi = x_lo + e / J, j = e - (e / J) * J;
             unsigned m = 0u;
 #pragma unroll
             for (int wv = 0; wv < LPV; ++wv) m = max(m, lxy[(wv * 64 + xi) * (4 * LPV) + j]);
-            if (MODE != 6 && m != 0u) xy_pl[((size_t)j * SX + xi) * SY + yg0] = __builtin_bit_cast(float, m);
+            if (MODE != 6 && m != 0u) xy_pl[((size_t)j * SX + xi) * SY + y] = __builtin_bit_cast(float, m);
         }
     }
 }
 
-#ifndef FVP_AB_XSPLIT_BIG
-#define FVP_AB_XSPLIT_BIG 1
-#endif
+// Small launches (per-frame calls) split each row's x walk over 2-4 blocks.
 static int person_xsplit(int P, int SY) {
     const long long rows = (long long)P * SY;
-    return rows >= 4096 ? FVP_AB_XSPLIT_BIG : rows >= 1024 ? 2 : 4;
+    return rows >= 4096 ? 1 : rows >= 1024 ? 2 : 4;
 }
 
 template <int LPV, bool OTF, bool CASC>
 static void launch_person_cl(const float *cl, const float *fgrid, const PersonCoords &pc, const float *props,
                              const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
                              float *offset, int P, int V, int J, int Jst, int H, int W, unsigned pix_bytes,
-                             hipStream_t st) {
+                             int xy_direct, hipStream_t st) {
     const int SY = s.bins[1];
-    // one y-row per block (the kernel also takes YG rows): with the planes-only
-    // fast path for x-planes outside the window, rows are the finer and better
-    // balanced unit -- measured (C3, 320 proposals): 1 row 6.24, 2 rows 6.85,
-    // 4 rows 7.4, 8 rows 8.8 us per proposal (4 rows were best, 10.7 us, before
-    // the fast path).  XCD-aware placement keeps a proposal's rows on one XCD.
-    // Small launches (per-frame calls) split each row's x walk over 2-4 blocks
-    // (the yz maxima then go through atomics into a pre-zeroed plane).
-    // Cubes deeper than 64 run as 64-deep z chunks, one block each (the xy and xz
-    // maxima already combine across blocks through atomics; yz is per (y, z)).
-#ifndef FVP_AB_PERSON_YG
-#define FVP_AB_PERSON_YG 1
-#endif
-    constexpr int YG = FVP_AB_PERSON_YG;
+    // one y-row per block: with the planes-only fast path for x-planes outside the
+    // window, rows are the finer and better balanced unit -- measured (C3, 320
+    // proposals): 1 row 6.24, 2 rows 6.85, 4 rows 7.4, 8 rows 8.8 us per proposal
+    // (round 2); two rows per block again in round 4 (sequential: 6.04 vs 5.86; two
+    // halves combining xz in LDS: 5.98 vs 5.45).  XCD-aware placement keeps a
+    // proposal's rows on one XCD.  Small launches (per-frame calls) split each row's
+    // x walk over 2-4 blocks (the yz maxima then go through atomics into a
+    // pre-zeroed plane).  Cubes deeper than 64 run as 64-deep z chunks, one block
+    // each (the xy and xz maxima combine across blocks through atomics; yz is per
+    // (y, z)).
     const int xmap = 1, xsplit = person_xsplit(P, SY), zsplit = (s.bins[2] + 63) / 64;
-    if constexpr (!OTF && !CASC && 2 * LPV >= 5) {
-        if (FVP_AB_PERSON_PIPE && V == 5) {
-            hipLaunchKernelGGL((person_cl_kernel<LPV, YG, OTF, CASC, 0, 5>),
-                               dim3((unsigned)((long long)P * ((SY + YG - 1) / YG) * xsplit * zsplit)), dim3(64 * LPV),
-                               0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H, W,
-                               xmap, xsplit, zsplit, pix_bytes);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((person_cl_kernel<LPV, YG, OTF, CASC>),
-                       dim3((unsigned)((long long)P * ((SY + YG - 1) / YG) * xsplit * zsplit)),
+    hipLaunchKernelGGL((person_cl_kernel<LPV, OTF, CASC>), dim3((unsigned)((long long)P * SY * xsplit * zsplit)),
                        dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H,
-                       W, xmap, xsplit, zsplit, pix_bytes);
+                       W, xmap, xsplit, zsplit, pix_bytes, xy_direct);
 }
 
 }  // namespace fvp
@@ -651,8 +485,13 @@ static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J,
         if (!workspace || workspace_bytes < need) return FVP_ERR_WORKSPACE;
     }
     hipStream_t st = (hipStream_t)stream;
-    if (planes) {  // xy, xz (and yz when x is split) are reduced with atomicMax over non-negative floats: from +0
-        const size_t n = (person_xsplit(P, SY) > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
+    // xy maxima stored by their row's block without atomics (person_cl_kernel
+    // xy_direct): one x part, one z chunk, S <= 64 and every joint slice at <= 4
+    // lanes per voxel
+    const int xsplit = person_xsplit(P, SY);
+    const int xy_direct = (planes && xsplit == 1 && SZ <= 64 && SX <= 64 && J <= 16) ? 1 : 0;
+    if (planes) {  // xy, xz (and yz when x is split) hold maxima over non-negative floats: from +0
+        const size_t n = (xsplit > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
         const hipError_t e = hipMemsetAsync(planes, 0, n * 4, st);
         if (e != hipSuccess) return (int)e;
     }
@@ -669,16 +508,16 @@ static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J,
     if (!cp) launch_layout<L, float>(heatmaps + j0 * HW, B, V, Jc, J, H, W, reinterpret_cast<float *>(workspace), st); \
     if (pc && V > 16)                                                                                                 \
         launch_person_cl<L, true, true>(cl, nullptr, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J, H,   \
-                                        W, pix_bytes, st);                                                            \
+                                        W, pix_bytes, xy_direct, st);                                                            \
     else if (pc)                                                                                                      \
         launch_person_cl<L, true, false>(cl, nullptr, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J, H,  \
-                                         W, pix_bytes, st);                                                           \
+                                         W, pix_bytes, xy_direct, st);                                                           \
     else if (V > 16)                                                                                                  \
         launch_person_cl<L, false, true>(cl, fine_grid, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J,   \
-                                         H, W, pix_bytes, st);                                                        \
+                                         H, W, pix_bytes, xy_direct, st);                                                        \
     else                                                                                                              \
         launch_person_cl<L, false, false>(cl, fine_grid, c, proposals, frame_of, *spec, cb, pl, offset, P, V, Jc, J,  \
-                                          H, W, pix_bytes, st);                                                       \
+                                          H, W, pix_bytes, xy_direct, st);                                                       \
     break;
         switch (lanes_per_voxel(Jc)) {
             case 1: FVP_PERSON_CASE(1)

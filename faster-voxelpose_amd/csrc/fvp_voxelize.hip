@@ -36,15 +36,6 @@
 
 #include "fvp_layout.h"
 
-#ifndef FVP_AB_VGRID_AUX
-#define FVP_AB_VGRID_AUX 0
-#endif
-#ifndef FVP_AB_VPIPE
-#define FVP_AB_VPIPE 0
-#endif
-#ifndef FVP_AB_VPIPE_MINB
-#define FVP_AB_VPIPE_MINB 8
-#endif
 
 namespace fvp {
 
@@ -115,7 +106,7 @@ __device__ __forceinline__ void store_stage(const float *__restrict__ stage, int
     }
 }
 
-template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, int VC = 0>
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
 __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, const CoordSource &src_,
                                                        const int32_t *__restrict__ grid_index, int frame0,
                                                        float *__restrict__ cube, float *__restrict__ xy, int V, int J,
@@ -123,10 +114,6 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
                                                        int col_blocks, int SP, int band, unsigned pixb,
                                                        bool cube16) {
     static_assert(!PAIR || LPV == 4, "the fp16 pair table has 4 lanes per voxel");
-    // VPIPE: the two-stage camera pipeline, for launches whose camera count VC is a
-    // compile-time constant (no conditional loads: a uniform branch around the next
-    // camera's loads would make the wait at the join cover them too)
-    constexpr bool VPIPE = VC > 0 && !PAIR && NF == 1;
     constexpr int JP = 4 * LPV;
     constexpr int VPP = 256 / LPV;  // voxels per pass
     constexpr int CPG = 2 * LPV;    // cameras per grid load (2 per lane)
@@ -214,7 +201,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
             } else {
                 // slots v0+2q, v0+2q+1 (past the row: the next voxel's or 0)
                 const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(
-                    grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, FVP_AB_VGRID_AUX);
+                    grs, (unsigned)((gn * GV + v0 + 2 * q) * 8), 0, 0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) g[k] = __builtin_bit_cast(float, (unsigned)graw[k]);
             }
@@ -222,54 +209,6 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
             for (int k = 0; k < 4; ++k) g[k] = valid ? g[k] : -2.0f;
             const Taps4<PAIR> t0 = setup_taps<PAIR>(g[0], g[1], sxs, sys, W, H, unit);
             const Taps4<PAIR> t1 = setup_taps<PAIR>(g[2], g[3], sxs, sys, W, H, unit);
-            if constexpr (VPIPE) {
-                // two-stage camera pipeline (fp32 table, one frame per entry): camera
-                // k+1's four tap loads are issued before camera k's are consumed; no
-                // per-camera wave skip (off-image loads are range-checked no-ops)
-                u32x4 tb[2][4];
-                float wb[2][4];
-                auto issue = [&](auto kc2) {
-                    constexpr int k = decltype(kc2)::value;
-                    constexpr int S = k >> 1;
-                    const Taps4<PAIR> &src = (k & 1) ? t1 : t0;
-                    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)(v0 + k) * img, img);
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const unsigned o = group_bcast<LPV, S>(src.o[m]);
-                        wb[k & 1][m] = group_bcast<LPV, S>(src.w[m]);
-                        tb[k & 1][m] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + qo, 0, 0);
-                    }
-                };
-                issue(std::integral_constant<int, 0>{});
-                static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    const int v = v0 + k;
-                    if constexpr (k < VC) {
-                        if constexpr (k + 1 < VC) issue(std::integral_constant<int, k + 1>{});
-                    if constexpr (CASC) {
-                        if ((v & 15) == 0 && v > 0) {
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) {
-                                blk[0][m] = blk[0][m] + acc[0][m];
-                                acc[0][m] = 0.0f;
-                            }
-                        }
-                    }
-                    const u32x4 *t = tb[k & 1];
-                    const float *w = wb[k & 1];
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const float fa = __builtin_bit_cast(float, (unsigned)t[0][m]);
-                        const float fb = __builtin_bit_cast(float, (unsigned)t[1][m]);
-                        const float fc = __builtin_bit_cast(float, (unsigned)t[2][m]);
-                        const float fd = __builtin_bit_cast(float, (unsigned)t[3][m]);
-                        acc[0][m] = acc[0][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
-                                                                __builtin_fmaf(fb, w[1], fa * w[0])));
-                    }
-                    }
-                });
-                continue;
-            }
             static_for(std::make_integer_sequence<int, CPG>{}, [&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = k >> 1;  // lane of the group that set this camera up
@@ -346,41 +285,7 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
         for (int f = 0; f < NF; ++f)
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc[f][m] = acc[f][m] + (CASC ? blk[f][m] : 0.0f);
-#ifndef FVP_AB_MEANDIV
-#define FVP_AB_MEANDIV 0
-#endif
-        if constexpr (FVP_AB_MEANDIV) {
-            // the mean's division by V through div_const when the whole wave's sums
-            // are finite and 0 or at least 2^-100 (normal quotients: exact for an
-            // integer V, tools/div_const_sweep.c); otherwise the IEEE division
-            bool ok = true;
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float a = fabsf(acc[f][m]);
-                    ok &= (a == 0.0f) | ((a >= 0x1p-100f) & (a <= 0x1p100f));
-                }
-            const float rV = 1.0f / fV;
-            if (!__builtin_amdgcn_ballot_w64(!ok)) {  // wave-uniform branch
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) acc[f][m] = div_const(acc[f][m], fV, rV);
-            } else {
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) acc[f][m] = acc[f][m] / fV;
-            }
-            if (valid) {
-#pragma unroll
-                for (int f = 0; f < NF; ++f)
-#pragma unroll
-                    for (int m = 0; m < 4; ++m)
-                        stage[(f * JP + 4 * q + m) * SP + ii] = clampf(acc[f][m], 0.0f, 1.0f);
-            }
-        } else if (valid) {
+        if (valid) {
 #pragma unroll
             for (int f = 0; f < NF; ++f)
 #pragma unroll
@@ -397,15 +302,15 @@ __device__ __forceinline__ void voxelize_body(const void *__restrict__ tab, cons
 // (C2 -4 %, C4 -8 % gather time, measured).
 // Cached-grid gather: <= 64 VGPRs so 8 waves/SIMD fit (32 waves/CU with the
 // 20 KB stage); the on-the-fly variant keeps its registers (no spills).
-template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, int VC = 0>
-__global__ __launch_bounds__(256, NF == 1 ? (VC ? FVP_AB_VPIPE_MINB : 8) : NF == 2 ? 5 : 4) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
+template <int LPV, bool PAIR, bool OTF, bool CASC, int NF>
+__global__ __launch_bounds__(256, NF == 1 ? 8 : NF == 2 ? 5 : 4) void voxelize_kernel(const void *__restrict__ tab, CoordSource src,
                                                           const int32_t *__restrict__ grid_index, int frame0,
                                                           float *__restrict__ cube, float *__restrict__ xy, int V,
                                                           int J, int Jst, int H, int W, int X, int Y, int Z,
                                                           int cols, int col_blocks, int SP, int band, unsigned pixb,
                                                           bool cube16) {
     static_assert(!OTF, "grid kernel");
-    voxelize_body<LPV, PAIR, OTF, CASC, NF, VC>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
+    voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
                                             col_blocks, SP, band, pixb, cube16);
 }
 
@@ -419,166 +324,6 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
     static_assert(OTF, "on-the-fly kernel");
     voxelize_body<LPV, PAIR, OTF, CASC, NF>(tab, src, grid_index, frame0, cube, xy, V, J, Jst, H, W, X, Y, Z, cols,
                                             col_blocks, SP, band, pixb, cube16);
-}
-
-// Camera-outer gather for the on-the-fly fp16 pair table (C5: 31 cameras).
-// voxelize_cams_kernel walks a block's voxels pass by pass with all cameras
-// inside, so the blocks resident on an XCD touch every camera's footprint at
-// once (31 cameras x a 16 x 16-column patch ~ 19 MB of pair entries against a
-// 4 MB L2: each table line is fetched many times).  Here a block's two passes
-// of 64 voxels (128 voxels: 2 columns x 64 z at C5) keep their sums in
-// registers while the cameras advance two at a time; one launch runs one round
-// of blocks that are resident together (`block0`: the round's first block), so
-// the blocks of an XCD start in step and move through the cameras together,
-// and the XCD's working set is a few cameras' footprints.  Per voxel the
-// cameras are summed in the same order (sequentially, with the 16-camera block
-// fold), so the cube is the voxelize_cams_kernel's bit for bit.  Lane q
-// projects camera c0v + (q >> 1) for pass q & 1; the group picks the four
-// setups up by DPP in the order (c, pass 0), (c, pass 1), (c + 1, pass 0),
-// (c + 1, pass 1).
-#ifndef FVP_AB_CO_MINB
-#define FVP_AB_CO_MINB 1
-#endif
-template <bool CASC, int NF>
-__global__ __launch_bounds__(256, FVP_AB_CO_MINB) void voxelize_co_kernel(const void *__restrict__ tab, CoordSource src_, int frame0,
-                                                          float *__restrict__ cube, float *__restrict__ xy, int V,
-                                                          int J, int Jst, int H, int W, int X, int Y, int Z,
-                                                          int cols, int col_blocks, int SP, int band, int block0,
-                                                          int nblocks, bool cube16) {
-    constexpr int LPV = 4, JP = 16, VPP = 64;
-    extern __shared__ __attribute__((aligned(16))) float stage[];  // [NF][JP][SP] + camera records
-    const int L = block0 + xcd_remap(blockIdx.x, gridDim.x);
-    if (L >= nblocks) return;  // (whole block: no barrier is left behind)
-    const int bl = L / col_blocks;
-    const int b = frame0 + bl * NF;
-    const int XY = X * Y;
-    int cb = L - bl * col_blocks;
-    if (band > 0) {  // as voxelize_body
-        const int gpr = Y / cols;
-        const int per_band = band * gpr;
-        const int bi = cb / per_band, r = cb - bi * per_band;
-        const int rows = min(band, X - bi * band);
-        const int gc = r / rows, xr = r - gc * rows;
-        cb = (bi * band + xr) * gpr + gc;
-    }
-    const int c0 = cb * cols;
-    const int ncols = min(cols, XY - c0);
-    const int T = ncols * Z;  // <= 2 * VPP (host)
-    const long long N = (long long)XY * Z;
-    const long long n0 = (long long)c0 * Z;
-    const int q = threadIdx.x % LPV;
-    const int GV = V + (V & 1);
-    const unsigned qo = (unsigned)q * 16u;
-    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
-    const float fV = (float)V;
-    float *lcam = stage + ((NF * JP * SP + 3) & ~3);
-    float rt[6];
-    for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256) lcam[e] = e < V * FVP_CAM_STRIDE ? src_.cams[e] : 0.0f;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) rt[k] = src_.resize_t[k];
-    __syncthreads();
-    constexpr unsigned pix = 64u, unit = pix * NF;
-    const unsigned img = (unsigned)(H * (W + 1)) * unit;
-    const char *__restrict__ frame_tab = (const char *)tab + (size_t)bl * V * img;
-    // the group's voxel in each pass (layer-major slots, as voxelize_body)
-    int ii[2];
-    bool valid[2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const int i = p * VPP + (int)threadIdx.x / LPV;
-        valid[p] = i < T;
-        const int sl = min(i, T - 1);
-        const int zl = sl / ncols, cl = sl - zl * ncols;
-        ii[p] = cl * Z + zl;
-    }
-    // the voxel this lane projects: pass q & 1 (compute_grid, project_whole.py:43-79)
-    const int pp = q & 1;
-    float wx_, wy_, wz_;
-    {
-        const int zl = ii[pp] % Z, cl = ii[pp] / Z;
-        const long long r = c0 + cl;
-        wx_ = axis_coord(src_.gs.start[0], src_.gs.end[0], src_.gs.bins[0], src_.x_off + (int)(r / Y),
-                         src_.gs.center[0]);
-        wy_ = axis_coord(src_.gs.start[1], src_.gs.end[1], Y, (int)(r % Y), src_.gs.center[1]);
-        wz_ = axis_coord(src_.gs.start[2], src_.gs.end[2], Z, zl, src_.gs.center[2]);
-    }
-    const bool pvalid = valid[pp];
-    float acc[2][NF][4], blk[2][NF][4];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) acc[p][f][m] = blk[p][f][m] = 0.0f;
-    for (int cv0 = 0; cv0 < V; cv0 += 2) {
-        float g[2];
-        {
-            const Cam c = load_cam(lcam + min(cv0 + (q >> 1), GV - 1) * FVP_CAM_STRIDE);
-            float px, py;
-            project_point(c, wx_, wy_, wz_, px, py);
-            pixel_to_sample(px, py, rt, src_.im, g[0], g[1]);
-        }
-        g[0] = pvalid ? g[0] : -2.0f;
-        g[1] = pvalid ? g[1] : -2.0f;
-        const Taps4<true> t = setup_taps<true>(g[0], g[1], sxs, sys, W, H, unit);
-        static_for(std::make_integer_sequence<int, 4>{}, [&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            constexpr int P = k & 1;  // pass
-            const int v = cv0 + (k >> 1);
-            if (v >= V) return;
-            if constexpr (CASC) {
-                if ((v & 15) == 0 && v > 0) {  // a block of 16 cameras is complete (fvp_device.h)
-#pragma unroll
-                    for (int f = 0; f < NF; ++f)
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            blk[P][f][m] = blk[P][f][m] + acc[P][f][m];
-                            acc[P][f][m] = 0.0f;
-                        }
-                }
-            }
-            unsigned o[2];
-            unsigned all = kOOB;
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                o[m] = group_bcast<LPV, k>(t.o[m]);
-                all &= o[m];
-            }
-            if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
-            float w[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) w[m] = group_bcast<LPV, k>(t.w[m]);
-            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
-            u32x4 r0[NF], r1[NF];
-#pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                r0[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + f * pix + qo, 0, 0);
-                r1[f] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + f * pix + qo, 0, 0);
-            }
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                static_for(std::make_integer_sequence<int, 4>{}, [&](auto mc) {
-                    constexpr int m = decltype(mc)::value, HI = m & 1;
-                    const unsigned ua = r0[f][m >> 1], ub = r0[f][2 + (m >> 1)];
-                    const unsigned uc = r1[f][m >> 1], ud = r1[f][2 + (m >> 1)];
-                    const float tt = fma_h<HI>(ua, w[0], -0.0f);
-                    acc[P][f][m] = acc[P][f][m] + fma_h<HI>(ud, w[3], fma_h<HI>(uc, w[2], fma_h<HI>(ub, w[1], tt)));
-                });
-        });
-    }
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        if (valid[p]) {
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    stage[(f * JP + 4 * q + m) * SP + ii[p]] =
-                        clampf((acc[p][f][m] + (CASC ? blk[p][f][m] : 0.0f)) / fV, 0.0f, 1.0f);
-        }
-    }
-    __syncthreads();
-    store_stage<NF, JP>(stage, SP, T, Z, N, n0, c0, ncols, XY, J, Jst, b, cube, xy, cube16);
 }
 
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
@@ -706,19 +451,10 @@ static void launch_gather(const void *tab, int f0, int nb, const GatherCfg &c, c
         hipLaunchKernelGGL((voxelize_cams_kernel<LPV, PAIR, true, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
                            pixb, cube16);
-    else {
-        if constexpr (!PAIR && NF == 1 && !CASC && 2 * LPV >= 5) {
-            if (FVP_AB_VPIPE && V == 5) {
-                hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF, 5>), grid, dim3(256), c.lds, s, tab,
-                                   src, grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP,
-                                   c.band, pixb, cube16);
-                return;
-            }
-        }
+    else
         hipLaunchKernelGGL((voxelize_kernel<LPV, PAIR, false, CASC, NF>), grid, dim3(256), c.lds, s, tab, src,
                            grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z, c.cols, c.col_blocks, c.SP, c.band,
                            pixb, cube16);
-    }
 }
 
 // One voxelize call's shapes.  Heatmaps with more than kJointSlice joints run
@@ -732,42 +468,6 @@ struct VoxJob {
     const int32_t *grid_index;
     float *cube, *xy;
 };
-
-// The camera-outer gather (voxelize_co_kernel) for nb frames of one chunk, in
-// rounds of `rounds_x` x the blocks that are resident at once; false when the
-// shape does not suit it (blocks over 128 voxels, LDS), the caller then runs
-// voxelize_cams_kernel.
-template <bool CASC, int NF>
-static bool launch_co(const void *tab, int f0, int nb, const CoordSource &src, const VoxJob &j, int rounds_x,
-                      hipStream_t s) {
-    GatherCfg c;
-    c.cols = max(1, 128 / j.Z);
-    while (c.cols > 1 && j.Y % c.cols != 0) --c.cols;
-    if (c.cols * j.Z > 128) return false;
-    const bool big = (long long)j.X * j.Y >= 4096;
-    c.band = (big && j.Y % c.cols == 0 && j.X > kBandRows) ? kBandRows : 0;
-    c.col_blocks = (j.X * j.Y + c.cols - 1) / c.cols;
-    c.SP = stage_pitch(4, c.cols, j.Z);
-    c.lds = ((size_t)NF * 16 * c.SP + 3) / 4 * 4 * sizeof(float) + (size_t)FVP_GRID_SLOTS(j.V) * FVP_CAM_STRIDE * 4;
-    if (c.lds > 160 * 1024) return false;
-    static int resident = 0;  // blocks resident at once on this device (occupancy x CUs), queried once
-    if (!resident) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, voxelize_co_kernel<CASC, NF>, 256, c.lds) != hipSuccess)
-            return false;
-        resident = max(1, cus * max(1, per));
-    }
-    const int nblocks = nb / NF * c.col_blocks;
-    const int round = resident * max(1, rounds_x);
-    const bool cube16 = ((unsigned long long)j.cube & 15ull) == 0;
-    for (int b0 = 0; b0 < nblocks; b0 += round)
-        hipLaunchKernelGGL((voxelize_co_kernel<CASC, NF>), dim3((unsigned)min(round, nblocks - b0)), dim3(256), c.lds,
-                           s, tab, src, f0, j.cube, j.xy, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y, j.Z, c.cols,
-                           c.col_blocks, c.SP, c.band, b0, nblocks, cube16);
-    return true;
-}
 
 // Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
 // layout pass into the workspace, then the gather, NF frames per table entry.
@@ -788,12 +488,6 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
                              reinterpret_cast<uint4 *>(ws), s);
         } else {
             launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
-        }
-#ifndef FVP_AB_CO
-#define FVP_AB_CO 0
-#endif
-        if constexpr (PAIR && OTF && NF >= 2 && FVP_AB_CO > 0) {
-            if (!j.grid_index && launch_co<CASC, NF>(ws, f0, nb, src, j, FVP_AB_CO, s)) continue;
         }
         launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
                                                j.Z, j.cube, j.xy, 4u * 4u * LPV, s);

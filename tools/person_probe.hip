@@ -16,9 +16,9 @@ template <int MODE>
 static void go(dim3 grid, hipStream_t s, const float *cl, const float *fgrid, const fvp_person_spec &spec,
                const float *props, const int32_t *frame_of, float *planes, float *offset, int P, int V, int J,
                int H, int W, int xsplit, unsigned pix_bytes) {
-    hipLaunchKernelGGL((fvp::person_cl_kernel<4, 1, false, false, MODE>), grid, dim3(256), 0, s, cl, fgrid,
+    hipLaunchKernelGGL((fvp::person_cl_kernel<4, false, false, MODE>), grid, dim3(256), 0, s, cl, fgrid,
                        fvp::PersonCoords{}, props, frame_of, spec, nullptr, planes, offset, P, V, J, J, H, W, 1,
-                       xsplit, 1, pix_bytes);
+                       xsplit, 1, pix_bytes, xsplit == 1 ? 1 : 0);
 }
 
 extern "C" int person_probe(int mode, const float *cl, int cp, const float *fgrid, const fvp_person_spec *spec,

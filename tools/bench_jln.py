@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--proposals", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--workload", default="c3")
+    ap.add_argument("--on-the-fly", action="store_true",
+                    help="project the fine grid in the kernel (fvp_person_planes_cams) instead of the packed grid")
     args = ap.parse_args()
 
     import numpy as np
@@ -36,6 +38,8 @@ def main():
     cams, seq = w.cameras()
     layer = ProjectLayer(w.cfg("cuda:0"))
     layer.verbose = False
+    if args.on_the_fly:
+        layer.on_the_fly = True
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(dev)
     F, P = args.frames, args.proposals
     hm = torch.from_numpy(synthetic.gaussian_heatmaps(w, F)).to(dev)
@@ -95,6 +99,19 @@ def main():
     ms_frame = timeit(per_frame)
     ms = timeit(batched)
 
+    # the same batched op on heatmaps held channels-last, as the fvp backbone writes
+    # them ([B,V,H,W,16]: no layout pass; the bench's other lines take planar input)
+    from fvp.heatmaps import ChannelsLastHeatmaps
+    cp = 16 * ((w.num_joints + 15) // 16)
+    hm_cl = torch.zeros(hm.shape[0], hm.shape[1], hm.shape[3], hm.shape[4], cp, device=dev)
+    hm_cl[..., : w.num_joints] = hm.permute(0, 1, 3, 4, 2)
+    hcl = ChannelsLastHeatmaps(hm_cl.contiguous(), w.num_joints)
+
+    def batched_cl():
+        layer.forward_batch(hcl, meta, allp, mask, cams, rt)
+
+    ms_cl = timeit(batched_cl)
+
     # JLN post-processing on device (soft-argmax + offsets + fusion) on stand-in
     # CNN outputs of the same shape: reads 3*J*S*S*4 B of joint maps per proposal
     from fvp import ops
@@ -133,6 +150,7 @@ def main():
         "config": f"{w.name}: {len(cams[seq])} cams, J={J}, 64^3 person cubes from a 253x253x64 fine grid",
         "cube_bytes_per_proposal": J * 64 ** 3 * 4, "plane_bytes_per_proposal": 3 * J * 64 * 64 * 4,
         "per_frame_calls_us_per_proposal": round(ms_frame * 1e3 / n_prop, 2),
+        "channels_last_input_us_per_proposal": round(ms_cl * 1e3 / n_prop, 2),
         "path": "forward_batch: one fvp_person_planes launch for all frames' proposals (fused planes, no cubes)",
         "cache_build": cache,
         "tap_stream": {"window_voxels_per_proposal": round(float(win.mean()), 1),

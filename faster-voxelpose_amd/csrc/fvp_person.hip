@@ -15,10 +15,6 @@
 // over x, xz a register + LDS max over y, xy a wave reduction over z.
 #include "fvp_layout.h"
 
-#ifndef FVP_AB_XB
-#define FVP_AB_XB 8
-#endif
-
 namespace fvp {
 
 struct Window {
@@ -423,206 +419,10 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     }
 }
 
-// 4 x 4 voxel tiles per wave (J <= 16: LPV = 4).  Block = (proposal, 4 y-rows,
-// x part, 16-deep z tile); wave w holds the 4 rows x z 4w..4w+3 of the tile,
-// lane = joint quad q + 4 row r + 16 z zz.  Against one row of 64 z per block:
-//   xz[x][z] = max_y   -> the 4 rows reduced in-wave (DPP row rotations), then ONE
-//                         atomicMax instruction per wave and x step (lane r sends
-//                         joint 4q + r): 16x fewer than 4 per wave and row -- the
-//                         xz atomics cost ~0.7 us per proposal through vmcnt
-//                         (probe modes 5 / 7: per instruction, not per lane)
-//   xy[x][y] = max_z   -> the wave's 4 z reduced by permlane swaps, then one LDS
-//                         ds_max per wave and x step into [x][r][joint]; the
-//                         block's z tile goes out as atomics once, at its end
-//   yz[y][z] = max_x   -> registers (the block owns its 4 rows x 16 z)
-// and a wave's 16 voxels are a 4 x 4 (y, z) patch of the x plane, whose taps
-// share more 128-B lines than 16 z of one column (CPU count on the C3 fine grid:
-// 0.34 vs 0.54 distinct lines per tap and camera).
-template <bool OTF, bool CASC, int MODE = 0>
-__global__ __launch_bounds__(256) void person_tile_kernel(const float *__restrict__ cl, const float *__restrict__ fgrid,
-                                                          PersonCoords pc, const float *__restrict__ props,
-                                                          const int32_t *__restrict__ frame_of, fvp_person_spec s,
-                                                          float *__restrict__ cubes, float *__restrict__ planes,
-                                                          float *__restrict__ offset, int P, int V, int J, int Jst,
-                                                          int H, int W, int xsplit, unsigned pix_bytes) {
-    constexpr int LPV = 4;
-    __shared__ float lcam[OTF ? 64 * FVP_CAM_STRIDE : 1];  // OTF: camera records (V <= 64)
-    __shared__ unsigned lxy[64 * 4 * 16];                   // [x][row][joint] z-tile maxima (SX <= 64)
-    const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
-    const int RQ = (SY + 3) / 4, ZT = (SZ + 15) / 16;
-    const int L = xcd_remap(blockIdx.x, gridDim.x);  // a proposal's blocks on one XCD
-    const int parts = xsplit * ZT;
-    const int p = L / (RQ * parts);
-    const int rem = L - p * RQ * parts;
-    const int rq = rem / parts;
-    const int part = rem - rq * parts;
-    const int xpart = part % xsplit, zt = part / xsplit;
-    const Window w = person_window(props + (size_t)p * 7, s);
-    if (offset && rq == 0 && part == 0 && threadIdx.x < 3) {
-        const int a = threadIdx.x;
-        offset[(size_t)p * 3 + a] =
-            ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
-    }
-    const int lane = threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
-    const int q = lane & 3, r = (lane >> 2) & 3, zz = lane >> 4;
-    const int y = rq * 4 + r, z = zt * 16 + wave * 4 + zz;
-    const int b = frame_of ? frame_of[p] : 0;
-    const unsigned img = (unsigned)(H * W) * pix_bytes;  // pix_bytes >= 64: one channels-last pixel
-    const unsigned qo = (unsigned)q * 16u;
-    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
-    const float fV = (float)V;
-    const int GV = V + (V & 1);
-    const long long FN = (long long)s.fine[0] * s.fine[1] * s.fine[2];
-    __amdgpu_buffer_rsrc_t grs;
-    float rt[6];
-    for (int e = threadIdx.x; e < 64 * 4 * 16; e += 256) lxy[e] = 0u;
-    if constexpr (OTF) {
-        for (int e = threadIdx.x; e < GV * FVP_CAM_STRIDE; e += 256) lcam[e] = e < V * FVP_CAM_STRIDE ? pc.cams[e] : 0.0f;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) rt[k] = pc.resize_t[k];
-    } else {
-        grs = uniform_rsrc(fgrid, (unsigned)(FN * GV * 8));
-    }
-    __syncthreads();
-    const char *__restrict__ frame_cl = (const char *)cl + (size_t)b * V * img;
-    const size_t S3 = (size_t)SX * SY * SZ;
-    float *xy_pl = planes ? planes + (size_t)p * Jst * SX * SY : nullptr;
-    float *xz_pl = planes ? planes + ((size_t)P + p) * Jst * SX * SZ : nullptr;
-    float *yz_pl = planes ? planes + ((size_t)2 * P + p) * Jst * SY * SZ : nullptr;
-    const bool here = y < SY && z < SZ;  // this lane's voxel is in the cube
-    const int gy = w.ctl[1] + y, gz = w.ctl[2] + z;
-    const bool yzin = here && gy >= w.start[1] && gy < w.end[1] && gz >= w.start[2] && gz < w.end[2];
-    bool rows_in = false;  // block-uniform: does any of the 4 rows meet the window?
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int g = w.ctl[1] + rq * 4 + rr;
-        rows_in |= rq * 4 + rr < SY && g >= w.start[1] && g < w.end[1];
-    }
-    unsigned yzacc[4] = {0u, 0u, 0u, 0u};  // plane maxima on the float bits (person_cl_kernel)
-    int x_lo = xpart * SX / xsplit, x_hi = (xpart + 1) * SX / xsplit;
-    if (!cubes) {  // planes only: walk the window's x range (zeros elsewhere change no maximum)
-        if (w.skip || !rows_in) {
-            x_hi = x_lo;
-        } else {
-            x_lo = max(x_lo, w.start[0] - w.ctl[0]);
-            x_hi = min(x_hi, w.end[0] - w.ctl[0]);
-        }
-    }
-    // xz maxima of the last XB x steps (a shift register, the newest last): one
-    // atomic per step and wave costs ~0.66 us per proposal however few lanes or
-    // instructions it has (probe modes 5 / 7 and the 4x fewer instructions of this
-    // kernel): non-returning atomics count in vmcnt, so the next step's first wait
-    // covers their L2 round trip.  Sent XB steps at a time, one wait in XB does.
-    constexpr int XB = FVP_AB_XB;
-    unsigned xzb[XB];
-#pragma unroll
-    for (int i = 0; i < XB; ++i) xzb[i] = 0u;
-    int xzn = 0;  // pending steps (block-uniform)
-    auto xz_flush = [&](int xend) {  // the pending steps are x = xend - xzn .. xend - 1
-#pragma unroll
-        for (int i = 0; i < XB; ++i) {
-            const int xi = xend - XB + i;
-            if (MODE != 5 && i >= XB - xzn && z < SZ && 4 * q + r < J && xzb[i] != 0u)
-                atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + r) * SX + xi) * SZ + z, xzb[i]);
-        }
-        xzn = 0;
-    };
-    for (int x = x_lo; x < x_hi; ++x) {
-        const int gx = w.ctl[0] + x;
-        const bool valid = !w.skip && yzin && gx >= w.start[0] && gx < w.end[0];
-        float acc[4];
-        person_voxel_sum<LPV, OTF, CASC, MODE>(acc, valid, gx, gy, gz, grs, lcam, rt, pc, s, frame_cl, img, qo, q, V, GV,
-                                               W, H, sxs, sys, pix_bytes);
-        float o[4];
-        unsigned ou[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            // clamp(0,1) of the mean; +0.0f turns a -0 into +0 (unsigned max order below)
-            o[k] = valid ? clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f : 0.0f;
-            ou[k] = here ? __builtin_bit_cast(unsigned, o[k]) : 0u;  // beyond the cube: neutral
-        }
-        if constexpr (MODE == 1 || MODE == 4) {  // probe: keep the sums live, no planes
-            if (offset && here && (acc[0] + acc[1] + acc[2] + acc[3]) == -1.0f) offset[(size_t)p * 3] = o[0];
-            continue;
-        }
-        if (cubes && here) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (4 * q + k < J) cubes[((size_t)p * Jst + 4 * q + k) * S3 + ((size_t)x * SY + y) * SZ + z] = o[k];
-        }
-        if (planes) {
-            unsigned xm[4], zm[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                yzacc[k] = max(yzacc[k], ou[k]);
-                // over the 4 rows (lane bits 2-3: rotations by 4 and 8 within each 16-lane row)
-                unsigned m = ou[k];
-                unsigned t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)m, 0x124, 0xf, 0xf, false);
-                m = max(m, t);
-                t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)m, 0x128, 0xf, 0xf, false);
-                xm[k] = max(m, t);
-                // over the 4 z (lane bits 4-5: the 16-lane rows)
-                const auto h = __builtin_amdgcn_permlane16_swap(ou[k], ou[k], false, false);
-                m = max((unsigned)h[0], (unsigned)h[1]);
-                const auto v = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-                zm[k] = max((unsigned)v[0], (unsigned)v[1]);
-            }
-            // xz: lane (q, r, zz) holds joint 4q + r at z; XB steps are batched in
-            // registers and sent together (see xz_flush)
-            const unsigned ux = r == 0 ? xm[0] : r == 1 ? xm[1] : r == 2 ? xm[2] : xm[3];
-#pragma unroll
-            for (int i = 0; i + 1 < XB; ++i) xzb[i] = xzb[i + 1];
-            xzb[XB - 1] = ux;
-            if (++xzn == XB) xz_flush(x + 1);
-            // xy: lane (q, r, zz) adds joint 4q + zz of row r to the block's LDS maxima
-            const unsigned uy = zz == 0 ? zm[0] : zz == 1 ? zm[1] : zz == 2 ? zm[2] : zm[3];
-            if (uy != 0u) atomicMax(&lxy[(x * 4 + r) * 16 + 4 * q + zz], uy);
-        }
-    }
-    if (planes && xzn > 0) xz_flush(x_hi);
-    if (planes && here) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (4 * q + k >= J) continue;
-            float *dst = yz_pl + ((size_t)(4 * q + k) * SY + y) * SZ + z;
-            if (xsplit == 1) *dst = __builtin_bit_cast(float, yzacc[k]);
-            else if (yzacc[k] != 0u) atomicMax(reinterpret_cast<unsigned *>(dst), yzacc[k]);  // pre-zeroed plane
-        }
-    }
-    if (planes) {  // the z tile's xy maxima, into the pre-zeroed plane (the other z tiles add theirs)
-        __syncthreads();
-        const int n = (x_hi - x_lo) * 4 * 16;
-        for (int e = threadIdx.x; e < n; e += 256) {
-            const int xi = x_lo + (e >> 6), rr = (e >> 4) & 3, j = e & 15;
-            const unsigned m = lxy[(xi * 4 + rr) * 16 + j];
-            if (MODE != 6 && m != 0u && j < J && rq * 4 + rr < SY)
-                atomicMax(reinterpret_cast<unsigned *>(xy_pl) + ((size_t)j * SX + xi) * SY + rq * 4 + rr, m);
-        }
-    }
-}
-
 // Small launches (per-frame calls) split each row's x walk over 2-4 blocks.
 static int person_xsplit(int P, int SY) {
     const long long rows = (long long)P * SY;
     return rows >= 4096 ? 1 : rows >= 1024 ? 2 : 4;
-}
-
-#ifndef FVP_AB_TILE
-#define FVP_AB_TILE 0
-#endif
-// 4 x 4 tiles (person_tile_kernel) for J <= 16 joints per slice and x <= 64 bins
-static bool person_tiles(int LPV, int SX) { return FVP_AB_TILE && LPV == 4 && SX <= 64; }
-
-template <bool OTF, bool CASC>
-static void launch_person_tile(const float *cl, const float *fgrid, const PersonCoords &pc, const float *props,
-                               const int32_t *frame_of, const fvp_person_spec &s, float *cubes, float *planes,
-                               float *offset, int P, int V, int J, int Jst, int H, int W, unsigned pix_bytes,
-                               hipStream_t st) {
-    const int SY = s.bins[1], SZ = s.bins[2];
-    const int xsplit = person_xsplit(P, SY);
-    const long long blocks = (long long)P * ((SY + 3) / 4) * xsplit * ((SZ + 15) / 16);
-    hipLaunchKernelGGL((person_tile_kernel<OTF, CASC>), dim3((unsigned)blocks), dim3(256), 0, st, cl, fgrid, pc, props,
-                       frame_of, s, cubes, planes, offset, P, V, J, Jst, H, W, xsplit, pix_bytes);
 }
 
 template <int LPV, bool OTF, bool CASC>
@@ -641,11 +441,6 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // pre-zeroed plane).  Cubes deeper than 64 run as 64-deep z chunks, one block
     // each (the xy and xz maxima combine across blocks through atomics; yz is per
     // (y, z)).
-    if (person_tiles(LPV, s.bins[0])) {
-        launch_person_tile<OTF, CASC>(cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H, W,
-                                      pix_bytes, st);
-        return;
-    }
     const int xmap = 1, xsplit = person_xsplit(P, SY), zsplit = (s.bins[2] + 63) / 64;
     hipLaunchKernelGGL((person_cl_kernel<LPV, OTF, CASC>), dim3((unsigned)((long long)P * SY * xsplit * zsplit)),
                        dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H,
@@ -712,8 +507,7 @@ static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J,
     // xy_direct): one x part, one z chunk, S <= 64 and every joint slice at <= 4
     // lanes per voxel
     const int xsplit = person_xsplit(P, SY);
-    const int xy_direct =
-        (planes && xsplit == 1 && SZ <= 64 && SX <= 64 && J <= 16 && !person_tiles(lanes_per_voxel(J), SX)) ? 1 : 0;
+    const int xy_direct = (planes && xsplit == 1 && SZ <= 64 && SX <= 64 && J <= 16) ? 1 : 0;
     if (planes) {  // xy, xz (and yz when x is split) hold maxima over non-negative floats: from +0
         const size_t n = (xsplit > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
         const hipError_t e = hipMemsetAsync(planes, 0, n * 4, st);

@@ -10,7 +10,6 @@
 //   5 NO_XZ_ATOMICS  FULL without the xz-plane atomics
 //   6 NO_XY_ATOMICS  FULL without the xy-plane atomics
 //   7 HALF_XZ_ATOMICS  xz atomics from half the lanes (lane-count vs instruction cost)
-//   10 + m      person_tile_kernel<packed grid> with MODE m (4 x 4 (y, z) tiles per wave)
 // Test tooling only (tools/person_probe.py); not part of libfvp.
 #include "../faster-voxelpose_amd/csrc/fvp_person.hip"
 
@@ -21,16 +20,6 @@ static void go(dim3 grid, hipStream_t s, const float *cl, const float *fgrid, co
     hipLaunchKernelGGL((fvp::person_cl_kernel<4, false, false, MODE>), grid, dim3(256), 0, s, cl, fgrid,
                        fvp::PersonCoords{}, props, frame_of, spec, nullptr, planes, offset, P, V, J, J, H, W, 1,
                        xsplit, 1, pix_bytes, xsplit == 1 ? 1 : 0);
-}
-
-template <int MODE>
-static void go_tile(hipStream_t s, const float *cl, const float *fgrid, const fvp_person_spec &spec, const float *props,
-                    const int32_t *frame_of, float *planes, float *offset, int P, int V, int J, int H, int W,
-                    int xsplit, unsigned pix_bytes) {
-    const long long blocks = (long long)P * ((spec.bins[1] + 3) / 4) * xsplit * ((spec.bins[2] + 15) / 16);
-    hipLaunchKernelGGL((fvp::person_tile_kernel<false, false, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, cl,
-                       fgrid, fvp::PersonCoords{}, props, frame_of, spec, nullptr, planes, offset, P, V, J, J, H, W,
-                       xsplit, pix_bytes);
 }
 
 extern "C" int person_probe(int mode, const float *cl, int cp, const float *fgrid, const fvp_person_spec *spec,
@@ -53,13 +42,6 @@ extern "C" int person_probe(int mode, const float *cl, int cp, const float *fgri
         case 5: go<5>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         case 6: go<6>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         case 7: go<7>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 10: go_tile<0>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 11: go_tile<1>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 12: go_tile<2>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 13: go_tile<3>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 14: go_tile<4>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 15: go_tile<5>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
-        case 16: go_tile<6>(s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         default: return FVP_ERR_SHAPE;
     }
     return (int)hipGetLastError();

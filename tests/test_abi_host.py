@@ -143,3 +143,26 @@ def test_synthetic_inputs_deterministic_and_peaked():
     assert a.shape == (2, 5, 15, 128, 240)
     assert 0.0 <= a.min() and a.max() <= 1.0 and a.max() > 0.9
     assert 0.001 < (a > 0).mean() < 0.2
+
+
+def test_eager_fast_path_routes_tracing_to_the_registered_op():
+    """fvp.ops names call the op implementations directly in eager mode (the
+    custom-op dispatcher costs ~17 us per call); under a dispatch mode -- here
+    FakeTensorMode, as torch.compile / export use -- they must go through the
+    registered op and its fake kernel instead (no native call on fake tensors)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    from fvp import ops
+
+    assert isinstance(ops.voxelize.op, torch._library.custom_ops.CustomOpDef)  # the registered op behind the name
+    with FakeTensorMode():
+        hm = torch.empty((2, 5, 15, 16, 24), device="cuda")
+        grid = torch.empty((4 * 4 * 3, 6, 2), device="cuda")
+        cube, xy = ops.voxelize(hm, grid, None, 4, 4, 3, True, True)
+        planes_out = ops.person_planes(hm, torch.empty((8 * 8 * 4, 6, 2), device="cuda"),
+                                       torch.empty((3, 7), device="cuda"), None, [8, 8, 4], [1.0] * 3, [0.0] * 3,
+                                       [1.0] * 3, [1.0] * 3, [4, 4, 4], False, True)
+    assert type(cube).__name__ == "FakeTensor" and tuple(cube.shape) == (2, 15, 4, 4, 3)
+    assert tuple(xy.shape) == (2, 15, 4, 4)
+    assert tuple(planes_out[1].shape) == (9, 15, 4, 4)

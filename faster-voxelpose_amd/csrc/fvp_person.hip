@@ -249,7 +249,8 @@ __device__ __forceinline__ void person_voxel_sum(float (&acc)[4], bool valid, in
 // plane reductions / stores (the sums folded into `offset`), 2 = zeros instead
 // of the tap loads, 3 = every tap offset off-image (range-checked loads, no
 // memory access), 4 = grid loads and tap setup only (no tap loads, no planes),
-// 5 / 6 = no xz / xy plane atomics or stores, 7 = xz atomics from even z lanes only.
+// 5 / 6 = no xz / xy plane atomics or stores, 7 = xz atomics from even z lanes only,
+// 8 = plain stores instead of the xz atomics (timing only: wrong maxima).
 template <int LPV, bool OTF, bool CASC, int MODE = 0>
 __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__restrict__ cl,
                                                              const float *__restrict__ fgrid, PersonCoords pc,
@@ -387,7 +388,9 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
                 for (int k = 0; k < 4; ++k) {
                     // +0 cannot raise the pre-zeroed plane: skip those atomics (most of the 64^3 cube)
                     const unsigned u = ou[k];
-                    if (MODE != 5 && (MODE != 7 || (zl & 1) == 0) && 4 * q + k < J && u != 0u)
+                    if (MODE == 8 && 4 * q + k < J && u != 0u)  // probe: plain stores instead (wrong maxima)
+                        reinterpret_cast<unsigned *>(xz_pl)[((size_t)(4 * q + k) * SX + x) * SZ + zl] = u;
+                    else if (MODE != 5 && MODE != 8 && (MODE != 7 || (zl & 1) == 0) && 4 * q + k < J && u != 0u)
                         atomicMax(reinterpret_cast<unsigned *>(xz_pl) + ((size_t)(4 * q + k) * SX + x) * SZ + zl, u);
                 }
             }

@@ -10,6 +10,7 @@
 //   5 NO_XZ_ATOMICS  FULL without the xz-plane atomics
 //   6 NO_XY_ATOMICS  FULL without the xy-plane atomics
 //   7 HALF_XZ_ATOMICS  xz atomics from half the lanes (lane-count vs instruction cost)
+//   8 XZ_STORES  plain stores instead of the xz atomics (timing only)
 // Test tooling only (tools/person_probe.py); not part of libfvp.
 #include "../faster-voxelpose_amd/csrc/fvp_person.hip"
 
@@ -42,6 +43,7 @@ extern "C" int person_probe(int mode, const float *cl, int cp, const float *fgri
         case 5: go<5>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         case 6: go<6>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         case 7: go<7>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
+        case 8: go<8>(grid, s, cl, fgrid, *spec, props, frame_of, planes, offset, P, V, J, H, W, xsplit, pb); break;
         default: return FVP_ERR_SHAPE;
     }
     return (int)hipGetLastError();

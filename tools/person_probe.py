@@ -16,7 +16,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "faster-voxelpose_amd")]
-MODES = {"FULL": 0, "NOPLANES": 1, "NOTAPS": 2, "ALL_OOB": 3, "SETUP": 4, "NO_XZ_ATOMICS": 5, "NO_XY_ATOMICS": 6, "HALF_XZ_ATOMICS": 7}
+MODES = {"FULL": 0, "NOPLANES": 1, "NOTAPS": 2, "ALL_OOB": 3, "SETUP": 4, "NO_XZ_ATOMICS": 5, "NO_XY_ATOMICS": 6, "HALF_XZ_ATOMICS": 7, "XZ_STORES": 8}
 
 
 def build():

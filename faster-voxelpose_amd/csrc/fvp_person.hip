@@ -422,121 +422,6 @@ __global__ __launch_bounds__(64 * LPV) void person_cl_kernel(const float *__rest
     }
 }
 
-// x-part blocks (A/B, FVP_AB_XPART): block = (proposal, XP consecutive x-planes),
-// 256 threads = 64 z x 4 joint quads (LPV = 4), walking the window's rows with
-// its x-planes inner.  The xz maxima (over y) stay in LDS for the whole walk
-// and leave as plain stores once; the xy maxima (over z, 4 waves) combine in
-// LDS through ds_max and leave once; only yz (over x) crosses blocks, one
-// atomic per wave, joint quad and ROW instead of xz's per x step: XP x fewer
-// L2 read-modify-write line touches than the row kernel (the atomics cost
-// 0.70 us per proposal there, plain stores 0.22 -- probe modes 5 / 8).
-template <bool CASC, int MODE = 0>
-__global__ __launch_bounds__(256) void person_xpart_kernel(const float *__restrict__ cl, const float *__restrict__ fgrid,
-                                                           const float *__restrict__ props,
-                                                           const int32_t *__restrict__ frame_of, fvp_person_spec s,
-                                                           float *__restrict__ planes, float *__restrict__ offset, int P,
-                                                           int V, int J, int Jst, int H, int W, unsigned pix_bytes) {
-    constexpr int LPV = 4, XP = 4;
-    extern __shared__ unsigned lds_xp[];  // lxz [XP][64 z][16 j], lxy [XP][64 y][16 j]
-    unsigned *lxz = lds_xp, *lxy = lds_xp + XP * 64 * 16;
-    const int SX = s.bins[0], SY = s.bins[1], SZ = s.bins[2];
-    const int NXP = (SX + XP - 1) / XP;
-    const int L = xcd_remap(blockIdx.x, gridDim.x);  // a proposal's blocks on one XCD
-    const int p = L / NXP, xa = (L - p * NXP) * XP;
-    const Window w = person_window(props + (size_t)p * 7, s);
-    if (offset && xa == 0 && threadIdx.x < 3) {
-        const int a = threadIdx.x;
-        offset[(size_t)p * 3 + a] =
-            ((float)w.ctl[a] / (float)(s.fine[a] - 1)) * s.whole_size[a] - s.whole_size[a] / 2.0f + s.ind_size[a] / 2.0f;
-    }
-    // the window's part of this block's x-planes and rows (outside it every voxel is 0:
-    // the pre-zeroed planes already hold those maxima)
-    const int x0 = max(xa, w.start[0] - w.ctl[0]), x1 = min(min(xa + XP, SX), w.end[0] - w.ctl[0]);
-    const int y0 = max(0, w.start[1] - w.ctl[1]), y1 = min(SY, w.end[1] - w.ctl[1]);
-    if (w.skip || x0 >= x1 || y0 >= y1) return;  // block-uniform, before any barrier
-    const int lane = threadIdx.x & 63;
-    const int zl = (int)threadIdx.x / LPV, q = threadIdx.x % LPV;
-    const int b = frame_of ? frame_of[p] : 0;
-    const unsigned img = (unsigned)(H * W) * pix_bytes;
-    const unsigned qo = (unsigned)q * 16u;
-    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
-    const float fV = (float)V;
-    const int GV = V + (V & 1);
-    const long long FN = (long long)s.fine[0] * s.fine[1] * s.fine[2];
-    const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(fgrid, (unsigned)(FN * GV * 8));
-    const char *__restrict__ frame_cl = (const char *)cl + (size_t)b * V * img;
-    float *xy_pl = planes + (size_t)p * Jst * SX * SY;
-    float *xz_pl = planes + ((size_t)P + p) * Jst * SX * SZ;
-    float *yz_pl = planes + ((size_t)2 * P + p) * Jst * SY * SZ;
-    const bool zok = zl < SZ;
-    const int gz = w.ctl[2] + zl;
-    const bool zin = zok && gz >= w.start[2] && gz < w.end[2];
-    for (int e = threadIdx.x; e < 2 * XP * 64 * 16; e += 256) lds_xp[e] = 0u;
-    __syncthreads();
-    float rt[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (on-the-fly coordinates only)
-    for (int y = y0; y < y1; ++y) {
-        const int gy = w.ctl[1] + y;
-        unsigned yzc[4] = {0u, 0u, 0u, 0u};
-        for (int x = x0; x < x1; ++x) {
-            const int gx = w.ctl[0] + x;
-            float acc[4];
-            person_voxel_sum<LPV, false, CASC, MODE>(acc, zin, gx, gy, gz, grs, nullptr, rt, PersonCoords{}, s,
-                                                     frame_cl, img, qo, q, V, GV, W, H, sxs, sys, pix_bytes);
-            unsigned ou[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)  // clamp(0,1) of the mean, +0.0f: -0 -> +0 (unsigned max order)
-                ou[k] = zin ? __builtin_bit_cast(unsigned, clampf(acc[k] / fV, 0.0f, 1.0f) + 0.0f) : 0u;
-            if constexpr (MODE == 1 || MODE == 4) {  // probe: keep the sums live, no planes
-                if (offset && zok && (acc[0] + acc[1] + acc[2] + acc[3]) == -1.0f)
-                    offset[(size_t)p * 3] = __builtin_bit_cast(float, ou[0]);
-                continue;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) yzc[k] = max(yzc[k], ou[k]);
-            // xz: this lane's (x, z, joints 4q..4q+3) entry, owned by it alone
-            u32x4 *e4 = reinterpret_cast<u32x4 *>(lxz + ((x - xa) * 64 + zl) * 16 + 4 * q);
-            u32x4 cur = *e4;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = max((unsigned)cur[k], ou[k]);
-            *e4 = cur;
-            // xy: the wave's z maxima (VALU), then ds_max across the block's 4 waves
-            unsigned zm[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) zm[k] = slot_umax<LPV>(ou[k]);
-            const int kk = lane / LPV;  // q == lane % LPV
-            const unsigned mv = kk == 0 ? zm[0] : kk == 1 ? zm[1] : kk == 2 ? zm[2] : zm[3];
-            if (lane < 4 * LPV && mv != 0u) atomicMax(lxy + ((x - xa) * 64 + y) * 16 + 4 * q + kk, mv);
-        }
-        if (zok) {  // yz[y][z]: this block's x-planes' maximum, into the pre-zeroed plane
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (MODE != 5 && 4 * q + k < J && yzc[k] != 0u)
-                    atomicMax(reinterpret_cast<unsigned *>(yz_pl) + ((size_t)(4 * q + k) * SY + y) * SZ + zl, yzc[k]);
-        }
-    }
-    __syncthreads();
-    // the block's xz and xy maxima, once (consecutive threads -> consecutive z / y)
-    const int nx = x1 - x0;
-    for (int e = threadIdx.x; e < nx * 16 * 64; e += 256) {
-        const int xi = x0 - xa + e / 1024, j = (e >> 6) & 15, c = e & 63;
-        if (j >= J) continue;
-        const unsigned vz = lxz[(xi * 64 + c) * 16 + j];
-        if (MODE != 6 && c < SZ && vz != 0u) xz_pl[((size_t)j * SX + xa + xi) * SZ + c] = __builtin_bit_cast(float, vz);
-        const unsigned vy = lxy[(xi * 64 + c) * 16 + j];
-        if (MODE != 6 && c < SY && vy != 0u) xy_pl[((size_t)j * SX + xa + xi) * SY + c] = __builtin_bit_cast(float, vy);
-    }
-}
-
-#ifndef FVP_AB_XPART
-#define FVP_AB_XPART 0
-#endif
-// the x-part kernel: packed grid, J <= 16 (LPV 4), planes only, S <= 64, and a launch
-// that would not split rows into x parts (person_xsplit == 1)
-static bool person_xpart(int LPV, const fvp_person_spec &s, bool cubes, bool planes, int xsplit) {
-    return FVP_AB_XPART && LPV == 4 && planes && !cubes && xsplit == 1 && s.bins[0] <= 64 && s.bins[1] <= 64 &&
-           s.bins[2] <= 64;
-}
-
 // Small launches (per-frame calls) split each row's x walk over 2-4 blocks.
 static int person_xsplit(int P, int SY) {
     const long long rows = (long long)P * SY;
@@ -560,15 +445,6 @@ static void launch_person_cl(const float *cl, const float *fgrid, const PersonCo
     // each (the xy and xz maxima combine across blocks through atomics; yz is per
     // (y, z)).
     const int xmap = 1, xsplit = person_xsplit(P, SY), zsplit = (s.bins[2] + 63) / 64;
-    if constexpr (LPV == 4 && !OTF) {
-        if (person_xpart(LPV, s, cubes != nullptr, planes != nullptr, xsplit)) {
-            const int nxp = (s.bins[0] + 3) / 4;
-            hipLaunchKernelGGL((person_xpart_kernel<CASC>), dim3((unsigned)((long long)P * nxp)), dim3(256),
-                               2 * 4 * 64 * 16 * sizeof(unsigned), st, cl, fgrid, props, frame_of, s, planes, offset,
-                               P, V, J, Jst, H, W, pix_bytes);
-            return;
-        }
-    }
     hipLaunchKernelGGL((person_cl_kernel<LPV, OTF, CASC>), dim3((unsigned)((long long)P * SY * xsplit * zsplit)),
                        dim3(64 * LPV), 0, st, cl, fgrid, pc, props, frame_of, s, cubes, planes, offset, P, V, J, Jst, H,
                        W, xmap, xsplit, zsplit, pix_bytes, xy_direct);
@@ -635,11 +511,8 @@ static int person_planes_any(const float *heatmaps, int cp, int B, int V, int J,
     // lanes per voxel
     const int xsplit = person_xsplit(P, SY);
     const int xy_direct = (planes && xsplit == 1 && SZ <= 64 && SX <= 64 && J <= 16) ? 1 : 0;
-    // (the x-part kernel reduces yz across blocks: all three planes from +0)
-    const bool xpart = !pc && person_xpart(lanes_per_voxel(J < kPersonSlice ? J : kPersonSlice), *spec,
-                                           cubes != nullptr, planes != nullptr, xsplit) && J <= kPersonSlice;
     if (planes) {  // xy, xz (and yz when x is split) hold maxima over non-negative floats: from +0
-        const size_t n = (xsplit > 1 || xpart ? 3 : 2) * (size_t)P * J * SX * SY;
+        const size_t n = (xsplit > 1 ? 3 : 2) * (size_t)P * J * SX * SY;
         const hipError_t e = hipMemsetAsync(planes, 0, n * 4, st);
         if (e != hipSuccess) return (int)e;
     }

@@ -150,17 +150,78 @@ __global__ __launch_bounds__(256) void pairs_rows_kernel(const _Float16 *__restr
     }
 }
 
+// The same table without LDS, 8 entries per thread (W % 8 == 0, 16-B aligned
+// rows): thread = (row, 8-pixel group m, frame f, joint quad q) loads pixels
+// 8m .. 8m+7 of its 4 joint rows with one 16-B load each (+ pixel 8m-1), and
+// writes entries 8m .. 8m+7 (pixels e-1, e) -- and entry W for the last group.
+// A wave's 16 (f, q) lanes of one m write 256 contiguous bytes per entry.
+template <int NF>
+__global__ __launch_bounds__(256) void pairs_vec8_kernel(const _Float16 *__restrict__ hm, uint4 *__restrict__ tab,
+                                                         int J, int H, int W, int V, long long total) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= total) return;
+    const int M = W / 8;
+    const int q = (int)(gid & 3);
+    const long long r1 = gid >> 2;
+    const int f = (int)(r1 % NF);
+    const long long r2 = r1 / NF;
+    const int m = (int)(r2 % M);
+    const long long row = r2 / M;  // (g * V + v) * H + y
+    const long long gv = row / H;
+    const int y = (int)(row - gv * H);
+    const long long g = gv / V, v = gv - g * V;
+    const size_t HW = (size_t)H * W;
+    unsigned px[4][4], prev[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * q + k;
+        const unsigned short *src = reinterpret_cast<const unsigned short *>(hm) +
+                                    (((size_t)(g * NF + f) * V + v) * J + j) * HW + (size_t)y * W;
+        uint4 a = make_uint4(0u, 0u, 0u, 0u);
+        unsigned b = 0u;
+        if (j < J) {
+            a = *reinterpret_cast<const uint4 *>(src + 8 * m);
+            b = m > 0 ? src[8 * m - 1] : 0u;
+        }
+        px[k][0] = a.x; px[k][1] = a.y; px[k][2] = a.z; px[k][3] = a.w;
+        prev[k] = b;
+    }
+    auto pix = [&](int k, int i) -> unsigned { return (px[k][i >> 1] >> (16 * (i & 1))) & 0xffffu; };
+    const int W1 = W + 1;
+    uint4 *__restrict__ dst = tab + ((size_t)row * W1 * NF + f) * 4 + q;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // entry e = 8m + i: pixels e - 1 and e
+        unsigned lo[4], hi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            lo[k] = i == 0 ? prev[k] : pix(k, i - 1);
+            hi[k] = pix(k, i);
+        }
+        dst[(size_t)(8 * m + i) * NF * 4] =
+            make_uint4(lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16));
+    }
+    if (m == M - 1) {  // entry W: pixel W - 1 and the zero past the row
+        dst[(size_t)W * NF * 4] = make_uint4(pix(0, 7) | (pix(1, 7) << 16), pix(2, 7) | (pix(3, 7) << 16), 0u, 0u);
+    }
+}
+
 inline size_t pair_frame_bytes(int V, int H, int W) { return (size_t)V * H * (W + 1) * 64; }
 
 // Launch the pair-table layout for nb frames (a multiple of NF).
 template <int NF>
 inline void launch_pairs(const _Float16 *hm, int nb, int V, int J, int H, int W, uint4 *tab, hipStream_t s) {
     const size_t lds = (size_t)NF * 16 * (W / 2 + 2) * 4;
-    // (one frame per entry: the per-entry kernel, 20.8 vs 40.8 us at C5 B = 1 --
-    // a 15 KB row per block leaves its load / store phases exposed; it also
-    // serves odd widths and fp16 pointers that are not 4-B aligned)
+    // 8 entries a thread wherever rows are 16-B aligned: C5, 4 frames per entry
+    // 98.2 -> 72.5 us, one frame 20.4 -> 15.9 us (profiles/round4/pairs8/).
+    // Otherwise row blocks for frame groups (a 15 KB row per block leaves its
+    // load / store phases exposed at one frame: 40.8 vs 20.8 us per entry), and
+    // the per-entry kernel for single frames, odd widths and 2-B-aligned pointers.
     const bool aligned = ((unsigned long long)hm & 3ull) == 0;  // 4-B row loads (a C-ABI caller may pass any fp16 pointer)
-    if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024) {
+    if (W % 8 == 0 && ((unsigned long long)hm & 15ull) == 0) {
+        const long long total = (long long)nb / NF * V * H * (W / 8) * NF * 4;
+        hipLaunchKernelGGL((pairs_vec8_kernel<NF>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, hm, tab,
+                           J, H, W, V, total);
+    } else if (NF > 1 && aligned && W % 2 == 0 && lds <= 64 * 1024) {
         hipLaunchKernelGGL((pairs_rows_kernel<NF>), dim3((unsigned)((long long)nb / NF * V * H)), dim3(256), lds, s, hm,
                            tab, J, H, W, V);
     } else {

@@ -468,11 +468,11 @@ def test_fp16_frame_pairs_batch_invariance(gpu_device, B, otf):
 
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "otf"])
 def test_fp16_pair_layouts_agree(gpu_device, otf):
-    """pairs_rows_kernel (a block per row, through LDS, 4-B row loads) and the
-    per-entry layout kernel (what fp16 heatmaps at a 2-B-aligned address and odd
-    heatmap widths use) build the same pair table: identical cubes and xy
-    planes for 7 frames (entries of 4, 2 and 1 frames), 31 ring cameras on a
-    small grid."""
+    """pairs_vec8_kernel (16-B-aligned heatmaps, width % 8 == 0: 8 entries a
+    thread), pairs_rows_kernel (4-B-aligned: a block per row, through LDS) and
+    the per-entry layout kernel (a 2-B-aligned address or an odd width) build
+    the same pair table: identical cubes and xy planes for 7 frames (entries of
+    4, 2 and 1 frames), 31 ring cameras on a small grid."""
     from fvp import geometry, synthetic
     from fvp.config import make_cfg
     from fvp.project_whole import ProjectLayer
@@ -487,12 +487,17 @@ def test_fp16_pair_layouts_agree(gpu_device, otf):
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
     hm = synthetic.uniform_heatmaps(w, 7, seed=23).half().to(gpu_device)
     cube, xy = layer.forward_fused(hm, {"seq": [seq] * 7}, cams, rt)
-    buf = torch.empty(hm.numel() + 1, dtype=torch.float16, device=gpu_device)
-    hm_odd = buf[1:].view(hm.shape)  # contiguous, 2 B past a 4-B boundary: the per-entry kernel
+    buf = torch.empty(hm.numel() + 8, dtype=torch.float16, device=gpu_device)
+    hm_odd = buf[1:1 + hm.numel()].view(hm.shape)  # contiguous, 2 B past a 4-B boundary: the per-entry kernel
     hm_odd.copy_(hm)
     assert hm_odd.is_contiguous() and hm_odd.data_ptr() % 4 == 2
     c_e, x_e = layer.forward_fused(hm_odd, {"seq": [seq] * 7}, cams, rt)
     assert torch.equal(cube, c_e) and torch.equal(xy, x_e)
+    hm_4 = buf[2:2 + hm.numel()].view(hm.shape)  # 4 B past a 16-B boundary: pairs_rows_kernel
+    hm_4.copy_(hm)
+    assert hm_4.data_ptr() % 16 == 4 and hm.data_ptr() % 16 == 0 and hm.shape[-1] % 8 == 0
+    c_r, x_r = layer.forward_fused(hm_4, {"seq": [seq] * 7}, cams, rt)
+    assert torch.equal(cube, c_r) and torch.equal(xy, x_r)
 
 
 def test_nms_on_channel_slice_without_copy(gpu_device):

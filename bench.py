@@ -31,9 +31,10 @@ sys.path.insert(0, os.path.join(REPO, "faster-voxelpose_amd"))
 
 METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# the fvp_voxelize op: layout pass (fp32 channels-last, fp16 pair table per entry or per row) + gather
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_pairs_kernel", "pairs_rows_kernel", "voxelize_kernel",
-               "voxelize_cams_kernel")
+# the fvp_voxelize op: layout pass (fp32 channels-last, fp16 pair table per 8 entries, per row or per
+# entry) + gather
+VOX_KERNELS = ("heatmaps_to_cl_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel", "pairs_rows_kernel",
+               "voxelize_kernel", "voxelize_cams_kernel")
 
 
 def parse():

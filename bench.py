@@ -12,6 +12,11 @@ BASELINE configs[1] (Shelf calibration, 5 cams, J=15, 128x240 -> 80x80x20).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+Without a launcher, `--gpus N > 1` starts `python -m torch.distributed.run
+--nproc-per-node N` on this same command line as a child process (this process
+never touches the GPU), relays rank 0's JSON line and exits with the child's
+status.  Under a launcher `--gpus` must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
@@ -37,7 +42,7 @@ VOX_KERNELS = ("heatmaps_to_cl_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_
                "voxelize_kernel", "voxelize_cams_kernel")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -62,7 +67,92 @@ def parse():
     ap.add_argument("--on-the-fly", choices=["auto", "on", "off"], default="auto",
                     help="sampling coordinates from the cached grid (off) or projected in-kernel (on)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# `--gpus N` without a launcher: spawn one.  Nothing here may initialise the
+# GPU (a process that has initialised it must not be replaced, and its ranks
+# need the devices): no torch import, the device count comes from a child.
+def visible_gpus():
+    """GPUs a rank could use, counted in a child process (torch.cuda.device_count
+    there; this process stays GPU-free).  FVP_BENCH_VISIBLE_GPUS overrides (tests)."""
+    if os.environ.get("FVP_BENCH_VISIBLE_GPUS", "").isdigit():
+        return int(os.environ["FVP_BENCH_VISIBLE_GPUS"])
+    out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                         capture_output=True, text=True, timeout=300)
+    try:
+        return int(out.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        raise SystemExit(f"bench: could not count the visible GPUs: {out.stderr.strip()[-300:]}")
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv, n, port):
+    """(argv, env) of the torch.distributed.run child that runs this benchmark as
+    n ranks on this node (rendezvous on 127.0.0.1; dmabuf IPC for RCCL)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return cmd, env
+
+
+def check_world(args, env=None):
+    """Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env and not args.child and args.gpus != int(env["WORLD_SIZE"]):
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env['WORLD_SIZE']} ranks")
+
+
+def maybe_launch(argv, json_out, popen=subprocess.Popen):
+    """If this is a bare `bench.py --gpus N` (N > 1, no WORLD_SIZE), run the
+    benchmark as N ranks in a torch.distributed.run child, relay rank 0's JSON
+    line to `json_out` and return the child's exit status; else return None."""
+    args = parse(argv)
+    if "WORLD_SIZE" in os.environ or args.child or args.gpus <= 1:
+        return None
+    gloo = os.environ.get("FVP_BENCH_BACKEND", "nccl") == "gloo"
+    if not gloo:
+        ndev = visible_gpus()
+        if args.gpus > ndev:
+            raise SystemExit(f"bench: --gpus {args.gpus} but {ndev} visible GPU(s); one rank per GPU "
+                             f"(FVP_BENCH_BACKEND=gloo for a shared-device rehearsal)")
+    cmd, env = launcher_command(argv, args.gpus, free_port())
+    note(f"launching {args.gpus} ranks: {' '.join(cmd[1:])}")
+    proc = popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    import signal
+
+    def forward(signum, _frame):
+        proc.send_signal(signum)
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    lines = 0
+    try:
+        for ln in proc.stdout:
+            s = ln.strip()
+            if s.startswith("{") and s.endswith("}"):
+                print(s, file=json_out, flush=True)  # rank 0's result line (only rank 0 prints one)
+                lines += 1
+            elif s:
+                print(ln.rstrip("\n"), file=sys.stderr, flush=True)
+        rc = proc.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    if rc == 0 and lines != 1:
+        note(f"expected one JSON line from rank 0, got {lines}")
+        return 1
+    return rc
 
 
 # ---------------------------------------------------------------------------
@@ -300,7 +390,12 @@ def main():
     # at stderr until the result is printed
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    rc = maybe_launch(sys.argv[1:], json_out)
+    if rc is not None:
+        json_out.close()
+        raise SystemExit(rc)
     args = parse()
+    check_world(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -150,9 +150,11 @@ struct ImageConsts {
     unsigned exact;
 };
 
-// Host: an integer divisor in [1, 65535] (the range tools/div_const_sweep.c covers).
+// Host: an integer divisor in [1, 4095] -- the range tests/test_div_const.py sweeps
+// with tools/div_const_sweep.c on every CPU run (every image and heatmap size of
+// the reference's configs); any other divisor takes the IEEE division.
 inline bool div_const_covered(float b) {
-    return b >= 1.0f && b <= 65535.0f && (float)(int)b == b;
+    return b >= 1.0f && b <= 4095.0f && (float)(int)b == b;
 }
 
 inline ImageConsts image_consts(const fvp_image_spec &im) {

@@ -50,8 +50,50 @@ def _dev_f32(t: torch.Tensor, name: str) -> torch.Tensor:
     return t.to(torch.float32).contiguous() if t.dtype != torch.float32 else t.contiguous()
 
 
+
+# -- eager fast path -------------------------------------------------------------------
+# torch.library.custom_op dispatch costs ~17 us of host time per call (measured on this
+# image: 20 vs 2.7 us for a no-op with the same signature), more than a one-frame
+# voxelize gather takes on the GPU.  The names in this module are therefore wrappers
+# that call the op's implementation directly when nothing needs the dispatcher, and the
+# registered op (torch.ops.fvp.*, with its fake kernel) otherwise: under torch.compile /
+# export, for tensor subclasses (fake, functional), under any TorchDispatchMode or
+# functorch transform (vmap, grad), and when grad mode is on and an input requires
+# grad (the op then raises its "no autograd formula" error instead of returning
+# outputs without a grad_fn).  `wrapper.op` is the registered op, `wrapper.impl` the
+# undecorated implementation.
+def _needs_dispatcher(args, kwargs) -> bool:
+    from torch.utils._python_dispatch import _get_current_dispatch_mode
+
+    if (torch.compiler.is_compiling() or _get_current_dispatch_mode() is not None
+            or torch._C._are_functorch_transforms_active()):
+        return True
+    grad = torch.is_grad_enabled()
+    for a in (*args, *kwargs.values()):
+        if isinstance(a, torch.Tensor) and (type(a) is not torch.Tensor or (grad and a.requires_grad)):
+            return True
+    return False
+
+
+def _custom_op(name: str, **kw):
+    def deco(impl):
+        op = torch.library.custom_op(name, **kw)(impl)
+
+        def call(*args, **kwargs):
+            if _needs_dispatcher(args, kwargs):
+                return op(*args, **kwargs)
+            return impl(*args, **kwargs)
+
+        call.__name__, call.__qualname__, call.__doc__ = impl.__name__, impl.__qualname__, impl.__doc__
+        call.op = op  # the registered custom op
+        call.impl = impl  # the implementation the fast path calls
+        call.register_fake = op.register_fake
+        return call
+
+    return deco
+
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("fvp::project_grid", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::project_grid", mutates_args=(), device_types="cuda")
 def project_grid(cams: torch.Tensor, resize_t: torch.Tensor, start: list[float], end: list[float],
                  center: list[float], bins: list[int], ori_max: float, img_w: float, img_h: float,
                  hm_w: int, hm_h: int) -> torch.Tensor:
@@ -77,7 +119,7 @@ def grid_slots(V: int) -> int:
     return V + (V & 1)
 
 
-@torch.library.custom_op("fvp::pack_grid", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::pack_grid", mutates_args=(), device_types="cuda")
 def pack_grid(sample_grid: torch.Tensor) -> torch.Tensor:
     """[V,N,2] (the reference's per-camera layout) -> voxel-major [N,GV,2] read by fvp_voxelize."""
     sg = _dev_f32(sample_grid, "sample_grid")
@@ -98,7 +140,7 @@ def packed_as_reference(packed: torch.Tensor, V: int) -> torch.Tensor:
     return packed.permute(1, 0, 2)[:V].unsqueeze(1)
 
 
-@torch.library.custom_op("fvp::voxelize", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::voxelize", mutates_args=(), device_types="cuda")
 def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
              X: int, Y: int, Z: int, want_cube: bool, want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
     """packed_grids: [S,N,GV,2] (or [N,GV,2]) from pack_grid; grid_index: int [B] sequence of frame b."""
@@ -129,7 +171,7 @@ def voxelize(heatmaps: torch.Tensor, packed_grids: torch.Tensor, grid_index: Opt
     return cube, xy
 
 
-@torch.library.custom_op("fvp::voxelize_cams", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::voxelize_cams", mutates_args=(), device_types="cuda")
 def voxelize_cams(heatmaps: torch.Tensor, cams: torch.Tensor, grid_index: Optional[torch.Tensor],
                   resize_t: torch.Tensor, start: list[float], end: list[float], center: list[float], bins: list[int],
                   ori_max: float, img_w: float, img_h: float, want_cube: bool,
@@ -218,7 +260,7 @@ def _cl_input(heatmaps_cl: torch.Tensor, J: int) -> torch.Tensor:
     return heatmaps_cl.contiguous()
 
 
-@torch.library.custom_op("fvp::voxelize_cl", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::voxelize_cl", mutates_args=(), device_types="cuda")
 def voxelize_cl(heatmaps_cl: torch.Tensor, J: int, packed_grids: torch.Tensor, grid_index: Optional[torch.Tensor],
                 X: int, Y: int, Z: int, want_cube: bool, want_xy: bool) -> tuple[torch.Tensor, torch.Tensor]:
     """voxelize on channels-last heatmaps [B,V,H,W,Cp] (joints in channels 0..J-1): no layout pass."""
@@ -247,7 +289,7 @@ def _(heatmaps_cl, J, packed_grids, grid_index, X, Y, Z, want_cube, want_xy):
             heatmaps_cl.new_empty((B, J, X, Y) if want_xy else (0,)))
 
 
-@torch.library.custom_op("fvp::voxelize_cl_cams", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::voxelize_cl_cams", mutates_args=(), device_types="cuda")
 def voxelize_cl_cams(heatmaps_cl: torch.Tensor, J: int, cams: torch.Tensor, grid_index: Optional[torch.Tensor],
                      resize_t: torch.Tensor, start: list[float], end: list[float], center: list[float],
                      bins: list[int], ori_max: float, img_w: float, img_h: float, want_cube: bool,
@@ -288,7 +330,7 @@ def _(heatmaps_cl, J, cams, grid_index, resize_t, start, end, center, bins, ori_
 
 
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("fvp::nms_topk", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::nms_topk", mutates_args=(), device_types="cuda")
 def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     if prob.device.type != "cuda":
         raise _lib.FvpError(f"fvp: prob_map must be on a HIP device, got {prob.device}")
@@ -312,7 +354,7 @@ def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, to
     return vals, xy, flat
 
 
-@torch.library.custom_op("fvp::nms_topk_columns", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::nms_topk_columns", mutates_args=(), device_types="cuda")
 def nms_topk_columns(prob: torch.Tensor, K: int,
                      cube: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """nms_topk + gather_columns in one launch (fvp_nms_topk_columns): the map's
@@ -355,7 +397,7 @@ def _(prob, K):
 
 
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("fvp::gather_columns", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::gather_columns", mutates_args=(), device_types="cuda")
 def gather_columns(cube: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
     c = _dev_f32(cube, "feature_cubes")
     B, J, X, Y, Z = c.shape
@@ -374,7 +416,7 @@ def _(cube, flat):
     return cube.new_empty((B, flat.shape[1], J, Z))
 
 
-@torch.library.custom_op("fvp::voxel_columns", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::voxel_columns", mutates_args=(), device_types="cuda")
 def voxel_columns(heatmaps: torch.Tensor, cl_joints: int, packed_grids: Optional[torch.Tensor],
                   cams: Optional[torch.Tensor], grid_index: Optional[torch.Tensor], resize_t: Optional[torch.Tensor],
                   start: list[float], end: list[float], center: list[float], bins: list[int], ori_max: float,
@@ -436,7 +478,7 @@ def _(heatmaps, cl_joints, packed_grids, cams, grid_index, resize_t, start, end,
     return heatmaps.new_empty((heatmaps.shape[0], flat.shape[1], J, int(bins[2])), dtype=torch.float32)
 
 
-@torch.library.custom_op("fvp::gather_bbox", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::gather_bbox", mutates_args=(), device_types="cuda")
 def gather_bbox(size: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
     s = _dev_f32(size, "bbox_preds")
     B, _, X, Y = s.shape
@@ -454,7 +496,7 @@ def _(size, flat):
     return size.new_empty((size.shape[0], flat.shape[1], 2))
 
 
-@torch.library.custom_op("fvp::proposal_centers", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::proposal_centers", mutates_args=(), device_types="cuda")
 def proposal_centers(index: torch.Tensor, hm1d: Optional[torch.Tensor], confs: torch.Tensor, match_bbox: torch.Tensor,
                      scale: list[float], bias: list[float], min_score: float) -> torch.Tensor:
     """Test-mode ProposalLayer.forward (fvp_proposal_centers): with hm1d [B,K,Z] the z pick
@@ -482,7 +524,7 @@ def _(index, hm1d, confs, match_bbox, scale, bias, min_score):
 
 
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("fvp::person_planes", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::person_planes", mutates_args=(), device_types="cuda")
 def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: torch.Tensor,
                   frame_of: Optional[torch.Tensor], fine: list[int], scale: list[float], bias: list[float],
                   whole_size: list[float], ind_size: list[float], bins: list[int], want_cubes: bool,
@@ -515,7 +557,7 @@ def person_planes(heatmaps: torch.Tensor, fine_grid: torch.Tensor, proposals: to
     return cubes, planes, offset
 
 
-@torch.library.custom_op("fvp::person_planes_cl", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::person_planes_cl", mutates_args=(), device_types="cuda")
 def person_planes_cl(heatmaps_cl: torch.Tensor, J: int, fine_grid: torch.Tensor, proposals: torch.Tensor,
                      frame_of: Optional[torch.Tensor], fine: list[int], scale: list[float], bias: list[float],
                      whole_size: list[float], ind_size: list[float], bins: list[int], want_cubes: bool,
@@ -554,7 +596,7 @@ def _(heatmaps_cl, J, fine_grid, proposals, frame_of, fine, scale, bias, whole_s
             heatmaps_cl.new_empty((P, 3)))
 
 
-@torch.library.custom_op("fvp::person_planes_cams", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::person_planes_cams", mutates_args=(), device_types="cuda")
 def person_planes_cams(heatmaps: torch.Tensor, cams: torch.Tensor, resize_t: torch.Tensor, start: list[float],
                        end: list[float], center: list[float], ori_max: float, img_w: float, img_h: float,
                        proposals: torch.Tensor, frame_of: Optional[torch.Tensor], fine: list[int], scale: list[float],
@@ -611,7 +653,7 @@ def _(heatmaps, fine_grid, proposals, frame_of, fine, scale, bias, whole_size, i
             heatmaps.new_empty((P, 3)))
 
 
-@torch.library.custom_op("fvp::max_planes", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::max_planes", mutates_args=(), device_types="cuda")
 def max_planes(cubes: torch.Tensor) -> torch.Tensor:
     c = _dev_f32(cubes, "cubes")
     P, J, S = c.shape[0], c.shape[1], c.shape[2]
@@ -630,7 +672,7 @@ def _(cubes):
 
 
 # ---------------------------------------------------------------------------
-@torch.library.custom_op("fvp::soft_argmax", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::soft_argmax", mutates_args=(), device_types="cuda")
 def soft_argmax(features: torch.Tensor, center_grid: torch.Tensor, offset: Optional[torch.Tensor],
                 beta: float) -> tuple[torch.Tensor, torch.Tensor]:
     """features [3,P,J,S,S] (or [3,P,J,S*S,1]) -> (pose [3,P,J,2] (+offset), maxprob [3,P,J])."""
@@ -654,7 +696,7 @@ def _(features, center_grid, offset, beta):
     return features.new_empty((3, P, J, 2)), features.new_empty((3, P, J))
 
 
-@torch.library.custom_op("fvp::fuse_poses", mutates_args=(), device_types="cuda")
+@_custom_op("fvp::fuse_poses", mutates_args=(), device_types="cuda")
 def fuse_poses(pose: torch.Tensor, weights: torch.Tensor, maxprob: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """pose [3,P,J,2], weights [3P,J,1] (WeightNet), maxprob [3,P,J] -> (fused [P,J,3], confs [P])."""
     pz = _dev_f32(pose, "pose")
@@ -673,34 +715,3 @@ def fuse_poses(pose: torch.Tensor, weights: torch.Tensor, maxprob: torch.Tensor)
 def _(pose, weights, maxprob):
     P, J = pose.shape[1], pose.shape[2]
     return pose.new_empty((P, J, 3)), pose.new_empty((P,))
-
-
-# -- eager fast path -------------------------------------------------------------------
-# torch.library.custom_op dispatch costs ~17 us of host time per call (measured on this
-# image: 20 vs 2.7 us for a no-op with the same signature), more than a one-frame
-# voxelize gather takes on the GPU.  The names below are therefore the ops'
-# implementations, called directly when nothing needs the dispatcher: every tensor
-# argument a plain torch.Tensor and no dispatch mode active.  Under torch.compile /
-# export, fake or functional tensors and any TorchDispatchMode the registered op
-# (torch.ops.fvp.*, with its fake kernel) runs instead.  Autograd is unaffected: the
-# module code rejects grad-requiring inputs first (forward_only), as the op would.
-def _eager_fast_path(op):
-    impl = op._init_fn
-    from torch.utils._python_dispatch import _get_current_dispatch_mode
-
-    def call(*args, **kwargs):
-        if (torch.compiler.is_compiling() or _get_current_dispatch_mode() is not None
-                or any(isinstance(a, torch.Tensor) and type(a) is not torch.Tensor
-                       for a in (*args, *kwargs.values()))):
-            return op(*args, **kwargs)
-        return impl(*args, **kwargs)
-
-    call.__name__, call.__qualname__, call.__doc__ = impl.__name__, impl.__qualname__, impl.__doc__
-    call.op = op  # the registered custom op
-    return call
-
-
-for _name, _obj in list(globals().items()):
-    if isinstance(_obj, torch._library.custom_ops.CustomOpDef):
-        globals()[_name] = _eager_fast_path(_obj)
-del _name, _obj

@@ -166,3 +166,24 @@ def test_eager_fast_path_routes_tracing_to_the_registered_op():
     assert type(cube).__name__ == "FakeTensor" and tuple(cube.shape) == (2, 15, 4, 4, 3)
     assert tuple(xy.shape) == (2, 15, 4, 4)
     assert tuple(planes_out[1].shape) == (9, 15, 4, 4)
+
+
+def test_eager_fast_path_sends_autograd_and_vmap_to_the_registered_op():
+    """A grad-requiring input (grad mode on) or an active functorch transform
+    must reach the registered op -- which has no autograd formula / batching
+    rule and raises -- never the ctypes implementation, which would return
+    outputs without a grad_fn.  Plain tensors take the fast path."""
+    import torch
+
+    from fvp import ops
+
+    t = torch.zeros(3, requires_grad=True)
+    assert ops._needs_dispatcher((t,), {})
+    with torch.no_grad():
+        assert not ops._needs_dispatcher((t,), {})
+    assert not ops._needs_dispatcher((torch.zeros(3),), {"x": 1})
+    hits = []
+    torch.func.vmap(lambda x: hits.append(ops._needs_dispatcher((x,), {})) or x)(torch.zeros(2, 3))
+    assert hits == [True]
+    assert callable(ops.fuse_poses.impl) and ops.fuse_poses.impl is not ops.fuse_poses
+    assert isinstance(ops.fuse_poses.op, torch._library.custom_ops.CustomOpDef)

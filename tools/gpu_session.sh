@@ -1,0 +1,49 @@
+#!/bin/bash
+# One gpurun session on one MI355X: the steps named on the command line, in order, each under its
+# own time limit; the first failing step ends the session.  Output under gpurun_out/$OUT (default s).
+#   tests   the -m gpu suite            smoke  __graft_entry__.smoke()
+#   bench   the default bench line (CPU baseline + traffic PMC)
+#   prof    rocprofv3 kernel trace of the default bench + per-launch-shape summary
+#   c3b8    bench.py --workload c3 --batch 8 over 200 steps
+#   jln     tools/bench_jln.py (32 frames)
+#   all     one bench line per config (C1-C5, C4/C5 at B=32)
+#   pipe    tools/bench_pipeline.py (heatmaps -> poses, and views)
+#   gloo2   bench.py --gpus 2 over gloo on the one GPU (a rehearsal of the N-rank launch)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
+O=gpurun_out/${OUT:-s}; mkdir -p $O
+fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/gpu_tests.log 2>&1 || fail tests $O/gpu_tests.log
+           tail -1 $O/gpu_tests.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+           tail -1 $O/smoke.log ;;
+    bench) timeout -k 10 600 python bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+           cut -c1-400 $O/bench.json ;;
+    prof)  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --traffic off --cpu-baseline off $BENCH_ARGS > $O/prof.log 2>&1 || fail prof $O/prof.log
+           python3 tools/launch_shapes.py $O/prof --csv $O/launch_shapes.csv --top 8 ;;
+    c3b8)  timeout -k 10 300 python bench.py --workload c3 --batch 8 --steps 200 --warmup 20 --traffic off --cpu-baseline off > $O/bench_c3_b8.json 2> $O/bench_c3_b8.err || fail c3b8 $O/bench_c3_b8.err
+           cut -c1-300 $O/bench_c3_b8.json ;;
+    jln)   timeout -k 10 300 python3 tools/bench_jln.py --frames 32 --steps 10 > $O/jln.json 2> $O/jln.err || fail jln $O/jln.err
+           cut -c1-300 $O/jln.json ;;
+    all)   for wl in c1 c2 c3 c4 c5; do
+             timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 2 --traffic off --cpu-baseline on > $O/all_$wl.json 2> $O/all_$wl.err || fail all_$wl $O/all_$wl.err
+             echo "$wl: $(cut -c1-200 $O/all_$wl.json)"
+           done
+           for wb in c4:32 c5:32; do
+             w=${wb%%:*}; b=${wb##*:}
+             timeout -k 10 300 python bench.py --workload $w --batch $b --steps 10 --warmup 2 --traffic off --cpu-baseline off > $O/all_${w}_b$b.json 2> $O/all_${w}_b$b.err || fail all_${w}_b$b $O/all_${w}_b$b.err
+           done ;;
+    pipe)  : > $O/pipeline.jsonl
+           for extra in "" "--views"; do
+             timeout -k 10 300 python3 tools/bench_pipeline.py $extra >> $O/pipeline.jsonl 2> $O/pipeline.err || fail pipe $O/pipeline.err
+           done
+           cut -c1-300 $O/pipeline.jsonl ;;
+    gloo2) FVP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 2 --traffic off --cpu-baseline off > $O/bench_gloo2.json 2> $O/bench_gloo2.err || fail gloo2 $O/bench_gloo2.err
+           cut -c1-400 $O/bench_gloo2.json ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session done $(date +%T)"

@@ -28,7 +28,7 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e6
 
-    raw = ops.nms_topk._init_fn
+    raw = ops.nms_topk.impl
     K = int(os.environ.get("NMS_K", "10"))
     print(f"nms_topk via dispatcher {bench(lambda: ops.nms_topk(prob, K)):.1f} us/call, "
           f"direct {bench(lambda: raw(prob, K)):.1f} us/call", flush=True)

@@ -1766,9 +1766,19 @@ extern "C" int fvp_maxpool2_nhwc(const float *in, int N, int H, int W, int C, fl
 extern "C" int fvp_nchw_to_nhwc(const float *in, int N, int C, int H, int W, int Cp, float *out, void *stream) {
     if (!in || !out) return FVP_ERR_NULL;
     if (N <= 0 || C <= 0 || Cp < C || H <= 0 || W <= 0) return FVP_ERR_SHAPE;
+    hipStream_t s = (hipStream_t)stream;
+    // pitches of 4..32 channels (heatmaps: 16 * ceil(J / 16)): the voxelize layout
+    // pass, one float4 per thread, a wave writing a contiguous 1 KiB run
+    switch (Cp) {
+        case 4: fvp::launch_layout<1, float>(in, N, 1, C, C, H, W, out, s); return (int)hipGetLastError();
+        case 8: fvp::launch_layout<2, float>(in, N, 1, C, C, H, W, out, s); return (int)hipGetLastError();
+        case 16: fvp::launch_layout<4, float>(in, N, 1, C, C, H, W, out, s); return (int)hipGetLastError();
+        case 32: fvp::launch_layout<8, float>(in, N, 1, C, C, H, W, out, s); return (int)hipGetLastError();
+        default: break;
+    }
     const long long total = (long long)N * H * W * Cp;
-    hipLaunchKernelGGL(fvp::nchw_to_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, in, out, N, C, H * W, Cp);
+    hipLaunchKernelGGL(fvp::nchw_to_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, out, N, C,
+                       H * W, Cp);
     return (int)hipGetLastError();
 }
 

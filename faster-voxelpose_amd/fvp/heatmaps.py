@@ -66,3 +66,40 @@ def channels_last_of(heatmaps) -> ChannelsLastHeatmaps | None:
     if mark is None or mark[1] != heatmaps._version:  # written in place since: stale
         return None
     return mark[0]
+
+
+def to_channels_last(planar: torch.Tensor) -> ChannelsLastHeatmaps:
+    """[B, V, J, H, W] fp32 on a HIP device -> its channels-last copy
+    [B, V, H, W, 16 * ceil(J / 16)] (J <= 32), one float4 layout launch
+    (fvp_nchw_to_nhwc: the voxelize layout pass over the whole batch)."""
+    from .ops import _ptr, _stream
+
+    if planar.dim() != 5 or planar.dtype != torch.float32 or planar.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: to_channels_last takes fp32 [B,V,J,H,W] on a HIP device, got "
+                            f"{tuple(planar.shape)} {planar.dtype} {planar.device}")
+    B, V, J, H, W = planar.shape
+    if J > 32:
+        raise _lib.FvpError(f"fvp: to_channels_last: {J} joints (at most 32 per pixel)")
+    cp = 16 * ((J + 15) // 16)
+    src = planar.contiguous()
+    t = torch.empty((B, V, H, W, cp), dtype=torch.float32, device=planar.device)
+    if t.numel():
+        _lib.call("fvp_nchw_to_nhwc", _ptr(src), B * V, J, H, W, cp, _ptr(t), _stream(t))
+    return ChannelsLastHeatmaps(t, J)
+
+
+def share_channels_last(heatmaps) -> ChannelsLastHeatmaps | None:
+    """Lay `heatmaps` out channels-last once and attach the copy (the fused
+    HDN forward does this so that the JLN, handed the same tensor object,
+    reads the same copy): planar fp32 tensors of <= 32 joints on a HIP device
+    that do not already carry a valid copy.  Returns the copy in use, if any."""
+    cl = channels_last_of(heatmaps)
+    if cl is not None or not isinstance(heatmaps, torch.Tensor):
+        return cl
+    if (heatmaps.dim() != 5 or heatmaps.dtype != torch.float32 or heatmaps.device.type != "cuda"
+            or heatmaps.shape[2] > 32 or heatmaps.shape[0] == 0
+            or (torch.is_grad_enabled() and heatmaps.requires_grad)):
+        return None
+    cl = to_channels_last(heatmaps)
+    attach(heatmaps, cl)
+    return cl

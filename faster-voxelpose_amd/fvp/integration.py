@@ -43,6 +43,7 @@ import torch
 
 from . import backbone as fvp_backbone
 from . import cnn as fvp_cnn
+from . import heatmaps as fvp_heatmaps
 from . import jln, project_individual, project_whole, proposal
 
 
@@ -72,7 +73,12 @@ class FvpOptions:
       fast or faster).  Default from the environment variable
       FVP_RECOMPUTE_COLUMNS (0 / 1) when set.
     c2c_graphs: with cnn, the launch-bound 1-D C2CNet replays from a
-      hipGraph per column-batch shape (fvp.cnn.GraphedCNN)."""
+      hipGraph per column-batch shape (fvp.cnn.GraphedCNN).
+    share_layout: fused_hdn_forward lays planar fp32 heatmaps out channels-last
+      ONCE for the batch (fvp.heatmaps.to_channels_last) and attaches the copy
+      to the heatmaps tensor, so its own gather and the JLN's person planes
+      (the same tensor object, faster_voxelpose.py:85-93) both read it in
+      place -- one layout pass per batch instead of one per consumer."""
     cnn: bool = False
     cnn_dtype: torch.dtype = torch.float32
     backbone: bool = False
@@ -80,6 +86,7 @@ class FvpOptions:
     recompute_columns: bool | None = dataclasses.field(default_factory=_env_recompute)
     recompute_cube_bytes: int = 512 << 20
     c2c_graphs: bool = True
+    share_layout: bool = True
 
 
 DEFAULT_OPTIONS = FvpOptions()
@@ -185,6 +192,8 @@ def fused_hdn_forward(self, heatmaps, meta, cameras, resize_transform):
     batch_size = heatmaps.shape[0]
     opts = options_of(self)
     pl_ = self.project_layer
+    if opts.share_layout:
+        fvp_heatmaps.share_channels_last(heatmaps)
     recompute = opts.recompute_columns
     if recompute is None:
         X, Y, Z = (int(v) for v in pl_.voxels_per_axis)

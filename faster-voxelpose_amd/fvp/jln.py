@@ -68,8 +68,9 @@ def fused_jln_forward(self, meta, heatmaps, proposal_centers, mask, cameras, res
 def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform, all_fused, all_pose, first):
     sub_meta = dict(meta)
     sub_meta["seq"] = [meta["seq"][first]] * heatmaps.shape[0]
+    idx = mask.nonzero()  # the batch's one host sync; the scatters below index with it (no further syncs)
     planes, offset, _ = self.project_layer.forward_batch(heatmaps, sub_meta, proposal_centers, mask, cameras,
-                                                         resize_transform)
+                                                         resize_transform, idx=idx)
     P = planes.shape[0] // 3
     if P == 0:
         return
@@ -84,6 +85,7 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
     wnet = cnn.cached(self.weight_net) if use and not self.weight_net.training else self.weight_net
     weights = wnet(features)                                                        # [3P,J,1]
     fused, confs = ops.fuse_poses(pose, weights, maxprob)
-    all_fused[mask] = fused
-    all_pose[:, mask] = pose
-    proposal_centers[mask, 4] = confs
+    fi, ki = idx[:, 0], idx[:, 1]  # mask's (frame, proposal) pairs in mask order, as the boolean scatters
+    all_fused[fi, ki] = fused
+    all_pose[:, fi, ki] = pose
+    proposal_centers[fi, ki, 4] = confs

@@ -354,11 +354,18 @@ def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, to
     return vals, xy, flat
 
 
-@_custom_op("fvp::nms_topk_columns", mutates_args=(), device_types="cuda")
-def nms_topk_columns(prob: torch.Tensor, K: int,
-                     cube: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
-    """nms_topk + gather_columns in one launch (fvp_nms_topk_columns): the map's
-    top-K and the winners' z-columns [B,K,J,Z] of cube [B,J,X,Y,Z]."""
+def proposal_buffers(B: int, K: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """(vals [B,K] fp32, flat [B,K] int64), both contiguous, back to back in ONE
+    buffer (flat's 8BK bytes, then vals' 4BK): the proposals leave a rank as that
+    one buffer (fvp.parallel.gather_proposals, no packing kernels)."""
+    buf = torch.empty((12 * B * K,), dtype=torch.uint8, device=device)
+    flat = buf[: 8 * B * K].view(torch.int64).view(B, K)
+    vals = buf[8 * B * K:].view(torch.float32).view(B, K)
+    return vals, flat
+
+
+def _nms_topk_columns_into(prob, K, cube, vals, flat):
+    """fvp_nms_topk_columns into the caller's vals [B,K] fp32 / flat [B,K] int64."""
     if prob.device.type != "cuda":
         raise _lib.FvpError(f"fvp: prob_map must be on a HIP device, got {prob.device}")
     c = _dev_f32(cube, "feature_cubes")
@@ -371,8 +378,6 @@ def nms_topk_columns(prob: torch.Tensor, K: int,
         p = p.to(torch.float32).contiguous()
     stride = p.stride()[0] if B > 1 else X * Y
     J, Z = c.shape[1], c.shape[4]
-    vals = torch.empty((B, K), dtype=torch.float32, device=p.device)
-    flat = torch.empty((B, K), dtype=torch.int64, device=p.device)
     xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
     cols = torch.empty((B, K, J, Z), dtype=torch.float32, device=p.device)
     if B == 0 or cols.numel() == 0:
@@ -380,6 +385,17 @@ def nms_topk_columns(prob: torch.Tensor, K: int,
     _lib.call("fvp_nms_topk_columns", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _ptr(c), J, Z,
               _ptr(cols), _stream(p))
     return vals, xy, flat, cols
+
+
+@_custom_op("fvp::nms_topk_columns", mutates_args=(), device_types="cuda")
+def nms_topk_columns(prob: torch.Tensor, K: int,
+                     cube: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """nms_topk + gather_columns in one launch (fvp_nms_topk_columns): the map's
+    top-K and the winners' z-columns [B,K,J,Z] of cube [B,J,X,Y,Z]."""
+    B = prob.shape[0]
+    vals = torch.empty((B, K), dtype=torch.float32, device=prob.device)
+    flat = torch.empty((B, K), dtype=torch.int64, device=prob.device)
+    return _nms_topk_columns_into(prob, K, cube, vals, flat)
 
 
 @nms_topk_columns.register_fake
@@ -715,3 +731,14 @@ def fuse_poses(pose: torch.Tensor, weights: torch.Tensor, maxprob: torch.Tensor)
 def _(pose, weights, maxprob):
     P, J = pose.shape[1], pose.shape[2]
     return pose.new_empty((P, J, 3)), pose.new_empty((P,))
+
+
+def nms_topk_columns_joint(prob: torch.Tensor, K: int, cube: torch.Tensor):
+    """nms_topk_columns with vals / flat in one buffer (proposal_buffers), so
+    fvp.parallel.gather_proposals sends them as they are -- eager only: a
+    custom op's outputs may not alias each other, so under the dispatcher
+    (compile, fake or functional tensors, dispatch modes) the registered op runs."""
+    if _needs_dispatcher((prob, cube), {}):
+        return nms_topk_columns(prob, K, cube)
+    vals, flat = proposal_buffers(prob.shape[0], K, prob.device)
+    return _nms_topk_columns_into(prob, K, cube, vals, flat)

@@ -39,16 +39,41 @@ def unpack_proposals(packed: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.
     return vals, flat
 
 
+def _joint_buffer(vals: torch.Tensor, flat: torch.Tensor):
+    """The uint8 buffer holding flat [B,K] int64 then vals [B,K] fp32 back to back
+    (fvp.ops.proposal_buffers, as the NMS writes them), or None."""
+    n = flat.numel()
+    if (flat.dtype != torch.int64 or vals.dtype != torch.float32 or vals.shape != flat.shape or n == 0
+            or not flat.is_contiguous() or not vals.is_contiguous()):
+        return None
+    st = flat.untyped_storage()
+    if (vals.untyped_storage().data_ptr() != st.data_ptr() or st.nbytes() != 12 * n or flat.storage_offset() != 0
+            or vals.data_ptr() != flat.data_ptr() + 8 * n):
+        return None
+    return torch.empty(0, dtype=torch.uint8, device=flat.device).set_(st, 0, (12 * n,))
+
+
 def gather_proposals(vals: torch.Tensor, flat: torch.Tensor, group=None) -> tuple[torch.Tensor, torch.Tensor]:
     """All ranks' proposals in rank order (every rank must hold the same number of frames)."""
-    K = vals.shape[1]
-    local = pack_proposals(vals, flat)
+    B, K = vals.shape
     world = dist.get_world_size(group)
-    out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype, device=local.device)
+    buf = _joint_buffer(vals, flat)
     # (nccl = RCCL and gloo both implement the fused form; any failure, a
     # timeout included, propagates -- no second collective is attempted)
-    dist.all_gather_into_tensor(out, local, group=group)
-    return unpack_proposals(out, K)
+    if buf is None:  # separate tensors: pack them into one (two small kernels)
+        local = pack_proposals(vals, flat)
+        out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local, group=group)
+        return unpack_proposals(out, K)
+    # the NMS wrote both into one buffer: it leaves as it is, and every rank's
+    # part is read back through views (copies only to merge ranks, N > 1)
+    n = B * K
+    out = torch.empty((world * 12 * n,), dtype=torch.uint8, device=buf.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    rows = out.view(world, 12 * n)
+    flat_all = rows[:, : 8 * n].contiguous().view(torch.int64) if world > 1 else rows[0, : 8 * n].view(torch.int64)
+    vals_all = rows[:, 8 * n:].contiguous().view(torch.float32) if world > 1 else rows[0, 8 * n:].view(torch.float32)
+    return vals_all.reshape(world * B, K), flat_all.reshape(world * B, K)
 
 
 def shard_slab(X: int, world: int, rank: int) -> tuple[int, int]:

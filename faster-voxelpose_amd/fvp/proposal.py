@@ -35,7 +35,7 @@ def nms2D(prob_map: torch.Tensor, max_num: int):
 def nms2D_columns(prob_map: torch.Tensor, max_num: int, feature_cubes: torch.Tensor):
     """nms2D followed by gather_columns at its winners (human_detection_net.py:188,
     :199-200) in one launch: (topk_values, topk_index, topk_flatten_index, feature_1d [B,K,J,Z])."""
-    return ops.nms_topk_columns(prob_map.detach(), int(max_num), feature_cubes)
+    return ops.nms_topk_columns_joint(prob_map.detach(), int(max_num), feature_cubes)
 
 
 def gather_columns(feature_cubes: torch.Tensor, topk_flatten_index: torch.Tensor) -> torch.Tensor:

@@ -44,12 +44,19 @@ def _frames_result(first, count):
     return torch.from_numpy(vals), torch.from_numpy(flat)
 
 
-def _worker(rank, world, port, total, q):
+def _worker(rank, world, port, total, q, joint=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         s, e = parallel.shard_frames(total, world, rank)
         vals, flat = _frames_result(s, e - s)
+        if joint:  # as the HIP NMS writes them: one buffer, sent without packing
+            from fvp import ops
+            jv, jf = ops.proposal_buffers(vals.shape[0], vals.shape[1], "cpu")
+            jv.copy_(vals)
+            jf.copy_(flat)
+            assert parallel._joint_buffer(jv, jf) is not None
+            vals, flat = jv, jf
         gv, gf = parallel.gather_proposals(vals, flat)
         if rank == 0:
             q.put((gv.numpy(), gf.numpy()))
@@ -68,6 +75,16 @@ def test_shard_frames_partitions_exactly():
         parallel.shard_frames(4, 2, 2)
 
 
+def test_joint_buffer_is_recognised_only_when_exact():
+    from fvp import ops
+
+    v, f = ops.proposal_buffers(2, 5, "cpu")
+    assert parallel._joint_buffer(v, f) is not None
+    assert parallel._joint_buffer(v.clone(), f) is None
+    assert parallel._joint_buffer(v, f.clone()) is None
+    assert parallel._joint_buffer(v[:1], f[:1]) is None
+
+
 def test_pack_roundtrip_is_lossless():
     g = torch.Generator().manual_seed(0)
     v = torch.randn(5, 10, generator=g)
@@ -79,12 +96,13 @@ def test_pack_roundtrip_is_lossless():
     assert torch.equal(v2.view(torch.int32), v.view(torch.int32))
 
 
-def test_two_rank_gloo_sharded_proposals_match_single_process():
-    world, total = 2, 4
+@pytest.mark.parametrize("world,joint", [(2, False), (2, True), (3, True)])
+def test_two_rank_gloo_sharded_proposals_match_single_process(world, joint):
+    total = 2 * world
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q, joint)) for r in range(world)]
     for p in procs:
         p.start()
     gv, gf = q.get(timeout=300)

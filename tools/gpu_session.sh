@@ -9,6 +9,9 @@
 #   all     one bench line per config (C1-C5, C4/C5 at B=32)
 #   pipe    tools/bench_pipeline.py (heatmaps -> poses, and views)
 #   gloo2   bench.py --gpus 2 over gloo on the one GPU (a rehearsal of the N-rank launch)
+#   ab      for each library ab_libs/<name>.so in $AB_LIBS (tools/ab_build.sh), REPEAT (2) rounds of:
+#           a bench line (no traffic / CPU baseline) + a kernel trace with its launch shapes
+#   step    tools/step_host.py (host / GPU time per part of the small-batch step; $STEP_ARGS)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 O=gpurun_out/${OUT:-s}; mkdir -p $O
@@ -43,6 +46,18 @@ for step in "$@"; do
            cut -c1-300 $O/pipeline.jsonl ;;
     gloo2) FVP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 2 --traffic off --cpu-baseline off > $O/bench_gloo2.json 2> $O/bench_gloo2.err || fail gloo2 $O/bench_gloo2.err
            cut -c1-400 $O/bench_gloo2.json ;;
+    ab)    for rep in $(seq 1 ${REPEAT:-2}); do
+             for lib in $AB_LIBS; do
+               FVP_LIB=ab_libs/$lib.so timeout -k 10 300 python bench.py --traffic off --cpu-baseline off $BENCH_ARGS > $O/ab_${lib}_$rep.json 2> $O/ab_${lib}_$rep.err || fail ab_$lib $O/ab_${lib}_$rep.err
+               echo "$lib $rep: $(python3 -c "import json,sys; b=json.loads(open(sys.argv[1]).readlines()[-1]); r=b['roofline']; print(b['value'], r['kernel_ms'], r['frac'], r.get('channels_last_input',{}).get('frac'))" $O/ab_${lib}_$rep.json)"
+               if [ "$rep" = 1 ]; then
+                 FVP_LIB=ab_libs/$lib.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/abprof_$lib -o run -- python3 bench.py --traffic off --cpu-baseline off $BENCH_ARGS > $O/abprof_$lib.log 2>&1 || fail abprof_$lib $O/abprof_$lib.log
+                 python3 tools/launch_shapes.py $O/abprof_$lib --csv $O/abprof_$lib.csv --top 4
+               fi
+             done
+           done ;;
+    step)  timeout -k 10 300 python3 tools/step_host.py $STEP_ARGS > $O/step.json 2> $O/step.err || fail step $O/step.err
+           cat $O/step.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -30,7 +30,7 @@ def main():
 
     raw = ops.nms_topk.impl
     K = int(os.environ.get("NMS_K", "10"))
-    print(f"nms_topk via dispatcher {bench(lambda: ops.nms_topk(prob, K)):.1f} us/call, "
+    print(f"nms_topk via dispatcher {bench(lambda: ops.nms_topk.op(prob, K)):.1f} us/call, "
           f"direct {bench(lambda: raw(prob, K)):.1f} us/call", flush=True)
 
 

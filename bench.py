@@ -6,7 +6,8 @@ resident in HBM:
   fvp_voxelize (cube [B,J,X,Y,Z] + xy max-plane, one launch)
   -> fvp_nms_topk_columns: NMS top-K on the root-joint xy plane (stand-in for
      CenterNet's map) and the winners' z-columns [B,K,J,Z] in one launch
-  -> (N > 1) one RCCL all_gather of the compact proposals.
+  -> (N > 1) one RCCL all_gather of the compact proposals (the NMS writes them
+     into one buffer, sent as it is; at N = 1 there is nothing to exchange).
 Frames are sharded across ranks (weak scaling).  Default workload: C2 =
 BASELINE configs[1] (Shelf calibration, 5 cams, J=15, 128x240 -> 80x80x20).
 
@@ -38,8 +39,8 @@ METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roo
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the fvp_voxelize op: layout pass (fp32 channels-last, fp16 pair table per 8 entries, per row or per
 # entry) + gather
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel", "pairs_rows_kernel",
-               "voxelize_kernel", "voxelize_cams_kernel")
+VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_cl_t16_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel",
+               "pairs_rows_kernel", "voxelize_kernel", "voxelize_cams_kernel")
 
 
 def parse(argv=None):
@@ -708,13 +709,14 @@ def main():
                 "global_batch": B if args.slabs else world * B,
                 "parallelism": ((f"x-slab x{world}" + (f" + {collective} all_gather of xy slabs, all_reduce of columns"
                                                        if world > 1 else "") if args.slabs else
-                                 f"frame-sharded x{world}" + (f" + {collective} all_gather of proposals" if grouped else ""))
+                                 f"frame-sharded x{world}" + (f" + {collective} all_gather of proposals" if grouped and world > 1
+                                                              else " (one rank: no collective)"))
                                 + (f" -- rehearsal (gloo, {world} ranks on {n_devices} shared device(s)), not a measurement"
                                    if rehearsal else "")),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("fvp_voxelize op = layout pass (heatmaps_to_cl / heatmaps_to_pairs) + voxelize_kernel per "
+                "kernel": ("fvp_voxelize op = layout pass (heatmaps_to_cl_t16 / pairs_vec8) + voxelize_kernel per "
                            "frame chunk" if args.heatmap_layout == "planar" else
                            "fvp_voxelize_cl op = voxelize_kernel on channels-last heatmaps (no layout pass)"),
                 "achieved": round(achieved, 1),

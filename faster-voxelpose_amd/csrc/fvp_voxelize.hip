@@ -652,6 +652,38 @@ struct VoxJob {
     float *cube, *xy;
 };
 
+// Layout of chunk k+1 on a side stream under the gather of chunk k (fp32
+// channels-last table): two tables in the workspace, events both ways.  The
+// layout is HBM-bound and light on the texture path (heatmaps_to_cl_t16_kernel),
+// the gather texture-path-bound.  One side stream per device, created on first
+// use (not thread-safe: one host thread per device, as the reference's loop).
+#ifndef FVP_LAYOUT_OVERLAP
+#define FVP_LAYOUT_OVERLAP 0
+#endif
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t start = nullptr, ready[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
+};
+
+static SideStream *side_stream() {
+    static SideStream sides[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream &sd = sides[dev];
+    if (!sd.s) {
+        if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        hipEvent_t *evs[5] = {&sd.start, &sd.ready[0], &sd.ready[1], &sd.freed[0], &sd.freed[1]};
+        for (hipEvent_t *e : evs)
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    return &sd;
+}
+
+// Frames per chunk and tables in the workspace: one table of chunk_frames(), or
+// with the overlap (fp32, not the pair table) two of kOverlapFrames.
+constexpr int kOverlapFrames = 8;
+static bool overlap_layout(bool pairs) { return FVP_LAYOUT_OVERLAP && !pairs; }
+
 // Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
 // layout pass into the workspace, then the gather, NF frames per table entry.
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, typename T>
@@ -659,23 +691,56 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
                       hipStream_t s) {
     const bool half = sizeof(T) == 2;
     const int B = last - first;
-    const int chunk = max(NF, chunk_frames(B, j.V, j.J, j.H, j.W, half) / NF * NF);
+    const bool ovl = !PAIR && overlap_layout(false) && B > min(kOverlapFrames, chunk_frames(B, j.V, j.J, j.H, j.W, half));
+    const int chunk = ovl ? min(kOverlapFrames, chunk_frames(B, j.V, j.J, j.H, j.W, half))
+                          : max(NF, chunk_frames(B, j.V, j.J, j.H, j.W, half) / NF * NF);
     GatherCfg c;
     if (gather_cfg<LPV, OTF>(min(chunk, B), NF, j.V, j.X, j.Y, j.Z, c) != FVP_OK) return FVP_ERR_SHAPE;
     const size_t frame_elems = (size_t)j.V * j.Jst * j.H * j.W;
-    for (int f0 = first; f0 < last; f0 += chunk) {
-        const int nb = min(chunk, last - f0);
+    auto layout = [&](int f0, int nb, void *buf, hipStream_t st) {
         const T *hsrc = hm + (size_t)f0 * frame_elems;
         if constexpr (PAIR) {  // (J <= 16: never sliced)
             launch_pairs<NF>(reinterpret_cast<const _Float16 *>(hsrc), nb, j.V, j.J, j.H, j.W,
-                             reinterpret_cast<uint4 *>(ws), s);
+                             reinterpret_cast<uint4 *>(buf), st);
         } else {
-            launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
+            launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(buf), st);
         }
-        launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
+    };
+    auto gather = [&](int f0, int nb, const void *buf) {
+        launch_gather<LPV, PAIR, OTF, CASC, NF>(buf, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
                                                j.Z, j.cube, j.xy, 4u * 4u * LPV, s);
+    };
+    SideStream *sd = ovl ? side_stream() : nullptr;
+    if (!sd) {
+        for (int f0 = first; f0 < last; f0 += chunk) {
+            const int nb = min(chunk, last - f0);
+            layout(f0, nb, ws, s);
+            gather(f0, nb, ws);
+        }
+        return (int)hipGetLastError();
     }
-    return (int)hipGetLastError();
+    void *bufs[2] = {ws, (char *)ws + (size_t)chunk * frame_bytes(j.V, j.J, j.H, j.W, half)};
+    const int n = (B + chunk - 1) / chunk;
+    hipError_t err = hipSuccess;
+    auto chk = [&](hipError_t r) {
+        if (r != hipSuccess && err == hipSuccess) err = r;
+    };
+    chk(hipEventRecord(sd->start, s));  // the side stream starts after the caller's earlier work
+    chk(hipStreamWaitEvent(sd->s, sd->start, 0));
+    layout(first, min(chunk, B), bufs[0], sd->s);
+    chk(hipEventRecord(sd->ready[0], sd->s));
+    for (int k = 0; k < n && err == hipSuccess; ++k) {
+        const int f0 = first + k * chunk;
+        if (k + 1 < n) {  // chunk k+1 into the table chunk k-1's gather has finished reading
+            if (k >= 1) chk(hipStreamWaitEvent(sd->s, sd->freed[(k - 1) & 1], 0));
+            layout(f0 + chunk, min(chunk, last - f0 - chunk), bufs[(k + 1) & 1], sd->s);
+            chk(hipEventRecord(sd->ready[(k + 1) & 1], sd->s));
+        }
+        chk(hipStreamWaitEvent(s, sd->ready[k & 1], 0));
+        gather(f0, min(chunk, last - f0), bufs[k & 1]);
+        chk(hipEventRecord(sd->freed[k & 1], s));
+    }
+    return err != hipSuccess ? (int)err : (int)hipGetLastError();
 }
 
 // -- the camera-synchronous gather's launches ------------------------------------
@@ -917,7 +982,10 @@ static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, c
 static size_t workspace_bytes(int B, int V, int J, int H, int W, bool half) {
     if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
     const int J1 = slice_joints(J);  // one joint slice's copy at a time
-    const size_t tab = (size_t)chunk_frames(B, V, J1, H, W, half) * frame_bytes(V, J1, H, W, half);
+    const int cf = chunk_frames(B, V, J1, H, W, half);
+    size_t tab = (size_t)cf * frame_bytes(V, J1, H, W, half);
+    if (overlap_layout(use_pairs(J1, half)) && B > min(kOverlapFrames, cf))  // run_chunks: two tables
+        tab = 2 * (size_t)min(kOverlapFrames, cf) * frame_bytes(V, J1, H, W, half);
     // fp32 with the sync gather: + its pacing counters (run_chunks_sync)
     return (half || !FVP_GATHER_SYNC) ? tab : ((tab + 255) & ~(size_t)255) + kSyncCtrBytes;
 }

@@ -57,6 +57,8 @@ def gather_proposals(vals: torch.Tensor, flat: torch.Tensor, group=None) -> tupl
     """All ranks' proposals in rank order (every rank must hold the same number of frames)."""
     B, K = vals.shape
     world = dist.get_world_size(group)
+    if world == 1:  # nothing to exchange: the rank's own proposals (no collective launch)
+        return vals, flat
     buf = _joint_buffer(vals, flat)
     # (nccl = RCCL and gloo both implement the fused form; any failure, a
     # timeout included, propagates -- no second collective is attempted)

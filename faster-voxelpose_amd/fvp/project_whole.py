@@ -54,6 +54,7 @@ class ProjectLayer(nn.Module):
         self._grid = None
         self.sample_grid = {}  # seq -> [V, 1, N, 2] fp32 (the reference's cache layout; a view of _packed)
         self._packed = {}      # seq -> [N, GV, 2] voxel-major copy read by the voxelize kernel
+        self._packed_of = {}   # seq -> (the sample_grid entry it was checked against, its packed grid)
         self._cams = {}        # seq -> [V, FVP_CAM_STRIDE] camera records (on-the-fly projection)
         self._stacked = (None, None)  # (key, [S,N,GV,2]) grids of the last mixed-sequence batch
         self.on_the_fly = None  # None: decide by grid size; True/False: force
@@ -101,25 +102,31 @@ class ProjectLayer(nn.Module):
 
     def _packed_grid(self, seq) -> torch.Tensor:
         sg = self.sample_grid[seq]
+        hit = self._packed_of.get(seq)
+        if hit is not None and hit[0] is sg:  # the cache entry is still the view this layer made
+            return hit[1]
         pg = self._packed.get(seq)
         if pg is None or ops.packed_as_reference(pg, sg.shape[0]).data_ptr() != sg.data_ptr():
             # a grid assigned from outside (e.g. a reference-layout tensor): pack it once
             pg = ops.pack_grid(sg[:, 0].to(torch.float32).contiguous())
             self._packed[seq] = pg
+        self._packed_of[seq] = (sg, pg)
         return pg
 
     def _grids_for_batch(self, heatmaps, meta, cameras, resize_transform):
         device = heatmaps.device
         n = heatmaps.shape[1]
         seqs = list(meta["seq"])[: heatmaps.shape[0]]
-        for curr_seq in seqs:
+        uniq = list(dict.fromkeys(seqs))
+        # project_whole.py:147-156 per frame; the checks and the cache depend on
+        # the sequence alone, so each distinct sequence is checked once, in order
+        for curr_seq in uniq:
             assert curr_seq in cameras.keys(), "missing camera parameters for the current sequence"
             assert len(cameras[curr_seq]) == n, "inconsistent number of cameras"
             if curr_seq not in self.sample_grid:
                 if self.verbose:
                     print("=> save the sampling grid in HDN for sequence", curr_seq)
                 self.sample_grid[curr_seq] = self.build_sample_grid(cameras, curr_seq, resize_transform, device)
-        uniq = list(dict.fromkeys(seqs))
         if len(uniq) == 1:
             return self._packed_grid(uniq[0]), None
         index = torch.tensor([uniq.index(s) for s in seqs], dtype=torch.int32).to(device, non_blocking=True)
@@ -147,12 +154,12 @@ class ProjectLayer(nn.Module):
         device = heatmaps.device
         n = heatmaps.shape[1]
         seqs = list(meta["seq"])[: heatmaps.shape[0]]
-        for curr_seq in seqs:
+        uniq = list(dict.fromkeys(seqs))
+        for curr_seq in uniq:
             assert curr_seq in cameras.keys(), "missing camera parameters for the current sequence"
             assert len(cameras[curr_seq]) == n, "inconsistent number of cameras"
             if curr_seq not in self._cams:
                 self._cams[curr_seq] = torch.from_numpy(geometry.pack_cameras(cameras, curr_seq)).to(device)
-        uniq = list(dict.fromkeys(seqs))
         if len(uniq) == 1:
             return self._cams[uniq[0]], None
         index = torch.tensor([uniq.index(s) for s in seqs], dtype=torch.int32).to(device, non_blocking=True)

@@ -112,6 +112,19 @@ def main():
 
     ms_cl = timeit(batched_cl)
 
+    # the drop-in flow on planar input: the fused HDN forward lays the batch out
+    # channels-last once and attaches the copy to the heatmaps tensor
+    # (fvp.heatmaps.share_channels_last, integration.FvpOptions.share_layout),
+    # and the JLN, handed the same tensor, reads it in place
+    from fvp.heatmaps import share_channels_last
+    hm_shared = hm.clone()
+    share_channels_last(hm_shared)
+
+    def batched_shared():
+        layer.forward_batch(hm_shared, meta, allp, mask, cams, rt)
+
+    ms_shared = timeit(batched_shared)
+
     # JLN post-processing on device (soft-argmax + offsets + fusion) on stand-in
     # CNN outputs of the same shape: reads 3*J*S*S*4 B of joint maps per proposal
     from fvp import ops
@@ -151,6 +164,7 @@ def main():
         "cube_bytes_per_proposal": J * 64 ** 3 * 4, "plane_bytes_per_proposal": 3 * J * 64 * 64 * 4,
         "per_frame_calls_us_per_proposal": round(ms_frame * 1e3 / n_prop, 2),
         "channels_last_input_us_per_proposal": round(ms_cl * 1e3 / n_prop, 2),
+        "planar_drop_in_us_per_proposal": round(ms_shared * 1e3 / n_prop, 2),
         "path": "forward_batch: one fvp_person_planes launch for all frames' proposals (fused planes, no cubes)",
         "cache_build": cache,
         "tap_stream": {"window_voxels_per_proposal": round(float(win.mean()), 1),

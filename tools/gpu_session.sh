@@ -12,6 +12,8 @@
 #   ab      for each library ab_libs/<name>.so in $AB_LIBS (tools/ab_build.sh), REPEAT (2) rounds of:
 #           a bench line (no traffic / CPU baseline) + a kernel trace with its launch shapes
 #   step    tools/step_host.py (host / GPU time per part of the small-batch step; $STEP_ARGS)
+#   overlap tools/overlap_probe2.py for each library in $AB_LIBS
+#   pmcl2   TCC_HIT / TCC_MISS (one counter pass each) of a short bench run per library in $AB_LIBS
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 O=gpurun_out/${OUT:-s}; mkdir -p $O
@@ -58,6 +60,16 @@ for step in "$@"; do
            done ;;
     step)  timeout -k 10 300 python3 tools/step_host.py $STEP_ARGS > $O/step.json 2> $O/step.err || fail step $O/step.err
            cat $O/step.json ;;
+    overlap) for lib in $AB_LIBS; do
+             FVP_LIB=ab_libs/$lib.so timeout -k 10 300 python3 tools/overlap_probe2.py $OVERLAP_ARGS > $O/overlap_$lib.jsonl 2> $O/overlap_$lib.err || fail overlap_$lib $O/overlap_$lib.err
+             cat $O/overlap_$lib.jsonl
+           done ;;
+    pmcl2) for lib in $AB_LIBS; do
+             for c in TCC_HIT_sum TCC_MISS_sum; do
+               FVP_LIB=ab_libs/$lib.so timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_${lib}_$c -o run -- python3 bench.py --traffic off --cpu-baseline off --steps 3 --warmup 1 $BENCH_ARGS > $O/pmc_${lib}_$c.log 2>&1 || fail pmc_${lib}_$c $O/pmc_${lib}_$c.log
+             done
+           done
+           python3 tools/pmc_kernels.py $O/pmc_* ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -49,7 +49,6 @@ def main():
     ref_cube, ref_xy = layer.forward_fused(hm, {"seq": [seq] * F}, cams, rt)
     frame_elems = V * J * Hd * Wd
     s_main = torch.cuda.current_stream(dev)
-    lo_pri, hi_pri = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
     s_lay = torch.cuda.Stream(dev)
     s_lay_hi = torch.cuda.Stream(dev, priority=-1)
     cube = torch.empty_like(ref_cube)
@@ -57,15 +56,18 @@ def main():
     csz, xsz = J * X * Y * Z, J * X * Y
 
     for C in [int(c) for c in args.chunks.split(",")]:
-        n = F // C
+        n = (F + C - 1) // C  # (the last chunk may be short)
         bufs = [torch.empty((C, V, Hd, Wd, 16), device=dev) for _ in range(2)]
 
+        def nb(k):
+            return min(C, F - k * C)
+
         def layout(k, buf, stream):
-            _lib.check(L.fvp_nchw_to_nhwc(hm.data_ptr() + k * C * frame_elems * 4, C * V, J, Hd, Wd, 16,
+            _lib.check(L.fvp_nchw_to_nhwc(hm.data_ptr() + k * C * frame_elems * 4, nb(k) * V, J, Hd, Wd, 16,
                                           buf.data_ptr(), stream.cuda_stream), "layout")
 
         def gather(k, buf, stream):
-            _lib.check(L.fvp_voxelize_cl(buf.data_ptr(), 16, C, V, J, Hd, Wd, grids.data_ptr(), None, X, Y, Z,
+            _lib.check(L.fvp_voxelize_cl(buf.data_ptr(), 16, nb(k), V, J, Hd, Wd, grids.data_ptr(), None, X, Y, Z,
                                          cube.data_ptr() + k * C * csz * 4, xy.data_ptr() + k * C * xsz * 4,
                                          stream.cuda_stream), "gather")
 

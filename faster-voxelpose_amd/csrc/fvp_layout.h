@@ -29,14 +29,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base,
 // one float4 (a wave writes a contiguous 1 KiB run; NF > 1: runs of JP*4 B,
 // the NF frames of a group interleaved per pixel: [b/NF][V][H*W][NF][JP]).
 // (J joints of a slice; Jst = the planes per (frame, view) of the source)
-// `zero` (optional): nzero words block 0 clears on the way -- the pacing
-// counters of the gather that follows on the same stream (voxelize_sync_kernel).
 template <int LPV, typename T, int NF = 1>
 __global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict__ hm, float4 *__restrict__ cl, int J,
-                                                             int Jst, int HW, int V, long long total_px,
-                                                             unsigned *__restrict__ zero, int nzero) {
-    if (zero && blockIdx.x == 0)
-        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0u;
+                                                             int Jst, int HW, int V, long long total_px) {
     const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
     const long long pxg = gid / LPV;
     const int q = (int)(gid - pxg * LPV);
@@ -56,63 +51,6 @@ __global__ __launch_bounds__(256) void heatmaps_to_cl_kernel(const T *__restrict
         const long long fr = bv / V;  // frame within the chunk
         const long long g = fr / NF, f = fr - (fr / NF) * NF, v = bv - fr * V;
         cl[(((g * V + v) * HW + pix) * NF + f) * LPV + q] = o;
-    }
-}
-
-// The same layout (LPV = 4: J <= 16, JP = 16, one frame per entry) with the
-// fewest vector-memory instructions: the texture path charges ~16 clocks per
-// wave instruction however many bytes it moves, and the thread-per-(pixel,
-// quad) kernel above issues 4-B loads whose adjacent lanes hit 4 different
-// planes.  Here a block takes 256 pixels of one (frame, view) image: each wave
-// loads 1 KiB runs of one plane (16 B = 4 pixels per lane), the 16 x 256 tile
-// is transposed through LDS, and each wave stores 1 KiB runs of [pixel][16]:
-// 32 wave instructions per 16 KB in and out, against 80 (and 4-way line
-// splits on every load) above.  Needs HW % 4 == 0 (16-B aligned plane rows).
-constexpr int kT16Pix = 256;
-constexpr int kT16Pitch = kT16Pix + 2;  // LDS row pitch: (8q + pixel) mod 32 distinct for the transposed reads
-
-template <typename T>
-__global__ __launch_bounds__(256) void heatmaps_to_cl_t16_kernel(const T *__restrict__ hm, f32x4 *__restrict__ cl,
-                                                                 int J, int Jst, int HW, int tiles_per_img,
-                                                                 unsigned *__restrict__ zero, int nzero) {
-    __shared__ float t[16 * kT16Pitch];
-    if (zero && blockIdx.x == 0)
-        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0u;
-    const int img = blockIdx.x / tiles_per_img;  // (frame, view)
-    const int p0 = (blockIdx.x - img * tiles_per_img) * kT16Pix;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const T *__restrict__ src = hm + (size_t)img * Jst * HW;
-    // wave w loads planes 4w .. 4w+3, lane l pixels p0 + 4l .. 4l + 3
-    const int px = p0 + 4 * lane;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int j = 4 * wave + k;
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
-        if (j < J && px < HW) {
-            if constexpr (sizeof(T) == 4) {
-                const f32x4 x = *reinterpret_cast<const f32x4 *>(src + (size_t)j * HW + px);
-                v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = to_f32(src[(size_t)j * HW + px + e]);
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) t[j * kT16Pitch + 4 * lane + e] = v[e];
-    }
-    __syncthreads();
-    // store r: pixel p0 + 64 r + lane / 4, joint quad lane % 4 -> one 1 KiB run per wave
-    f32x4 *__restrict__ dst = cl + ((size_t)img * HW + p0) * 4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int s = r * 256 + threadIdx.x;  // (pixel, quad) slot of the tile
-        const int pl = s >> 2, q = s & 3;
-        if (p0 + pl < HW) {
-            f32x4 o;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) o[m] = t[(4 * q + m) * kT16Pitch + pl];
-            dst[s] = o;
-        }
     }
 }
 
@@ -428,26 +366,12 @@ inline size_t cl_frame_bytes(int V, int J, int H, int W) {
     return (size_t)V * H * W * 4 * lanes_per_voxel(J) * sizeof(float);
 }
 
-#ifndef FVP_LAYOUT_T16
-#define FVP_LAYOUT_T16 1
-#endif
-
 template <int LPV, typename T, int NF = 1>
-inline void launch_layout(const T *hm, int nb, int V, int J, int Jst, int H, int W, float *cl, hipStream_t s,
-                          unsigned *zero = nullptr, int nzero = 0) {
-    if constexpr (LPV == 4 && NF == 1 && sizeof(T) == 4) {
-        const int HW = H * W;
-        if (FVP_LAYOUT_T16 && HW % 4 == 0 && ((unsigned long long)hm & 15ull) == 0) {
-            const int tiles = (HW + kT16Pix - 1) / kT16Pix;
-            hipLaunchKernelGGL((heatmaps_to_cl_t16_kernel<T>), dim3((unsigned)((long long)nb * V * tiles)), dim3(256), 0,
-                               s, hm, reinterpret_cast<f32x4 *>(cl), J, Jst, HW, tiles, zero, nzero);
-            return;
-        }
-    }
+inline void launch_layout(const T *hm, int nb, int V, int J, int Jst, int H, int W, float *cl, hipStream_t s) {
     const long long px = (long long)nb * V * H * W;
     const long long threads = px * LPV;
     hipLaunchKernelGGL((heatmaps_to_cl_kernel<LPV, T, NF>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                       hm, reinterpret_cast<float4 *>(cl), J, Jst, H * W, V, px, zero, nzero);
+                       hm, reinterpret_cast<float4 *>(cl), J, Jst, H * W, V, px);
 }
 
 }  // namespace fvp

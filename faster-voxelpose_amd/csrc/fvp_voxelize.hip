@@ -55,7 +55,7 @@ struct CoordSource {
 
 // Epilogue of a gather block: the stage [NF][JP][SP] (clamped means, column-
 // major within the block's columns) -> the cube runs and the xy max over z.
-template <int NF, int JP, int NT = 256>
+template <int NF, int JP>
 __device__ __forceinline__ void store_stage(const float *__restrict__ stage, int SP, int T, int Z, long long N,
                                             long long n0, int c0, int ncols, int XY, int J, int Jst, int b,
                                             float *__restrict__ cube, float *__restrict__ xy, bool cube16) {
@@ -73,7 +73,7 @@ __device__ __forceinline__ void store_stage(const float *__restrict__ stage, int
         if (cube) {
             if (vec) {
                 const int T4 = T >> 2;
-                for (int e = threadIdx.x; e < J * T4; e += NT) {
+                for (int e = threadIdx.x; e < J * T4; e += 256) {
                     const int j = e / T4, r = e - (e / T4) * T4;
                     const f32x4 v = *reinterpret_cast<const f32x4 *>(fst + j * SP + 4 * r);
                     __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(cube + (bf * Jst + j) * N + n0) + r);
@@ -81,12 +81,12 @@ __device__ __forceinline__ void store_stage(const float *__restrict__ stage, int
             } else {
                 for (int j = 0; j < J; ++j) {
                     float *__restrict__ dst = cube + (bf * Jst + j) * N + n0;
-                    for (int e = threadIdx.x; e < T; e += NT) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
+                    for (int e = threadIdx.x; e < T; e += 256) __builtin_nontemporal_store(fst[j * SP + e], dst + e);
                 }
             }
         }
         if (xy) {
-            for (int e = threadIdx.x; e < J * ncols; e += NT) {
+            for (int e = threadIdx.x; e < J * ncols; e += 256) {
                 const int j = e / ncols, cc = e - (e / ncols) * ncols;
                 const float *s = fst + j * SP + cc * Z;
                 float m = -INFINITY;
@@ -326,189 +326,6 @@ __global__ __launch_bounds__(256) void voxelize_cams_kernel(const void *__restri
                                             col_blocks, SP, band, pixb, cube16);
 }
 
-// -- camera-synchronous gather (fp32 channels-last, packed grid, V <= 16) ---------
-// The L2 re-fetch of the block gather follows the cameras' rays: every block
-// cycles through all V cameras per 64-voxel pass, so an XCD's L2 holds V
-// camera images of the region its resident blocks cover, and voxels that share
-// a pixel meet far apart in time.  Here the loop nest is
-// turned around at the XCD level: a persistent block owns a tile of `cols`
-// whole columns (T = cols * Z voxels, one slot per (wave, round, lane group):
-// WAVES waves x 2 rounds x 16 groups), and walks its tile camera pair by
-// camera pair; all blocks that share an XCD (blockIdx % 8, round-robin
-// placement) take consecutive tiles of the same frames and advance through the
-// same phases (tile round k, camera pair), so at any time the XCD's L2 serves
-// two to four cameras' images of one frame region.  Optional pacing (PACE): a
-// wave starts phase p only when every block of its XCD group has finished
-// phase p - 2 -- per-(group, phase) counters, sharded 4 ways, one arrival per
-// block (the last of its waves, counted in LDS); polls are sc1 loads (L1
-// bypassed) with a bounded spin, so a block never waits forever: the pacing
-// orders work, it never guards data, and the result does not depend on it.
-//
-// Per wave and camera pair (v0, v0 + 1): lane 4*grp + q sets up the taps of
-// slot (round q & 1, group grp) for camera v0 + (q >> 1) from the packed grid
-// (one 16-B load holds both cameras), and the group's four lanes take lane
-// 2*h + r's setup by a DPP quad broadcast for camera v0 + h, round r -- one
-// coordinate load per voxel-camera pair and one tap setup per voxel-camera, as
-// in voxelize_body.  Each voxel keeps the reference's per-voxel arithmetic and
-// camera order (acc = acc + fma chain, view 0 first): bit-identical.
-constexpr int kSyncShards = 4;
-constexpr int kSyncLine = 16;  // counter words apart (64 B: one line each)
-
-__device__ __forceinline__ unsigned load_sc1(const unsigned *p) {
-    unsigned v;
-    asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-
-__device__ __forceinline__ void atomic_add_vec(unsigned *p, unsigned x) {
-    asm volatile("global_atomic_add %0, %1, off" ::"v"(p), "v"(x) : "memory");
-}
-
-struct SyncPlan {
-    int tiles;   // tiles of the launch (frames * tiles per frame)
-    int nbg;     // blocks per XCD group
-    int nphase;  // phases per group (rounds * camera pairs)
-};
-
-template <int WAVES, bool PACE>
-__global__ __launch_bounds__(64 * WAVES, 8 * 4 / WAVES) void voxelize_sync_kernel(
-    const void *__restrict__ tab, const float *__restrict__ grids, const int32_t *__restrict__ grid_index, int frame0,
-    float *__restrict__ cube, float *__restrict__ xy, int V, int J, int Jst, int H, int W, int X, int Y, int Z,
-    int cols, int col_blocks, int SP, int band, bool cube16, SyncPlan plan, unsigned *__restrict__ ctr) {
-    constexpr int NT = 64 * WAVES;
-    constexpr unsigned pixb = 64u;  // the workspace's fp32 pixel: 16 joints
-    extern __shared__ __attribute__((aligned(16))) float stage[];  // [16][SP]
-    __shared__ unsigned lds_arr[4];
-    __shared__ int lds_done;
-    const int g = blockIdx.x & 7, bl = blockIdx.x >> 3;
-    const int lo = (int)((long long)plan.tiles * g / 8), hi = (int)((long long)plan.tiles * (g + 1) / 8);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int q = lane & 3, grp = lane >> 2;
-    const unsigned qo = (unsigned)q * 16u;
-    const int GV = V + (V & 1), NPP = GV >> 1;
-    const int XY = X * Y;
-    const float sxs = (float)(W - 1) * 0.5f, sys = (float)(H - 1) * 0.5f;
-    const unsigned img = (unsigned)(H * W) * pixb;  // bytes per camera image
-    if (PACE) {
-        if (threadIdx.x < 4) lds_arr[threadIdx.x] = 0u;
-        if (threadIdx.x == 0) lds_done = -1;
-        __syncthreads();
-    }
-    // (counter of group g, phase p, shard s)
-    auto counter = [&](int p, int s) { return ctr + ((g * plan.nphase + p) * kSyncShards + s) * kSyncLine; };
-
-    for (int k = 0;; ++k) {
-        const int t = lo + k * plan.nbg + bl;
-        if (t >= hi) break;
-        const int fr = t / col_blocks;  // frame within the launch
-        int cb = t - fr * col_blocks;
-        if (band > 0) {  // voxelize_body's band walk
-            const int gpr = Y / cols, per_band = band * gpr;
-            const int bi = cb / per_band, r = cb - bi * per_band;
-            const int rows = min(band, X - bi * band);
-            const int gc = r / rows, xr = r - gc * rows;
-            cb = (bi * band + xr) * gpr + gc;
-        }
-        const int b = frame0 + fr;
-        const int c0 = cb * cols, ncols = min(cols, XY - c0), T = ncols * Z;
-        const int gsel = grid_index ? grid_index[b] : 0;
-        const __amdgpu_buffer_rsrc_t grs =
-            uniform_rsrc(grids + (size_t)gsel * XY * Z * GV * 2, (unsigned)((size_t)XY * Z * GV * 8));
-        const char *__restrict__ frame_tab = (const char *)tab + (size_t)fr * V * img;
-        // this lane's setup slot (round q & 1, group grp), its voxel and camera half
-        const int ms = wave * 32 + 16 * (q & 1) + grp;
-        const bool mvalid = ms < T;
-        const int msl = min(ms, T - 1);
-        const int mzl = msl / ncols, mcl = msl - mzl * ncols;
-        const unsigned mrec = (unsigned)((c0 + mcl) * Z + mzl) * (unsigned)GV * 8u;
-        const int h = q >> 1;
-        // blocks of the group with a tile in round k (the counts every phase of the round waits for)
-        const int nbk = min(plan.nbg, hi - (lo + k * plan.nbg));
-        float acc[2][4];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) acc[r][m] = 0.0f;
-        for (int pp = 0; pp < NPP; ++pp) {
-            const int p = k * NPP + pp, v0 = 2 * pp;
-            if (PACE && p >= 2 && *(volatile int *)&lds_done < p - 2) {
-                // every block of the group done with phase p - 2 (its round: k, or k - 1 when pp < 2)
-                const int pw = p - 2;
-                const int nb = pw >= k * NPP ? nbk : min(plan.nbg, hi - (lo + (k - 1) * plan.nbg));
-                for (int it = 0; it < (1 << 14); ++it) {
-                    bool ok = true;
-#pragma unroll
-                    for (int s = 0; s < kSyncShards; ++s) {
-                        const int need = (nb - s + kSyncShards - 1) / kSyncShards;
-                        if (need > 0 && (int)load_sc1(counter(pw, s)) < need) ok = false;
-                    }
-                    if (ok) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (lane == 0) atomicMax(&lds_done, pw);
-            }
-            const u32x4 graw = __builtin_amdgcn_raw_buffer_load_b128(grs, mrec + (unsigned)v0 * 8u, 0, 0);
-            const bool mv = mvalid && v0 + h < V;
-            const float gx = mv ? __builtin_bit_cast(float, (unsigned)(h ? graw[2] : graw[0])) : -2.0f;
-            const float gy = mv ? __builtin_bit_cast(float, (unsigned)(h ? graw[3] : graw[1])) : -2.0f;
-            const Taps4<false> mt = setup_taps<false>(gx, gy, sxs, sys, W, H, pixb);
-            static_for(std::make_integer_sequence<int, 4>{}, [&](auto sc) {
-                constexpr int S = decltype(sc)::value, hh = S >> 1, r = S & 1;
-                const int v = v0 + hh;
-                if (v >= V) return;
-                unsigned o[4];
-                unsigned all = kOOB;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    o[m] = group_bcast<4, S>(mt.o[m]);
-                    all &= o[m];
-                }
-                if (!__builtin_amdgcn_ballot_w64((all & kOOB) == 0u)) return;
-                float w[4];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) w[m] = group_bcast<4, S>(mt.w[m]);
-                const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(frame_tab + (size_t)v * img, img);
-                const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, o[0] + qo, 0, 0);
-                const u32x4 bq = __builtin_amdgcn_raw_buffer_load_b128(rs, o[1] + qo, 0, 0);
-                const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, o[2] + qo, 0, 0);
-                const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(rs, o[3] + qo, 0, 0);
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float fa = __builtin_bit_cast(float, (unsigned)a[m]);
-                    const float fb = __builtin_bit_cast(float, (unsigned)bq[m]);
-                    const float fc = __builtin_bit_cast(float, (unsigned)c[m]);
-                    const float fd = __builtin_bit_cast(float, (unsigned)d[m]);
-                    acc[r][m] = acc[r][m] + __builtin_fmaf(fd, w[3], __builtin_fmaf(fc, w[2],
-                                                           __builtin_fmaf(fb, w[1], fa * w[0])));
-                }
-            });
-            if (PACE && lane == 0) {  // this wave is done with phase p; the block's last wave arrives
-                const unsigned old = atomicAdd(&lds_arr[p & 3], 1u);
-                if (old == (unsigned)WAVES - 1) {
-                    lds_arr[p & 3] = 0u;
-                    atomic_add_vec(counter(p, bl & (kSyncShards - 1)), 1u);
-                }
-            }
-        }
-        // the mean's final level (+ 0: a -0 sum becomes +0), / V, clamp -> stage (column-major)
-        const float fV = (float)V;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int s = wave * 32 + 16 * r + grp;
-            if (s < T) {
-                const int zl = s / ncols, cl = s - zl * ncols;
-                const int ii = cl * Z + zl;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) stage[(4 * q + m) * SP + ii] = clampf((acc[r][m] + 0.0f) / fV, 0.0f, 1.0f);
-            }
-        }
-        __syncthreads();
-        store_stage<1, 16, NT>(stage, SP, T, Z, (long long)XY * Z, (long long)c0 * Z, c0, ncols, XY, J, Jst, b, cube, xy,
-                               cube16);
-        __syncthreads();
-    }
-}
-
 // [V][N][2] -> [N][GV][2], padding slots (-2,-2) (off-image)
 __global__ __launch_bounds__(256) void pack_grid_kernel(const float2 *__restrict__ g, float2 *__restrict__ out, int V,
                                                         int GV, long long N) {
@@ -652,38 +469,6 @@ struct VoxJob {
     float *cube, *xy;
 };
 
-// Layout of chunk k+1 on a side stream under the gather of chunk k (fp32
-// channels-last table): two tables in the workspace, events both ways.  The
-// layout is HBM-bound and light on the texture path (heatmaps_to_cl_t16_kernel),
-// the gather texture-path-bound.  One side stream per device, created on first
-// use (not thread-safe: one host thread per device, as the reference's loop).
-#ifndef FVP_LAYOUT_OVERLAP
-#define FVP_LAYOUT_OVERLAP 0
-#endif
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t start = nullptr, ready[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
-};
-
-static SideStream *side_stream() {
-    static SideStream sides[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SideStream &sd = sides[dev];
-    if (!sd.s) {
-        if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        hipEvent_t *evs[5] = {&sd.start, &sd.ready[0], &sd.ready[1], &sd.freed[0], &sd.freed[1]};
-        for (hipEvent_t *e : evs)
-            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    }
-    return &sd;
-}
-
-// Frames per chunk and tables in the workspace: one table of chunk_frames(), or
-// with the overlap (fp32, not the pair table) two of kOverlapFrames.
-constexpr int kOverlapFrames = 8;
-static bool overlap_layout(bool pairs) { return FVP_LAYOUT_OVERLAP && !pairs; }
-
 // Frames [first, last) of the batch (a multiple of NF of them), chunk by chunk:
 // layout pass into the workspace, then the gather, NF frames per table entry.
 template <int LPV, bool PAIR, bool OTF, bool CASC, int NF, typename T>
@@ -691,166 +476,21 @@ static int run_chunks(const T *hm, int first, int last, const VoxJob &j, const C
                       hipStream_t s) {
     const bool half = sizeof(T) == 2;
     const int B = last - first;
-    const bool ovl = !PAIR && overlap_layout(false) && B > min(kOverlapFrames, chunk_frames(B, j.V, j.J, j.H, j.W, half));
-    const int chunk = ovl ? min(kOverlapFrames, chunk_frames(B, j.V, j.J, j.H, j.W, half))
-                          : max(NF, chunk_frames(B, j.V, j.J, j.H, j.W, half) / NF * NF);
+    const int chunk = max(NF, chunk_frames(B, j.V, j.J, j.H, j.W, half) / NF * NF);
     GatherCfg c;
     if (gather_cfg<LPV, OTF>(min(chunk, B), NF, j.V, j.X, j.Y, j.Z, c) != FVP_OK) return FVP_ERR_SHAPE;
     const size_t frame_elems = (size_t)j.V * j.Jst * j.H * j.W;
-    auto layout = [&](int f0, int nb, void *buf, hipStream_t st) {
+    for (int f0 = first; f0 < last; f0 += chunk) {
+        const int nb = min(chunk, last - f0);
         const T *hsrc = hm + (size_t)f0 * frame_elems;
         if constexpr (PAIR) {  // (J <= 16: never sliced)
             launch_pairs<NF>(reinterpret_cast<const _Float16 *>(hsrc), nb, j.V, j.J, j.H, j.W,
-                             reinterpret_cast<uint4 *>(buf), st);
+                             reinterpret_cast<uint4 *>(ws), s);
         } else {
-            launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(buf), st);
+            launch_layout<LPV, T, NF>(hsrc, nb, j.V, j.J, j.Jst, j.H, j.W, reinterpret_cast<float *>(ws), s);
         }
-    };
-    auto gather = [&](int f0, int nb, const void *buf) {
-        launch_gather<LPV, PAIR, OTF, CASC, NF>(buf, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
+        launch_gather<LPV, PAIR, OTF, CASC, NF>(ws, f0, nb, c, src, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y,
                                                j.Z, j.cube, j.xy, 4u * 4u * LPV, s);
-    };
-    SideStream *sd = ovl ? side_stream() : nullptr;
-    if (!sd) {
-        for (int f0 = first; f0 < last; f0 += chunk) {
-            const int nb = min(chunk, last - f0);
-            layout(f0, nb, ws, s);
-            gather(f0, nb, ws);
-        }
-        return (int)hipGetLastError();
-    }
-    void *bufs[2] = {ws, (char *)ws + (size_t)chunk * frame_bytes(j.V, j.J, j.H, j.W, half)};
-    const int n = (B + chunk - 1) / chunk;
-    hipError_t err = hipSuccess;
-    auto chk = [&](hipError_t r) {
-        if (r != hipSuccess && err == hipSuccess) err = r;
-    };
-    chk(hipEventRecord(sd->start, s));  // the side stream starts after the caller's earlier work
-    chk(hipStreamWaitEvent(sd->s, sd->start, 0));
-    layout(first, min(chunk, B), bufs[0], sd->s);
-    chk(hipEventRecord(sd->ready[0], sd->s));
-    for (int k = 0; k < n && err == hipSuccess; ++k) {
-        const int f0 = first + k * chunk;
-        if (k + 1 < n) {  // chunk k+1 into the table chunk k-1's gather has finished reading
-            if (k >= 1) chk(hipStreamWaitEvent(sd->s, sd->freed[(k - 1) & 1], 0));
-            layout(f0 + chunk, min(chunk, last - f0 - chunk), bufs[(k + 1) & 1], sd->s);
-            chk(hipEventRecord(sd->ready[(k + 1) & 1], sd->s));
-        }
-        chk(hipStreamWaitEvent(s, sd->ready[k & 1], 0));
-        gather(f0, min(chunk, last - f0), bufs[k & 1]);
-        chk(hipEventRecord(sd->freed[k & 1], s));
-    }
-    return err != hipSuccess ? (int)err : (int)hipGetLastError();
-}
-
-// -- the camera-synchronous gather's launches ------------------------------------
-#ifndef FVP_GATHER_SYNC
-#define FVP_GATHER_SYNC 0  // measured slower: kept off, the block gather ships
-#endif
-#ifndef FVP_SYNC_PACE
-#define FVP_SYNC_PACE 1
-#endif
-// Pacing counters at the end of the fp32 workspace (cleared by each chunk's
-// layout launch): 8 groups x phases x 4 shards x 64 B.
-constexpr size_t kSyncCtrBytes = 1u << 20;
-constexpr int kSyncMaxPhases = (int)(kSyncCtrBytes / (8 * kSyncShards * kSyncLine * 4));
-
-struct SyncShape {
-    int cols, waves, T, band, col_blocks, SP;
-    size_t lds;
-};
-
-// Tile = `cols` whole columns, T = cols * Z <= 128 slots (4 waves x 2 rounds x
-// 16 groups), as many as fit; walked in bands of x-rows (as gather_cfg) when
-// the columns tile the x-rows.  False when a column does not fit (Z > 128) or
-// the tile would leave more than a quarter of the slots empty.
-static bool sync_shape(int X, int Y, int Z, SyncShape &sh) {
-    const int c = 128 / Z;
-    if (c < 1 || c * Z < 96) return false;
-    sh.cols = min(c, X * Y);
-    sh.T = sh.cols * Z;
-    sh.waves = 4;
-    sh.band = ((long long)X * Y >= 4096 && Y % sh.cols == 0 && X > kBandRows) ? kBandRows : 0;
-    sh.col_blocks = (X * Y + sh.cols - 1) / sh.cols;
-    sh.SP = sh.T % 4 ? sh.T + 1 : sh.T + 4;
-    sh.lds = (size_t)16 * sh.SP * sizeof(float);
-    return true;
-}
-
-// Resident blocks per CU by the occupancy query (cached per stage size; one device type per process).
-template <int WAVES>
-static int sync_blocks_per_cu(size_t lds) {
-    static size_t cached_lds = 0;
-    static int cached = 0;
-    if (cached_lds != lds) {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, voxelize_sync_kernel<WAVES, FVP_SYNC_PACE != 0>,
-                                                         64 * WAVES, lds) != hipSuccess || n < 1)
-            n = 1;
-        cached = n;
-        cached_lds = lds;
-    }
-    return cached;
-}
-
-static int device_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            cus = n;
-        else
-            cus = 256;
-    }
-    return cus;
-}
-
-// One chunk of nb frames: layout (clearing the counters), then the persistent
-// gather: per XCD group ceil(tiles / 8) tiles in `rounds` rounds of nbg blocks,
-// nbg <= the resident blocks per XCD, balanced so every round is nearly full.
-template <int WAVES>
-static int launch_sync(const void *tab, int f0, int nb, const SyncShape &sh, const float *grids,
-                       const int32_t *grid_index, int V, int J, int Jst, int H, int W, int X, int Y, int Z, float *cube,
-                       float *xy, unsigned *ctr, hipStream_t s) {
-    SyncPlan plan;
-    plan.tiles = nb * sh.col_blocks;
-    const int per_group = (plan.tiles + 7) / 8;
-    const int nbg_max = max(1, sync_blocks_per_cu<WAVES>(sh.lds) * device_cus() / 8);
-    const int rounds = (per_group + nbg_max - 1) / nbg_max;
-    plan.nbg = (per_group + rounds - 1) / rounds;
-    plan.nphase = rounds * ((V + 1) / 2);
-    if (FVP_SYNC_PACE && plan.nphase > kSyncMaxPhases) return FVP_ERR_SHAPE;
-    const bool cube16 = ((unsigned long long)cube & 15ull) == 0;
-    hipLaunchKernelGGL((voxelize_sync_kernel<WAVES, FVP_SYNC_PACE != 0>), dim3((unsigned)(8 * plan.nbg)),
-                       dim3(64 * WAVES), sh.lds, s, tab, grids, grid_index, f0, cube, xy, V, J, Jst, H, W, X, Y, Z,
-                       sh.cols, sh.col_blocks, sh.SP, sh.band, cube16, plan, ctr);
-    return FVP_OK;
-}
-
-static int sync_phase_words(int nb, const SyncShape &sh, int V) {
-    (void)nb;
-    (void)sh;
-    return 8 * kSyncMaxPhases * kSyncShards * kSyncLine;
-}
-
-// The whole batch through the sync gather (fp32 heatmaps, J <= 16, V <= 16,
-// packed grid).  ws: the chunk's channels-last copy, then the counters.
-static int run_chunks_sync(const float *hm, int B, const VoxJob &j, const float *grids, void *ws, size_t ws_bytes,
-                           const SyncShape &sh, hipStream_t s) {
-    const int chunk = chunk_frames(B, j.V, j.J, j.H, j.W, false);
-    const size_t tab_bytes = (size_t)chunk * cl_frame_bytes(j.V, j.J, j.H, j.W);
-    unsigned *ctr = reinterpret_cast<unsigned *>((char *)ws + ((tab_bytes + 255) & ~(size_t)255));
-    if (((tab_bytes + 255) & ~(size_t)255) + kSyncCtrBytes > ws_bytes) return FVP_ERR_WORKSPACE;
-    const size_t frame_elems = (size_t)j.V * j.Jst * j.H * j.W;
-    for (int f0 = 0; f0 < B; f0 += chunk) {
-        const int nb = min(chunk, B - f0);
-        launch_layout<4, float, 1>(hm + (size_t)f0 * frame_elems, nb, j.V, j.J, j.Jst, j.H, j.W,
-                                   reinterpret_cast<float *>(ws), s, FVP_SYNC_PACE ? ctr : nullptr,
-                                   FVP_SYNC_PACE ? sync_phase_words(nb, sh, j.V) : 0);
-        const int st = launch_sync<4>(ws, f0, nb, sh, grids, j.grid_index, j.V, j.J, j.Jst, j.H, j.W, j.X, j.Y, j.Z,
-                                      j.cube, j.xy, ctr, s);
-        if (st != FVP_OK) return st;
     }
     return (int)hipGetLastError();
 }
@@ -908,14 +548,8 @@ static int run_frames(const T *hm, int B, const VoxJob &j, const CoordSource &sr
 }
 
 template <bool OTF, bool CASC, typename T>
-static int voxelize_lpv(const T *hm, int B, const VoxJob &j, const CoordSource &src, void *ws, size_t ws_bytes,
-                        hipStream_t s) {
+static int voxelize_lpv(const T *hm, int B, const VoxJob &j, const CoordSource &src, void *ws, hipStream_t s) {
     const bool half = sizeof(T) == 2;
-    if constexpr (!OTF && !CASC && std::is_same<T, float>::value) {
-        SyncShape sh;
-        if (FVP_GATHER_SYNC && lanes_per_voxel(j.J) == 4 && sync_shape(j.X, j.Y, j.Z, sh))
-            return run_chunks_sync(hm, B, j, src.grids, ws, ws_bytes, sh, s);
-    }
     if (use_pairs(j.Jst, half)) return run_frames<4, true, OTF, CASC, T>(hm, B, j, src, ws, s);
     switch (lanes_per_voxel(j.J)) {
         case 1: return run_frames<1, false, OTF, CASC, T>(hm, B, j, src, ws, s);
@@ -944,8 +578,8 @@ static int voxelize_any(const T *hm, int B, int V, int J, int H, int W, const Co
         const VoxJob job{V, min(kJointSlice, J - j0), J, H, W, X, Y, Z, grid_index, cube ? cube + j0 * N : nullptr,
                          xy ? xy + j0 * XY : nullptr};
         const T *h = hm + j0 * HW;
-        const int st = V > 16 ? voxelize_lpv<OTF, true, T>(h, B, job, src, ws, ws_bytes, s)
-                              : voxelize_lpv<OTF, false, T>(h, B, job, src, ws, ws_bytes, s);
+        const int st = V > 16 ? voxelize_lpv<OTF, true, T>(h, B, job, src, ws, s)
+                              : voxelize_lpv<OTF, false, T>(h, B, job, src, ws, s);
         if (st != FVP_OK) return st;
     }
     return FVP_OK;
@@ -982,12 +616,7 @@ static int check_args(const void *heatmaps, int B, int V, int J, int H, int W, c
 static size_t workspace_bytes(int B, int V, int J, int H, int W, bool half) {
     if (B <= 0 || V <= 0 || J <= 0 || J > FVP_MAX_JOINTS || H <= 0 || W <= 0) return 0;
     const int J1 = slice_joints(J);  // one joint slice's copy at a time
-    const int cf = chunk_frames(B, V, J1, H, W, half);
-    size_t tab = (size_t)cf * frame_bytes(V, J1, H, W, half);
-    if (overlap_layout(use_pairs(J1, half)) && B > min(kOverlapFrames, cf))  // run_chunks: two tables
-        tab = 2 * (size_t)min(kOverlapFrames, cf) * frame_bytes(V, J1, H, W, half);
-    // fp32 with the sync gather: + its pacing counters (run_chunks_sync)
-    return (half || !FVP_GATHER_SYNC) ? tab : ((tab + 255) & ~(size_t)255) + kSyncCtrBytes;
+    return (size_t)chunk_frames(B, V, J1, H, W, half) * frame_bytes(V, J1, H, W, half);
 }
 
 // -- winners' columns without the cube ----------------------------------------

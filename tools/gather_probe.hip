@@ -573,15 +573,9 @@ extern "C" int layout_stride_probe(const float *hm, float *cl, int B, int V, int
 extern "C" int layout_probe(int mode, const float *hm, float *cl, int B, int V, int J, int H, int W, void *stream) {
     const long long px = (long long)B * V * H * W;
     hipStream_t s = (hipStream_t)stream;
-    if (mode == 3) {  // heatmaps_to_cl_t16_kernel: 1 KiB plane loads, LDS transpose (round 5)
-        const int tiles = (H * W + kT16Pix - 1) / kT16Pix;
-        hipLaunchKernelGGL((heatmaps_to_cl_t16_kernel<float>), dim3((unsigned)((long long)B * V * tiles)), dim3(256), 0,
-                           s, hm, reinterpret_cast<f32x4 *>(cl), J, J, H * W, tiles, nullptr, 0);
-        return (int)hipGetLastError();
-    }
     if (mode == 0) {  // the thread-per-(pixel, quad) kernel (round 2's layout pass)
         hipLaunchKernelGGL((heatmaps_to_cl_kernel<4, float, 1>), dim3((unsigned)((px * 4 + 255) / 256)), dim3(256), 0, s,
-                           hm, reinterpret_cast<float4 *>(cl), J, J, H * W, V, px, nullptr, 0);
+                           hm, reinterpret_cast<float4 *>(cl), J, J, H * W, V, px);
     } else {
         if ((H * W) % 64 || J > 16) return -1;
         const dim3 grid((unsigned)(px / 64));

@@ -39,7 +39,7 @@ METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roo
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the fvp_voxelize op: layout pass (fp32 channels-last, fp16 pair table per 8 entries, per row or per
 # entry) + gather
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "heatmaps_to_cl_t16_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel",
+VOX_KERNELS = ("heatmaps_to_cl_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel",
                "pairs_rows_kernel", "voxelize_kernel", "voxelize_cams_kernel")
 
 
@@ -716,7 +716,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("fvp_voxelize op = layout pass (heatmaps_to_cl_t16 / pairs_vec8) + voxelize_kernel per "
+                "kernel": ("fvp_voxelize op = layout pass (heatmaps_to_cl / pairs_vec8) + voxelize_kernel per "
                            "frame chunk" if args.heatmap_layout == "planar" else
                            "fvp_voxelize_cl op = voxelize_kernel on channels-last heatmaps (no layout pass)"),
                 "achieved": round(achieved, 1),

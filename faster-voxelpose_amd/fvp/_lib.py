@@ -104,10 +104,12 @@ SIGNATURES = {
                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_copy_f4": [c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv3x3_wino_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_int, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 _LIB = None
 
 

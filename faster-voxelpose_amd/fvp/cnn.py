@@ -36,6 +36,11 @@ from .ops import _ptr, _stream
 # CONV_AUTO_NO_DMA is AUTO without it (the A/B arm against the [Krows][Cpo_w]
 # kernels; FVP_F32_DMA=0 makes it the default of layers built without ``algo``).
 CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA, CONV_AUTO_NO_DMA = 0, 1, 2, 3, 4, 5
+# CONV_WINO (host side only): every 3x3 stride-1 "same" fp32 layer with Cpi % 16 == 0
+# and Cout padded to 32 runs Winograd F(2x2, 3x3) (fvp_conv3x3_wino_nhwc); AUTO
+# picks it for those layers too (FVP_CONV_WINO=0: never, the A/B arm).
+CONV_WINO = 6
+WINO_AUTO = os.environ.get("FVP_CONV_WINO", "1") != "0"
 DEFAULT_ALGO = CONV_AUTO if os.environ.get("FVP_F32_DMA", "1") != "0" else CONV_AUTO_NO_DMA
 FVP_CONV_F32_KC = 8
 
@@ -87,7 +92,8 @@ class ConvLayer:
     def __init__(self, conv, bn=None, dtype=torch.float32, cpi: int | None = None, algo: int | None = None):
         dev = conv.weight.device
         self.algo = DEFAULT_ALGO if algo is None else int(algo)
-        if self.algo not in (CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA, CONV_AUTO_NO_DMA):
+        if self.algo not in (CONV_AUTO, CONV_PER_TAP, CONV_HALO, CONV_PER_TAP_NOSPLIT, CONV_DMA, CONV_AUTO_NO_DMA,
+                             CONV_WINO):
             raise _lib.FvpError(f"ConvLayer: kernel choice {algo}")
         w = conv.weight.detach().float()
         if isinstance(conv, (nn.Conv1d, nn.ConvTranspose1d)):  # 1-D: rows of height 1, kernel (1, k)
@@ -151,6 +157,11 @@ class ConvLayer:
             self.wpack_bf16 = pack.transpose(1, 2).contiguous().to(torch.bfloat16)
         elif self.Cpi % 16 == 0 and taps <= 32:  # the same layout in fp32 for the LDS-DMA kernel
             self.wpack_kc = pack.transpose(1, 2).contiguous()
+        # Winograd F(2x2, 3x3) weights U = G g G^T (fp64, rounded once), [16][Cpi/16][Cpo][2][8]
+        self.wino = None
+        if (not self.bf16 and self.mode == 0 and (self.KH, self.KW) == (3, 3) and self.stride == (1, 1)
+                and self.pad == (1, 1) and self.Cpi % 16 == 0 and self.Cpo % 32 == 0):
+            self.wino = wino_weights(w, self.Cpi, self.Cpo)
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
         if bn is not None:  # eval BatchNorm: (x - mean) / sqrt(var + eps) * gamma + beta
             s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
@@ -191,9 +202,14 @@ class ConvLayer:
             flags = 1 | (2 if x.t.dtype == torch.bfloat16 else 0) | (4 if odt == torch.bfloat16 else 0)
             wp = self.wpack_bf16
         key = (x.N, x.H, x.W)
-        if key not in self._ws:  # (split-K scratch bytes, LDS-DMA kernel) of this input size
+        if key not in self._ws:  # (split-K scratch bytes, kernel: "dma" / "wino" / None) of this input size
             self._ws[key] = self._plan(x)
         nws, dma = self._ws[key]
+        if dma == "wino":
+            _lib.call("fvp_conv3x3_wino_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wino), self.Cpo,
+                      _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
+                      _ptr(res_post.t) if res_post else None, int(relu), _ptr(out), _stream(out))
+            return Act(out, self.Cout)
         if dma:
             flags, wp = FVP_CONV_F32_KC, self.wpack_kc
         # allocated per call: the caching allocator is stream-ordered, so two
@@ -208,12 +224,16 @@ class ConvLayer:
 
     def _abi_algo(self) -> int:
         """The FVP_CONV_* value the C ABI takes (the DMA choices are made here on the host)."""
-        return CONV_AUTO if self.algo in (CONV_DMA, CONV_AUTO_NO_DMA) else self.algo
+        return CONV_AUTO if self.algo in (CONV_DMA, CONV_AUTO_NO_DMA, CONV_WINO) else self.algo
 
     def _plan(self, x: Act) -> tuple[int, bool]:
-        """(split-K scratch bytes, use the fp32 LDS-DMA kernel) for input x under self.algo."""
+        """(split-K scratch bytes, kernel) for input x under self.algo: kernel "wino"
+        (Winograd), True (the fp32 LDS-DMA kernel) or False (fvp_conv2d_nhwc_ex's choice)."""
         if self.bf16:
             return 0, False
+        if self.wino is not None and (self.algo == CONV_WINO or (self.algo == CONV_AUTO and WINO_AUTO
+                                                                  and self._wino_pays(x))):
+            return 0, "wino"
         dma = hasattr(self, "wpack_kc") and self.algo in (CONV_DMA, CONV_AUTO)
         if dma:  # the kernel's limits (fvp.h FVP_CONV_F32_KC): 32-bit offsets, row decode
             Ho, Wo = self.out_hw(x.H, x.W)
@@ -242,10 +262,44 @@ class ConvLayer:
         return _lib.load().fvp_conv2d_ex_workspace_bytes(x.N, x.H, x.W, x.Cp, self.KH, self.KW, self.Cpo,
                                                          *self.geom(), self._abi_algo()), False
 
+    def _wino_pays(self, x: Act) -> bool:
+        """AUTO's Winograd rule, from tools/wino_probe.py (profiles/round5/wino): it wins
+        on 64-column blocks (Cpo % 64 == 0) with at least two 16-channel K steps
+        (P2PNet 32->64 .. 128->128: 1.04-1.26x, ResNet-50 3x3: 1.29-1.62x) unless
+        the 8 x 16 output tiles overhang the image by more than a quarter
+        (CenterNet at 20 x 20: 1.9x the pixels, 0.75x); with 32 columns or one K
+        step the transforms outweigh the MFMA savings (P2PNet 32->32 at 64^2: 0.62x)."""
+        tiles = -(-x.H // 8) * 8 * (-(-x.W // 16) * 16)
+        return self.Cpo % 64 == 0 and self.Cpi >= 32 and tiles <= 1.25 * x.H * x.W
+
     def flops(self, x: Act) -> int:
         Ho, Wo = self.out_hw(x.H, x.W)
         rows = x.N * (x.H * x.W if self.mode else Ho * Wo)  # GEMM rows (row grid) per parity group
         return 2 * rows * self.G * self.nq * self.Cout * self.Cin * self.KH * self.KW
+
+
+_WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+WINO_LAYOUT = int(os.environ.get("FVP_WINO_LAYOUT", "1"))  # (A/B builds: 0 = the exchange kernel's layout)
+
+
+def wino_weights(w: torch.Tensor, cpi: int, cpo: int, layout: int | None = None) -> torch.Tensor:
+    """[Cout][Cin][3][3] -> U = G g G^T, fp32 (computed in fp64, rounded once), laid
+    out for fvp_conv3x3_wino_nhwc (include/fvp.h): [16][cpi/16][4][cpo][4] with
+    ci = 16 k + 4 c4 + cm -> element (xi, k, cm, co, c4); layout 0: [16][cpi/16][cpo][2][8]
+    with ci = 16 k + 2 h + p -> (xi, k, co, p, h)."""
+    layout = WINO_LAYOUT if layout is None else layout
+    cout, cin = w.shape[:2]
+    g = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
+    u = torch.einsum("ri,ocij,sj->ocrs", g, w.double(), g)  # [cout][cin][4][4]
+    full = torch.zeros((cpo, cpi, 16), dtype=torch.float64, device=w.device)
+    full[:cout, :cin] = u.reshape(cout, cin, 16)
+    if layout == 0:
+        t = full.permute(2, 1, 0).reshape(16, cpi // 16, 8, 2, cpo).permute(0, 1, 4, 3, 2)
+    else:  # [xi][k][c4][cm][co] -> [xi][k][cm][co][c4]
+        t = full.permute(2, 1, 0).reshape(16, cpi // 16, 4, 4, cpo).permute(0, 1, 3, 4, 2)
+    return t.contiguous().float()
 
 
 def maxpool2(x: Act, dim: int = 2) -> Act:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 12
+#define FVP_ABI_VERSION 13
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -386,6 +386,22 @@ int fvp_conv2d_nhwc_ex(const float *in, int N, int H, int W, int Cpi, const void
 #define FVP_CONV_F32_KC 8
 size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int KW, int Cpo, int mode, int sy,
                                      int sx, int py, int px, int algo);
+/* 3x3 stride-1 padding-1 Conv2d (cnns_2d.py:12-64 Basic2DBlock / Res2DBlock
+ * 3x3 layers; resnet.py:60-95 Bottleneck conv2 at stride 1) by Winograd
+ * F(2x2, 3x3) on the fp32 matrix cores, with the epilogue of
+ * fvp_conv2d_nhwc_ex (out = act(acc * scale + shift + res_pre) + res_post):
+ *   in    device [N][H][W][Cpi] fp32, Cpi % 16 == 0
+ *   u     device [16][Cpi/16][Cpo][2][8] fp32: U = G g G^T of the [Cout][Cin][3][3]
+ *         weights, G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]], element
+ *         (xi = 4r + s, step k, co, parity p, h) = U[co][ci = 16k + 2h + p][r][s]
+ *         (zero for padding channels)
+ *   out   device [N][H][W][Cpo] fp32, Cpo % 32 == 0
+ * The transforms are exact sums and differences (the weight transform is the
+ * caller's, in fp64): the result equals the direct convolution up to their
+ * rounding.  FVP_ERR_SHAPE otherwise. */
+int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo, const float *scale,
+                          const float *shift, const float *res_pre, const float *res_post, int relu, float *out,
+                          void *stream);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
 int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf

@@ -30,15 +30,17 @@ def gpu_device():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=["halo", "pertap", "pertap-nosplit", "dma"])
+@pytest.fixture(params=["halo", "pertap", "pertap-nosplit", "dma", "wino"])
 def conv_kernel(request):
     """The fp32 kernel choice a test builds its layers with (``algo`` of
     fvp.cnn.ConvLayer / FvpCNN): the halo-tiled KxK kernel on every eligible
     layer (so small test shapes take it too), the per-tap kernel only (split-K
     where a launch is under-filled), neither halo nor split-K
     (FVP_CONV_HALO / _PER_TAP / _PER_TAP_NOSPLIT of fvp_conv2d_nhwc_ws), and the
-    LDS-DMA kernel on every layer it takes (FVP_CONV_F32_KC)."""
+    LDS-DMA kernel on every layer it takes (FVP_CONV_F32_KC), and Winograd
+    F(2x2, 3x3) on every 3x3 stride-1 "same" layer (fvp_conv3x3_wino_nhwc; the
+    other layers as AUTO)."""
     from fvp import cnn
 
     return {"halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP, "pertap-nosplit": cnn.CONV_PER_TAP_NOSPLIT,
-            "dma": cnn.CONV_DMA}[request.param]
+            "dma": cnn.CONV_DMA, "wino": cnn.CONV_WINO}[request.param]

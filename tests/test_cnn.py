@@ -97,11 +97,42 @@ def test_conv_layer_vs_torch(gpu_device, conv_kernel, cin, cout, k, hw, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,hw,res", [(16, 32, (13, 21), None), (48, 64, (9, 30), "pre"),
+                                             (32, 96, (17, 17), "post"), (128, 128, (16, 16), "pre"),
+                                             (1, 64, (8, 16), None), (64, 64, (2, 3), "post")])
+def test_wino_conv_vs_torch(gpu_device, cin, cout, hw, res):
+    """Winograd F(2x2, 3x3) (fvp_conv3x3_wino_nhwc) on ragged images (partial
+    8 x 16 output tiles, images smaller than one tile), one and several
+    16-channel K steps, 32- and 64-column blocks (Cout padded to 32 / 64),
+    BN folded, the residual added before or after the ReLU: fp32 tolerance."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    seq = nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1), nn.BatchNorm2d(cout)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, 3 * cin + cout))
+    seq = seq.to(gpu_device)
+    g = torch.Generator().manual_seed(cout)
+    x = (torch.rand((2, cin) + hw, generator=g) - 0.5).to(gpu_device)
+    r = torch.rand((2, cout) + hw, generator=g).to(gpu_device) if res else None
+    with torch.no_grad():
+        ref = seq(x)
+        ref = torch.relu(ref + r) if res == "pre" else torch.relu(ref) + r if res == "post" else torch.relu(ref)
+    layer = cnn.ConvLayer(seq[0], seq[1], algo=cnn.CONV_WINO)
+    ra = cnn.to_nhwc(r) if res else None
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=ra if res == "pre" else None,
+                            res_post=ra if res == "post" else None))
+    assert [k for _, k in layer._ws.values()] == ["wino"]
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"wino conv {cin}->{cout} {hw} {res}")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,hw,res", [(64, 128, 3, (256, 250), True), (256, 512, 1, (100, 90), False),
                                                (48, 96, 1, (160, 150), True)])
 def test_auto_takes_f32_dma_kernel(gpu_device, cin, cout, k, hw, res):
     """AUTO (the product setting) on launches that fill the chip runs the fp32
-    LDS-DMA kernel (FVP_CONV_F32_KC, k-paired MFMA order): fp32 tolerance vs torch."""
+    LDS-DMA kernel (FVP_CONV_F32_KC, k-paired MFMA order), or Winograd on 3x3
+    "same" layers: fp32 tolerance vs torch."""
     import torch.nn as nn
 
     from fvp import cnn, synthetic
@@ -118,8 +149,10 @@ def test_auto_takes_f32_dma_kernel(gpu_device, cin, cout, k, hw, res):
     layer = cnn.ConvLayer(seq[0], seq[1])
     assert layer.algo == cnn.CONV_AUTO == cnn.DEFAULT_ALGO
     got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=cnn.to_nhwc(r) if res else None))
-    assert any(dma for _, dma in layer._ws.values()), "AUTO did not pick the LDS-DMA kernel"
-    _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv {cin}->{cout} k{k} (DMA)")
+    # (3x3 "same" layers: Winograd F(2x2, 3x3) when the product enables it)
+    want = "wino" if (k == 3 and cnn.WINO_AUTO and layer._wino_pays(cnn.to_nhwc(x))) else True
+    assert any(kind == want for _, kind in layer._ws.values()), f"AUTO did not pick {want}"
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"conv {cin}->{cout} k{k} (AUTO: {want})")
 
 
 @pytest.mark.gpu

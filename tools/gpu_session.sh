@@ -14,6 +14,8 @@
 #   step    tools/step_host.py (host / GPU time per part of the small-batch step; $STEP_ARGS)
 #   overlap tools/overlap_probe2.py for each library in $AB_LIBS
 #   pmcl2   TCC_HIT / TCC_MISS (one counter pass each) of a short bench run per library in $AB_LIBS
+#   wino    tools/wino_probe.py (Winograd vs direct 3x3 layers)
+#   cnn     tools/bench_cnn.py
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 O=gpurun_out/${OUT:-s}; mkdir -p $O
@@ -70,6 +72,19 @@ for step in "$@"; do
              done
            done
            python3 tools/pmc_kernels.py $O/pmc_* ;;
+    wino)  timeout -k 10 300 python3 tools/wino_probe.py > $O/wino.jsonl 2> $O/wino.err || fail wino $O/wino.err
+           cat $O/wino.jsonl ;;
+    winoab) for lib in $AB_LIBS; do
+             L=1; case $lib in wa*) L=0 ;; esac  # (wa*: the exchange kernel's weight layout)
+             FVP_WINO_LAYOUT=$L FVP_LIB=ab_libs/$lib.so timeout -k 10 300 python3 tools/wino_probe.py $WINO_ARGS > $O/wino_$lib.jsonl 2> $O/wino_$lib.err || fail wino_$lib $O/wino_$lib.err
+             echo "== $lib"; python3 -c "
+import json,sys
+for l in open(sys.argv[1]):
+    d=json.loads(l); print(f\"{d['layer']:24s} direct {d['direct']['us']:8.1f} wino {d['wino']['us']:8.1f} x{d['speedup']:.2f} err {d['wino']['err']:.2e}\")
+" $O/wino_$lib.jsonl
+           done ;;
+    cnn)   timeout -k 10 300 python3 tools/bench_cnn.py > $O/cnn.jsonl 2> $O/cnn.err || fail cnn $O/cnn.err
+           cut -c1-400 $O/cnn.jsonl ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

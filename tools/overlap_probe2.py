@@ -1,14 +1,13 @@
 #!/usr/bin/env python3
 """Layout of chunk k+1 under the gather of chunk k, on the product kernels
 (round 5).  The layout pass is fvp_nchw_to_nhwc into a [C][V][H][W][16]
-buffer (the fp32 channels-last table: heatmaps_to_cl_t16_kernel, or the
-thread-per-(pixel, quad) kernel in a library built with -DFVP_LAYOUT_T16=0),
+buffer (the fp32 channels-last table, heatmaps_to_cl_kernel),
 the gather is fvp_voxelize_cl on that buffer (the chunked gather's kernel).
 256 C2 frames read from HBM in chunks of C: (a) sequential on one stream;
 (b) two streams, double-buffered, events both ways (optionally the layout
 stream at high priority).  Cubes are checked against the product op.
 
-    FVP_LIB=ab_libs/t16.so python3 tools/overlap_probe2.py [--chunks 4,8,12] [--reps 3]
+    [FVP_LIB=ab_libs/<lib>.so] python3 tools/overlap_probe2.py [--chunks 4,8,12] [--reps 3]
 """
 import argparse
 import json

@@ -263,14 +263,13 @@ class ConvLayer:
                                                          *self.geom(), self._abi_algo()), False
 
     def _wino_pays(self, x: Act) -> bool:
-        """AUTO's Winograd rule, from tools/wino_probe.py (profiles/round5/wino): it wins
-        on 64-column blocks (Cpo % 64 == 0) with at least two 16-channel K steps
-        (P2PNet 32->64 .. 128->128: 1.04-1.26x, ResNet-50 3x3: 1.29-1.62x) unless
+        """AUTO's Winograd rule, from tools/wino_probe.py (profiles/round5/wino): every
+        eligible layer measured gains (P2PNet 16->32 .. 128->128: 1.28-1.60x,
+        CenterNet 32 / 64 channels 1.48 / 1.19x, ResNet-50 3x3: 1.50-1.80x) unless
         the 8 x 16 output tiles overhang the image by more than a quarter
-        (CenterNet at 20 x 20: 1.9x the pixels, 0.75x); with 32 columns or one K
-        step the transforms outweigh the MFMA savings (P2PNet 32->32 at 64^2: 0.62x)."""
+        (CenterNet at 20 x 20: 1.9x the pixels, 0.88x)."""
         tiles = -(-x.H // 8) * 8 * (-(-x.W // 16) * 16)
-        return self.Cpo % 64 == 0 and self.Cpi >= 32 and tiles <= 1.25 * x.H * x.W
+        return tiles <= 1.25 * x.H * x.W
 
     def flops(self, x: Act) -> int:
         Ho, Wo = self.out_hw(x.H, x.W)
@@ -281,24 +280,17 @@ class ConvLayer:
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 
 
-WINO_LAYOUT = int(os.environ.get("FVP_WINO_LAYOUT", "1"))  # (A/B builds: 0 = the exchange kernel's layout)
-
-
-def wino_weights(w: torch.Tensor, cpi: int, cpo: int, layout: int | None = None) -> torch.Tensor:
+def wino_weights(w: torch.Tensor, cpi: int, cpo: int) -> torch.Tensor:
     """[Cout][Cin][3][3] -> U = G g G^T, fp32 (computed in fp64, rounded once), laid
     out for fvp_conv3x3_wino_nhwc (include/fvp.h): [16][cpi/16][4][cpo][4] with
-    ci = 16 k + 4 c4 + cm -> element (xi, k, cm, co, c4); layout 0: [16][cpi/16][cpo][2][8]
-    with ci = 16 k + 2 h + p -> (xi, k, co, p, h)."""
-    layout = WINO_LAYOUT if layout is None else layout
+    ci = 16 k + 4 c4 + cm -> element (xi, k, cm, co, c4)."""
     cout, cin = w.shape[:2]
     g = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
     u = torch.einsum("ri,ocij,sj->ocrs", g, w.double(), g)  # [cout][cin][4][4]
     full = torch.zeros((cpo, cpi, 16), dtype=torch.float64, device=w.device)
     full[:cout, :cin] = u.reshape(cout, cin, 16)
-    if layout == 0:
-        t = full.permute(2, 1, 0).reshape(16, cpi // 16, 8, 2, cpo).permute(0, 1, 4, 3, 2)
-    else:  # [xi][k][c4][cm][co] -> [xi][k][cm][co][c4]
-        t = full.permute(2, 1, 0).reshape(16, cpi // 16, 4, 4, cpo).permute(0, 1, 3, 4, 2)
+    # [xi][ci][co] -> [xi][k][c4][cm][co] -> [xi][k][cm][co][c4]
+    t = full.permute(2, 1, 0).reshape(16, cpi // 16, 4, 4, cpo).permute(0, 1, 3, 4, 2)
     return t.contiguous().float()
 
 

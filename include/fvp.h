@@ -391,9 +391,9 @@ size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int K
  * F(2x2, 3x3) on the fp32 matrix cores, with the epilogue of
  * fvp_conv2d_nhwc_ex (out = act(acc * scale + shift + res_pre) + res_post):
  *   in    device [N][H][W][Cpi] fp32, Cpi % 16 == 0
- *   u     device [16][Cpi/16][Cpo][2][8] fp32: U = G g G^T of the [Cout][Cin][3][3]
+ *   u     device [16][Cpi/16][4][Cpo][4] fp32: U = G g G^T of the [Cout][Cin][3][3]
  *         weights, G = [[1,0,0],[1/2,1/2,1/2],[1/2,-1/2,1/2],[0,0,1]], element
- *         (xi = 4r + s, step k, co, parity p, h) = U[co][ci = 16k + 2h + p][r][s]
+ *         (xi = 4r + s, step k, cm, co, c4) = U[co][ci = 16k + 4c4 + cm][r][s]
  *         (zero for padding channels)
  *   out   device [N][H][W][Cpo] fp32, Cpo % 32 == 0
  * The transforms are exact sums and differences (the weight transform is the

@@ -16,6 +16,7 @@
 #   pmcl2   TCC_HIT / TCC_MISS (one counter pass each) of a short bench run per library in $AB_LIBS
 #   wino    tools/wino_probe.py (Winograd vs direct 3x3 layers)
 #   cnn     tools/bench_cnn.py
+#   cntrace rocprofv3 kernel trace of one CenterNet (8 frames) and one P2PNet (240 images) forward, per dispatch
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 O=gpurun_out/${OUT:-s}; mkdir -p $O
@@ -75,8 +76,7 @@ for step in "$@"; do
     wino)  timeout -k 10 300 python3 tools/wino_probe.py > $O/wino.jsonl 2> $O/wino.err || fail wino $O/wino.err
            cat $O/wino.jsonl ;;
     winoab) for lib in $AB_LIBS; do
-             L=1; case $lib in wa*) L=0 ;; esac  # (wa*: the exchange kernel's weight layout)
-             FVP_WINO_LAYOUT=$L FVP_LIB=ab_libs/$lib.so timeout -k 10 300 python3 tools/wino_probe.py $WINO_ARGS > $O/wino_$lib.jsonl 2> $O/wino_$lib.err || fail wino_$lib $O/wino_$lib.err
+             FVP_LIB=ab_libs/$lib.so timeout -k 10 300 python3 tools/wino_probe.py $WINO_ARGS > $O/wino_$lib.jsonl 2> $O/wino_$lib.err || fail wino_$lib $O/wino_$lib.err
              echo "== $lib"; python3 -c "
 import json,sys
 for l in open(sys.argv[1]):
@@ -85,6 +85,12 @@ for l in open(sys.argv[1]):
            done ;;
     cnn)   timeout -k 10 300 python3 tools/bench_cnn.py > $O/cnn.jsonl 2> $O/cnn.err || fail cnn $O/cnn.err
            cut -c1-400 $O/cnn.jsonl ;;
+    cntrace) for nt in centernet:8 p2p:240; do
+             net=${nt%%:*}; im=${nt##*:}
+             timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/trace_$net -o run -- python3 tools/cnn_trace.py run --net $net --images $im --algo auto > $O/trace_$net.log 2>&1 || fail trace_$net $O/trace_$net.log
+             python3 tools/cnn_trace.py parse $O/trace_$net > $O/trace_$net.json || fail parse_$net $O/trace_$net.json
+             python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['last_busy_us'], d['last_span_us'], d['dispatches']); [print('  %7.2f %s' % (t, k[:90])) for t, k in d['kernels']]" $O/trace_$net.json $net
+           done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

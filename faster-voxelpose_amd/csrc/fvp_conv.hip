@@ -1210,6 +1210,110 @@ __global__ __launch_bounds__(256) void conv_front7_bf16_kernel(const float *__re
     }
 }
 
+// ---- the same front conv on the fp32 matrix cores, from the NCHW maps -------
+// 7x7, stride 1, pad 3, C <= 16 planes -> 16 channels + BN + ReLU, fp32 NHWC16
+// out.  The generic kernels walk K = 49 taps x 16 channels in 49 chunks with a
+// global round trip each (CenterNet at 8 frames: 42 us for 1.3 GFLOP); here a
+// persistent block stages all 49 taps' weights in LDS once ([tap][co][16 c],
+// 16-B quads XOR-swizzled by co so the A reads are conflict-free) and walks
+// 8 x 16 output tiles: the 14 x 22 x 16 input halo goes to LDS ([pixel][c],
+// 80-B pitch; the next tile's halo is loaded into registers during this tile's
+// MFMAs, straight from the C planes: no layout pass), then 49 taps x 4
+// v_mfma_f32_16x16x4f32 per 16-pixel row with the weights as the A operand
+// (D[co][pixel]: lane -> pixel, its 4 registers -> 4 consecutive channels, one
+// 16-B store per lane).  Exact fp32 products; the sum runs tap by tap in
+// channel quads (an order of its own, like every fp32 kernel here).
+constexpr int kF32TH = 8, kF32TW = 16, kF32HR = kF32TH + 6, kF32HX = kF32TW + 6, kF32HP = 20;
+constexpr int kF32Halo = kF32HR * kF32HX;                          // 308 halo pixels
+constexpr int kF32HaloItems = kF32Halo * 4;                        // (pixel, channel quad)
+constexpr int kF32HU = (kF32HaloItems + 255) / 256;                // halo items per thread
+constexpr int kF32Lds = 49 * 16 * 16 + kF32Halo * kF32HP;          // floats: 12,544 + 6,160
+
+__global__ __launch_bounds__(256, 2) void conv_front7_f32_kernel(const float *__restrict__ x, int C, int H, int W,
+                                                                 int tiles_x, int tiles_y, int ntiles,
+                                                                 const float *__restrict__ wpk,
+                                                                 const float *__restrict__ scale,
+                                                                 const float *__restrict__ shift,
+                                                                 float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float f32lds[];
+    float *wl = f32lds, *halo = f32lds + 49 * 16 * 16;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int px = lane & 15, g = lane >> 4;  // pixel of a 16-pixel row; channel quad
+    const int per_img = tiles_x * tiles_y;
+    const size_t plane = (size_t)H * W;
+    // weights [tap][co][c] -> LDS quad (c / 4) ^ ((co >> 2) & 3)
+    for (int e = t; e < 49 * 16 * 4; e += 256) {
+        const int row = e >> 2, q = e & 3, co = row & 15;
+        *reinterpret_cast<f32x4 *>(wl + row * 16 + 4 * (q ^ ((co >> 2) & 3))) =
+            *reinterpret_cast<const f32x4 *>(wpk + row * 16 + 4 * q);
+    }
+    auto origin = [&](int tile, int &n, int &oy0, int &ox0) {
+        n = tile / per_img;
+        const int tr = tile - n * per_img, ty = tr / tiles_x;
+        oy0 = ty * kF32TH;
+        ox0 = (tr - ty * tiles_x) * kF32TW;
+    };
+    f32x4 hv[kF32HU];
+    auto load_halo = [&](int tile) {
+        int n, oy0, ox0;
+        origin(tile, n, oy0, ox0);
+        const float *__restrict__ src = x + (size_t)n * C * plane;
+#pragma unroll
+        for (int u = 0; u < kF32HU; ++u) {
+            const int e = t + 256 * u;
+            const int p = e >> 2, q = e & 3;
+            const int r = p / kF32HX, c = p - r * kF32HX;
+            const int y = oy0 - 3 + r, xx = ox0 - 3 + c;
+            const bool in = e < kF32HaloItems && (unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W;
+            const size_t o = (size_t)(in ? y : 0) * W + (in ? xx : 0);
+            f32x4 v;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = (in && 4 * q + k < C) ? src[(size_t)(4 * q + k) * plane + o] : 0.0f;
+            hv[u] = v;
+        }
+    };
+    const f32x4 sc = *reinterpret_cast<const f32x4 *>(scale + 4 * g);
+    const f32x4 sh = *reinterpret_cast<const f32x4 *>(shift + 4 * g);
+    int tile = blockIdx.x;
+    if (tile < ntiles) load_halo(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        __syncthreads();  // every wave is past the previous tile's halo reads (and the weights are stored)
+#pragma unroll
+        for (int u = 0; u < kF32HU; ++u) {
+            const int e = t + 256 * u;
+            if (e < kF32HaloItems) *reinterpret_cast<f32x4 *>(halo + (e >> 2) * kF32HP + 4 * (e & 3)) = hv[u];
+        }
+        if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);  // in flight during the MFMAs
+        __syncthreads();
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        // wave w: output rows 2w, 2w + 1 (16 pixels each)
+#pragma unroll 7
+        for (int tap = 0; tap < 49; ++tap) {
+            const int ky = tap / 7, kx = tap - ky * 7;
+            const f32x4 fw = *reinterpret_cast<const f32x4 *>(wl + (tap * 16 + px) * 16 + 4 * (g ^ ((px >> 2) & 3)));
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const f32x4 fa =
+                    *reinterpret_cast<const f32x4 *>(halo + ((2 * wave + i + ky) * kF32HX + px + kx) * kF32HP + 4 * g);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(fw[k], fa[k], acc[i], 0, 0, 0);
+            }
+        }
+        int n, oy0, ox0;
+        origin(tile, n, oy0, ox0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // D[co][pixel]: this lane = pixel px of row 2w + i, channels 4g .. 4g + 3
+            const int oy = oy0 + 2 * wave + i, ox = ox0 + px;
+            if (oy < H && ox < W) {
+                f32x4 o;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] = fmaxf(acc[i][k] * sc[k] + sh[k], 0.0f);
+                *reinterpret_cast<f32x4 *>(out + (((size_t)n * H + oy) * W + ox) * 16 + 4 * g) = o;
+            }
+        }
+    }
+}
+
 // KHxKW / stride-(KH,KW) max pool, KH, KW in {1, 2}, NHWC (F.max_pool2d(x, 2, 2),
 // cnns_2d.py Pool2DBlock; F.max_pool1d(x, 2, 2) on H == 1 rows, cnns_1d.py Pool1DBlock)
 template <int KH, int KW>
@@ -1810,6 +1914,24 @@ extern "C" int fvp_conv_front7_bf16(const float *x, int N, int C, int H, int W, 
     hipLaunchKernelGGL(fvp::conv_front7_bf16_kernel, dim3((unsigned)(N * tx * ty)), dim3(256), 0, (hipStream_t)stream,
                        x, C, H, W, tx, ty, reinterpret_cast<const __bf16 *>(wpack), scale, shift,
                        reinterpret_cast<__bf16 *>(out));
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_conv_front7_f32(const float *x, int N, int C, int H, int W, const float *wpack, const float *scale,
+                                   const float *shift, float *out, void *stream) {
+    if (!x || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
+    if (N <= 0 || C < 1 || C > 16 || H < 1 || W < 1) return FVP_ERR_SHAPE;
+    const int tx = (W + fvp::kF32TW - 1) / fvp::kF32TW, ty = (H + fvp::kF32TH - 1) / fvp::kF32TH;
+    if ((long long)N * tx * ty > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    const int ntiles = N * tx * ty;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;  // persistent: 2 blocks per CU walk the tiles
+    hipLaunchKernelGGL(fvp::conv_front7_f32_kernel, dim3((unsigned)blocks), dim3(256),
+                       (size_t)fvp::kF32Lds * sizeof(float), (hipStream_t)stream, x, C, H, W, tx, ty, ntiles, wpack,
+                       scale, shift, out);
     return (int)hipGetLastError();
 }
 

@@ -13,10 +13,11 @@
 // the transforms' rounding (a few ulp of the partial sums; tests/test_cnn.py
 // bounds it with the other fp32 kernels).
 //
-// Block = 256 threads, an 8 x 16 output tile (32 Winograd tiles) of one image
-// x NB*32 output channels.  Per 16-channel K step:
-//   1. the 10 x 18 x 16 input halo -> LDS (float4 loads issued a step ahead,
-//      zero outside the image)
+// Block = 256 * XS threads, a TR x TC grid of Winograd tiles (<= 32: an 8 x 16
+// output tile by default, 5 x 5 tiles on 20 x 20 maps, chosen by wino_plan) of
+// one image x NB*32 output channels.  Per 16-channel K step:
+//   1. the (2TR+2) x (2TC+2) x 16 input halo -> LDS (float4 loads issued a step
+//      ahead, zero outside the image)
 //   2. input transform: thread (tile, channel) -> V[xi][c mod 4][tile][c / 4]
 //   3. v_mfma_f32_16x16x4f32 (16 tiles x 16 columns x 4 channels): A = V (one
 //      ds_read_b128 per lane and 4 channels), B = the transformed weights
@@ -27,9 +28,11 @@
 // (+ res_post), NHWC stores.
 #include "fvp_layout.h"
 
-namespace fvp {
+#ifndef FVP_WINO_XS_MAX  // (A/B builds: 1 = never split the transform positions)
+#define FVP_WINO_XS_MAX 2
+#endif
 
-typedef float wf32x16 __attribute__((ext_vector_type(16)));
+namespace fvp {
 
 struct WinoArgs {
     const float *in;        // [N][H][W][Cpi]
@@ -40,31 +43,46 @@ struct WinoArgs {
     const float *res_post;  // [N][H][W][Cpo] or null
     float *out;             // [N][H][W][Cpo]
     int N, H, W, Cpi, Cpo, relu;
-    int tiles_y, tiles_x;   // ceil(H / 8), ceil(W / 16)
+    int tr, tc;             // Winograd tiles per block: tr rows x tc columns (tr * tc <= 32)
+    int tiles_y, tiles_x;   // blocks per image: ceil(H / 2tr), ceil(W / 2tc)
 };
 
-constexpr int kWinoTH = 8, kWinoTW = 16;                  // output pixels per block
-constexpr int kWinoHH = kWinoTH + 2, kWinoHW = kWinoTW + 2;  // input halo
-constexpr int kWinoHP = 20;                                // halo LDS floats per pixel (16 + pad, 16-B aligned)
-constexpr int kWinoHalo = kWinoHH * kWinoHW * kWinoHP;     // 3,600 floats
+constexpr int kWinoHP = 20;                  // halo LDS floats per pixel (16 + pad, 16-B aligned)
+constexpr int kWinoHaloPx = 180;             // halo pixels: (2tr + 2)(2tc + 2) <= 180 (10 x 18 for 4 x 8 tiles)
+constexpr int kWinoHalo = kWinoHaloPx * kWinoHP;  // 3,600 floats
+constexpr int kWinoV = 16 * 4 * 32 * 4;      // 8,192 floats: V[xi][c mod 4][32 tiles][c / 4]
 
-// The MFMA tile is 16 tiles x 16 columns and all 16 xi accumulators of a lane
-// stay in registers (no LDS exchange, no barrier after the K loop, 46 KB of
-// LDS per block).  NB = 2 (64 columns per block): wave w owns the 16 columns
-// 16 w .. and both 16-tile halves, so every wave loads different weights (no B
-// fragment is fetched twice per block); NB = 1 (32 columns): wave w owns tile
-// half w & 1 of column block w >> 1.
+// The MFMA tile is 16 tiles x 16 columns (v_mfma_f32_16x16x4f32).  A lane keeps
+// the 16 / XS transform positions xi of its (tile, column) pairs in registers.
+// XS = 1: all 16, so the output transform runs in registers with no exchange.
+// XS = 2 (under-filled launches): 8 waves, wave set xs = w >> 2 owns xi 8 xs ..
+// 8 xs + 7 (the rows r = 2 xs, 2 xs + 1 of m = A-side 4 x 4); after the K loop
+// the two sets swap the halves of their accumulators through LDS so that set
+// xs finishes accumulator rows 2 xs, 2 xs + 1 -- twice the waves per block and
+// half the MFMA chain per wave.  Within a set: NB = 2 (64 columns per block):
+// wave w owns the 16 columns 16 w .. and both 16-tile halves, so every wave
+// loads different weights; NB = 1 (32 columns): wave w owns tile half w & 1 of
+// column block w >> 1.
 // V in LDS: [xi][c mod 4][tile ^ 2 (c mod 4)][c / 4] (the XOR keeps the
 // transform's stores conflict-free, the MFMA reads stay 16 contiguous tiles);
 // U: [16][Cpi/16][c mod 4][Cpo][c/4 (4)].
-constexpr int kWinoRV = 16 * 4 * 32 * 4;                    // 8,192 floats
-constexpr int kWinoRLds = kWinoHalo + kWinoRV;
+__host__ __device__ constexpr int wino_lds_floats(int NB, int XS) {
+    return XS == 1 ? kWinoHalo + kWinoV
+                   : (kWinoHalo + kWinoV > 8 * 16 * NB * 64 ? kWinoHalo + kWinoV : 8 * 16 * NB * 64);
+}
 
-template <int NB>
-__global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoArgs a) {
+template <int V>
+struct WinoIC {
+    static constexpr int value = V;
+};
+
+template <int NB, int XS>
+__global__ __launch_bounds__(256 * XS, XS == 1 ? 2 : 1) void conv_wino_kernel(WinoArgs a) {
+    constexpr int NT = 256 * XS, NX = 16 / XS;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *halo = lds, *vt = lds + kWinoHalo;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int xs = XS == 1 ? 0 : wave >> 2, w4 = wave & 3;
     int bid = blockIdx.x;
     const int nblk = a.Cpo / (32 * NB);
     const int cbk = bid % nblk;
@@ -73,28 +91,35 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoArgs a) {
     bid /= a.tiles_x;
     const int ty = bid % a.tiles_y;
     const int img = bid / a.tiles_y;
-    const int y0 = ty * kWinoTH, x0 = tx * kWinoTW;
-    const int th0 = NB == 2 ? 0 : (wave & 1);                                   // first tile half
-    const int nw = cbk * 32 * NB + 16 * (NB == 2 ? wave : (wave >> 1));          // this wave's 16 columns
+    const int tr = a.tr, tc = a.tc, ntiles = tr * tc;
+    const int hh = 2 * tr + 2, hw = 2 * tc + 2;
+    // exact quotients by multiply-shift: t / tc for t < 32 and p / hw for p < 180 (tc <= 16, hw <= 34:
+    // the error of 65536 / d + 1 times x < 2^16 / d stays under 1 / d)
+    const int mtc = 65536 / tc + 1, mhw = 65536 / hw + 1;
+    const int y0 = ty * 2 * tr, x0 = tx * 2 * tc;
+    const int th0 = NB == 2 ? 0 : (w4 & 1);                                 // first tile half
+    const int nw = cbk * 32 * NB + 16 * (NB == 2 ? w4 : (w4 >> 1));          // this wave's 16 columns
     const float *__restrict__ src = a.in + (size_t)img * a.H * a.W * a.Cpi;
     const int ksteps = a.Cpi / 16;
     const int l16 = lane & 15, cm = lane >> 4;
 
-    f32x4 acc[16][NB];  // [xi][tile half]
+    f32x4 acc[NX][NB];  // [xi - NX xs][tile half]
 #pragma unroll
-    for (int x = 0; x < 16; ++x)
+    for (int x = 0; x < NX; ++x)
 #pragma unroll
         for (int h = 0; h < NB; ++h) acc[x][h] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto halo_load = [&](int ks, f32x4 (&hl)[3]) {
+    constexpr int HU = (kWinoHaloPx * 4 + NT - 1) / NT;  // halo float4 slots per thread
+    const int hslots = hh * hw * 4;
+    auto halo_load = [&](int ks, f32x4 (&hl)[HU]) {
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int s = tid + 256 * u;
-            const int p = s >> 2, q = s & 3;
-            const int hy = p / kWinoHW, hx = p - hy * kWinoHW;
+        for (int u = 0; u < HU; ++u) {
+            const int sl = tid + NT * u;
+            const int p = sl >> 2, q = sl & 3;
+            const int hy = (p * mhw) >> 16, hx = p - hy * hw;
             const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (s < kWinoHH * kWinoHW * 4 && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+            if (sl < hslots && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
                 v = *reinterpret_cast<const f32x4 *>(src + ((size_t)gy * a.W + gx) * a.Cpi + ks * 16 + 4 * q);
             hl[u] = v;
         }
@@ -104,137 +129,254 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoArgs a) {
     auto b_at = [&](int xi, int ks) {
         return *reinterpret_cast<const f32x4 *>(ub + ((size_t)xi * ksteps + ks) * 16 * a.Cpo);
     };
-    f32x4 hnext[3];
+    // XS = 2 (NB = 1, few blocks, registers to spare): the whole step's B (8 fragments) is loaded one
+    // step ahead; otherwise groups of 4 xi, the next group loading while one is used (a cross-step
+    // prefetch here measured slower: the copy at the loop's back edge waits for the loads, and the
+    // extra registers cost the large launches occupancy)
+    constexpr bool kPF = NB == 1 && XS == 2;
+    constexpr int NBQ = kPF ? NX : 4;
+    f32x4 bcur[NBQ], bnext[NBQ], bq[2][4];
+    if constexpr (kPF) {
+#pragma unroll
+        for (int x = 0; x < NBQ; ++x) bcur[x] = b_at(NX * xs + x, 0);
+    }
+    f32x4 hnext[HU];
     halo_load(0, hnext);
     for (int ks = 0; ks < ksteps; ++ks) {
         __syncthreads();  // the previous step's transform has read the halo
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int s = tid + 256 * u;
-            if (s < kWinoHH * kWinoHW * 4)
-                *reinterpret_cast<f32x4 *>(halo + (s >> 2) * kWinoHP + 4 * (s & 3)) = hnext[u];
+        for (int u = 0; u < HU; ++u) {
+            const int sl = tid + NT * u;
+            if (sl < hslots) *reinterpret_cast<f32x4 *>(halo + (sl >> 2) * kWinoHP + 4 * (sl & 3)) = hnext[u];
         }
-        if (ks + 1 < ksteps) halo_load(ks + 1, hnext);
-        f32x4 bq[2][4];  // B of 4 xi at a time, the next group loading while one is used
+        if (ks + 1 < ksteps) {
+            halo_load(ks + 1, hnext);
+            if constexpr (kPF) {
 #pragma unroll
-        for (int x = 0; x < 4; ++x) bq[0][x] = b_at(x, ks);
+                for (int x = 0; x < NBQ; ++x) bnext[x] = b_at(NX * xs + x, ks + 1);
+            }
+        }
+        if constexpr (!kPF) {
+#pragma unroll
+            for (int x = 0; x < 4; ++x) bcur[x] = b_at(NX * xs + x, ks);
+        }
         __syncthreads();  // halo written; the previous step's MFMAs have read V
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {  // input transform: item = tile * 16 + c
-            const int item = tid + 256 * it;
+        for (int it = 0; it < 512 / NT; ++it) {  // input transform: item = tile * 16 + c
+            const int item = tid + NT * it;
             const int t = item >> 4, c = item & 15;
-            const int ti = t >> 3, tj = t & 7;
-            const float *hp = halo + ((2 * ti) * kWinoHW + 2 * tj) * kWinoHP + c;
-            float d[4][4];
+            if (t < ntiles) {  // (tiles past tr * tc: their V rows stay unwritten and their outputs unstored)
+                const int ti = (t * mtc) >> 16, tj = t - ti * tc;
+                const float *hp = halo + ((2 * ti) * hw + 2 * tj) * kWinoHP + c;
+                float d[4][4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+                for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2) d[r][s2] = hp[(r * kWinoHW + s2) * kWinoHP];
-            float e[4][4];
+                    for (int s2 = 0; s2 < 4; ++s2) d[r][s2] = hp[(r * hw + s2) * kWinoHP];
+                float e[4][4];
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                e[0][s2] = d[0][s2] - d[2][s2];
-                e[1][s2] = d[1][s2] + d[2][s2];
-                e[2][s2] = d[2][s2] - d[1][s2];
-                e[3][s2] = d[1][s2] - d[3][s2];
-            }
-            const int cmod = c & 3;
-            float *vp = vt + (cmod * 32 + (t ^ (2 * cmod))) * 4 + (c >> 2);
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    e[0][s2] = d[0][s2] - d[2][s2];
+                    e[1][s2] = d[1][s2] + d[2][s2];
+                    e[2][s2] = d[2][s2] - d[1][s2];
+                    e[3][s2] = d[1][s2] - d[3][s2];
+                }
+                const int cmod = c & 3;
+                float *vp = vt + (cmod * 32 + (t ^ (2 * cmod))) * 4 + (c >> 2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                vp[(r * 4 + 0) * 4 * 32 * 4] = e[r][0] - e[r][2];
-                vp[(r * 4 + 1) * 4 * 32 * 4] = e[r][1] + e[r][2];
-                vp[(r * 4 + 2) * 4 * 32 * 4] = e[r][2] - e[r][1];
-                vp[(r * 4 + 3) * 4 * 32 * 4] = e[r][1] - e[r][3];
+                for (int r = 0; r < 4; ++r) {
+                    vp[(r * 4 + 0) * 4 * 32 * 4] = e[r][0] - e[r][2];
+                    vp[(r * 4 + 1) * 4 * 32 * 4] = e[r][1] + e[r][2];
+                    vp[(r * 4 + 2) * 4 * 32 * 4] = e[r][2] - e[r][1];
+                    vp[(r * 4 + 3) * 4 * 32 * 4] = e[r][1] - e[r][3];
+                }
             }
         }
         __syncthreads();
-        // MFMAs: 16 xi x NB tile halves x 4 channel quads
+        // MFMAs: NX xi x NB tile halves x 4 channel quads
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (g < 3) {
+        for (int g = 0; g < NX / 4; ++g) {
+            if constexpr (!kPF) {
+                if (g + 1 < NX / 4) {
 #pragma unroll
-                for (int x = 0; x < 4; ++x) bq[(g + 1) & 1][x] = b_at(4 * (g + 1) + x, ks);
+                    for (int x = 0; x < 4; ++x) bq[(g + 1) & 1][x] = b_at(NX * xs + 4 * (g + 1) + x, ks);
+                }
             }
 #pragma unroll
             for (int x = 0; x < 4; ++x) {
-                const int xi = 4 * g + x;
+                const int xl = 4 * g + x, xi = NX * xs + xl;
+                const f32x4 bv = kPF ? bcur[xl] : (g == 0 ? bcur[x] : bq[g & 1][x]);
 #pragma unroll
                 for (int h = 0; h < NB; ++h) {
                     const int ta = (16 * (th0 + h) + l16) ^ (2 * cm);
                     const f32x4 av = *reinterpret_cast<const f32x4 *>(vt + ((xi * 4 + cm) * 32 + ta) * 4);
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        acc[xi][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k], bq[g & 1][x][k], acc[xi][h], 0, 0, 0);
+                        acc[xl][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k], bv[k], acc[xl][h], 0, 0, 0);
                 }
             }
         }
+        if constexpr (kPF) {
+#pragma unroll
+            for (int x = 0; x < NBQ; ++x) bcur[x] = bnext[x];
+        }
     }
-    // output transform in registers: lane holds tiles 16 (th0 + h) + 4 cm + r (r < 4), column nw + l16
+    // m[xi][r]: accumulator row r (tile 16 (th0 + h) + 4 cm + r) of transform position xi.  XS = 2: the
+    // sets swap halves so that set xs holds all 16 xi of rows r = 2 xs, 2 xs + 1.
+    constexpr int NR = 4 / XS;  // accumulator rows finished per lane
+    // slot: [set that receives][w4][h][xi 0..7][row 0..1][lane]
+    auto slot = [&](int to, int h, int x, int rr) {
+        return lds + ((((to * 4 + w4) * NB + h) * 8 + x) * 2 + rr) * 64 + lane;
+    };
+    if constexpr (XS == 2) {
+        __syncthreads();  // every wave's MFMAs have read V
+        auto send = [&](auto to_c) {
+            constexpr int TO = decltype(to_c)::value;
+#pragma unroll
+            for (int h = 0; h < NB; ++h)
+#pragma unroll
+                for (int x = 0; x < 8; ++x)
+#pragma unroll
+                    for (int rr = 0; rr < 2; ++rr) *slot(TO, h, x, rr) = acc[x][h][2 * TO + rr];
+        };
+        if (xs == 0) send(WinoIC<1>{});
+        else send(WinoIC<0>{});
+        __syncthreads();
+    }
     const float *__restrict__ rpre_p = a.res_pre;
     const float *__restrict__ rpost_p = a.res_post;
     const float *__restrict__ rfirst = rpre_p ? rpre_p : rpost_p;
     auto out_off = [&](int t, int q, int co, bool &ok) {
-        const int oy = y0 + 2 * (t >> 3) + (q >> 1), ox = x0 + 2 * (t & 7) + (q & 1);
-        ok = oy < a.H && ox < a.W;
+        const int ti = (t * mtc) >> 16, tj = t - ti * tc;
+        const int oy = y0 + 2 * ti + (q >> 1), ox = x0 + 2 * tj + (q & 1);
+        ok = t < ntiles && oy < a.H && ox < a.W;
         return (((size_t)img * a.H + oy) * a.W + ox) * a.Cpo + co;
     };
     const int co = nw + l16;
     const float sc = a.scale[co], sh = a.shift[co];
+    auto finish = [&](auto xs_c) {
+        constexpr int XSI = decltype(xs_c)::value;
+        float m[16][NB][NR];
 #pragma unroll
-    for (int h = 0; h < NB; ++h) {
-        float rv[4][4];
+        for (int h = 0; h < NB; ++h)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+            for (int rr = 0; rr < NR; ++rr)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                bool ok;
-                const size_t off = out_off(16 * (th0 + h) + 4 * cm + r, q, co, ok);
-                rv[r][q] = (rfirst && ok) ? rfirst[off] : 0.0f;
-            }
+                for (int x = 0; x < NX; ++x) {
+                    m[NX * XSI + x][h][rr] = acc[x][h][NR * XSI + rr];
+                    if constexpr (XS == 2) m[8 * (1 - XSI) + x][h][rr] = *slot(XSI, h, x, rr);
+                }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int t = 16 * (th0 + h) + 4 * cm + r;
-            float f[2][4];
+        for (int h = 0; h < NB; ++h) {
+            float rv[NR][4];
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                f[0][s2] = (acc[s2][h][r] + acc[4 + s2][h][r]) + acc[8 + s2][h][r];
-                f[1][s2] = (acc[4 + s2][h][r] - acc[8 + s2][h][r]) - acc[12 + s2][h][r];
-            }
+            for (int rr = 0; rr < NR; ++rr)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int dy = q >> 1, dx = q & 1;
-                bool ok;
-                const size_t off = out_off(t, q, co, ok);
-                if (!ok) continue;
-                float v = dx == 0 ? (f[dy][0] + f[dy][1]) + f[dy][2] : (f[dy][1] - f[dy][2]) - f[dy][3];
-                v = v * sc + sh;
-                if (rpre_p) v = v + rv[r][q];
-                if (a.relu) v = fmaxf(v, 0.0f);
-                if (rpost_p) v = v + (rpre_p ? rpost_p[off] : rv[r][q]);
-                a.out[off] = v;
+                for (int q = 0; q < 4; ++q) {
+                    bool ok;
+                    const size_t off = out_off(16 * (th0 + h) + 4 * cm + NR * XSI + rr, q, co, ok);
+                    rv[rr][q] = (rfirst && ok) ? rfirst[off] : 0.0f;
+                }
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const int t = 16 * (th0 + h) + 4 * cm + NR * XSI + rr;
+                float f[2][4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    f[0][s2] = (m[s2][h][rr] + m[4 + s2][h][rr]) + m[8 + s2][h][rr];
+                    f[1][s2] = (m[4 + s2][h][rr] - m[8 + s2][h][rr]) - m[12 + s2][h][rr];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int dy = q >> 1, dx = q & 1;
+                    bool ok;
+                    const size_t off = out_off(t, q, co, ok);
+                    if (!ok) continue;
+                    float v = dx == 0 ? (f[dy][0] + f[dy][1]) + f[dy][2] : (f[dy][1] - f[dy][2]) - f[dy][3];
+                    v = v * sc + sh;
+                    if (rpre_p) v = v + rv[rr][q];
+                    if (a.relu) v = fmaxf(v, 0.0f);
+                    if (rpost_p) v = v + (rpre_p ? rpost_p[off] : rv[rr][q]);
+                    a.out[off] = v;
+                }
             }
         }
-    }
+    };
+    if (xs == 0) finish(WinoIC<0>{});
+    else if constexpr (XS == 2) finish(WinoIC<1>{});
+}
+
+// Launch plan: the tile grid with the fewest 32-tile slots over the image (ties:
+// fewer tiles past the image, then the wider grid), NB = 2 where Cpo % 64 == 0 unless that leaves
+// fewer than 2 blocks per CU, XS = 2 where the launch still has at most one block per CU.
+struct WinoPlan {
+    int tr, tc, nb, xs;
+    long long blocks;
+};
+
+static WinoPlan wino_plan(int N, int H, int W, int Cpo) {
+    WinoPlan p{4, 8, 1, 1, 0};
+    long long best = -1, best_cov = 0;
+    const int ty = (H + 1) / 2, tx = (W + 1) / 2;  // Winograd tiles of the image
+    for (int tr = 2; tr <= 16; ++tr)
+        for (int tc = 2; tc <= 16; ++tc) {
+            if (tr * tc > 32 || (2 * tr + 2) * (2 * tc + 2) > kWinoHaloPx) continue;
+            const long long nblk = (long long)((ty + tr - 1) / tr) * ((tx + tc - 1) / tc);
+            const long long slots = nblk * 32, covered = nblk * tr * tc;
+            const bool better = best < 0 || slots < best ||
+                                (slots == best && (covered < best_cov || (covered == best_cov && tc > p.tc)));
+            if (better) {
+                best = slots;
+                best_cov = covered;
+                p.tr = tr;
+                p.tc = tc;
+            }
+        }
+    const long long per_img = (long long)((ty + p.tr - 1) / p.tr) * ((tx + p.tc - 1) / p.tc);
+    const long long b1 = (long long)N * per_img * (Cpo / 32);
+    p.nb = (Cpo % 64 == 0 && b1 / 2 >= 512) ? 2 : 1;
+    p.blocks = b1 / p.nb;
+    p.xs = (FVP_WINO_XS_MAX > 1 && p.blocks <= 256) ? 2 : 1;
+    return p;
 }
 
 }  // namespace fvp
+
+extern "C" int fvp_conv3x3_wino_plan(int N, int H, int W, int Cpo, int *plan) {
+    if (!plan) return FVP_ERR_NULL;
+    if (N <= 0 || H <= 0 || W <= 0 || Cpo <= 0 || Cpo % 32) return FVP_ERR_SHAPE;
+    const fvp::WinoPlan p = fvp::wino_plan(N, H, W, Cpo);
+    const long long covered = (long long)((((H + 1) / 2) + p.tr - 1) / p.tr) * p.tr * 2 *
+                              ((((W + 1) / 2) + p.tc - 1) / p.tc) * p.tc * 2;
+    plan[0] = p.tr;
+    plan[1] = p.tc;
+    plan[2] = p.nb;
+    plan[3] = p.xs;
+    plan[4] = (int)((p.blocks > 0x7fffffffLL) ? 0x7fffffff : p.blocks);
+    // slot coverage: 1000 x (32-tile slots x 4 px) / (H x W)
+    plan[5] = (int)(1000 * ((covered / (4LL * p.tr * p.tc)) * 32 * 4) / ((long long)H * W));
+    return FVP_OK;
+}
 
 extern "C" int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo,
                                      const float *scale, const float *shift, const float *res_pre,
                                      const float *res_post, int relu, float *out, void *stream) {
     if (!in || !u || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 32) return FVP_ERR_SHAPE;
-    fvp::WinoArgs a{in, u, scale, shift, res_pre, res_post, out, N, H, W, Cpi, Cpo, relu,
-                    (H + fvp::kWinoTH - 1) / fvp::kWinoTH, (W + fvp::kWinoTW - 1) / fvp::kWinoTW};
-    const int nb = Cpo % 64 == 0 ? 2 : 1;
-    const long long blocks = (long long)N * a.tiles_y * a.tiles_x * (Cpo / (32 * nb));
-    if (blocks > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    const fvp::WinoPlan p = fvp::wino_plan(N, H, W, Cpo);
+    if (p.blocks > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    fvp::WinoArgs a{in, u, scale, shift, res_pre, res_post, out, N, H, W, Cpi, Cpo, relu, p.tr, p.tc,
+                    (H + 2 * p.tr - 1) / (2 * p.tr), (W + 2 * p.tc - 1) / (2 * p.tc)};
     hipStream_t s = (hipStream_t)stream;
-    const size_t lds = (size_t)fvp::kWinoRLds * sizeof(float);
-    if (nb == 2)
-        hipLaunchKernelGGL(fvp::conv_wino_kernel<2>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+    const dim3 grid((unsigned)p.blocks);
+    auto go = [&](auto kernel, int nb, int xs) {
+        hipLaunchKernelGGL(kernel, grid, dim3(256 * xs), (size_t)fvp::wino_lds_floats(nb, xs) * sizeof(float), s, a);
+    };
+    if (p.nb == 2)  // (NB = 2 implies >= 512 blocks, so XS = 1)
+        go(fvp::conv_wino_kernel<2, 1>, 2, 1);
+    else if (p.xs == 2)
+        go(fvp::conv_wino_kernel<1, 2>, 1, 2);
     else
-        hipLaunchKernelGGL(fvp::conv_wino_kernel<1>, dim3((unsigned)blocks), dim3(256), lds, s, a);
+        go(fvp::conv_wino_kernel<1, 1>, 1, 1);
     return (int)hipGetLastError();
 }

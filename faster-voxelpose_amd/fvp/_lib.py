@@ -94,6 +94,7 @@ SIGNATURES = {
     "fvp_conv2d_ex_workspace_bytes": [c_int] * 13,
     "fvp_conv2d_geom": [c_int] * 10 + [ctypes.POINTER(c_int)],
     "fvp_maxpool_pad_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv_front7_f32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_front7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_stem7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_maxpool_pad_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
@@ -104,12 +105,13 @@ SIGNATURES = {
                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_copy_f4": [c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv3x3_wino_plan": [c_int, c_int, c_int, c_int, c_void_p],
     "fvp_conv3x3_wino_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 15
 _LIB = None
 
 

@@ -264,12 +264,10 @@ class ConvLayer:
 
     def _wino_pays(self, x: Act) -> bool:
         """AUTO's Winograd rule, from tools/wino_probe.py (profiles/round5/wino): every
-        eligible layer measured gains (P2PNet 16->32 .. 128->128: 1.28-1.60x,
-        CenterNet 32 / 64 channels 1.48 / 1.19x, ResNet-50 3x3: 1.50-1.80x) unless
-        the 8 x 16 output tiles overhang the image by more than a quarter
-        (CenterNet at 20 x 20: 1.9x the pixels, 0.88x)."""
-        tiles = -(-x.H // 8) * 8 * (-(-x.W // 16) * 16)
-        return tiles <= 1.25 * x.H * x.W
+        eligible layer measured gains (P2PNet 16->32 .. 128->128: 1.24-1.61x,
+        CenterNet 1.33-1.93x, ResNet-50 3x3: 1.45-1.79x) unless the launch's tile
+        slots (fvp_conv3x3_wino_plan) exceed the image by more than 30 %."""
+        return wino_plan(x.N, x.H, x.W, self.Cpo)[5] <= 1300
 
     def flops(self, x: Act) -> int:
         Ho, Wo = self.out_hw(x.H, x.W)
@@ -278,6 +276,13 @@ class ConvLayer:
 
 
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+def wino_plan(N: int, H: int, W: int, Cpo: int) -> tuple:
+    """fvp_conv3x3_wino_plan: (tile rows, tile columns, NB, XS, blocks, 1000 x slot coverage)."""
+    plan = (ctypes.c_int * 6)()
+    _lib.check(_lib.load().fvp_conv3x3_wino_plan(N, H, W, Cpo, plan), "fvp_conv3x3_wino_plan")
+    return tuple(plan)
 
 
 def wino_weights(w: torch.Tensor, cpi: int, cpo: int) -> torch.Tensor:
@@ -467,11 +472,13 @@ class FvpCNN:
                 inner += [c for c, _ in self.hm[:-1]] + [c for c, _ in self.size[:-1]]
             for c in inner:
                 c.act_bf16 = c.bf16
-            self._compile_front7()
+        if self.kind in ("p2p", "centernet") and (dtype == torch.bfloat16 or algo in (None, CONV_AUTO)):
+            self._compile_front7(dtype)
 
-    def _compile_front7(self):
-        """The front Basic2DBlock(J <= 16, 16, 7) as fvp_conv_front7_bf16 straight
-        from the NCHW maps (2-D nets, bf16): weights [16][50 taps][16]."""
+    def _compile_front7(self, dtype):
+        """The front Basic2DBlock(J <= 16, 16, 7) straight from the NCHW maps (no
+        layout pass): fvp_conv_front7_f32 (weights [49 taps][16 co][16 c], fp32) or
+        fvp_conv_front7_bf16 ([16 co][50 taps][16 c], bf16)."""
         f = self.front
         if f.kind != "chain" or not f.parts or f.parts[0].kind != "seq" or len(f.parts[0].parts) != 1:
             return
@@ -480,20 +487,25 @@ class FvpCNN:
                 and c.Cin <= 16 and c.Cpo == 16):
             return
         w = self.module.front_layers[0].block[0].weight.detach().float()  # [Cout][Cin][7][7]
-        wp = torch.zeros((16, 50, 16), dtype=torch.float32, device=w.device)
-        wp[:c.Cout, :49, :c.Cin] = w.permute(0, 2, 3, 1).reshape(c.Cout, 49, c.Cin)
-        self.front7 = (wp.reshape(16, 800).to(torch.bfloat16).contiguous(), c)
+        if dtype == torch.bfloat16:
+            wp = torch.zeros((16, 50, 16), dtype=torch.float32, device=w.device)
+            wp[:c.Cout, :49, :c.Cin] = w.permute(0, 2, 3, 1).reshape(c.Cout, 49, c.Cin)
+            self.front7 = ("fvp_conv_front7_bf16", wp.reshape(16, 800).to(torch.bfloat16).contiguous(), c)
+        else:
+            wp = torch.zeros((49, 16, 16), dtype=torch.float32, device=w.device)
+            wp[:, :c.Cout, :c.Cin] = w.permute(2, 3, 0, 1).reshape(49, c.Cout, c.Cin)
+            self.front7 = ("fvp_conv_front7_f32", wp.contiguous(), c)
 
     def _front(self, x: torch.Tensor) -> Act:
         """front_layers(x) for NCHW fp32 maps x."""
         if self.front7 is None:
             return self.front(to_nhwc(x))
-        wp, c = self.front7
+        fn, wp, c = self.front7
         x = x.float().contiguous()
         N, C, H, W = x.shape
-        out = torch.empty((N, H, W, 16), dtype=torch.bfloat16, device=x.device)
-        _lib.call("fvp_conv_front7_bf16", _ptr(x), N, C, H, W, _ptr(wp), _ptr(c.scale), _ptr(c.shift), _ptr(out),
-                  _stream(out))
+        odt = torch.bfloat16 if fn.endswith("bf16") else torch.float32
+        out = torch.empty((N, H, W, 16), dtype=odt, device=x.device)
+        _lib.call(fn, _ptr(x), N, C, H, W, _ptr(wp), _ptr(c.scale), _ptr(c.shift), _ptr(out), _stream(out))
         a = Act(out, c.Cout)
         for sub in self.front.parts[1:]:
             a = sub(a)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 13
+#define FVP_ABI_VERSION 15
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -402,6 +402,12 @@ size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int K
 int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo, const float *scale,
                           const float *shift, const float *res_pre, const float *res_post, int relu, float *out,
                           void *stream);
+/* The launch fvp_conv3x3_wino_nhwc makes for a shape (host only): plan[0..5] =
+ * {tile rows, tile columns (Winograd 2x2 tiles per block), 32-column blocks
+ * per block (1 or 2), waves sets splitting the 16 transform positions (1 or 2),
+ * blocks, 1000 x (tile slots x 4 px) / (H x W)} -- the last is the MFMA work
+ * over the useful work, what the AUTO rule of fvp/cnn.py reads. */
+int fvp_conv3x3_wino_plan(int N, int H, int W, int Cpo, int *plan);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
 int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf
@@ -424,6 +430,13 @@ int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W, const void
  * c >= C; scale / shift: fp32 [16].  Opt-in precision. */
 int fvp_conv_front7_bf16(const float *x, int N, int C, int H, int W, const void *wpack, const float *scale,
                          const float *shift, void *out, void *stream);
+/* The same front Basic2DBlock on the fp32 matrix cores (exact fp32 products,
+ * fp32 sums), NCHW fp32 maps [N][C][H][W] -> fp32 NHWC [N][H][W][16]: wpack
+ * fp32 [49][16][16] = W[co][c][ky][kx] at (7*ky + kx, co, c), zero for c >= C;
+ * scale / shift: fp32 [16] (BN folded).  The default fp32 front layer of
+ * fvp/cnn.py FvpCNN (P2PNet, CenterNet). */
+int fvp_conv_front7_f32(const float *x, int N, int C, int H, int W, const float *wpack, const float *scale,
+                        const float *shift, float *out, void *stream);
 int fvp_maxpool_pad_nhwc_bf16(const void *in, int N, int H, int W, int C, int K, int S, int P, void *out,
                               void *stream);
 /* 2x2 / stride-2 max pool of NHWC activations (C % 4 == 0), NaN-propagating. */

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 13
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 15
     assert lib.fvp_status_string(0) == b"success"
 
 
@@ -89,6 +89,22 @@ def test_argument_validation_without_gpu():
     assert lib.fvp_conv2d_nhwc(1, 1, 1, 8, 16, 1, 1, 1, 16, 128, 1, 1, None, None, 0, 3, 1, None) == 1002  # upsample2
     with pytest.raises(_lib.FvpError, match="NULL"):
         _lib.check(1001, "fvp_voxelize")
+
+
+@pytest.mark.parametrize("shape, want", [
+    ((240, 64, 64, 64), (4, 8, 2, 1, 7680, 1000)),   # P2PNet 64 px: exact 8 x 16 px tiles, 64 columns a block
+    ((240, 64, 64, 32), (4, 8, 1, 1, 7680, 1000)),   # 32 output channels: NB = 1
+    ((240, 16, 16, 128), (4, 8, 2, 1, 960, 1000)),   # >= 512 blocks at NB = 2
+    ((8, 80, 80, 32), (4, 8, 1, 1, 400, 1000)),      # CenterNet 80 px: > 256 blocks, 4-wave blocks
+    ((8, 40, 40, 64), (3, 10, 1, 2, 224, 1120)),     # 20 x 20 tiles: 3 x 10 grids (7 x 2 per image)
+    ((8, 20, 20, 128), (5, 5, 1, 2, 128, 1280)),     # 10 x 10 tiles: 5 x 5 grids, 25 of 32 slots
+    ((40, 16, 30, 512), (4, 8, 2, 1, 1280, 1066)),   # ResNet-50 stage 4: 8 x 15 tiles
+])
+def test_wino_plan(shape, want):
+    """fvp_conv3x3_wino_plan (host only): tile grid, NB, XS, blocks, slot coverage."""
+    from fvp import cnn
+
+    assert cnn.wino_plan(*shape) == want
 
 
 def test_ops_refuse_cpu_tensors():

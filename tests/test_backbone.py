@@ -79,6 +79,8 @@ def test_conv_geometry_host():
     assert lib.fvp_conv_stem7_bf16(None, 1, 3, 64, 64, 1, 1, 1, 1, None) == 1001
     assert lib.fvp_conv_front7_bf16(1, 1, 17, 64, 64, 1, 1, 1, 1, None) == 1002     # > 16 input planes
     assert lib.fvp_conv_front7_bf16(None, 1, 15, 64, 64, 1, 1, 1, 1, None) == 1001
+    assert lib.fvp_conv_front7_f32(1, 1, 17, 64, 64, 1, 1, 1, 1, None) == 1002
+    assert lib.fvp_conv_front7_f32(None, 1, 15, 64, 64, 1, 1, 1, 1, None) == 1001
     # FVP_CONV_F32_KC (fp32 LDS-DMA kernel): not with bf16 operands, Cpi % 16 only
     conv = lambda cpi, flags: lib.fvp_conv2d_nhwc_ex(1, 1, 8, 8, cpi, 1, 3, 3, 16, 128, 1, 1, None, None, 0,
                                                       0, 1, 1, 1, 1, flags, 0, 1, None, 0, None)

@@ -97,14 +97,18 @@ def test_conv_layer_vs_torch(gpu_device, conv_kernel, cin, cout, k, hw, res):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cin,cout,hw,res", [(16, 32, (13, 21), None), (48, 64, (9, 30), "pre"),
-                                             (32, 96, (17, 17), "post"), (128, 128, (16, 16), "pre"),
-                                             (1, 64, (8, 16), None), (64, 64, (2, 3), "post")])
-def test_wino_conv_vs_torch(gpu_device, cin, cout, hw, res):
+@pytest.mark.parametrize("n,cin,cout,hw,res", [
+    (2, 16, 32, (13, 21), None), (2, 48, 64, (9, 30), "pre"), (2, 32, 96, (17, 17), "post"),
+    (2, 128, 128, (16, 16), "pre"), (2, 1, 64, (8, 16), None), (2, 64, 64, (2, 3), "post"),
+    (3, 128, 128, (20, 20), "pre"), (2, 64, 64, (40, 40), "post"), (70, 32, 64, (30, 34), "pre"),
+    (80, 64, 64, (32, 32), None), (40, 64, 64, (32, 32), "post")])
+def test_wino_conv_vs_torch(gpu_device, n, cin, cout, hw, res):
     """Winograd F(2x2, 3x3) (fvp_conv3x3_wino_nhwc) on ragged images (partial
-    8 x 16 output tiles, images smaller than one tile), one and several
-    16-channel K steps, 32- and 64-column blocks (Cout padded to 32 / 64),
-    BN folded, the residual added before or after the ReLU: fp32 tolerance."""
+    tile grids, images smaller than one tile, the 5 x 5 and 3 x 10 grids of
+    20^2 / 40^2 maps), one and several 16-channel K steps, 32- and 64-column
+    blocks (Cout padded to 32 / 64), the 8-wave xi-split blocks of small
+    launches and the 4-wave blocks of large ones (fvp_conv3x3_wino_plan), BN
+    folded, the residual added before or after the ReLU: fp32 tolerance."""
     import torch.nn as nn
 
     from fvp import cnn, synthetic
@@ -113,12 +117,21 @@ def test_wino_conv_vs_torch(gpu_device, cin, cout, hw, res):
     seq.load_state_dict(synthetic.seeded_state_dict(seq, 3 * cin + cout))
     seq = seq.to(gpu_device)
     g = torch.Generator().manual_seed(cout)
-    x = (torch.rand((2, cin) + hw, generator=g) - 0.5).to(gpu_device)
-    r = torch.rand((2, cout) + hw, generator=g).to(gpu_device) if res else None
+    x = (torch.rand((n, cin) + hw, generator=g) - 0.5).to(gpu_device)
+    r = torch.rand((n, cout) + hw, generator=g).to(gpu_device) if res else None
     with torch.no_grad():
         ref = seq(x)
         ref = torch.relu(ref + r) if res == "pre" else torch.relu(ref) + r if res == "post" else torch.relu(ref)
     layer = cnn.ConvLayer(seq[0], seq[1], algo=cnn.CONV_WINO)
+    plan = cnn.wino_plan(n, hw[0], hw[1], layer.Cpo)
+    if (n, hw) == (70, (30, 34)):
+        assert plan[2:4] == (2, 1), plan  # 64-column 4-wave blocks
+    if (n, hw) == (80, (32, 32)):
+        assert plan[2:4] == (2, 1), plan
+    if (n, hw) == (40, (32, 32)):
+        assert plan[2:4] == (1, 1), plan  # 32-column 4-wave blocks
+    if n <= 3:
+        assert plan[3] == 2, plan  # 8-wave xi-split blocks
     ra = cnn.to_nhwc(r) if res else None
     got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=ra if res == "pre" else None,
                             res_post=ra if res == "post" else None))
@@ -307,7 +320,8 @@ def test_bf16_front7_vs_torch(gpu_device, cin, hw):
     assert f.front7 is not None
     x = torch.rand((3, cin) + hw, generator=torch.Generator().manual_seed(cin)).to(gpu_device)
     x = x.to(torch.bfloat16).float()
-    wp, c = f.front7
+    fn, wp, c = f.front7
+    assert fn == "fvp_conv_front7_bf16"
     out = torch.empty((3,) + hw + (16,), dtype=torch.bfloat16, device=gpu_device)
     from fvp import _lib
     from fvp.ops import _ptr, _stream
@@ -319,6 +333,33 @@ def test_bf16_front7_vs_torch(gpu_device, cin, hw):
     got = out.float().permute(0, 3, 1, 2)
     err = float((got - ref).abs().max()) / float(ref.abs().max())
     assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,cin,hw", [(3, 15, (64, 64)), (2, 15, (37, 50)), (8, 3, (80, 80)), (2, 16, (9, 70)),
+                                      (3, 1, (5, 3)), (80, 15, (64, 64))])
+def test_f32_front7_vs_torch(gpu_device, n, cin, hw):
+    """fvp_conv_front7_f32 (the fp32 nets' Basic2DBlock(J, 16, 7) from the NCHW
+    maps, AUTO's front layer): fp32 tolerance against torch's Basic2DBlock,
+    ragged 8 x 16 tiles, images smaller than a tile, fewer than 16 planes and a
+    launch whose persistent blocks walk several tiles each (80 x 64^2: 2,560
+    tiles)."""
+    import cnn_arch
+    from fvp import _lib, cnn, synthetic
+    from fvp.ops import _ptr, _stream
+
+    p2p = cnn_arch.P2PNet(cin, 15).eval()
+    p2p.load_state_dict(synthetic.seeded_state_dict(p2p, 50 + cin))
+    p2p = p2p.to(gpu_device)
+    f = cnn.FvpCNN(p2p)
+    fn, wp, c = f.front7
+    assert fn == "fvp_conv_front7_f32"
+    x = torch.rand((n, cin) + hw, generator=torch.Generator().manual_seed(cin + n)).to(gpu_device)
+    out = torch.empty((n,) + hw + (16,), device=gpu_device)
+    _lib.call(fn, _ptr(x), n, cin, hw[0], hw[1], _ptr(wp), _ptr(c.scale), _ptr(c.shift), _ptr(out), _stream(out))
+    with torch.no_grad():
+        ref = p2p.front_layers[0](x)
+    _close(out.permute(0, 3, 1, 2).cpu().numpy(), ref.cpu().numpy(), f"front7 f32 {n} {cin} {hw}")
 
 
 @pytest.mark.gpu

@@ -49,8 +49,9 @@ def main():
     f_p2p, f_cn = cnn.FvpCNN(p2p, algo=cnn_algo), cnn.FvpCNN(cn, algo=cnn_algo)
     b_p2p, b_cn = cnn.FvpCNN(p2p, torch.bfloat16), cnn.FvpCNN(cn, torch.bfloat16)
 
-    def flops(plan_net, x):
-        # count with the fvp layer descriptions: 2*M*N*K per conv
+    def flops(plan_net, x, net=None):
+        # count with the fvp layer descriptions: 2*M*N*K per conv (the front 7x7 layer counted
+        # through its ConvLayer: net.front7, the NCHW front kernel, is off while counting)
         tot = 0
         orig = cnn.ConvLayer.__call__
 
@@ -59,10 +60,15 @@ def main():
             tot += self.flops(a)
             return orig(self, a, relu, res_pre, res_post)
         cnn.ConvLayer.__call__ = counting
+        front7 = getattr(net, "front7", None)
+        if net is not None:
+            net.front7 = None
         try:
             plan_net(x)
         finally:
             cnn.ConvLayer.__call__ = orig
+            if net is not None:
+                net.front7 = front7
         return tot
 
     def timeit(fn):
@@ -82,11 +88,12 @@ def main():
 
     out = {}
     with torch.no_grad():
-        for name, fv, bv, tv, x in (("p2pnet_jln", lambda: f_p2p(x_jln), lambda: b_p2p(x_jln), lambda: p2p(x_jln),
-                                     x_jln),
+        for name, fv, bv, tv, x in (("p2pnet_jln", lambda: f_p2p(x_jln), lambda: b_p2p(x_jln),
+                                     lambda: p2p(x_jln), x_jln),
                                     ("centernet_hdn", lambda: f_cn.from_xy(x_hdn), lambda: b_cn.from_xy(x_hdn),
                                      lambda: (cn.output_hm(cn.encoder_decoder(cn.front_layers(x_hdn))),), x_hdn)):
-            fl = flops(f_p2p if name.startswith("p2p") else (lambda t: f_cn.from_xy(t)), x)
+            p2p_line = name.startswith("p2p")
+            fl = flops(f_p2p if p2p_line else (lambda t: f_cn.from_xy(t)), x, f_p2p if p2p_line else f_cn)
             t_f, t_t, t_b = timeit(fv), timeit(tv), timeit(bv)
             from fvp.graphs import CapturedStep
             t_g = timeit(CapturedStep(fv).replay)  # the same launches replayed from one hipGraph

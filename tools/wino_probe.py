@@ -3,7 +3,7 @@
 (AUTO without Winograd) on the 3x3 layer shapes of P2PNet (240 plane images of
 64^2 -- C3 B=8, 10 proposals), CenterNet (8 frames of 80^2) and PoseResNet-50
 (40 images), fused BN + ReLU (+ residual): kernel time by HIP events (mean of
---reps back-to-back calls), TF/s of the direct-conv FLOPs, and the max error of
+--reps back-to-back calls, the median of 3 such batches), TF/s of the direct-conv FLOPs, and the max error of
 each against torch's conv (fraction of the output scale).  One JSON line each.
 
     python3 tools/wino_probe.py [--reps 20]
@@ -60,15 +60,18 @@ def main():
                 layer = cnn.ConvLayer(seq[0], seq[1], algo=algo)
                 out = layer(xa, relu=True, res_pre=ra)
                 torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(args.reps):
-                    layer(xa, relu=True, res_pre=ra, out=out.t)
-                e1.record()
-                torch.cuda.synchronize()
+                times = []
+                for _ in range(3):  # (the median of 3 batches: a host stall inside one batch idles the GPU)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.reps):
+                        layer(xa, relu=True, res_pre=ra, out=out.t)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times.append(e0.elapsed_time(e1) / args.reps)
             finally:
                 cnn.WINO_AUTO = wino_auto
-            ms = e0.elapsed_time(e1) / args.reps
+            ms = sorted(times)[1]
             got = cnn.to_nchw(out)
             err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-6))
             line[tag] = {"us": round(ms * 1e3, 1), "tflops": round(line["gflop"] / ms, 1), "err": float(f"{err:.3g}"),

@@ -25,7 +25,9 @@
 // All 16 xi accumulators of a (tile, column) sit in one lane, so after the K
 // loop the output transform runs in registers and the epilogue of
 // fvp_conv2d_nhwc_ex is applied: acc * scale + shift (+ res_pre), ReLU,
-// (+ res_post), NHWC stores.
+// (+ res_post), NHWC stores -- and optionally the 2 x 2 max pool that follows
+// (Pool2DBlock, cnns_2d.py:67-79): a Winograd tile's four outputs are exactly
+// one pool window, so the pooled map is written from the same registers.
 #include "fvp_layout.h"
 
 
@@ -39,6 +41,7 @@ struct WinoArgs {
     const float *res_pre;   // [N][H][W][Cpo] or null
     const float *res_post;  // [N][H][W][Cpo] or null
     float *out;             // [N][H][W][Cpo]
+    float *pool;            // [N][H/2][W/2][Cpo]: max_pool2d(out, 2, 2), or null
     int N, H, W, Cpi, Cpo, relu;
     int tr, tc;             // Winograd tiles per block: tr rows x tc columns (tr * tc <= 32)
     int tiles_y, tiles_x;   // blocks per image: ceil(H / 2tr), ceil(W / 2tc)
@@ -283,18 +286,27 @@ __global__ __launch_bounds__(256 * XS, XS == 1 ? 2 : 1) void conv_wino_kernel(Wi
                     f[0][s2] = (m[s2][h][rr] + m[4 + s2][h][rr]) + m[8 + s2][h][rr];
                     f[1][s2] = (m[4 + s2][h][rr] - m[8 + s2][h][rr]) - m[12 + s2][h][rr];
                 }
+                float pv[4];
+                bool full = true;  // the tile's 2 x 2 outputs all inside the image: one max_pool2d(2, 2) window
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int dy = q >> 1, dx = q & 1;
                     bool ok;
                     const size_t off = out_off(t, q, co, ok);
-                    if (!ok) continue;
+                    full = full && ok;
                     float v = dx == 0 ? (f[dy][0] + f[dy][1]) + f[dy][2] : (f[dy][1] - f[dy][2]) - f[dy][3];
                     v = v * sc + sh;
                     if (rpre_p) v = v + rv[rr][q];
                     if (a.relu) v = fmaxf(v, 0.0f);
-                    if (rpost_p) v = v + (rpre_p ? rpost_p[off] : rv[rr][q]);
-                    a.out[off] = v;
+                    if (rpost_p) v = v + (rpre_p ? (ok ? rpost_p[off] : 0.0f) : rv[rr][q]);
+                    pv[q] = v;
+                    if (ok) a.out[off] = v;
+                }
+                if (a.pool && full) {  // F.max_pool2d's window order (fvp_maxpool_nhwc): NaN-propagating
+                    const int ti = (t * mtc) >> 16, tj = t - ti * tc;
+                    const int py = (y0 >> 1) + ti, pxo = (x0 >> 1) + tj;
+                    a.pool[(((size_t)img * (a.H >> 1) + py) * (a.W >> 1) + pxo) * a.Cpo + co] =
+                        nanmax(nanmax(nanmax(pv[0], pv[1]), pv[2]), pv[3]);
                 }
             }
         }
@@ -357,12 +369,12 @@ extern "C" int fvp_conv3x3_wino_plan(int N, int H, int W, int Cpo, int *plan) {
 
 extern "C" int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo,
                                      const float *scale, const float *shift, const float *res_pre,
-                                     const float *res_post, int relu, float *out, void *stream) {
+                                     const float *res_post, int relu, float *out, float *pool, void *stream) {
     if (!in || !u || !scale || !shift || !out) return FVP_ERR_NULL;
     if (N <= 0 || H <= 0 || W <= 0 || Cpi <= 0 || Cpi % 16 || Cpo <= 0 || Cpo % 32) return FVP_ERR_SHAPE;
     const fvp::WinoPlan p = fvp::wino_plan(N, H, W, Cpo);
     if (p.blocks > 0x7fffffffLL) return FVP_ERR_SHAPE;
-    fvp::WinoArgs a{in, u, scale, shift, res_pre, res_post, out, N, H, W, Cpi, Cpo, relu, p.tr, p.tc,
+    fvp::WinoArgs a{in, u, scale, shift, res_pre, res_post, out, pool, N, H, W, Cpi, Cpo, relu, p.tr, p.tc,
                     (H + 2 * p.tr - 1) / (2 * p.tr), (W + 2 * p.tc - 1) / (2 * p.tc)};
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)p.blocks);

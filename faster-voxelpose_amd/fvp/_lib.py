@@ -107,11 +107,11 @@ SIGNATURES = {
     "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv3x3_wino_plan": [c_int, c_int, c_int, c_int, c_void_p],
     "fvp_conv3x3_wino_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                              c_void_p, c_int, c_void_p, c_void_p],
+                              c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 _LIB = None
 
 

@@ -60,7 +60,10 @@ def _rup(x: int, m: int) -> int:
 
 
 class Act:
-    """NHWC activation [N,H,W,Cp] with C logical channels (padding channels are zero)."""
+    """NHWC activation [N,H,W,Cp] with C logical channels (padding channels are zero).
+    ``pooled``: its max_pool2d(2, 2) when the producing launch wrote that too."""
+
+    pooled = None
 
     def __init__(self, t: torch.Tensor, C: int):
         self.t, self.C = t, C
@@ -183,8 +186,10 @@ class ConvLayer:
         return hw[0], hw[1]
 
     def __call__(self, x: Act, relu: bool, res_pre: Act | None = None, res_post: Act | None = None,
-                 out: torch.Tensor | None = None) -> Act:
-        """out: optional preallocated [N, Ho, Wo, Cpo] fp32 destination (e.g. a slice of a larger buffer)."""
+                 out: torch.Tensor | None = None, pool: bool = False) -> Act:
+        """out: optional preallocated [N, Ho, Wo, Cpo] fp32 destination (e.g. a slice of a larger buffer);
+        pool: also write max_pool2d(out, 2, 2) as the result's ``pooled`` where the kernel can
+        (the Winograd epilogue; otherwise ``pooled`` stays None)."""
         assert x.Cp == self.Cpi, (x.Cp, self.Cpi)
         if x.t.dtype == torch.bfloat16 and (not self.bf16 or self.Cpi % 16):  # fp32 kernels / 4-12 channel input
             x = Act(x.t.float(), x.C)
@@ -206,10 +211,15 @@ class ConvLayer:
             self._ws[key] = self._plan(x)
         nws, dma = self._ws[key]
         if dma == "wino":
+            pt = torch.empty((x.N, x.H // 2, x.W // 2, self.Cpo), device=out.device) if pool else None
             _lib.call("fvp_conv3x3_wino_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wino), self.Cpo,
                       _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
-                      _ptr(res_post.t) if res_post else None, int(relu), _ptr(out), _stream(out))
-            return Act(out, self.Cout)
+                      _ptr(res_post.t) if res_post else None, int(relu), _ptr(out), _ptr(pt) if pool else None,
+                      _stream(out))
+            y = Act(out, self.Cout)
+            if pool:
+                y.pooled = Act(pt, self.Cout)
+            return y
         if dma:
             flags, wp = FVP_CONV_F32_KC, self.wpack_kc
         # allocated per call: the caching allocator is stream-ordered, so two
@@ -332,6 +342,51 @@ def to_nchw(x: Act) -> torch.Tensor:
     return out
 
 
+def to_nchw_from(x: Act, c0: int, C: int) -> torch.Tensor:
+    """Channels c0 .. c0 + C - 1 of NHWC activations -> NCHW fp32 (fvp_nhwc_to_nchw on the
+    channel offset: the row pitch stays x.Cp)."""
+    if x.t.dtype != torch.float32:
+        x = Act(x.t.float(), x.C)
+    out = torch.empty((x.N, C, x.H, x.W), dtype=torch.float32, device=x.t.device)
+    _lib.call("fvp_nhwc_to_nchw", _ptr(x.t) + 4 * c0, x.N, C, x.H, x.W, x.Cp, _ptr(out), _stream(out))
+    return out
+
+
+def _merged_heads(hm: nn.Module, size: nn.Module, dtype, algo):
+    """CenterNet's two heads (cnns_2d.py:264-275: Conv3x3(32, hc) + ReLU + Conv1x1(hc, c)
+    each, both on the decoder output) as ONE Conv3x3(32, 2 hc) + ReLU and ONE block-diagonal
+    Conv1x1(2 hc, c_hm + c_size): at 8 frames each head layer is a latency-bound launch,
+    and the merged pair computes the same per-channel sums (the zero blocks add exact
+    zeros).  None if the heads have another shape."""
+    a, b = list(hm.children()), list(size.children())
+    shape = [nn.Conv2d, nn.ReLU, nn.Conv2d]
+    if [type(m) for m in a] != shape or [type(m) for m in b] != shape:
+        return None
+    a3, a1, b3, b1 = a[0], a[2], b[0], b[2]
+    for c3, c1 in ((a3, a1), (b3, b1)):
+        if (tuple(c3.kernel_size) != (3, 3) or tuple(c3.padding) != (1, 1) or tuple(c3.stride) != (1, 1)
+                or tuple(c1.kernel_size) != (1, 1) or tuple(c1.padding) != (0, 0) or tuple(c1.stride) != (1, 1)
+                or c3.groups != 1 or c1.groups != 1 or tuple(c3.dilation) != (1, 1)):
+            return None
+    if a3.in_channels != b3.in_channels:
+        return None
+    ha, hb = a3.out_channels, b3.out_channels
+    dev = a3.weight.device
+    m3 = nn.Conv2d(a3.in_channels, ha + hb, 3, padding=1).to(dev)
+    m1 = nn.Conv2d(ha + hb, a1.out_channels + b1.out_channels, 1).to(dev)
+    with torch.no_grad():
+        def bias(c):
+            return c.bias.detach().float() if c.bias is not None else torch.zeros(c.out_channels, device=dev)
+
+        m3.weight.copy_(torch.cat([a3.weight.detach().float(), b3.weight.detach().float()]))
+        m3.bias.copy_(torch.cat([bias(a3), bias(b3)]))
+        m1.weight.zero_()
+        m1.weight[:a1.out_channels, :ha] = a1.weight.detach().float()
+        m1.weight[a1.out_channels:, ha:] = b1.weight.detach().float()
+        m1.bias.copy_(torch.cat([bias(a1), bias(b1)]))
+    return ConvLayer(m3, None, dtype, algo=algo), ConvLayer(m1, None, dtype, algo=algo), a1.out_channels
+
+
 # ---------------------------------------------------------------------------
 _CONVS = (nn.Conv2d, nn.ConvTranspose2d, nn.Conv1d, nn.ConvTranspose1d)
 _BNS = (nn.BatchNorm2d, nn.BatchNorm1d)
@@ -358,6 +413,7 @@ class _Plan:
 
     def __init__(self, m: nn.Module, dtype=torch.float32, dim: int = 2, algo: int | None = None):
         self.dtype, self.dim, self.algo = dtype, dim, algo
+        self.pool_next = False  # a 2x2 pool follows: a Res2DBlock asks its last conv for the pooled map too
         self.kind, self.parts = self._compile(m)
 
     def layers(self):
@@ -386,7 +442,9 @@ class _Plan:
         if hasattr(m, "encoder_pool1") and hasattr(m, "skip_res1"):  # EncoderDecorder (:123-183)
             names = ["skip_res1", "encoder_pool1", "encoder_res1", "skip_res2", "encoder_pool2", "encoder_res2",
                      "mid_res", "decoder_res2", "decoder_upsample2", "decoder_res1", "decoder_upsample1"]
-            return "encdec", {n: _Plan(getattr(m, n), self.dtype, self.dim, self.algo) for n in names}
+            parts = {n: _Plan(getattr(m, n), self.dtype, self.dim, self.algo) for n in names}
+            parts["encoder_res1"].pool_next = True  # encoder_pool2 pools its output
+            return "encdec", parts
         if isinstance(m, nn.Sequential):
             kids = list(m.children())
             if kids and all(isinstance(k, _CONVS + _BNS + (nn.ReLU,)) for k in kids):
@@ -399,9 +457,12 @@ class _Plan:
         if k == "res":
             c1, c2, skip = p
             skip_x = x if skip is None else skip(x, relu=False)
-            return c2(c1(x, relu=True), relu=True, res_pre=skip_x, res_post=res_post)
+            return c2(c1(x, relu=True), relu=True, res_pre=skip_x, res_post=res_post,
+                      pool=self.pool_next and self.dim == 2)
         if k == "pool":
             assert res_post is None
+            if x.pooled is not None and self.dim == 2:  # written by the producing conv's epilogue
+                return x.pooled
             return maxpool2(x, self.dim)
         if k == "seq":
             for i, (c, relu) in enumerate(p):
@@ -455,6 +516,7 @@ class FvpCNN:
             self.encdec = _Plan(module.encoder_decoder, dtype, algo=algo)
             self.hm = _seq_convs(module.output_hm, dtype, algo)
             self.size = _seq_convs(module.output_size, dtype, algo)
+            self.heads = _merged_heads(module.output_hm, module.output_size, dtype, algo)
         elif hasattr(module, "output_layer"):  # P2PNet
             self.kind = "p2p"
             self.front = _Plan(module.front_layers, dtype, algo=algo)
@@ -463,6 +525,8 @@ class FvpCNN:
         else:
             self.kind = "plain"
             self.plan = _Plan(module, dtype, algo=algo)
+        if self.kind in ("p2p", "centernet") and self.front.kind == "chain" and self.front.parts:
+            self.front.parts[-1].pool_next = True  # encoder_pool1 pools the front layers' output
         self.front7 = None
         if dtype == torch.bfloat16 and self.kind != "plain":
             # bf16 activations between the layers (half the bytes, no per-chunk
@@ -470,6 +534,8 @@ class FvpCNN:
             inner = self.front.layers() + self.encdec.layers()
             if self.kind == "centernet":
                 inner += [c for c, _ in self.hm[:-1]] + [c for c, _ in self.size[:-1]]
+                if self.heads is not None:
+                    inner.append(self.heads[0])
             for c in inner:
                 c.act_bf16 = c.bf16
         if self.kind in ("p2p", "centernet") and (dtype == torch.bfloat16 or algo in (None, CONV_AUTO)):
@@ -532,7 +598,11 @@ class FvpCNN:
     def from_xy(self, xy: torch.Tensor):
         assert self.kind == "centernet"
         f = self.encdec(self._front(xy))
-        return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
+        if self.heads is None:
+            return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
+        c3, c1, n_hm = self.heads  # both heads as one 3x3 and one 1x1 launch
+        y = c1(c3(f, relu=True), relu=False)
+        return to_nchw(Act(y.t, n_hm)), to_nchw_from(y, n_hm, y.C - n_hm)
 
 
 class FvpWeightNet:

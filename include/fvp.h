@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 15
+#define FVP_ABI_VERSION 16
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -396,12 +396,14 @@ size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int K
  *         (xi = 4r + s, step k, cm, co, c4) = U[co][ci = 16k + 4c4 + cm][r][s]
  *         (zero for padding channels)
  *   out   device [N][H][W][Cpo] fp32, Cpo % 32 == 0
+ *   pool  device [N][H/2][W/2][Cpo] fp32 or NULL: F.max_pool2d(out, 2, 2) (NaN-propagating,
+ *         the window order of fvp_maxpool_nhwc) written by the same launch
  * The transforms are exact sums and differences (the weight transform is the
  * caller's, in fp64): the result equals the direct convolution up to their
  * rounding.  FVP_ERR_SHAPE otherwise. */
 int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo, const float *scale,
                           const float *shift, const float *res_pre, const float *res_post, int relu, float *out,
-                          void *stream);
+                          float *pool, void *stream);
 /* The launch fvp_conv3x3_wino_nhwc makes for a shape (host only): plan[0..5] =
  * {tile rows, tile columns (Winograd 2x2 tiles per block), 32-column blocks
  * per block (1 or 2), waves sets splitting the 16 transform positions (1 or 2),

@@ -70,6 +70,26 @@ def test_fvp_cnn_matches_reference(gpu_device):
 
 
 @pytest.mark.gpu
+def test_centernet_merged_heads_match_separate(gpu_device):
+    """FvpCNN runs CenterNet's hm and size heads as one 3x3 (32 -> 64) and one
+    block-diagonal 1x1 launch (cnn._merged_heads): the same outputs as the two
+    heads run separately, to fp32 tolerance, both contiguous NCHW tensors."""
+    from fvp import cnn
+
+    _, cn, _, x_cn = _nets()
+    cn = cn.to(gpu_device)
+    xy = torch.from_numpy(x_cn).to(gpu_device).max(dim=4)[0].repeat(8, 1, 1, 1)
+    f = cnn.FvpCNN(cn)
+    assert f.heads is not None
+    hm, size = f.from_xy(xy)
+    f.heads = None
+    hm1, size1 = f.from_xy(xy)
+    assert hm.is_contiguous() and size.is_contiguous() and hm.shape == hm1.shape and size.shape == size1.shape
+    _close(hm.cpu().numpy(), hm1.cpu().numpy(), "merged hm head")
+    _close(size.cpu().numpy(), size1.cpu().numpy(), "merged size head")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,hw,res", [(15, 16, 7, (64, 64), False), (16, 32, 3, (33, 17), True),
                                                (128, 128, 3, (16, 16), True), (32, 15, 1, (20, 20), False),
                                                (1, 20, 3, (64, 64), False), (40, 70, 5, (9, 11), True),
@@ -133,10 +153,13 @@ def test_wino_conv_vs_torch(gpu_device, n, cin, cout, hw, res):
     if n <= 3:
         assert plan[3] == 2, plan  # 8-wave xi-split blocks
     ra = cnn.to_nhwc(r) if res else None
-    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=ra if res == "pre" else None,
-                            res_post=ra if res == "post" else None))
+    y = layer(cnn.to_nhwc(x), relu=True, res_pre=ra if res == "pre" else None,
+              res_post=ra if res == "post" else None, pool=True)
+    got = cnn.to_nchw(y)
     assert [k for _, k in layer._ws.values()] == ["wino"]
     _close(got.cpu().numpy(), ref.cpu().numpy(), f"wino conv {cin}->{cout} {hw} {res}")
+    # the fused 2 x 2 max pool: exactly max_pool2d of the conv output the same launch wrote
+    assert torch.equal(cnn.to_nchw(y.pooled), torch.nn.functional.max_pool2d(got, 2, 2))
 
 
 @pytest.mark.gpu

@@ -55,10 +55,10 @@ def main():
         tot = 0
         orig = cnn.ConvLayer.__call__
 
-        def counting(self, a, relu, res_pre=None, res_post=None):
+        def counting(self, a, relu, res_pre=None, res_post=None, **kw):
             nonlocal tot
             tot += self.flops(a)
-            return orig(self, a, relu, res_pre, res_post)
+            return orig(self, a, relu, res_pre, res_post, **kw)
         cnn.ConvLayer.__call__ = counting
         front7 = getattr(net, "front7", None)
         if net is not None:

@@ -43,10 +43,10 @@ def main():
     rec = []
     orig = cnn.ConvLayer.__call__
 
-    def timed(self, a, relu, res_pre=None, res_post=None, out=None):
+    def timed(self, a, relu, res_pre=None, res_post=None, out=None, pool=False):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        y = orig(self, a, relu, res_pre, res_post, out)
+        y = orig(self, a, relu, res_pre, res_post, out, pool)
         e1.record()
         rec.append((self, a.H, a.W, a.Cp, a.t.dtype, e0, e1, self.flops(a)))
         return y

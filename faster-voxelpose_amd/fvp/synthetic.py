@@ -151,6 +151,20 @@ def proposals_for_frame(w, frame: int, people: int = 4, bbox=(0.45, 0.55)) -> np
     return out
 
 
+def jln_batch_proposals(w, frame: int, rng: np.random.Generator, n_extra: int) -> np.ndarray:
+    """A frame's JLN proposals [4 + n_extra, 7]: the 4 synthetic people plus n_extra
+    random centres over the whole space with bbox sizes in [-0.2, 1.2] -- windows
+    clipped at either end, skipped (start >= end) and with negative margins
+    (project_individual.py:251-263)."""
+    base = proposals_for_frame(w, frame, 4)
+    extra = np.zeros((n_extra, 7), np.float32)
+    extra[:, 0] = rng.uniform(-4600, 4600, n_extra)
+    extra[:, 1] = -500 + rng.uniform(-4600, 4600, n_extra)
+    extra[:, 2] = rng.uniform(200, 1500, n_extra)
+    extra[:, 5:7] = rng.uniform(-0.2, 1.2, (n_extra, 2))
+    return np.concatenate([base, extra])
+
+
 def joint_features(P: int, J: int, S: int = 64, seed: int = 0) -> np.ndarray:
     """Stand-in P2PNet output [3, P, J, S, S] (fp32): one Gaussian peak (height
     0.15, sigma 3 cells) per (plane, proposal, joint) on N(0, 0.02) noise, so that

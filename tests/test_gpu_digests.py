@@ -86,7 +86,7 @@ def test_sample_grid_digest(gpu_device, wname):
     assert not bad, f"{wname}: sample grid of cameras {bad} differs from the reference's"
 
 
-@pytest.mark.parametrize("key", ["c5_g4", "c5_u"])
+@pytest.mark.parametrize("key", ["c5_g4", "c5_g8", "c5_u"])
 def test_c5_x_slabs_on_the_fly_match_reference(gpu_device, key):
     """Large-frame mode at full C5 geometry (31 ring cameras,
     fp16 heatmaps, the 16-camera cascade, 4 frames per pair-table entry): each

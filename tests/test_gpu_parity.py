@@ -686,6 +686,31 @@ def test_person_planes_batched_matches_per_frame(gpu_device, otf):
     assert k == P
 
 
+@pytest.mark.parametrize("otf", [True, False], ids=["onthefly", "finegrid"])
+def test_person_planes_batched_match_reference_digests(gpu_device, otf):
+    """The JLN's batched launch (forward_batch: 8 C3 frames x 10 proposals, one
+    launch, 4-row blocks) against the REFERENCE's per-person ProjectLayer run frame
+    by frame (tools/gen_golden.py -> individual_batch_c3.npz): every person's xy /
+    xz / yz max-plane hashes to the reference's SHA-256, and the offsets are equal."""
+    import digest_cases as dc
+
+    g = golden("individual_batch_c3.npz")
+    w, layer, cams, seq, rt, hm = _jln_setup(gpu_device, frames=8)
+    assert np.array_equal(dc.input_sha(hm.cpu().numpy()), g["heatmaps_sha256"])
+    layer.on_the_fly = otf
+    props = torch.from_numpy(g["proposals"]).to(gpu_device)  # [8, 10, 7]
+    F_, P_ = props.shape[:2]
+    mask = torch.ones((F_, P_), dtype=torch.bool, device=gpu_device)
+    planes, offset, frame_of = layer.forward_batch(hm, {"seq": [seq] * F_}, props, mask, cams, rt)
+    P = F_ * P_
+    assert planes.shape[0] == 3 * P
+    pl = planes.cpu().numpy()
+    bad = [(f, k, i) for f in range(F_) for k in range(P_) for i in range(3)
+           if not np.array_equal(dc.input_sha(pl[i * P + f * P_ + k]), g["plane_sha256"][f, k, i])]
+    assert not bad, f"planes differing from the reference's (frame, proposal, plane): {bad[:8]}"
+    assert np.array_equal(offset.cpu().numpy().reshape(F_, P_, 3), g["offset"])
+
+
 @pytest.mark.parametrize("K", [1, 16, 17, 40])
 def test_nms_topk_both_paths_vs_oracle(gpu_device, K):
     """K <= 16 takes the register top-K kernel, larger K the rescan kernel; both

@@ -12,7 +12,7 @@ attribute-dict cfg, so lib/core/config.py (easydict) is not imported.
 Outputs: tests/golden/*.npz (inputs that cannot be regenerated bit-exactly
 elsewhere are stored; uniform-random inputs are regenerated from torch seeds).
 
-    python3 -B tools/gen_golden.py [--only whole,c4,c5,e2e,backbone]
+    python3 -B tools/gen_golden.py [--only whole,c4,c5,e2e,backbone,digests,digests:<case>,jlnbatch]
 """
 from __future__ import annotations
 
@@ -110,7 +110,7 @@ def backbone_case(torch, synthetic):
     print("wrote backbone", {k: v.shape for k, v in d.items()})
 
 
-def digest_cases(torch, pw, geometry, WORKLOADS, make_cfg):
+def digest_cases(torch, pw, geometry, WORKLOADS, make_cfg, keys=None):
     """Whole-cube pins: for every case of tests/digest_cases.py, the
     reference's ProjectLayer.forward (project_whole.py:119-168) on the case's
     input; stored are the SHA-256 digests of each frame's full fp32 cube and
@@ -121,8 +121,14 @@ def digest_cases(torch, pw, geometry, WORKLOADS, make_cfg):
     import digest_cases as dc
     from oracle import fvp_oracle as O
 
+    path = os.path.join(OUT, "cube_digests.npz")
     d = {}
+    if keys:  # only these cases, merged into the existing file
+        with np.load(path) as old:
+            d = {k: old[k] for k in old.files}
     for key, (wname, src, frames) in dc.CASES.items():
+        if keys and key not in keys:
+            continue
         w = WORKLOADS[wname]
         hm, _ = dc.inputs(key)
         cams, seq = w.cameras()
@@ -137,8 +143,48 @@ def digest_cases(torch, pw, geometry, WORKLOADS, make_cfg):
         sg = np.ascontiguousarray(layer.sample_grid[seq][:, 0].numpy(), "<f4")  # [V,N,2]: the per-sequence cache
         d[f"grid_{wname}_sha256"] = np.stack([dc.input_sha(sg[v]) for v in range(sg.shape[0])])
         print(f"digest {key}: {frames} x {cube.shape[1:]}  sum {d[f'{key}_sum64']}", flush=True)
-    np.savez_compressed(os.path.join(OUT, "cube_digests.npz"), **d)
+    np.savez_compressed(path, **d)
     print("wrote cube_digests", len(d), "arrays")
+
+
+def individual_batch(torch, pi, geometry, synthetic, WORKLOADS, make_cfg):
+    """The JLN's batched per-person launch pinned to the reference: the
+    reference's per-person ProjectLayer (project_individual.py:222-293) frame by frame
+    on 8 C3 frames x 10 proposals (Gaussian-blob heatmaps, J = 15; each frame's
+    proposals = 4 synthetic people + 6 random centres with clipped, skipped and
+    negative-margin windows), stored as the SHA-256 of each person's xy / xz / yz
+    max-planes (the planes the JLN's CNN reads) plus the offsets and the plane sums."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    sys.path.insert(0, REPO)
+    import digest_cases as dc
+
+    w = WORKLOADS["c3"]
+    F_, P_ = 8, 10
+    cams, seq = w.cameras()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float)
+    layer = pi.ProjectLayer(make_cfg(w, device="cpu"))
+    hm = synthetic.gaussian_heatmaps(w, F_)
+    rng = np.random.default_rng(2)
+    props = np.stack([synthetic.jln_batch_proposals(w, f, rng, P_ - 4) for f in range(F_)])  # [F, P, 7]
+    dig = np.zeros((F_, P_, 3, 32), np.uint8)
+    sums = np.zeros((F_, P_, 3), np.float64)
+    offs = np.zeros((F_, P_, 3), np.float32)
+    x = torch.from_numpy(hm)
+    meta = {"seq": [seq] * F_}
+    with torch.no_grad():
+        for f in range(F_):
+            cubes, offset = layer(x, f, meta, torch.from_numpy(props[f]), cams, rt)
+            parts = (torch.max(cubes, dim=4)[0], torch.max(cubes, dim=3)[0], torch.max(cubes, dim=2)[0])
+            for i, pl in enumerate(parts):
+                a = pl.numpy()
+                for k in range(P_):
+                    dig[f, k, i] = dc.input_sha(a[k])
+                    sums[f, k, i] = a[k].astype(np.float64).sum()
+            offs[f] = offset.numpy()
+            print(f"individual batch frame {f}: {P_} people", flush=True)
+    np.savez_compressed(os.path.join(OUT, "individual_batch_c3.npz"), heatmaps_sha256=dc.input_sha(hm),
+                        proposals=props, plane_sha256=dig, plane_sum64=sums, offset=offs)
+    print("wrote individual_batch_c3")
 
 
 def main():
@@ -221,6 +267,11 @@ def main():
         whole_case("whole_c5", "c5", batch=1, stride=997, store_heatmaps=False)
     if only is None or "digests" in only:  # whole-cube SHA-256 pins of every config
         digest_cases(torch, pw, geometry, WORKLOADS, make_cfg)
+    picked = [k.split(":", 1)[1] for k in (only or ()) if k.startswith("digests:")]
+    if picked:  # --only digests:c5_g8 -> those cases only, merged into cube_digests.npz
+        digest_cases(torch, pw, geometry, WORKLOADS, make_cfg, keys=set(picked))
+    if only is None or "jlnbatch" in only:
+        individual_batch(torch, pi, geometry, synthetic, WORKLOADS, make_cfg)
     if only is None or "e2e" in only:
         e2e_case(torch, geometry, synthetic, WORKLOADS, make_cfg)
     if only is None or "backbone" in only:

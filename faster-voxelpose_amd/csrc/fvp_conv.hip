@@ -1480,6 +1480,32 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float *__restri
     out[gid] = in[((size_t)img * HW + p) * Cp + c];
 }
 
+// The same through LDS: a block moves 64 pixels x Cp channels of one image --
+// 16-B loads of whole pixels, then per channel 64 consecutive pixels (odd LDS
+// pitch: conflict-free column reads).  Cp % 4 == 0, Cp <= 128, 16-B aligned input.
+__global__ __launch_bounds__(256) void nhwc_to_nchw_tiled_kernel(const float *__restrict__ in,
+                                                                 float *__restrict__ out, int C, int HW, int Cp,
+                                                                 int tiles_per_img) {
+    __shared__ float t[64 * 129];
+    const int img = blockIdx.x / tiles_per_img, p0 = (blockIdx.x - img * tiles_per_img) * 64;
+    const int np = HW - p0 < 64 ? HW - p0 : 64, pitch = Cp + 1, nq = Cp >> 2;
+    const float *__restrict__ src = in + ((size_t)img * HW + p0) * Cp;
+    for (int e = threadIdx.x; e < 64 * nq; e += 256) {
+        const int p = e / nq, q = e - p * nq;
+        if (p < np) {
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(src + (size_t)p * Cp + 4 * q);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) t[p * pitch + 4 * q + k] = v[k];
+        }
+    }
+    __syncthreads();
+    float *__restrict__ dst = out + (size_t)img * C * HW + p0;
+    for (int e = threadIdx.x; e < C * 64; e += 256) {
+        const int c = e >> 6, p = e & 63;
+        if (p < np) dst[(size_t)c * HW + p] = t[p * pitch + c];
+    }
+}
+
 }  // namespace fvp
 
 namespace fvp {
@@ -1939,7 +1965,13 @@ extern "C" int fvp_nhwc_to_nchw(const float *in, int N, int C, int H, int W, int
     if (!in || !out) return FVP_ERR_NULL;
     if (N <= 0 || C <= 0 || Cp < C || H <= 0 || W <= 0) return FVP_ERR_SHAPE;
     const long long total = (long long)N * C * H * W;
+    const int HW = H * W, tiles = (HW + 63) / 64;
+    if (Cp % 4 == 0 && Cp <= 128 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (long long)N * tiles <= 0x7fffffffLL) {
+        hipLaunchKernelGGL(fvp::nhwc_to_nchw_tiled_kernel, dim3((unsigned)(N * tiles)), dim3(256), 0,
+                           (hipStream_t)stream, in, out, C, HW, Cp, tiles);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(fvp::nhwc_to_nchw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, in, out, N, C, H * W, Cp);
+                       (hipStream_t)stream, in, out, N, C, HW, Cp);
     return (int)hipGetLastError();
 }

@@ -70,6 +70,21 @@ def test_fvp_cnn_matches_reference(gpu_device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,c,cp,hw", [(3, 15, 16, (64, 64)), (2, 1, 16, (80, 80)), (2, 70, 80, (9, 11)),
+                                       (1, 128, 128, (5, 3)), (4, 3, 4, (1, 7)), (2, 5, 6, (10, 13))])
+def test_nhwc_to_nchw_layouts(gpu_device, n, c, cp, hw):
+    """fvp_nhwc_to_nchw (the LDS-tiled kernel for 16-B aligned pitches <= 128, the
+    element kernel otherwise, and a channel offset via cnn.to_nchw_from): exactly
+    the permuted channels."""
+    from fvp import cnn
+
+    t = torch.randn((n,) + hw + (cp,), generator=torch.Generator().manual_seed(c)).to(gpu_device)
+    assert torch.equal(cnn.to_nchw(cnn.Act(t, c)), t[..., :c].permute(0, 3, 1, 2))
+    if c > 1:
+        assert torch.equal(cnn.to_nchw_from(cnn.Act(t, c), 1, c - 1), t[..., 1:c].permute(0, 3, 1, 2))
+
+
+@pytest.mark.gpu
 def test_centernet_merged_heads_match_separate(gpu_device):
     """FvpCNN runs CenterNet's hm and size heads as one 3x3 (32 -> 64) and one
     block-diagonal 1x1 launch (cnn._merged_heads): the same outputs as the two

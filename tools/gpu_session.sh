@@ -2,9 +2,9 @@
 # One gpurun session on one MI355X: the steps named on the command line, in order, each under its
 # own time limit; the first failing step ends the session.  Output under gpurun_out/$OUT (default s).
 #   tests   the -m gpu suite            smoke  __graft_entry__.smoke()
-#   bench   the default bench line (CPU baseline + traffic PMC)
+#   bench   the default bench line (CPU baseline + traffic PMC; the PMC CSVs copied to $O/bench_pmc)
 #   prof    rocprofv3 kernel trace of the default bench + per-launch-shape summary
-#   c3b8    bench.py --workload c3 --batch 8 over 200 steps
+#   c3b8    bench.py --workload c3 --batch 8 over 200 steps (c3b8g: the same replayed from hipGraphs)
 #   jln     tools/bench_jln.py (32 frames)
 #   all     one bench line per config (C1-C5, C4/C5 at B=32)
 #   pipe    tools/bench_pipeline.py (heatmaps -> poses, and views)
@@ -28,12 +28,16 @@ for step in "$@"; do
            tail -1 $O/gpu_tests.log ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
            tail -1 $O/smoke.log ;;
-    bench) timeout -k 10 600 python bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+    bench) rm -rf gpurun_out/bench_pmc
+           timeout -k 10 600 python bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+           if [ -d gpurun_out/bench_pmc ]; then mkdir -p $O/bench_pmc && cp -r gpurun_out/bench_pmc/. $O/bench_pmc/; fi
            cut -c1-400 $O/bench.json ;;
     prof)  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --traffic off --cpu-baseline off $BENCH_ARGS > $O/prof.log 2>&1 || fail prof $O/prof.log
            python3 tools/launch_shapes.py $O/prof --csv $O/launch_shapes.csv --top 8 ;;
     c3b8)  timeout -k 10 300 python bench.py --workload c3 --batch 8 --steps 200 --warmup 20 --traffic off --cpu-baseline off > $O/bench_c3_b8.json 2> $O/bench_c3_b8.err || fail c3b8 $O/bench_c3_b8.err
            cut -c1-300 $O/bench_c3_b8.json ;;
+    c3b8g) timeout -k 10 300 python bench.py --workload c3 --batch 8 --steps 200 --warmup 20 --graph on --traffic off --cpu-baseline off > $O/bench_c3_b8_graph.json 2> $O/bench_c3_b8_graph.err || fail c3b8g $O/bench_c3_b8_graph.err
+           cut -c1-300 $O/bench_c3_b8_graph.json ;;
     jln)   timeout -k 10 300 python3 tools/bench_jln.py --frames 32 --steps 10 > $O/jln.json 2> $O/jln.err || fail jln $O/jln.err
            cut -c1-300 $O/jln.json ;;
     all)   for wl in c1 c2 c3 c4 c5; do

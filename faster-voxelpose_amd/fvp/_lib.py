@@ -94,6 +94,9 @@ SIGNATURES = {
     "fvp_conv2d_ex_workspace_bytes": [c_int] * 13,
     "fvp_conv2d_geom": [c_int] * 10 + [ctypes.POINTER(c_int)],
     "fvp_maxpool_pad_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv1d_net_lds_bytes": [c_int, c_int],
+    "fvp_conv1d_net": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                       c_int, c_void_p, c_void_p],
     "fvp_conv_front7_f32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_front7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_stem7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -111,7 +114,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 _LIB = None
 
 
@@ -134,7 +137,8 @@ def load():
                       "fvp_voxelize_f16_workspace_bytes": ctypes.c_size_t,
                       "fvp_person_workspace_bytes": ctypes.c_size_t,
                       "fvp_conv2d_workspace_bytes": ctypes.c_size_t,
-                      "fvp_conv2d_ex_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
+                      "fvp_conv2d_ex_workspace_bytes": ctypes.c_size_t,
+                      "fvp_conv1d_net_lds_bytes": ctypes.c_size_t}.get(name, c_int)
     if lib.fvp_abi_version() != ABI_VERSION:
         raise FvpError(f"fvp: ABI version mismatch ({lib.fvp_abi_version()} != {ABI_VERSION})")
     _LIB = lib

@@ -489,6 +489,162 @@ class _Plan:
         raise AssertionError(k)
 
 
+class Net1D:
+    """C2CNet (cnns_1d.py:182-241) compiled into ONE fvp_conv1d_net launch: a block
+    per column runs every layer with the activations in LDS (csrc/fvp_c2c.hip).
+    The program is the layer list of C2CNet.forward / EncoderDecorder.forward
+    (:203-241, :156-179) over activation buffers; params hold each conv's weights
+    as [cin][k][cout] followed by its folded BN scale and shift.  ``None`` from
+    ``build`` when the module has another shape or the buffers exceed LDS."""
+
+    W_CHUNK = 12288  # floats per weight chunk (csrc/fvp_c2c.hip kC2CWChunk)
+
+    def __init__(self):
+        self.ops, self.params, self.off = [], [], 0
+        self.free, self.nbuf, self.slot = [], 0, 0
+
+    def _buf(self, C, L):
+        self.slot = max(self.slot, C * (L + 6) + 16)  # rows [3 zeros, L, 3 zeros]; slack for the last row's reads
+        if self.free:
+            return self.free.pop()
+        self.nbuf += 1
+        return self.nbuf - 1
+
+    def _release(self, *bufs):
+        for b in bufs:
+            if b is not None and b not in self.free:
+                self.free.append(b)
+
+    def _pack(self, w, scale, shift):
+        """w [cin][k][cout]: append W, scale, shift (block padded to 16 B); -> offset."""
+        block = torch.cat([w.reshape(-1), scale, shift])
+        pad = (-block.numel()) % 4
+        if pad:
+            block = torch.cat([block, block.new_zeros(pad)])
+        off = self.off
+        self.params.append(block)
+        self.off += block.numel()
+        return off
+
+    @staticmethod
+    def _fold(conv, bn):
+        cout = conv.weight.shape[1] if isinstance(conv, nn.ConvTranspose1d) else conv.weight.shape[0]
+        dev = conv.weight.device
+        bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
+        if bn is None:
+            return torch.ones(cout, device=dev), bias
+        sc = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+        return sc, (bias - bn.running_mean.detach().float()) * sc + bn.bias.detach().float()
+
+    def conv(self, conv, bn, src, C, L, relu, res_pre=None, res_post=None):
+        """-> (dst, cout, Lout)"""
+        if isinstance(conv, nn.ConvTranspose1d):
+            if tuple(conv.kernel_size) != (2,) or tuple(conv.stride) != (2,) or tuple(conv.padding) != (0,):
+                raise ValueError("ConvTranspose1d(k 2, s 2) only")
+            w = conv.weight.detach().float().permute(0, 2, 1)  # [cin][cout][2] -> [cin][2][cout]
+            kind, Lout = 1, 2 * L
+        else:
+            k = conv.kernel_size[0]
+            if conv.stride[0] != 1 or conv.padding[0] != (k - 1) // 2 or k % 2 == 0 or conv.dilation[0] != 1:
+                raise ValueError("same-padded stride-1 Conv1d only")
+            w = conv.weight.detach().float().permute(1, 2, 0)  # [cout][cin][k] -> [cin][k][cout]
+            kind, Lout = 0, L
+        cin, k, cout = w.shape
+        if cin > C or C % 4 or conv.groups != 1:
+            raise ValueError("channel mismatch")
+        if cin < C:  # the input's zero rows past its channels (the network input padded to 4)
+            w = torch.cat([w, w.new_zeros((C - cin, k, cout))])
+            cin = C
+        cic = min(cin, (self.W_CHUNK // (k * cout)) // 4 * 4)  # 4 channels per product step
+        if cic < 4 or (cic * k * cout) % 4 or ((cin % cic) * k * cout) % 4:
+            raise ValueError("weight chunk alignment")
+        sc, sh = self._fold(conv, bn)
+        dst = self._buf(cout, Lout)
+        self.ops.append([kind, cin, cout, k, L, src, dst, -1 if res_pre is None else res_pre,
+                         -1 if res_post is None else res_post, int(relu), self._pack(w.contiguous(), sc, sh), cic])
+        return dst, cout, Lout
+
+    def pool(self, src, C, L):
+        dst = self._buf(C, L // 2)
+        self.ops.append([2, C, C, 2, L, src, dst, -1, -1, 0, 0, 1])
+        return dst, C, L // 2
+
+    def res(self, m, src, C, L, res_post=None):
+        """Res1DBlock (cnns_1d.py:37-74): relu(c2(relu(c1(x))) + skip(x)) (+ res_post)."""
+        r = list(m.res_branch.children())
+        sk = list(m.skip_con.children())
+        skip = src
+        if sk:
+            skip, _, _ = self.conv(sk[0], sk[1], src, C, L, relu=False)
+        t, Ct, _ = self.conv(r[0], r[1], src, C, L, relu=True)
+        out, Co, _ = self.conv(r[3], r[4], t, Ct, L, relu=True, res_pre=skip, res_post=res_post)
+        self._release(t)
+        if sk:
+            self._release(skip)
+        return out, Co, L
+
+    @classmethod
+    def build(cls, module, cin0: int, L0: int):
+        n = cls()
+        try:
+            cin4 = (cin0 + 3) // 4 * 4
+            x = n._buf(cin4, L0)
+            f = list(module.front_layers.children())
+            b = list(f[0].block.children())
+            y, C, L = n.conv(b[0], b[1], x, cin4, L0, relu=True)
+            n._release(x)
+            x, C, L = n.res(f[1], y, C, L)
+            n._release(y)
+            e = module.encoder_decoder
+            s1, C1, L1 = n.res(e.skip_res1, x, C, L)
+            p, C, L = n.pool(x, C, L)
+            n._release(x)
+            x, C, L = n.res(e.encoder_res1, p, C, L)
+            n._release(p)
+            s2, C2, L2 = n.res(e.skip_res2, x, C, L)
+            p, C, L = n.pool(x, C, L)
+            n._release(x)
+            for name in ("encoder_res2", "mid_res", "decoder_res2"):
+                y, C, L = n.res(getattr(e, name), p, C, L)
+                n._release(p)
+                p = y
+            u = list(e.decoder_upsample2.block.children())
+            x, C, L = n.conv(u[0], u[1], p, C, L, relu=True, res_post=s2)  # upsample(x) + skip_x2
+            n._release(p, s2)
+            y, C, L = n.res(e.decoder_res1, x, C, L)
+            n._release(x)
+            u = list(e.decoder_upsample1.block.children())
+            x, C, L = n.conv(u[0], u[1], y, C, L, relu=True, res_post=s1)  # upsample(x) + skip_x1
+            n._release(y, s1)
+            out, Cf, Lf = n.conv(module.output_hm, None, x, C, L, relu=False)
+        except (ValueError, AttributeError, IndexError):
+            return None
+        shapes = [(o[2], 2 * o[4] if o[0] == 1 else o[4]) for o in n.ops if o[0] != 2]  # (cout, Lout)
+        # positions per thread item: 4 (4 FMAs per LDS weight read), 8 where cout x ceil(L / 4)
+        # exceeds the kernel's 4 items x 256 threads
+        lg = next((g for g in (4, 8) if all(c * -(-Lo // g) <= 1024 for c, Lo in shapes)), None)
+        if lg is None:
+            return None
+        lds = _lib.load().fvp_conv1d_net_lds_bytes(n.slot, n.nbuf)
+        if lds > 160 * 1024:
+            return None
+        dev = module.output_hm.weight.device
+        n.prog = torch.tensor(n.ops, dtype=torch.int32, device=dev).contiguous()
+        n.param = torch.cat(n.params).contiguous().to(dev)
+        n.cin0, n.L0, n.out_buf, n.cout, n.Lout, n.lg = cin0, L0, out, Cf, Lf, lg
+        return n
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.float().contiguous()
+        N = x.shape[0]
+        y = torch.empty((N, self.cout, self.Lout), dtype=torch.float32, device=x.device)
+        if N:
+            _lib.call("fvp_conv1d_net", _ptr(x), N, self.cin0, self.L0, _ptr(self.prog), len(self.ops),
+                      _ptr(self.param), self.slot, self.nbuf, self.out_buf, self.cout, self.Lout, self.lg, _ptr(y),
+                      _stream(y))
+        return y
+
+
 class FvpCNN:
     """Eval-mode P2PNet / CenterNet (or a block of them) on fvp conv kernels.
 
@@ -510,6 +666,8 @@ class FvpCNN:
             self.front = _Plan(module.front_layers, dtype, dim=1, algo=algo)
             self.encdec = _Plan(module.encoder_decoder, dtype, dim=1, algo=algo)
             self.out = ConvLayer(module.output_hm, None, dtype, algo=algo)
+            self.net1d = {}  # (C, L) -> Net1D (fp32 AUTO: the whole net in one launch) or None
+            self.one_launch = dtype == torch.float32 and algo in (None, CONV_AUTO)
         elif hasattr(module, "output_hm") and hasattr(module, "output_size"):  # CenterNet
             self.kind = "centernet"
             self.front = _Plan(module.front_layers, dtype, algo=algo)
@@ -586,6 +744,12 @@ class FvpCNN:
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
         if self.kind == "c2c":  # [N, C, L] as [N, C, 1, L]
+            if self.one_launch:
+                key = tuple(x.shape[1:])
+                if key not in self.net1d:
+                    self.net1d[key] = Net1D.build(self.module, *key)
+                if self.net1d[key] is not None:
+                    return self.net1d[key](x)
             y = self.out(self.encdec(self.front(to_nhwc(x.unsqueeze(2)))), relu=False)
             return to_nchw(y).squeeze(2)
         if self.kind == "p2p":

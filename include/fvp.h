@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 16
+#define FVP_ABI_VERSION 17
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -410,6 +410,22 @@ int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const f
  * blocks, 1000 x (tile slots x 4 px) / (H x W)} -- the last is the MFMA work
  * over the useful work, what the AUTO rule of fvp/cnn.py reads. */
 int fvp_conv3x3_wino_plan(int N, int H, int W, int Cpo, int *plan);
+/* A whole 1-D conv net in one launch (csrc/fvp_c2c.hip): C2CNet
+ * (cnns_1d.py:182-241) on ncols columns x [ncols][cin0][L0] fp32 -> y
+ * [ncols][cout_final][Lfinal]; one block per column, every activation in LDS.
+ * prog: device int32 [nops][12] = {kind (0 conv, 1 ConvTranspose1d(2, 2),
+ * 2 max_pool1d(2, 2)), cin, cout, k, L (input length), src, dst, res_pre,
+ * res_post (activation buffers 0 .. nbuf-1 of slot floats each; -1 none),
+ * relu, w_off, cic}; params: device fp32, at w_off (% 4 == 0) W [cin][k][cout]
+ * then the folded BN scale [cout] and shift [cout]; a conv's weights stream
+ * through LDS in chunks of cic input channels (cic * k * cout % 4 == 0,
+ * <= 12288 floats).  out = act(scale * sum W x + shift (+ res_pre)) (+ res_post);
+ * the input is buffer 0, the output buffer out_buf.  lg in {4, 8}:
+ * output positions per thread item, cout * ceil(Lout / lg) <= 1024 for every
+ * conv.  fvp/cnn.py Net1D builds the program. */
+size_t fvp_conv1d_net_lds_bytes(int slot, int nbuf);
+int fvp_conv1d_net(const float *x, int ncols, int cin0, int L0, const int *prog, int nops, const float *params,
+                   int slot, int nbuf, int out_buf, int cout_final, int Lfinal, int lg, float *y, void *stream);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
 int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf

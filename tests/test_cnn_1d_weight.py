@@ -138,17 +138,26 @@ def test_transposed_conv1d_and_pool1d_vs_torch(gpu_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("L", [20, 32])
-def test_c2c_large_batch_vs_torch(gpu_device, L):
-    """80 columns (8 frames x K=10) at the C2 (Z=20) and C4 (Z=32) column lengths."""
+@pytest.mark.parametrize("N,L", [(80, 20), (80, 32), (40, 64), (1, 20), (320, 20)])
+def test_c2c_large_batch_vs_torch(gpu_device, N, L):
+    """N columns (80 = 8 frames x K=10) at the C2 / C3 (Z=20), C4 (Z=32) and C5
+    (Z=64) column lengths, through the one-launch net (fvp_conv1d_net, the AUTO
+    path) and the per-layer kernels: both against torch's C2CNet."""
+    from fvp import cnn
     from fvp.cnn import FvpCNN
 
     c2c, _, _, _ = _nets()
     c2c = c2c.to(gpu_device)
-    x = torch.rand((80, 15, L), generator=torch.Generator().manual_seed(L)).to(gpu_device)
+    x = torch.rand((N, 15, L), generator=torch.Generator().manual_seed(L + N)).to(gpu_device)
     with torch.no_grad():
         ref = c2c(x)
-    _close(FvpCNN(c2c)(x).cpu().numpy(), ref.cpu().numpy(), f"C2CNet, 80 columns of {L}")
+    net = FvpCNN(c2c)
+    y = net(x)
+    if L <= 32:  # (Z = 64 exceeds the one-launch net's LDS: the per-layer kernels run)
+        assert net.net1d[(15, L)] is not None, "the one-launch path was not taken"
+    _close(y.cpu().numpy(), ref.cpu().numpy(), f"C2CNet one launch, {N} columns of {L}")
+    per_layer = FvpCNN(c2c, algo=cnn.CONV_PER_TAP)(x)
+    _close(per_layer.cpu().numpy(), ref.cpu().numpy(), f"C2CNet per layer, {N} columns of {L}")
 
 
 @pytest.mark.gpu

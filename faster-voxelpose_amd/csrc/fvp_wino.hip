@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256 * XS, XS == 1 ? 2 : 1) void conv_wino_kernel(Wi
     // extra registers cost the large launches occupancy)
     constexpr bool kPF = NB == 1 && XS == 2;
     constexpr int NBQ = kPF ? NX : 4;
-    f32x4 bcur[NBQ], bnext[NBQ], bq[2][4];
+    f32x4 bcur[NBQ], bnext[NBQ], bq[3][4];  // (bq: groups of 4 xi, a ring of 3 -- two groups in flight)
     if constexpr (kPF) {
 #pragma unroll
         for (int x = 0; x < NBQ; ++x) bcur[x] = b_at(NX * xs + x, 0);
@@ -156,9 +156,12 @@ __global__ __launch_bounds__(256 * XS, XS == 1 ? 2 : 1) void conv_wino_kernel(Wi
                 for (int x = 0; x < NBQ; ++x) bnext[x] = b_at(NX * xs + x, ks + 1);
             }
         }
-        if constexpr (!kPF) {
+        if constexpr (!kPF) {  // groups 0 and 1 land during the input transform
 #pragma unroll
-            for (int x = 0; x < 4; ++x) bcur[x] = b_at(NX * xs + x, ks);
+            for (int x = 0; x < 4; ++x) {
+                bq[0][x] = b_at(NX * xs + x, ks);
+                bq[1][x] = b_at(NX * xs + 4 + x, ks);
+            }
         }
         __syncthreads();  // halo written; the previous step's MFMAs have read V
 #pragma unroll
@@ -196,16 +199,16 @@ __global__ __launch_bounds__(256 * XS, XS == 1 ? 2 : 1) void conv_wino_kernel(Wi
         // MFMAs: NX xi x NB tile halves x 4 channel quads
 #pragma unroll
         for (int g = 0; g < NX / 4; ++g) {
-            if constexpr (!kPF) {
-                if (g + 1 < NX / 4) {
+            if constexpr (!kPF) {  // group g + 2 into the slot group g - 1 used (ResNet-50 512->512: -4 %)
+                if (g + 2 < NX / 4) {
 #pragma unroll
-                    for (int x = 0; x < 4; ++x) bq[(g + 1) & 1][x] = b_at(NX * xs + 4 * (g + 1) + x, ks);
+                    for (int x = 0; x < 4; ++x) bq[(g + 2) % 3][x] = b_at(NX * xs + 4 * (g + 2) + x, ks);
                 }
             }
 #pragma unroll
             for (int x = 0; x < 4; ++x) {
                 const int xl = 4 * g + x, xi = NX * xs + xl;
-                const f32x4 bv = kPF ? bcur[xl] : (g == 0 ? bcur[x] : bq[g & 1][x]);
+                const f32x4 bv = kPF ? bcur[xl] : bq[g % 3][x];
 #pragma unroll
                 for (int h = 0; h < NB; ++h) {
                     const int ta = (16 * (th0 + h) + l16) ^ (2 * cm);

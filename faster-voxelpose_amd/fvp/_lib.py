@@ -109,12 +109,14 @@ SIGNATURES = {
     "fvp_copy_f4": [c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_nchw_to_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv3x3_wino_plan": [c_int, c_int, c_int, c_int, c_void_p],
+    "fvp_deconv4s2_wino_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int, c_void_p, c_void_p],
     "fvp_conv3x3_wino_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 _LIB = None
 
 

@@ -165,6 +165,9 @@ class ConvLayer:
         if (not self.bf16 and self.mode == 0 and (self.KH, self.KW) == (3, 3) and self.stride == (1, 1)
                 and self.pad == (1, 1) and self.Cpi % 16 == 0 and self.Cpo % 32 == 0):
             self.wino = wino_weights(w, self.Cpi, self.Cpo)
+        self.wino_dc = None  # ConvTranspose2d(4, 2, 1) by Winograd F(2x2, 2x2) per parity class
+        if not self.bf16 and self.mode == 3 and self.Cpi % 16 == 0 and self.Cpo % 32 == 0:
+            self.wino_dc = wino_deconv_weights(w, self.Cpi, self.Cpo)
         bias = conv.bias.detach().float() if conv.bias is not None else torch.zeros(cout, device=dev)
         if bn is not None:  # eval BatchNorm: (x - mean) / sqrt(var + eps) * gamma + beta
             s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
@@ -210,6 +213,11 @@ class ConvLayer:
         if key not in self._ws:  # (split-K scratch bytes, kernel: "dma" / "wino" / None) of this input size
             self._ws[key] = self._plan(x)
         nws, dma = self._ws[key]
+        if dma == "wino_dc":
+            _lib.call("fvp_deconv4s2_wino_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wino_dc), self.Cpo,
+                      _ptr(self.scale), _ptr(self.shift), _ptr(res_pre.t) if res_pre else None,
+                      _ptr(res_post.t) if res_post else None, int(relu), _ptr(out), _stream(out))
+            return Act(out, self.Cout)
         if dma == "wino":
             pt = torch.empty((x.N, x.H // 2, x.W // 2, self.Cpo), device=out.device) if pool else None
             _lib.call("fvp_conv3x3_wino_nhwc", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(self.wino), self.Cpo,
@@ -244,6 +252,8 @@ class ConvLayer:
         if self.wino is not None and (self.algo == CONV_WINO or (self.algo == CONV_AUTO and WINO_AUTO
                                                                   and self._wino_pays(x))):
             return 0, "wino"
+        if self.wino_dc is not None and (self.algo == CONV_WINO or (self.algo == CONV_AUTO and WINO_AUTO)):
+            return 0, "wino_dc"
         dma = hasattr(self, "wpack_kc") and self.algo in (CONV_DMA, CONV_AUTO)
         if dma:  # the kernel's limits (fvp.h FVP_CONV_F32_KC): 32-bit offsets, row decode
             Ho, Wo = self.out_hw(x.H, x.W)
@@ -293,6 +303,24 @@ def wino_plan(N: int, H: int, W: int, Cpo: int) -> tuple:
     plan = (ctypes.c_int * 6)()
     _lib.check(_lib.load().fvp_conv3x3_wino_plan(N, H, W, Cpo, plan), "fvp_conv3x3_wino_plan")
     return tuple(plan)
+
+
+def wino_deconv_weights(w: torch.Tensor, cpi: int, cpo: int) -> torch.Tensor:
+    """ConvTranspose2d(4, 2, 1) weights [Cin][Cout][4][4] -> per output parity class (ry, rx)
+    the F(2x2, 2x2) transform U = G g G^T (G = [[1,0],[1,1],[0,1]]) of its 2x2 taps
+    g[i][j] = W[ci][co][3-2i-ry][3-2j-rx], fp64 rounded once, laid out for
+    fvp_deconv4s2_wino_nhwc: [4][9][cpi/16][4][cpo][4] (ci = 16 k + 4 c4 + cm)."""
+    cin, cout = w.shape[:2]
+    G = torch.tensor([[1.0, 0.0], [1.0, 1.0], [0.0, 1.0]], dtype=torch.float64, device=w.device)
+    out = []
+    for cls in range(4):
+        ry, rx = cls >> 1, cls & 1
+        g = w.double()[:, :, [3 - ry, 1 - ry]][:, :, :, [3 - rx, 1 - rx]]  # [cin][cout][i][j]
+        u = torch.einsum("ai,xyij,bj->yxab", G, g, G)  # [cout][cin][3][3]
+        full = torch.zeros((cpo, cpi, 9), dtype=torch.float64, device=w.device)
+        full[:cout, :cin] = u.reshape(cout, cin, 9)
+        out.append(full.permute(2, 1, 0).reshape(9, cpi // 16, 4, 4, cpo).permute(0, 1, 3, 4, 2))
+    return torch.stack(out).contiguous().float()
 
 
 def wino_weights(w: torch.Tensor, cpi: int, cpo: int) -> torch.Tensor:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 17
+#define FVP_ABI_VERSION 18
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -404,6 +404,20 @@ size_t fvp_conv2d_ex_workspace_bytes(int N, int H, int W, int Cpi, int KH, int K
 int fvp_conv3x3_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo, const float *scale,
                           const float *shift, const float *res_pre, const float *res_post, int relu, float *out,
                           float *pool, void *stream);
+/* ConvTranspose2d(kernel 4, stride 2, padding 1) (resnet.py:147-158, the
+ * PoseResNet deconvolution head) by Winograd F(2x2, 2x2) on the fp32 matrix
+ * cores, one 2x2 convolution per output parity (ry, rx): output (2y+ry, 2x+rx)
+ * = sum_{i,j} W[ci][co][3-2i-ry][3-2j-rx] in[y-1+ry+i][x-1+rx+j], with the
+ * epilogue of fvp_conv2d_nhwc_ex.
+ *   in   device [N][H][W][Cpi] fp32, Cpi % 16 == 0;  out  device [N][2H][2W][Cpo], Cpo % 32 == 0
+ *   u    device [4][9][Cpi/16][4][Cpo][4] fp32: per class c = 2 ry + rx, U = G g G^T
+ *        (G = [[1,0],[1,1],[0,1]]) of its 2x2 taps, element (c, xi = 3a + b, k, cm, co, c4)
+ *        = U[co][ci = 16k + 4c4 + cm][a][b] (zero for padding channels)
+ * Exact sums and differences around fp32 products (the weight transform is the
+ * caller's, in fp64). */
+int fvp_deconv4s2_wino_nhwc(const float *in, int N, int H, int W, int Cpi, const float *u, int Cpo,
+                            const float *scale, const float *shift, const float *res_pre, const float *res_post,
+                            int relu, float *out, void *stream);
 /* The launch fvp_conv3x3_wino_nhwc makes for a shape (host only): plan[0..5] =
  * {tile rows, tile columns (Winograd 2x2 tiles per block), 32-column blocks
  * per block (1 or 2), waves sets splitting the 16 transform positions (1 or 2),

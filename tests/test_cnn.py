@@ -70,6 +70,38 @@ def test_fvp_cnn_matches_reference(gpu_device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,cin,cout,hw,res", [(2, 256, 256, (16, 30), None), (3, 64, 32, (7, 9), "pre"),
+                                               (2, 48, 96, (5, 13), "post"), (1, 32, 64, (1, 1), None),
+                                               (40, 64, 64, (8, 12), None)])
+def test_wino_deconv_vs_torch(gpu_device, n, cin, cout, hw, res):
+    """ConvTranspose2d(4, 2, 1) + BN + ReLU by Winograd F(2x2, 2x2) per output
+    parity (fvp_deconv4s2_wino_nhwc, the PoseResNet head's layers): fp32
+    tolerance against torch on ragged class-space tile grids, one and several
+    K steps, 32- and 64-column blocks, residual before / after the ReLU."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    seq = nn.Sequential(nn.ConvTranspose2d(cin, cout, 4, stride=2, padding=1, bias=False),
+                        nn.BatchNorm2d(cout)).eval()
+    seq.load_state_dict(synthetic.seeded_state_dict(seq, cin + 5 * cout))
+    seq = seq.to(gpu_device)
+    g = torch.Generator().manual_seed(cin + n)
+    x = (torch.rand((n, cin) + hw, generator=g) - 0.5).to(gpu_device)
+    ho = (2 * hw[0], 2 * hw[1])
+    r = torch.rand((n, cout) + ho, generator=g).to(gpu_device) if res else None
+    with torch.no_grad():
+        ref = seq(x)
+        ref = torch.relu(ref + r) if res == "pre" else torch.relu(ref) + r if res == "post" else torch.relu(ref)
+    layer = cnn.ConvLayer(seq[0], seq[1], algo=cnn.CONV_WINO)
+    ra = cnn.to_nhwc(r) if res else None
+    got = cnn.to_nchw(layer(cnn.to_nhwc(x), relu=True, res_pre=ra if res == "pre" else None,
+                            res_post=ra if res == "post" else None))
+    assert [k for _, k in layer._ws.values()] == ["wino_dc"]
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"wino deconv {cin}->{cout} {hw} {res}")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,c,cp,hw", [(3, 15, 16, (64, 64)), (2, 1, 16, (80, 80)), (2, 70, 80, (9, 11)),
                                        (1, 128, 128, (5, 3)), (4, 3, 4, (1, 7)), (2, 5, 6, (10, 13))])
 def test_nhwc_to_nchw_layouts(gpu_device, n, c, cp, hw):

@@ -232,9 +232,16 @@ __device__ __forceinline__ void write_winner(int b, int K, int slot, int idx, fl
 // A list longer than kSelCap (only for adversarial value layouts) falls back
 // to K block-wide extraction rounds of the largest key below the previous
 // winner (no taken bitmap: keys are unique).
-template <int E>
+//
+// STRIP (Y <= 1024, es = ceil(X / (1024 / Y)) <= E): thread (xb, y) owns the
+// column strip (xb*es .. xb*es + es - 1, y), so the 3x3 window maxima come from
+// the row maxima of es + 2 rows -- 3 LDS reads per element instead of 9, with
+// no index division (C3 / C2 frames: this phase 4.6 -> ~1.5 us of a 1-CU
+// launch).  Otherwise thread tid owns elements tid + i*1024 (masked_value).
+template <int E, bool STRIP>
 __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__restrict__ prob, long long stride,
-                                                                 int X, int Y, int K, float *__restrict__ vals,
+                                                                 int X, int Y, int K, int es,
+                                                                 float *__restrict__ vals,
                                                                  int64_t *__restrict__ flat,
                                                                  int64_t *__restrict__ xy, ColGather cg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -266,11 +273,43 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
 
     unsigned long long key[E];
     unsigned long long best = 0;
+    if constexpr (STRIP) {
+        // the window maximum with NaN propagating (nanmax): NaN anywhere in the window makes c == m
+        // false, as masked_value's nan flag does; otherwise m is its maximum (+-0 compare equal)
+        const int xb = tid / Y, y = tid - xb * Y;
+        const int x0 = xb * es;
+        const bool act = xb < kSelThreads / Y;
+        const int yl = y > 0 ? y - 1 : y, yr = y + 1 < Y ? y + 1 : y;  // (the centre stands in for a missing tap)
+        // row r = x0 - 1 + r (clamped into the map; unused when outside): centre c and row maximum h,
+        // a window of three rows rolled down the strip
+        auto row_at = [&](int r, float &c, float &h) {
+            const float *row = map + min(max(x0 - 1 + r, 0), X - 1) * Y;
+            c = row[y];
+            h = nanmax(nanmax(c, row[yl]), row[yr]);
+        };
+        float c0, h0, c1, h1;
+        row_at(0, c0, h0);
+        row_at(1, c1, h1);
 #pragma unroll
-    for (int i = 0; i < E; ++i) {
-        const int e = tid + i * kSelThreads;
-        key[i] = e < M ? cand_key(Cand{masked_value(map, e, X, Y, rY), e}) : 0ull;
-        best = key[i] > best ? key[i] : best;
+        for (int i = 0; i < E; ++i) {
+            float c2, h2;
+            row_at(i + 2, c2, h2);
+            const int x = x0 + i;
+            const float up = x > 0 ? h0 : h1, dn = x + 1 < X ? h2 : h1;
+            const float m = nanmax(nanmax(h1, up), dn);
+            key[i] = (act && i < es && x < X) ? cand_key(Cand{(c1 == m ? 1.0f : 0.0f) * c1, x * Y + y}) : 0ull;
+            best = key[i] > best ? key[i] : best;
+            h0 = h1;
+            c1 = c2;
+            h1 = h2;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            const int e = tid + i * kSelThreads;
+            key[i] = e < M ? cand_key(Cand{masked_value(map, e, X, Y, rY), e}) : 0ull;
+            best = key[i] > best ? key[i] : best;
+        }
     }
     best = wave_max_key(best);
     if (lane == 0) wmax[wave] = best;
@@ -285,17 +324,22 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     __syncthreads();
     const unsigned long long t = thr > 0 ? thr : 1ull;  // waves without elements hold the 0 sentinel
 
+    // one LDS atomic per wave for all its candidates (the ballots first)
+    int tot = 0;  // (the ballots are recomputed below rather than held: E of them would spill at E = 32)
 #pragma unroll
-    for (int i = 0; i < E; ++i) {
-        const bool pred = key[i] >= t;
-        const unsigned long long bal = __builtin_amdgcn_ballot_w64(pred);
-        if (bal == 0) continue;
+    for (int i = 0; i < E; ++i) tot += (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(key[i] >= t));
+    if (tot > 0) {
         int base = 0;
-        if (lane == 0) base = atomicAdd(&count, (int)__builtin_popcountll(bal));
+        if (lane == 0) base = atomicAdd(&count, tot);
         base = __builtin_amdgcn_readfirstlane(base);
-        const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-        if (pred && pos < kSelCap) lkey[pos] = key[i];
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(key[i] >= t);
+            const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+            if (key[i] >= t && pos < kSelCap) lkey[pos] = key[i];
+            base += (int)__builtin_popcountll(bal);
+        }
     }
     __syncthreads();
     const int C = count;
@@ -333,10 +377,19 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     if (!cg.cols) return;
     __syncthreads();
     const int JZ = cg.J * cg.Z, KJZ = K * JZ;
-    for (int e = tid; e < KJZ; e += kSelThreads) {
-        const int k = e / JZ, r = e - k * JZ;
-        const int j = r / cg.Z, z = r - j * cg.Z;
-        cg.cols[(size_t)b * KJZ + e] = cg.cube[(((size_t)b * cg.J + j) * M + widx[k]) * cg.Z + z];
+    constexpr int CU = 4;  // column elements per thread in flight: the loads of a round issue together
+    for (int e0 = tid; e0 < KJZ; e0 += CU * kSelThreads) {
+        float cv[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+            const int e = min(e0 + u * kSelThreads, KJZ - 1);
+            const int k = e / JZ, r = e - k * JZ;
+            const int j = r / cg.Z, z = r - j * cg.Z;
+            cv[u] = cg.cube[(((size_t)b * cg.J + j) * M + widx[k]) * cg.Z + z];
+        }
+#pragma unroll
+        for (int u = 0; u < CU; ++u)
+            if (e0 + u * kSelThreads < KJZ) cg.cols[(size_t)b * KJZ + e0 + u * kSelThreads] = cv[u];
     }
 }
 
@@ -427,12 +480,27 @@ static int nms_any(const float *prob, int B, int X, int Y, long long frame_strid
     const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)kSelCap * 8;
     if (K <= kSelWaves && E <= kSelMaxE && sel_lds <= 159 * 1024) {
         const dim3 g(B), blk(kSelThreads);
-        if (E <= 1) hipLaunchKernelGGL((nms_select_kernel<1>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
-        else if (E <= 2) hipLaunchKernelGGL((nms_select_kernel<2>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
-        else if (E <= 4) hipLaunchKernelGGL((nms_select_kernel<4>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
-        else if (E <= 8) hipLaunchKernelGGL((nms_select_kernel<8>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
-        else if (E <= 16) hipLaunchKernelGGL((nms_select_kernel<16>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
-        else hipLaunchKernelGGL((nms_select_kernel<32>), g, blk, sel_lds, st, prob, frame_stride, X, Y, K, vals, flat, xy, cg);
+        // column strips when every column fits one thread row of the block and a strip <= kSelMaxE
+        const int nxb = Y <= kSelThreads ? kSelThreads / Y : 0;
+        const int es = nxb ? (X + nxb - 1) / nxb : 0;
+        auto go = [&](auto kernel, int e_arg) {
+            hipLaunchKernelGGL(kernel, g, blk, sel_lds, st, prob, frame_stride, X, Y, K, e_arg, vals, flat, xy, cg);
+        };
+        if (nxb && es <= kSelMaxE) {
+            if (es <= 1) go(nms_select_kernel<1, true>, es);
+            else if (es <= 2) go(nms_select_kernel<2, true>, es);
+            else if (es <= 4) go(nms_select_kernel<4, true>, es);
+            else if (es <= 8) go(nms_select_kernel<8, true>, es);
+            else if (es <= 16) go(nms_select_kernel<16, true>, es);
+            else go(nms_select_kernel<32, true>, es);
+        } else {
+            if (E <= 1) go(nms_select_kernel<1, false>, 0);
+            else if (E <= 2) go(nms_select_kernel<2, false>, 0);
+            else if (E <= 4) go(nms_select_kernel<4, false>, 0);
+            else if (E <= 8) go(nms_select_kernel<8, false>, 0);
+            else if (E <= 16) go(nms_select_kernel<16, false>, 0);
+            else go(nms_select_kernel<32, false>, 0);
+        }
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(nms_topk_kernel, dim3(B), dim3(kNmsThreads), lds, st, prob, frame_stride, X, Y, K, vals, flat,

@@ -730,18 +730,22 @@ def test_nms_topk_both_paths_vs_oracle(gpu_device, K):
     assert np.array_equal(xy.cpu().numpy()[1:], oxy[1:])
 
 
-@pytest.mark.parametrize("kind", ["zeros", "nan", "negative", "tiny", "big_noise", "big_smooth", "row", "ragged"])
+@pytest.mark.parametrize("kind", ["zeros", "nan", "negative", "tiny", "big_noise", "big_smooth", "row", "ragged",
+                                  "column", "wide_row", "nan_spots"])
 def test_nms_select_degenerate_maps_vs_oracle(gpu_device, kind):
     """The threshold-select top-K on plateaus (all-zero, all-NaN, all-negative
     maps: ties broken by index), maps smaller than K waves, 128x128 maps
-    (16 elements per thread) and ragged shapes, against the oracle bit for bit."""
+    (16 elements per thread), ragged shapes, a 300 x 1 column (one-element
+    strips), a 2 x 1500 row (wider than the block: element-per-thread mapping)
+    and scattered NaNs (windows that hold one), against the oracle bit for bit."""
     from fvp.proposal import nms2D
 
     g = torch.Generator().manual_seed(11)
     shape, K = {"zeros": ((3, 1, 80, 80), 10), "nan": ((2, 1, 80, 80), 10), "negative": ((2, 1, 40, 40), 16),
                 "tiny": ((4, 1, 4, 4), 16), "big_noise": ((3, 1, 128, 128), 10),
                 "big_smooth": ((3, 1, 128, 128), 16), "row": ((2, 1, 1, 300), 5),
-                "ragged": ((5, 1, 37, 53), 7)}[kind]
+                "ragged": ((5, 1, 37, 53), 7), "column": ((2, 1, 300, 1), 5), "wide_row": ((2, 1, 2, 1500), 5),
+                "nan_spots": ((3, 1, 80, 80), 10)}[kind]
     if kind == "zeros":
         prob = torch.zeros(shape)
     elif kind == "nan":
@@ -753,6 +757,8 @@ def test_nms_select_degenerate_maps_vs_oracle(gpu_device, kind):
         prob = torch.nn.functional.avg_pool2d(torch.rand((B, 1, X + 8, Y + 8), generator=g), 9, 1)
     else:
         prob = torch.rand(shape, generator=g)
+    if kind == "nan_spots":
+        prob.view(-1)[torch.randperm(prob.numel(), generator=g)[:12]] = float("nan")
     v, xy, fl = nms2D(prob.to(gpu_device), K)
     ov, oxy, ofl = O.nms2d(prob.numpy(), K)
     got = v.cpu().numpy()

@@ -521,10 +521,12 @@ def main():
     else:
         run_vox, run_post = vox, post
 
+    pool = []  # timing events, created before the timed region (creation is a HIP call per event)
+
     def step(record):
         if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
+            e0, e1 = pool.pop() if pool else (torch.cuda.Event(enable_timing=True),
+                                              torch.cuda.Event(enable_timing=True))
             e0.record(stream)
             ev.append((e0, e1))
         return run_step(run_vox, run_post, collect, after_vox=(lambda: e1.record(stream)) if record else None)[2]
@@ -535,10 +537,15 @@ def main():
     torch.cuda.synchronize()
     if grouped:
         dist.barrier()
+    # the op's HIP-event pair (roofline kernel_ms) on at most ~50 of the timed steps: each record is a
+    # marker in the stream, ~5 % of a C3 B=8 step (profiles/round5/c3_b8/event_sampling.txt)
+    rec_every = max(1, args.steps // 50)
+    pool.extend((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.steps))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        step(i % rec_every == 0)
     torch.cuda.synchronize()
     if grouped:
         dist.barrier()
@@ -726,6 +733,7 @@ def main():
                 "traffic": None if traffic is None else round(traffic["corrected"]),
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": round(vox_ms, 4),
+                "kernel_ms_steps": len(ev),  # timed steps that carried the event pair (every steps // 50-th)
                 "measured_copy_gbs": round(extra.get("copy_gbs", 0.0), 1),
                 "frac_of_measured_copy": round(achieved / extra["copy_gbs"], 4) if extra.get("copy_gbs") else None,
                 "tap_rate": {"bound": "vector-memory 64 B/clk/CU", "achieved": round(tap_rate, 3),

@@ -233,11 +233,15 @@ __device__ __forceinline__ void write_winner(int b, int K, int slot, int idx, fl
 // to K block-wide extraction rounds of the largest key below the previous
 // winner (no taken bitmap: keys are unique).
 //
-// STRIP (Y <= 1024, es = ceil(X / (1024 / Y)) <= E): thread (xb, y) owns the
-// column strip (xb*es .. xb*es + es - 1, y), so the 3x3 window maxima come from
-// the row maxima of es + 2 rows -- 3 LDS reads per element instead of 9, with
-// no index division (C3 / C2 frames: this phase 4.6 -> ~1.5 us of a 1-CU
-// launch).  Otherwise thread tid owns elements tid + i*1024 (masked_value).
+// STRIP (Y <= 1024, es = ceil(X / (1024 / Y)) <= E <= 16): the masked map is
+// computed by column strips -- thread (xb, y) owns (xb*es .. xb*es + es - 1, y),
+// so the 3x3 window maxima come from the row maxima of es + 2 rows: 3 LDS reads
+// per element instead of 9, no index division (C3 / C2 frames: 4.6 -> ~2 us of
+// a 1-CU launch) -- and written over the map in LDS; the keys are then read
+// back with the element-per-thread mapping (tid + i*1024), whose wave maxima
+// keep the candidate list short on plateaus (a masked map is mostly zeros:
+// strip-wise wave maxima would admit thousands of zeros by index).  Otherwise
+// thread tid computes its elements' masked values itself (masked_value).
 template <int E, bool STRIP>
 __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__restrict__ prob, long long stride,
                                                                  int X, int Y, int K, int es,
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             c = row[y];
             h = nanmax(nanmax(c, row[yl]), row[yr]);
         };
-        float c0, h0, c1, h1;
+        float c0, h0, c1, h1, mv[E];
         row_at(0, c0, h0);
         row_at(1, c1, h1);
 #pragma unroll
@@ -297,11 +301,21 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             const int x = x0 + i;
             const float up = x > 0 ? h0 : h1, dn = x + 1 < X ? h2 : h1;
             const float m = nanmax(nanmax(h1, up), dn);
-            key[i] = (act && i < es && x < X) ? cand_key(Cand{(c1 == m ? 1.0f : 0.0f) * c1, x * Y + y}) : 0ull;
-            best = key[i] > best ? key[i] : best;
+            mv[i] = (c1 == m ? 1.0f : 0.0f) * c1;
             h0 = h1;
             c1 = c2;
             h1 = h2;
+        }
+        __syncthreads();  // every window has read the raw map
+#pragma unroll
+        for (int i = 0; i < E; ++i)
+            if (act && i < es && x0 + i < X) map[(x0 + i) * Y + y] = mv[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < E; ++i) {  // (E >= es >= ceil(M / 1024): every element has a slot)
+            const int e = tid + i * kSelThreads;
+            key[i] = e < M ? cand_key(Cand{map[e], e}) : 0ull;
+            best = key[i] > best ? key[i] : best;
         }
     } else {
 #pragma unroll
@@ -350,7 +364,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             for (int j = 0; j < C; ++j) rank += lkey[j] > k;
             if (rank < K) {
                 const int idx = (int)~(unsigned)k;
-                write_winner(b, K, rank, idx, masked_value(map, idx, X, Y, rY), X, vals, flat, xy, widx);
+                write_winner(b, K, rank, idx, (STRIP ? map[idx] : masked_value(map, idx, X, Y, rY)), X, vals, flat, xy, widx);
             }
         }
     } else {  // K rounds, each the largest key below the previous winner
@@ -368,7 +382,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             for (int q = 0; q < kSelWaves; ++q) w = wmax[q] > w ? wmax[q] : w;
             if (tid == 0) {
                 const int idx = (int)~(unsigned)w;
-                write_winner(b, K, r, idx, masked_value(map, idx, X, Y, rY), X, vals, flat, xy, widx);
+                write_winner(b, K, r, idx, (STRIP ? map[idx] : masked_value(map, idx, X, Y, rY)), X, vals, flat, xy, widx);
             }
             prev = w;
             __syncthreads();
@@ -480,19 +494,18 @@ static int nms_any(const float *prob, int B, int X, int Y, long long frame_strid
     const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)kSelCap * 8;
     if (K <= kSelWaves && E <= kSelMaxE && sel_lds <= 159 * 1024) {
         const dim3 g(B), blk(kSelThreads);
-        // column strips when every column fits one thread row of the block and a strip <= kSelMaxE
+        // column strips when every column fits one thread row of the block and a strip <= 16
         const int nxb = Y <= kSelThreads ? kSelThreads / Y : 0;
         const int es = nxb ? (X + nxb - 1) / nxb : 0;
         auto go = [&](auto kernel, int e_arg) {
             hipLaunchKernelGGL(kernel, g, blk, sel_lds, st, prob, frame_stride, X, Y, K, e_arg, vals, flat, xy, cg);
         };
-        if (nxb && es <= kSelMaxE) {
+        if (nxb && es <= 16) {  // (strips of up to 16: at 32 the strip's values and keys spill)
             if (es <= 1) go(nms_select_kernel<1, true>, es);
             else if (es <= 2) go(nms_select_kernel<2, true>, es);
             else if (es <= 4) go(nms_select_kernel<4, true>, es);
             else if (es <= 8) go(nms_select_kernel<8, true>, es);
-            else if (es <= 16) go(nms_select_kernel<16, true>, es);
-            else go(nms_select_kernel<32, true>, es);
+            else go(nms_select_kernel<16, true>, es);
         } else {
             if (E <= 1) go(nms_select_kernel<1, false>, 0);
             else if (E <= 2) go(nms_select_kernel<2, false>, 0);

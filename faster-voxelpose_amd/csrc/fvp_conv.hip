@@ -1482,20 +1482,28 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const float *__restri
 
 // The same through LDS: a block moves 64 pixels x Cp channels of one image --
 // 16-B loads of whole pixels, then per channel 64 consecutive pixels (odd LDS
-// pitch: conflict-free column reads).  Cp % 4 == 0, Cp <= 128, 16-B aligned input.
+// pitch: conflict-free column reads).  Cp % 4 == 0, C <= 128, 16-B aligned input.
+// Only channels 0 .. C-1 of a pixel are read (a partial last quad by scalars):
+// `in` may point at channel c0 of a wider pitch (fvp.cnn.to_nchw_from), where a
+// whole-pitch read would run c0 floats past the allocation at the last pixel.
 __global__ __launch_bounds__(256) void nhwc_to_nchw_tiled_kernel(const float *__restrict__ in,
                                                                  float *__restrict__ out, int C, int HW, int Cp,
                                                                  int tiles_per_img) {
     __shared__ float t[64 * 129];
     const int img = blockIdx.x / tiles_per_img, p0 = (blockIdx.x - img * tiles_per_img) * 64;
-    const int np = HW - p0 < 64 ? HW - p0 : 64, pitch = Cp + 1, nq = Cp >> 2;
+    const int np = HW - p0 < 64 ? HW - p0 : 64, pitch = 129, nq = (C + 3) >> 2;
     const float *__restrict__ src = in + ((size_t)img * HW + p0) * Cp;
     for (int e = threadIdx.x; e < 64 * nq; e += 256) {
         const int p = e / nq, q = e - p * nq;
         if (p < np) {
-            const f32x4 v = *reinterpret_cast<const f32x4 *>(src + (size_t)p * Cp + 4 * q);
+            const float *px = src + (size_t)p * Cp + 4 * q;
+            if (4 * q + 4 <= C) {
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(px);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) t[p * pitch + 4 * q + k] = v[k];
+                for (int k = 0; k < 4; ++k) t[p * pitch + 4 * q + k] = v[k];
+            } else {
+                for (int k = 0; 4 * q + k < C; ++k) t[p * pitch + 4 * q + k] = px[k];
+            }
         }
     }
     __syncthreads();
@@ -1966,7 +1974,7 @@ extern "C" int fvp_nhwc_to_nchw(const float *in, int N, int C, int H, int W, int
     if (N <= 0 || C <= 0 || Cp < C || H <= 0 || W <= 0) return FVP_ERR_SHAPE;
     const long long total = (long long)N * C * H * W;
     const int HW = H * W, tiles = (HW + 63) / 64;
-    if (Cp % 4 == 0 && Cp <= 128 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (long long)N * tiles <= 0x7fffffffLL) {
+    if (Cp % 4 == 0 && C <= 128 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (long long)N * tiles <= 0x7fffffffLL) {
         hipLaunchKernelGGL(fvp::nhwc_to_nchw_tiled_kernel, dim3((unsigned)(N * tiles)), dim3(256), 0,
                            (hipStream_t)stream, in, out, C, HW, Cp, tiles);
         return (int)hipGetLastError();

@@ -400,8 +400,10 @@ def _merged_heads(hm: nn.Module, size: nn.Module, dtype, algo):
         return None
     ha, hb = a3.out_channels, b3.out_channels
     dev = a3.weight.device
-    m3 = nn.Conv2d(a3.in_channels, ha + hb, 3, padding=1).to(dev)
-    m1 = nn.Conv2d(ha + hb, a1.out_channels + b1.out_channels, 1).to(dev)
+    # skip_init: no default initialisation, so wrapping a CenterNet draws nothing from the
+    # global RNG (every weight and bias is written below).
+    m3 = torch.nn.utils.skip_init(nn.Conv2d, a3.in_channels, ha + hb, 3, padding=1, device=dev)
+    m1 = torch.nn.utils.skip_init(nn.Conv2d, ha + hb, a1.out_channels + b1.out_channels, 1, device=dev)
     with torch.no_grad():
         def bias(c):
             return c.bias.detach().float() if c.bias is not None else torch.zeros(c.out_channels, device=dev)
@@ -613,6 +615,11 @@ class Net1D:
 
     @classmethod
     def build(cls, module, cin0: int, L0: int):
+        if L0 % 4:
+            # two pools then two upsamples only restore L0 when 4 | L0; otherwise the
+            # reference fails at `x + skip_x2` (cnns_1d.py) and so does the per-layer path
+            # (ConvLayer's res_post shape assert) -- the one-launch net must not run it
+            return None
         n = cls()
         try:
             cin4 = (cin0 + 3) // 4 * 4

@@ -47,25 +47,43 @@ class ChannelsLastHeatmaps:
         return attach(out, self)
 
 
-def attach(planar: torch.Tensor, cl: ChannelsLastHeatmaps) -> torch.Tensor:
+def attach(planar: torch.Tensor, cl: ChannelsLastHeatmaps, shared: bool = False) -> torch.Tensor:
     """Mark `planar` (the same values in the reference layout) as also held
     channels-last.  Only this tensor object carries the mark: any op on it
     (view, stack, slice, in-place write) yields a tensor without it, so a
-    consumer never reads a stale copy through the mark."""
+    consumer never reads a stale copy through the mark.  `shared`: the mark is
+    a fused HDN's one-forward layout (share_channels_last), never reused by a
+    later HDN call and dropped by the JLN that consumes it (release)."""
     if tuple(planar.shape) != cl.shape:
         raise _lib.FvpError(f"fvp: planar {tuple(planar.shape)} and channels-last {cl.shape} heatmaps differ")
-    planar._fvp_cl = (cl, planar._version)
+    planar._fvp_cl = (cl, planar._version, bool(shared))
     return planar
 
 
-def channels_last_of(heatmaps) -> ChannelsLastHeatmaps | None:
-    """The channels-last copy of `heatmaps`, if it is one or carries one still valid."""
+def channels_last_of(heatmaps, reuse_shared: bool = True) -> ChannelsLastHeatmaps | None:
+    """The channels-last copy of `heatmaps`, if it is one or carries one still valid
+    (reuse_shared=False: not a copy an earlier share_channels_last made)."""
     if isinstance(heatmaps, ChannelsLastHeatmaps):
         return heatmaps
     mark = getattr(heatmaps, "_fvp_cl", None)
     if mark is None or mark[1] != heatmaps._version:  # written in place since: stale
         return None
+    if mark[2] and not reuse_shared:
+        return None
     return mark[0]
+
+
+def release(heatmaps) -> None:
+    """Drop the channels-last copy `heatmaps` carries (its memory goes with it)."""
+    if isinstance(heatmaps, torch.Tensor) and getattr(heatmaps, "_fvp_cl", None) is not None:
+        del heatmaps._fvp_cl
+
+
+def release_shared(heatmaps) -> None:
+    """Drop the copy only if share_channels_last made it (the JLN, its last consumer)."""
+    mark = getattr(heatmaps, "_fvp_cl", None) if isinstance(heatmaps, torch.Tensor) else None
+    if mark is not None and mark[2]:
+        del heatmaps._fvp_cl
 
 
 def to_channels_last(planar: torch.Tensor) -> ChannelsLastHeatmaps:
@@ -91,15 +109,20 @@ def to_channels_last(planar: torch.Tensor) -> ChannelsLastHeatmaps:
 def share_channels_last(heatmaps) -> ChannelsLastHeatmaps | None:
     """Lay `heatmaps` out channels-last once and attach the copy (the fused
     HDN forward does this so that the JLN, handed the same tensor object,
-    reads the same copy): planar fp32 tensors of <= 32 joints on a HIP device
-    that do not already carry a valid copy.  Returns the copy in use, if any."""
-    cl = channels_last_of(heatmaps)
+    reads the same copy, then drops it: release_shared): planar fp32 tensors of
+    <= 32 joints on a HIP device.  A copy attached by the backbone path is used
+    as it is; one left by an earlier call of this function is NOT -- the caller
+    may have refilled the same buffer through ``.data``, DLPack or the C ABI,
+    which do not move ``_version`` -- so every fused forward lays out anew.
+    Returns the copy in use, if any."""
+    cl = channels_last_of(heatmaps, reuse_shared=False)
     if cl is not None or not isinstance(heatmaps, torch.Tensor):
         return cl
+    release(heatmaps)
     if (heatmaps.dim() != 5 or heatmaps.dtype != torch.float32 or heatmaps.device.type != "cuda"
             or heatmaps.shape[2] > 32 or heatmaps.shape[0] == 0
             or (torch.is_grad_enabled() and heatmaps.requires_grad)):
         return None
     cl = to_channels_last(heatmaps)
-    attach(heatmaps, cl)
+    attach(heatmaps, cl, shared=True)
     return cl

@@ -246,10 +246,16 @@ def fused_fvp_forward(self, backbone=None, views=None, meta=None, targets=None, 
     written channels-last once and handed to the HDN / JLN gathers in place
     (fvp.heatmaps.attach); everything after it is the reference's forward."""
     opts = options_of(self)
+    attached = None
     if (views is not None and backbone is not None and not self.training and hasattr(backbone, "deconv_layers")
             and _fvp_backbone_ok(backbone, views, opts)):
         cl = fvp_backbone.cached(backbone, opts.backbone_dtype).heatmaps_cl(views)
         input_heatmaps, views = cl.planar(), None  # [B,V,J,H,W], carrying the channels-last copy
-    return type(self)._fvp_original_forward(self, backbone=backbone, views=views, meta=meta, targets=targets,
-                                            input_heatmaps=input_heatmaps, cameras=cameras,
-                                            resize_transform=resize_transform)
+        attached = input_heatmaps
+    try:
+        return type(self)._fvp_original_forward(self, backbone=backbone, views=views, meta=meta, targets=targets,
+                                                input_heatmaps=input_heatmaps, cameras=cameras,
+                                                resize_transform=resize_transform)
+    finally:
+        # the caller gets the reference's plain planar heatmaps: the copy does not outlive the forward
+        fvp_heatmaps.release(attached)

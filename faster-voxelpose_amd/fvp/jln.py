@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from .heatmaps import release_shared
 
 
 class SoftArgmaxLayer(nn.Module):
@@ -60,8 +61,12 @@ def fused_jln_forward(self, meta, heatmaps, proposal_centers, mask, cameras, res
             sel = torch.tensor([q == s for q in seqs], device=device)
             _jln_batch(self, meta, heatmaps, proposal_centers, mask & sel[:, None], cameras, resize_transform,
                        all_fused, all_pose, first=seqs.index(s))
-        return all_fused, all_pose
-    _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform, all_fused, all_pose, first=0)
+    else:
+        _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform, all_fused, all_pose,
+                   first=0)
+    # the HDN's one-forward channels-last copy (fvp.heatmaps.share_channels_last) ends here,
+    # with its last consumer: it is not kept alive on the caller's tensor
+    release_shared(heatmaps)
     return all_fused, all_pose
 
 

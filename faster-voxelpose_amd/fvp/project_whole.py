@@ -54,7 +54,7 @@ class ProjectLayer(nn.Module):
         self._grid = None
         self.sample_grid = {}  # seq -> [V, 1, N, 2] fp32 (the reference's cache layout; a view of _packed)
         self._packed = {}      # seq -> [N, GV, 2] voxel-major copy read by the voxelize kernel
-        self._packed_of = {}   # seq -> (the sample_grid entry it was checked against, its packed grid)
+        self._packed_of = {}   # seq -> (sample_grid entry, its packed grid, entry is a view of it, entry._version)
         self._cams = {}        # seq -> [V, FVP_CAM_STRIDE] camera records (on-the-fly projection)
         self._stacked = (None, None)  # (key, [S,N,GV,2]) grids of the last mixed-sequence batch
         self.on_the_fly = None  # None: decide by grid size; True/False: force
@@ -103,14 +103,18 @@ class ProjectLayer(nn.Module):
     def _packed_grid(self, seq) -> torch.Tensor:
         sg = self.sample_grid[seq]
         hit = self._packed_of.get(seq)
-        if hit is not None and hit[0] is sg:  # the cache entry is still the view this layer made
+        # the same tensor object, and either a view of the packed grid itself (in-place
+        # writes land in the packed grid) or unchanged since it was packed (_version)
+        if hit is not None and hit[0] is sg and (hit[2] or hit[3] == sg._version):
             return hit[1]
         pg = self._packed.get(seq)
-        if pg is None or ops.packed_as_reference(pg, sg.shape[0]).data_ptr() != sg.data_ptr():
-            # a grid assigned from outside (e.g. a reference-layout tensor): pack it once
+        own = pg is not None and ops.packed_as_reference(pg, sg.shape[0]).data_ptr() == sg.data_ptr()
+        if not own:
+            # a grid assigned from outside (e.g. a reference-layout tensor): pack it, and
+            # again whenever it is modified in place
             pg = ops.pack_grid(sg[:, 0].to(torch.float32).contiguous())
             self._packed[seq] = pg
-        self._packed_of[seq] = (sg, pg)
+        self._packed_of[seq] = (sg, pg, own, sg._version)
         return pg
 
     def _grids_for_batch(self, heatmaps, meta, cameras, resize_transform):

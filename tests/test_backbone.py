@@ -354,7 +354,8 @@ def _fake_reference(mods_cls):
                     resize_transform=None):
             if views is not None:
                 input_heatmaps = torch.stack([backbone(views[:, c]) for c in range(views.shape[1])], dim=1)
-            self.seen = input_heatmaps
+            from fvp.heatmaps import channels_last_of
+            self.seen = channels_last_of(input_heatmaps)  # what the HDN / JLN are handed
             cube = self.project_layer(input_heatmaps, meta, cameras, resize_transform)
             return cube, input_heatmaps
 
@@ -422,7 +423,8 @@ def test_installed_views_path_matches_reference_flow(gpu_device):
         try:
             integration.install(fused=True, modules=mods, backbone=True)
             cube, hm = model(backbone=m, views=views, meta=meta, cameras=cams, resize_transform=rt)
-            assert channels_last_of(model.seen) is not None  # the HDN got the channels-last copy
+            assert model.seen is not None  # the HDN got the channels-last copy
+            assert channels_last_of(hm) is None  # and it does not outlive the forward
         finally:
             _restore(ResNet)
             _restore(FVP)

@@ -114,6 +114,11 @@ def test_nhwc_to_nchw_layouts(gpu_device, n, c, cp, hw):
     assert torch.equal(cnn.to_nchw(cnn.Act(t, c)), t[..., :c].permute(0, 3, 1, 2))
     if c > 1:
         assert torch.equal(cnn.to_nchw_from(cnn.Act(t, c), 1, c - 1), t[..., 1:c].permute(0, 3, 1, 2))
+    if cp % 4 == 0 and cp > 4:
+        # c0 % 4 == 0 takes the tiled kernel on an offset pointer: it must read only
+        # channels c0 .. c0 + C - 1 (a whole-pitch read runs c0 floats past the end).
+        for c0, cc in ((4, cp - 4), (4, min(5, cp - 4))):
+            assert torch.equal(cnn.to_nchw_from(cnn.Act(t, cp), c0, cc), t[..., c0:c0 + cc].permute(0, 3, 1, 2))
 
 
 @pytest.mark.gpu

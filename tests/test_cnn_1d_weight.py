@@ -160,6 +160,31 @@ def test_c2c_large_batch_vs_torch(gpu_device, N, L):
     _close(per_layer.cpu().numpy(), ref.cpu().numpy(), f"C2CNet per layer, {N} columns of {L}")
 
 
+def test_one_launch_c2c_refuses_lengths_the_reference_cannot_run():
+    """Z % 4 != 0: two pools then two upsamples do not restore Z, and the reference
+    fails at ``x + skip_x2`` (cnns_1d.py:223-233).  The one-launch net must not be
+    planned for such a length (it would read the skip buffer at the wrong pitch)."""
+    from fvp.cnn import Net1D
+
+    c2c, _, _, _ = _nets()
+    for L in (30, 18, 22, 2):
+        assert Net1D.build(c2c, 15, L) is None
+        with pytest.raises(RuntimeError):  # and the reference itself refuses it
+            with torch.no_grad():
+                c2c(torch.zeros((1, 15, L)))
+
+
+@pytest.mark.gpu
+def test_c2c_odd_length_raises_like_the_reference(gpu_device):
+    from fvp.cnn import FvpCNN
+
+    c2c, _, _, _ = _nets()
+    net = FvpCNN(c2c.to(gpu_device))
+    with pytest.raises((AssertionError, RuntimeError)):
+        net(torch.rand((4, 15, 30), device=gpu_device))
+    assert net.net1d.get((15, 30)) is None
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("feat,hidden,hw,P", [(32, 64, (64, 64), 10), (16, 32, (33, 18), 3), (64, 100, (40, 40), 2)])
 def test_weight_net_shapes_vs_torch(gpu_device, feat, hidden, hw, P):

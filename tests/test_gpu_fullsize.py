@@ -273,6 +273,49 @@ def test_fused_jln_forward_matches_reference_jln(gpu_device, cnn):
     assert not np.any(fused[~d["mask"]])
 
 
+def test_shared_layout_follows_a_reused_buffer(gpu_device):
+    """The fused HDN lays planar heatmaps out channels-last once per forward
+    (share_layout) and the JLN drops that copy.  A caller that refills the same
+    tensor through ``.data`` (which, like DLPack or the C ABI, does not move
+    ``_version``) must get the new values' results, not the old copy's."""
+    import types
+
+    from fvp import geometry, integration, jln
+    from fvp.heatmaps import channels_last_of
+    from fvp.workloads import WORKLOADS
+
+    w = WORKLOADS["c3"]
+    cams, seq = w.cameras()
+    net = _hdn(w, gpu_device)
+    a = torch.from_numpy(golden("whole_c3.npz")["heatmaps"]).to(gpu_device)
+    b = (a.flip(0) * 0.75).contiguous()
+    rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
+    meta = {"seq": [seq] * 2}
+    with torch.no_grad():
+        want = integration.fused_hdn_forward(net, b.clone(), meta, cams, rt)
+        buf = a.clone()
+        integration.fused_hdn_forward(net, buf, meta, cams, rt)  # HDN alone: its copy stays attached
+        assert channels_last_of(buf) is not None
+        v = buf._version
+        buf.data.copy_(b)
+        assert buf._version == v  # invisible to the version counter
+        got = integration.fused_hdn_forward(net, buf, meta, cams, rt)
+        for g, r in zip(got, want):
+            assert torch.equal(g, r)
+        # the JLN is the copy's last consumer and drops it
+        jnet = types.SimpleNamespace(training=False, project_layer=None)
+        from fvp.project_individual import ProjectLayer
+        jnet.project_layer = ProjectLayer(w.cfg(str(gpu_device)))
+        jnet.project_layer.verbose = False
+        jnet.conv_net = torch.nn.Identity()
+        jnet.weight_net = lambda f: torch.ones(f.shape[0] * f.shape[1], f.shape[2], 1, device=f.device)
+        jnet.soft_argmax_layer = types.SimpleNamespace(beta=100.0)
+        pc = got[2].clone()
+        pc[..., 3] = 0.0
+        jln.fused_jln_forward(jnet, meta, buf, pc, pc[..., 3] >= 0, cams, rt)
+        assert channels_last_of(buf) is None
+
+
 def test_proposal_layer_test_mode_matches_reference_semantics(gpu_device):
     """fvp.proposal.ProposalLayer (and the fused z pick) vs human_detection_net.py:
     36-37, 99-124 restated with torch ops: bit-exact centres, confidences,

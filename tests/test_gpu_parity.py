@@ -281,6 +281,14 @@ def test_sample_grid_is_view_of_packed_grid(gpu_device):
     other.sample_grid[seq] = sg.contiguous().clone()  # reference-layout tensor from outside
     cube2, _ = other.forward_fused(hm, {"seq": [seq] * 2}, cams, rt)
     assert torch.equal(cube, cube2)
+    # the outside grid modified in place is repacked (its _version moved), not read stale
+    other.sample_grid[seq][0].copy_(sg[1])
+    cube3, _ = other.forward_fused(hm, {"seq": [seq] * 2}, cams, rt)
+    fresh = ProjectLayer(w.cfg(str(gpu_device)))
+    fresh.verbose = False
+    fresh.sample_grid[seq] = other.sample_grid[seq].clone()
+    cube4, _ = fresh.forward_fused(hm, {"seq": [seq] * 2}, cams, rt)
+    assert torch.equal(cube3, cube4) and not torch.equal(cube3, cube)
 
 
 @pytest.mark.parametrize("otf", [False, True], ids=["grid", "onthefly"])

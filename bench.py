@@ -39,8 +39,18 @@ METRIC = "voxelize+project FPS (5 cams, 80×80×20 grid) @1/2/4/8 GPU; % HBM roo
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the fvp_voxelize op: layout pass (fp32 channels-last, fp16 pair table per 8 entries, per row or per
 # entry) + gather
-VOX_KERNELS = ("heatmaps_to_cl_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel",
-               "pairs_rows_kernel", "voxelize_kernel", "voxelize_cams_kernel")
+LAYOUT_KERNELS = ("heatmaps_to_cl_kernel", "pairs_vec8_kernel", "heatmaps_to_pairs_kernel", "pairs_rows_kernel")
+GATHER_KERNELS = ("voxelize_kernel", "voxelize_cams_kernel")
+VOX_KERNELS = LAYOUT_KERNELS + GATHER_KERNELS
+# The gather's tap-instruction floor: one wave-load (64 lanes x 16 B = 1 KiB) costs
+# 16.5 cycles of a CU's vector-memory path whether its lanes hit L1, miss, or are
+# off-image (tools/gather_probe.hip replay of the C2 gather: TAPS_ALL_OOB = 34.5 us
+# per 8 frames = 1.28 M wave-loads over 256 CUs at 2.4 GHz;
+# profiles/round3/gather_probe_c2_modes.jsonl, DESIGN.md §5 "The C2 ceiling").
+TAP_CYCLES_PER_WAVELOAD = 16.5
+TAP_PROBE = "profiles/round3/gather_probe_c2_modes.jsonl (TAPS_ALL_OOB)"
+CUS, CLOCK_HZ = 256, 2.4e9
+JOINT_SLICE = 32  # fvp_voxelize's joints per slice (kJointSlice)
 
 
 def parse(argv=None):
@@ -165,13 +175,52 @@ WORKLOAD_DESC = {"c1": "BASELINE configs[0] (1 demo camera)", "c2": "BASELINE co
 DEFAULT_BATCH = {"c1": 256, "c2": 256, "c3": 256, "c4": 64, "c5": 8, "shelf_native": 256}
 
 
+def traffic_from_csvs(fetch_csvs, write_csvs, ops):
+    """Per-op HBM bytes of the fvp_voxelize op from rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE counter CSVs (KB per dispatch), split into the layout pass and the
+    gather.  Which FETCH correction each gets (MI355X_MICROARCH.md §HBM):
+    * the layout pass is a wide coalesced stream (16 B per lane, whole lines): the
+      guide's calibrated case, where FETCH_SIZE reads exactly half the bytes -> x2;
+    * the gather's loads are scattered 16-B lanes (4 lanes of a voxel share one
+      64-B pixel): the guide leaves other access widths uncalibrated, so its fetch
+      is reported raw (x1, `traffic`) and doubled (`traffic_upper`) -- the true
+      value lies between.
+    Returns None if a counter has no rows for these kernels."""
+    out = {}
+    for counter, files in (("FETCH_SIZE", fetch_csvs), ("WRITE_SIZE", write_csvs)):
+        tot = {"layout": 0.0, "gather": 0.0}
+        rows = 0
+        for f in files:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Counter_Name") != counter:
+                        continue
+                    name = row.get("Kernel_Name", "")
+                    kind = ("layout" if any(k in name for k in LAYOUT_KERNELS) else
+                            "gather" if any(k in name for k in GATHER_KERNELS) else None)
+                    if kind:
+                        tot[kind] += float(row["Counter_Value"]) * 1024.0 / ops  # KB per dispatch -> B per op
+                        rows += 1
+        if not rows:
+            return None
+        out[counter] = tot
+    f, w = out["FETCH_SIZE"], out["WRITE_SIZE"]
+    layout = 2.0 * f["layout"] + w["layout"]
+    return {"layout_fetch_raw": f["layout"], "layout_write": w["layout"], "layout": layout,
+            "layout_fetch_correction": 2.0,
+            "gather_fetch_raw": f["gather"], "gather_write": w["gather"],
+            "gather": f["gather"] + w["gather"], "gather_fetch_correction": "1 (raw; uncalibrated width) .. 2",
+            "traffic": layout + f["gather"] + w["gather"],
+            "traffic_upper": layout + 2.0 * f["gather"] + w["gather"]}
+
+
 def collect_traffic(args):
     """Run this benchmark twice under rocprofv3 (one counter pass each, as
     MI355X_MICROARCH.md prescribes) BEFORE this process touches the GPU, and
-    return per-launch HBM bytes of the voxelize kernel."""
-    res = {}
+    return per-op HBM bytes of the voxelize op's layout pass and gather."""
     out_root = os.path.join(REPO, "gpurun_out", "bench_pmc")
     os.makedirs(out_root, exist_ok=True)
+    files = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"pmc_{counter}_", dir=out_root)
         cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
@@ -187,22 +236,63 @@ def collect_traffic(args):
                            cwd=REPO)
         except Exception as e:  # profiler unavailable or failed: report null, never fake
             return None, f"rocprofv3 {counter} failed: {e}"
-        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        total, rows = 0.0, 0
-        for f in files:
-            with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    if any(k in row.get("Kernel_Name", "") for k in VOX_KERNELS) and row.get("Counter_Name") == counter:
-                        total += float(row["Counter_Value"])
-                        rows += 1
-        if not rows:
-            return None, f"no {counter} rows for {VOX_KERNELS}"
-        res[counter] = total / CHILD_OPS  # per fvp_voxelize op (one batch of B frames)
-    # rocprofv3 reports KB; gfx950 FETCH_SIZE counts half of a wide streaming
-    # read (MI355X_MICROARCH.md §HBM) -> the guide's correction doubles it.
-    fetch = res["FETCH_SIZE"] * 1024.0
-    write = res["WRITE_SIZE"] * 1024.0
-    return {"fetch_raw": fetch, "write": write, "corrected": 2.0 * fetch + write}, None
+        files[counter] = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    t = traffic_from_csvs(files["FETCH_SIZE"], files["WRITE_SIZE"], CHILD_OPS)
+    if t is None:
+        return None, f"no FETCH_SIZE / WRITE_SIZE rows for {VOX_KERNELS}"
+    t["csv_dirs"] = [os.path.relpath(os.path.dirname(v[0]), REPO) for v in files.values() if v]
+    return t, None
+
+
+def lanes_per_voxel(J):
+    """fvp_layout.h lanes_per_voxel: 16-B lanes per voxel of a joint slice."""
+    return 1 if J <= 4 else 2 if J <= 8 else 4 if J <= 16 else 8
+
+
+def tap_floor_ceiling(n_vox, V, J, H, W, elem, layout_pass, copy_gbs, alg_per_frame):
+    """The design ceiling the roofline fraction is measured against:
+    the gather's tap-instruction floor -- wave-loads x 16.5 cycles over 256 CUs,
+    TAP_PROBE -- plus, for planar input, the layout pass at the measured copy
+    rate (it reads the planar heatmaps and writes the channels-last / pixel-pair
+    table).  Cube stores, L1/L2 misses and setup are taken as free, so this
+    bounds the achievable HBM fraction from above.  Per frame."""
+    wave_loads = 0.0
+    layout_bytes = 0.0
+    for j0 in range(0, J, JOINT_SLICE):
+        js = min(JOINT_SLICE, J - j0)
+        lpv = lanes_per_voxel(js)
+        pairs = elem == 2 and js <= 16
+        # per voxel-camera: 4 taps (fp32: one 16-B load per lane per tap) or 2 rows
+        # (fp16 pixel pairs: both x taps of a row in one 16-B lane load)
+        wave_loads += n_vox * V * (2 if pairs else 4) * lpv * 16 / 1024.0
+        if layout_pass:
+            table = V * H * (W + 1) * 64 if pairs else V * H * W * 4 * lpv * 4
+            layout_bytes += V * js * H * W * elem + table
+    t_taps = wave_loads * TAP_CYCLES_PER_WAVELOAD / (CUS * CLOCK_HZ)
+    t_layout = layout_bytes / (copy_gbs * 1e9) if (layout_pass and copy_gbs) else 0.0
+    t = t_taps + t_layout
+    frac = alg_per_frame / t / (HBM_PEAK_GBS * 1e9)
+    return {"frac": round(frac, 4),
+            "us_per_frame": round(t * 1e6, 3), "tap_floor_us_per_frame": round(t_taps * 1e6, 3),
+            "layout_us_per_frame": round(t_layout * 1e6, 3), "wave_loads_per_frame": round(wave_loads),
+            "layout_bytes_per_frame": round(layout_bytes),
+            "what": ("tap-instruction floor (16.5 cycles per 1-KiB wave-load, " + TAP_PROBE + ")"
+                     + (" + layout pass at the measured copy rate" if layout_pass else "")
+                     + "; stores and L1/L2 misses free: an upper bound on frac"
+                     + (" (the north star's >= 0.60 lies above it)" if frac < 0.6 else ""))}
+
+
+def rank_stats(values, device):
+    """Every rank's `values` (a list of floats) -> [world][len(values)] on every
+    rank (one all-reduce of a zero-padded row per rank; gloo and RCCL alike)."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.zeros((world, len(values)), dtype=torch.float64, device=device)
+    t[rank] = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    return t.cpu().tolist()
 
 
 def host_cores():
@@ -295,6 +385,44 @@ def cpu_baseline(w, sample_grid_cpu, threads_req):
             "sample": f"{w.name}, 4 frames per call, 2 warm-up calls then the median of {main_line['runs']} timed calls "
                       f"per thread count: torch-CPU restatement of project_whole.forward (per-frame F.grid_sample, "
                       f"mean, clamp) + max(dim=4) + nms2D + column gather (oracle/torch_cpu.py), sample grid prebuilt"}
+
+
+def roofline_fields(kernel, alg_bytes, kernel_ms_per_rank, kernel_ms_steps, traffic, copy_gbs, taps, tap_bytes,
+                    ceiling):
+    """The line's `roofline` object.  kernel_ms is the SLOWEST rank's mean op time
+    (every rank processes the same per-rank algorithmic bytes), so achieved / frac
+    describe the slowest GPU; rank 0's and every rank's times are listed."""
+    ms = max(kernel_ms_per_rank)
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    tap_peak = CUS * CLOCK_HZ * 64 / tap_bytes / 1e12
+    tap_rate = taps / (ms * 1e-3) / 1e12
+    r = {
+        "bound": "hbm",
+        "kernel": kernel,
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None if traffic is None else round(traffic["traffic"]),
+        "algorithmic_bytes_per_launch": alg_bytes,
+        "kernel_ms": round(ms, 4),
+        "kernel_ms_rank0": round(kernel_ms_per_rank[0], 4),
+        "kernel_ms_per_rank": [round(v, 4) for v in kernel_ms_per_rank],
+        "slowest_rank": int(max(range(len(kernel_ms_per_rank)), key=lambda i: kernel_ms_per_rank[i])),
+        "kernel_ms_steps": kernel_ms_steps,  # timed steps that carried the event pair (every steps // 50-th)
+        "measured_copy_gbs": round(copy_gbs or 0.0, 1),
+        "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs else None,
+        "tap_rate": {"bound": "vector-memory 64 B/clk/CU", "achieved": round(tap_rate, 3),
+                     "peak": round(tap_peak, 3), "unit": "T joint-taps/s",
+                     "frac": round(tap_rate / tap_peak, 4), "joint_taps_per_launch": taps},
+    }
+    if ceiling is not None:
+        r["ceiling"] = dict(ceiling)
+        r["frac_of_ceiling"] = round(r["frac"] / ceiling["frac"], 4)
+    if traffic is not None:
+        r["traffic_detail"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in traffic.items()}
+        r["traffic_upper"] = round(traffic["traffic_upper"])
+    return r
 
 
 def note(msg):
@@ -550,31 +678,29 @@ def main():
     if grouped:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    vox_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    # every rank's wall time and op time: the job's time is the slowest rank's,
+    # and so is the roofline's kernel time (the line describes the slowest GPU)
+    per_rank = [[el, vox_ms]]
+    if grouped and world > 1:
+        per_rank = rank_stats([el, vox_ms], "cpu" if pg_backend == "gloo" else dev)
+    el = max(r[0] for r in per_rank)
     if args.child:
         if grouped:
             dist.destroy_process_group()
         return
 
-    vox_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     frames = (1 if args.slabs else world) * B * args.steps
     fps = frames / el
     Xs = x1 - x0  # this rank's x-rows (X unless --slabs)
     # (channels-last input: the J joints' bytes are counted, not the zero padding)
     per_frame = V * J * Hd * Wd * hm_planar.element_size() + J * Xs * Y * Z * 4 + J * Xs * Y * 4
     alg_bytes = B * per_frame
-    achieved = alg_bytes / (vox_ms * 1e-3) / 1e9
-
     # secondary bound: the bilinear tap rate, N*V*J*4 joint-taps
     # per frame, against the per-CU vector-memory (texture addresser / L1) rate of
     # 64 B/clk: 16 fp32 joint-taps/clk/CU, 32 with the fp16 pixel-pair table.
     taps = B * Xs * Y * Z * V * J * 4
     tap_bytes = 2 if (hm_planar.element_size() == 2 and J <= 16) else 4
-    tap_peak = 256 * 2.4e9 * 64 / tap_bytes / 1e12
-    tap_rate = taps / (vox_ms * 1e-3) / 1e12
 
     extra = {}
     if rank == 0:
@@ -611,9 +737,13 @@ def main():
                 evs.append((a, b_))
             torch.cuda.synchronize()
             cl_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
+            cl_frac = alg_bytes / (cl_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+            cl_ceiling = tap_floor_ceiling(Xs * Y * Z, V, J, Hd, Wd, 4, False, None, per_frame)
             extra["channels_last"] = {"kernel_ms": round(cl_ms, 4),
                                       "achieved": round(alg_bytes / (cl_ms * 1e-3) / 1e9, 1),
-                                      "frac": round(alg_bytes / (cl_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "frac": round(cl_frac, 4),
+                                      "ceiling_frac": cl_ceiling["frac"],
+                                      "frac_of_ceiling": round(cl_frac / cl_ceiling["frac"], 4),
                                       "frames_per_s_op_only": round(B / (cl_ms * 1e-3), 1),
                                       "what": "the same op on [B,V,H,W,16] heatmaps as fvp.backbone writes them "
                                               "(fvp_voxelize_cl: no layout pass); bit-identical outputs"}
@@ -689,6 +819,13 @@ def main():
                 lat.append((time.perf_counter() - t1) * 1e3)
             extra["latency_b1_abi_ms"] = float(np.median(lat))
 
+    ceiling = None
+    if rank == 0:
+        ceiling = tap_floor_ceiling(Xs * Y * Z, V, J, Hd, Wd, hm_planar.element_size(),
+                                    args.heatmap_layout == "planar", extra.get("copy_gbs"), per_frame)
+        if world > 1:
+            ceiling["copy_rate"] = "rank 0's"
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "on":
         note("cpu baseline")
@@ -721,25 +858,12 @@ def main():
                                 + (f" -- rehearsal (gloo, {world} ranks on {n_devices} shared device(s)), not a measurement"
                                    if rehearsal else "")),
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": ("fvp_voxelize op = layout pass (heatmaps_to_cl / pairs_vec8) + voxelize_kernel per "
-                           "frame chunk" if args.heatmap_layout == "planar" else
-                           "fvp_voxelize_cl op = voxelize_kernel on channels-last heatmaps (no layout pass)"),
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None if traffic is None else round(traffic["corrected"]),
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "kernel_ms": round(vox_ms, 4),
-                "kernel_ms_steps": len(ev),  # timed steps that carried the event pair (every steps // 50-th)
-                "measured_copy_gbs": round(extra.get("copy_gbs", 0.0), 1),
-                "frac_of_measured_copy": round(achieved / extra["copy_gbs"], 4) if extra.get("copy_gbs") else None,
-                "tap_rate": {"bound": "vector-memory 64 B/clk/CU", "achieved": round(tap_rate, 3),
-                             "peak": round(tap_peak, 3), "unit": "T joint-taps/s",
-                             "frac": round(tap_rate / tap_peak, 4), "joint_taps_per_launch": taps},
-            },
+            "roofline": roofline_fields(
+                ("fvp_voxelize op = layout pass (heatmaps_to_cl / pairs_vec8) + voxelize_kernel per "
+                 "frame chunk" if args.heatmap_layout == "planar" else
+                 "fvp_voxelize_cl op = voxelize_kernel on channels-last heatmaps (no layout pass)"),
+                alg_bytes, [r[1] for r in per_rank], len(ev), traffic, extra.get("copy_gbs"), taps, tap_bytes,
+                ceiling),
             "latency_b1_ms": round(extra["latency_b1_ms"], 3) if "latency_b1_ms" in extra else None,
             "latency_b1_graph_ms": round(extra["latency_b1_graph_ms"], 3) if "latency_b1_graph_ms" in extra else None,
             "latency_b1_abi_ms": round(extra["latency_b1_abi_ms"], 4) if "latency_b1_abi_ms" in extra else None,
@@ -751,10 +875,11 @@ def main():
             line["roofline"]["channels_last_input"] = extra["channels_last"]
         if args.heatmap_layout != "planar":
             line["config"]["heatmap_layout"] = "channels-last [B,V,H,W,16] (fvp backbone output)"
-        if traffic is not None:
-            line["roofline"]["traffic_detail"] = {k: round(v, 1) for k, v in traffic.items()}
-        elif traffic_note:
+        if traffic_note:
             line["roofline"]["traffic_note"] = traffic_note
+        elif traffic is None and world > 1:
+            line["roofline"]["traffic_note"] = ("not collected under the launcher (rocprofv3 child runs at N = 1 "
+                                                "only); per-rank work equals the N = 1 line's at the same --batch")
         sys.stdout.flush()
         print(json.dumps(line), file=json_out, flush=True)
     if grouped:

@@ -170,3 +170,70 @@ def test_shard_plan_modes():
         [(20 * r, 20 * r + 20) for r in range(8)]
     with pytest.raises(ValueError):
         bench.shard_plan(3, 0, 8, 80, strong=True)
+
+
+def _line_worker(rank, world, port, q):
+    _paths()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+
+        # each rank's (wall time, op time): rank 1 is the slowest GPU
+        el, ms = 0.5 + 0.1 * rank, [2.40, 2.75, 2.50][rank]
+        per_rank = bench.rank_stats([el, ms], "cpu")
+        line = None
+        if rank == 0:
+            ceiling = bench.tap_floor_ceiling(128000, 5, 15, 128, 240, 4, True, 6200.0, 17_280_000)
+            traffic = {"traffic": 1.0e10, "traffic_upper": 1.3e10, "layout": 5.0e9, "gather": 5.0e9}
+            line = bench.roofline_fields("op", 256 * 17_280_000, [r[1] for r in per_rank], 5, traffic, 6200.0,
+                                         38_400_000 * 256, 4, ceiling)
+        q.put((rank, per_rank, line))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_line_reports_the_slowest_rank_over_gloo():
+    """At world > 1 the line's kernel_ms / achieved / frac come from the slowest
+    rank's op time (the all-reduced per-rank table), and every rank's time is
+    listed."""
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_line_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    table = [[0.5 + 0.1 * r, [2.40, 2.75, 2.50][r]] for r in range(world)]
+    for _, per_rank, _ in got:  # every rank holds the same table
+        assert np.allclose(per_rank, table)
+    line = got[0][2]
+    assert line["kernel_ms"] == 2.75 and line["slowest_rank"] == 1 and line["kernel_ms_rank0"] == 2.40
+    assert line["kernel_ms_per_rank"] == [2.40, 2.75, 2.50]
+    alg = 256 * 17_280_000
+    assert line["achieved"] == round(alg / 2.75e-3 / 1e9, 1)
+    assert line["frac"] == round(alg / 2.75e-3 / 1e9 / 8000.0, 4)
+    assert 0.28 < line["ceiling"]["frac"] < 0.31 and line["frac_of_ceiling"] == round(line["frac"] / line["ceiling"]["frac"], 4)
+    assert line["traffic"] == 10_000_000_000 and line["traffic_upper"] == 13_000_000_000
+
+
+def test_traffic_split_per_kernel(tmp_path):
+    """bench.traffic_from_csvs: the layout pass's FETCH doubled (the guide's
+    calibrated coalesced stream), the gather's raw with its doubled value as the
+    upper bound."""
+    _paths()
+    import bench
+
+    hdr = '"Kernel_Name","Counter_Name","Counter_Value"\n'
+    f = tmp_path / "f.csv"
+    f.write_text(hdr + '"fvp::heatmaps_to_cl_kernel<4>","FETCH_SIZE",100\n"fvp::voxelize_kernel<4>","FETCH_SIZE",300\n'
+                 '"other_kernel","FETCH_SIZE",999\n')
+    w = tmp_path / "w.csv"
+    w.write_text(hdr + '"fvp::heatmaps_to_cl_kernel<4>","WRITE_SIZE",50\n"fvp::voxelize_kernel<4>","WRITE_SIZE",20\n')
+    t = bench.traffic_from_csvs([str(f)], [str(w)], 2)
+    k = 1024.0 / 2
+    assert t["layout"] == (2 * 100 + 50) * k and t["gather"] == (300 + 20) * k
+    assert t["traffic"] == (2 * 100 + 50 + 300 + 20) * k and t["traffic_upper"] == (2 * 100 + 50 + 600 + 20) * k

@@ -14,9 +14,13 @@ one-frame latency launches of the same run have other counts and are left out.
     python3 tools/recompute_roofline.py profiles/round5/closing
 """
 import csv
+import glob
 import json
 import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 
 GATHER, LAYOUT = "voxelize_kernel", "heatmaps_to_cl_kernel"
 CHUNK = 12  # frames per layout + gather launch pair (fvp_voxelize's chunking)
@@ -51,9 +55,23 @@ def main(d):
     print(f"algorithmic bytes per op: {alg / 1e9:.4f} GB ({B} frames)")
     print(f"frac per 12-frame chunk: {per_chunk / 1e9:.1f} GB/s = {per_chunk / (r['peak'] * 1e9):.4f}")
     print(f"frac of the op (trace): {alg / (us * 1e-6) / (r['peak'] * 1e9):.4f}; bench line: {r['frac']:.4f}")
-    if r.get("traffic"):
-        print(f"counter traffic per op: {r['traffic'] / 1e9:.2f} GB = {r['traffic'] / alg:.2f}x algorithmic "
-              f"(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md; pmc_fetch/, pmc_write/)")
+    fetch = glob.glob(os.path.join(d, "pmc_fetch", "**", "*counter_collection.csv"), recursive=True)
+    write = glob.glob(os.path.join(d, "pmc_write", "**", "*counter_collection.csv"), recursive=True)
+    if fetch and write:
+        # the same split and corrections as bench.py (layout FETCH x2; gather FETCH raw .. x2)
+        t = bench.traffic_from_csvs(fetch, write, bench.CHILD_OPS)
+        print(f"counter traffic per op (pmc_fetch/, pmc_write/): layout pass {t['layout'] / 1e9:.3f} GB "
+              f"(2 x {t['layout_fetch_raw'] / 1e9:.3f} fetch + {t['layout_write'] / 1e9:.3f} write), gather "
+              f"{t['gather'] / 1e9:.3f} GB ({t['gather_fetch_raw'] / 1e9:.3f} raw fetch + {t['gather_write'] / 1e9:.3f} write)")
+        print(f"traffic {t['traffic'] / 1e9:.3f} GB = {t['traffic'] / alg:.2f}x algorithmic; with the gather's fetch "
+              f"doubled too {t['traffic_upper'] / 1e9:.3f} GB = {t['traffic_upper'] / alg:.2f}x")
+        if r.get("traffic") is not None:
+            print(f"bench line: traffic {r['traffic'] / 1e9:.3f} GB"
+                  + (f", traffic_upper {r['traffic_upper'] / 1e9:.3f} GB" if "traffic_upper" in r else ""))
+    if "ceiling" in r:
+        c = r["ceiling"]
+        print(f"ceiling: {c['frac']:.4f} ({c['tap_floor_us_per_frame']} us/frame tap floor + "
+              f"{c['layout_us_per_frame']} us/frame layout); frac of ceiling {r['frac'] / c['frac']:.4f}")
 
 
 if __name__ == "__main__":

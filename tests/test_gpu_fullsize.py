@@ -292,6 +292,9 @@ def test_shared_layout_follows_a_reused_buffer(gpu_device):
     rt = torch.as_tensor(geometry.resize_transform(w.ori_image_size, w.image_size), dtype=torch.float).to(gpu_device)
     meta = {"seq": [seq] * 2}
     with torch.no_grad():
+        # (torch's GPU convolutions in CenterNet are not bit-reproducible from call to
+        # call: the maps are compared to 1e-5 of their scale, against the stale result too)
+        stale = integration.fused_hdn_forward(net, a.clone(), meta, cams, rt)
         want = integration.fused_hdn_forward(net, b.clone(), meta, cams, rt)
         buf = a.clone()
         integration.fused_hdn_forward(net, buf, meta, cams, rt)  # HDN alone: its copy stays attached
@@ -300,8 +303,12 @@ def test_shared_layout_follows_a_reused_buffer(gpu_device):
         buf.data.copy_(b)
         assert buf._version == v  # invisible to the version counter
         got = integration.fused_hdn_forward(net, buf, meta, cams, rt)
-        for g, r in zip(got, want):
-            assert torch.equal(g, r)
+        torch.cuda.synchronize()
+        for i in (0, 3):  # hm2d and bbox (proposal picks could swap near-ties between runs)
+            g, r, s = got[i], want[i], stale[i]
+            tol = 1e-5 * float(r.abs().max())
+            assert float((g - r).abs().max()) <= tol
+            assert float((s - r).abs().max()) > 100 * tol  # the stale copy would have been visible
         # the JLN is the copy's last consumer and drops it
         jnet = types.SimpleNamespace(training=False, project_layer=None)
         from fvp.project_individual import ProjectLayer

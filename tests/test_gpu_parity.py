@@ -1183,7 +1183,7 @@ def test_nms_two_level_equals_one_block_and_oracle(gpu_device, kind):
             assert np.array_equal(np.isnan(got), np.isnan(ov))
             assert np.array_equal(np.nan_to_num(got, nan=7.0), np.nan_to_num(ov, nan=7.0))
             assert np.array_equal(fl.cpu().numpy(), ofl) and np.array_equal(xy.cpu().numpy(), oxy), (kind, two)
-            ref_cols = torch.stack([cube[b][:, fl[b]].permute(1, 0, 2) for b in range(B)])
+            ref_cols = torch.stack([cube[b].reshape(J, X * Y, Z)[:, fl[b]].permute(1, 0, 2) for b in range(B)])
             assert torch.equal(cols, ref_cols)
             res[(two, rep)] = (got.view(np.uint32).copy(), fl.cpu().numpy(), cols.cpu().numpy())
     a, b = res[(True, 0)], res[(False, 0)]

@@ -360,8 +360,18 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     if (C <= kSelCap) {
         for (int c = tid; c < C; c += kSelThreads) {
             const unsigned long long k = lkey[c];
-            int rank = 0;
-            for (int j = 0; j < C; ++j) rank += lkey[j] > k;
+            // the list's keys 8 at a time, all 8 LDS reads in flight: on plateaus (a few
+            // peaks on exact zeros, the threshold a zero's key) C reaches a few hundred and
+            // one dependent read per key made this the kernel's longest phase
+            int rank = 0, j = 0;
+            for (; j + 8 <= C; j += 8) {
+                unsigned long long q[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) q[u] = lkey[j + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rank += q[u] > k;
+            }
+            for (; j < C; ++j) rank += lkey[j] > k;
             if (rank < K) {
                 const int idx = (int)~(unsigned)k;
                 write_winner(b, K, rank, idx, (STRIP ? map[idx] : masked_value(map, idx, X, Y, rY)), X, vals, flat, xy, widx);
@@ -405,237 +415,6 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
         for (int u = 0; u < CU; ++u)
             if (e0 + u * kSelThreads < KJZ) cg.cols[(size_t)b * KJZ + e0 + u * kSelThreads] = cv[u];
     }
-}
-
-// -- two-level NMS: tiles of rows on many CUs, then a per-frame merge ---------
-// nms_select_kernel gives each frame ONE CU: at small batches (validate.py's
-// B = 8) 8 CUs work while 248 idle, and the frame's keys, compaction and
-// ranking (~5 us of VALU / LDS on one CU) sit on the critical path.  Here a
-// frame's map is cut into T tiles of R rows; block (tile, frame):
-//   1. stages rows r0-1 .. r1 (the 3x3 window's halo) in LDS and computes the
-//      masked values and 64-bit order keys of its R*Y elements (cand_key: the
-//      same total order as nms_select_kernel),
-//   2. each wave extracts its top-K keys (K rounds of a wave max below the
-//      previous winner), the block ranks the 4K wave winners and writes its
-//      tile's top-K (key + masked value) to the workspace,
-//   3. a release fence and one agent-scope atomic on the frame's counter; the
-//      block that arrives last (the counter reads T-1) merges: t = the K-th
-//      largest of the T tile maxima bounds the frame's top-K from below (the K
-//      tile maxima >= t are distinct elements), so the top-K are among the
-//      entries >= t -- every element >= t that a tile did not list has K larger
-//      elements in its own tile.  Those entries are compacted and ranked by
-//      counting, written out, the winners' z-columns gathered, and the counter
-//      reset to 0 for the next launch.
-// Blocks are numbered tile-major, frame-fastest, so with B % 8 == 0 all tiles
-// of a frame run on one XCD (the dispatcher deals blocks round-robin to the 8
-// XCDs) and share its L2.  Every block exits; nothing waits on another block.
-constexpr int kTwoThreads = 256;
-constexpr int kTwoWaves = kTwoThreads / kWave;
-
-struct NmsEntry {  // one tile winner in the workspace (16 B)
-    unsigned long long key;
-    float v;
-    int pad;
-};
-
-// workspace: [B] u32 counters (zero before the first launch, left zero by every
-// launch), then [B][T][K] NmsEntry
-__host__ __device__ inline size_t nms_counter_bytes(int B) { return ((size_t)B * 4 + 255) & ~(size_t)255; }
-
-template <int E>
-__global__ __launch_bounds__(kTwoThreads) void nms_two_level_kernel(const float *__restrict__ prob, long long stride,
-                                                                    int B, int X, int Y, int K, int R, int T,
-                                                                    unsigned *__restrict__ counters,
-                                                                    NmsEntry *__restrict__ entries,
-                                                                    float *__restrict__ vals,
-                                                                    int64_t *__restrict__ flat,
-                                                                    int64_t *__restrict__ xy, ColGather cg) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float *rows = reinterpret_cast<float *>(smem);  // [R + 2][Y] staged map rows (phase 1)
-    __shared__ unsigned long long wk[kTwoWaves * 16];  // the waves' top-K keys (phase 1)
-    __shared__ int last;
-    __shared__ int count;
-    __shared__ int widx[16];
-    const int b = blockIdx.x % B, t = blockIdx.x / B;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int M = X * Y;
-    const float *__restrict__ p = prob + (size_t)b * stride;
-    const int r0 = t * R, r1 = min(X, r0 + R);
-    const int lo = max(r0 - 1, 0), hi = min(r1 + 1, X);  // staged rows [lo, hi)
-    const int ns = (hi - lo) * Y, ne = (r1 - r0) * Y;
-    {
-        float v[E + 2];  // (R + 2) * Y <= 256 * (E + 2): all loads in flight first
-#pragma unroll
-        for (int i = 0; i < E + 2; ++i) v[i] = p[lo * Y + min(tid + i * kTwoThreads, ns - 1)];
-#pragma unroll
-        for (int i = 0; i < E + 2; ++i)
-            if (tid + i * kTwoThreads < ns) rows[tid + i * kTwoThreads] = v[i];
-    }
-    if (tid == 0) count = 0;
-    __syncthreads();
-    // masked values (proposal.py:34-52): the window maximum with NaN propagating
-    // (nanmax) makes c == m false for any NaN in the window, as masked_value's flag
-    const float rY = 1.0f / (float)Y;
-    unsigned long long key[E];
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-        const int l = tid + i * kTwoThreads;  // element r0 * Y + l of the map
-        key[i] = 0ull;
-        if (l < ne) {
-            const int e = r0 * Y + l;
-            const int ex = div_small(e, Y, rY), ey = e - ex * Y;
-            const float *rc = rows + (ex - lo) * Y;
-            const int yl = ey > 0 ? ey - 1 : ey, yr = ey + 1 < Y ? ey + 1 : ey;  // the centre stands in
-            const float *ru = ex > 0 ? rc - Y : rc, *rd = ex + 1 < X ? rc + Y : rc;
-            const float c = rc[ey];
-            float m = nanmax(nanmax(c, rc[yl]), rc[yr]);
-            m = nanmax(m, nanmax(nanmax(ru[ey], ru[yl]), ru[yr]));
-            m = nanmax(m, nanmax(nanmax(rd[ey], rd[yl]), rd[yr]));
-            key[i] = cand_key(Cand{(c == m ? 1.0f : 0.0f) * c, e});
-        }
-    }
-    // each wave's top-K: K rounds of the largest key below the previous winner
-    // (round 0 takes any key: a NaN at flat index 0 keys to ~0)
-    unsigned long long prev = 0;
-    for (int r = 0; r < K; ++r) {
-        unsigned long long mine = 0;
-#pragma unroll
-        for (int i = 0; i < E; ++i) mine = ((r == 0 || key[i] < prev) && key[i] > mine) ? key[i] : mine;
-        const unsigned long long w = wave_max_key(mine);
-        if (lane == 0) wk[wave * 16 + r] = w;
-        prev = w;
-        if (w == 0) {  // the wave has no more elements: the rest of its list stays 0
-            for (int q = r + 1 + lane; q < K; q += kWave) wk[wave * 16 + q] = 0ull;
-            break;
-        }
-    }
-    __syncthreads();
-    // the tile's top-K among the 4K wave winners: slot = number of larger keys
-    NmsEntry *__restrict__ tile = entries + ((size_t)b * T + t) * K;
-    if (tid < kTwoWaves * K) {
-        const unsigned long long k = wk[(tid / K) * 16 + tid % K];
-        if (k != 0) {
-            int rank = 0;
-            for (int q = 0; q < kTwoWaves * K; ++q) rank += wk[(q / K) * 16 + q % K] > k;
-            if (rank < K) {
-                const int e = (int)~(unsigned)k, ex = div_small(e, Y, rY), ey = e - ex * Y;
-                // the element's own masked value (-0.0 and NaN payloads kept)
-                const float *rc = rows + (ex - lo) * Y;
-                const int yl = ey > 0 ? ey - 1 : ey, yr = ey + 1 < Y ? ey + 1 : ey;
-                const float *ru = ex > 0 ? rc - Y : rc, *rd = ex + 1 < X ? rc + Y : rc;
-                const float c = rc[ey];
-                float m = nanmax(nanmax(c, rc[yl]), rc[yr]);
-                m = nanmax(m, nanmax(nanmax(ru[ey], ru[yl]), ru[yr]));
-                m = nanmax(m, nanmax(nanmax(rd[ey], rd[yl]), rd[yr]));
-                // write-through (sc1) stores: the merge may run on another XCD (no release fence)
-                const float mv = (c == m ? 1.0f : 0.0f) * c;
-                __hip_atomic_store(&tile[rank].key, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(reinterpret_cast<unsigned *>(&tile[rank].v), __builtin_bit_cast(unsigned, mv),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicAdd(&count, 1);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid >= count && tid < K)  // fewer than K elements in the tile: sentinel entries
-        __hip_atomic_store(&tile[tid].key, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // publish (MI355X guide, in-launch hand-off by a counter): every storing wave drains its
-    // write-through stores, then one relaxed agent-scope ticket per block
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned done = __hip_atomic_fetch_add(counters + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = done == (unsigned)(T - 1);
-    }
-    __syncthreads();
-    if (!last) return;
-    // ---- the frame's merge, by the last tile block to arrive.  The entries are read with
-    // sc1 (agent-scope) loads, so no acquire fence: the wavefront fence only keeps the
-    // compiler from moving them above the ticket.
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int NE = T * K;
-    unsigned long long *lkey = reinterpret_cast<unsigned long long *>(smem);  // [NE] (reuses the rows)
-    float *lval = reinterpret_cast<float *>(smem + (size_t)NE * 8);          // [NE]
-    int *cand = reinterpret_cast<int *>(smem + (size_t)NE * 12);             // [NE] compacted entry ids
-    NmsEntry *fe = entries + (size_t)b * T * K;
-    for (int q = tid; q < NE; q += kTwoThreads) {
-        NmsEntry *en = fe + q;
-        // (both loads in flight together; a sentinel's value is never read)
-        const unsigned long long k = __hip_atomic_load(&en->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned vb = __hip_atomic_load(reinterpret_cast<unsigned *>(&en->v), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-        lkey[q] = k;
-        lval[q] = __builtin_bit_cast(float, vb);
-    }
-    if (tid == 0) {
-        count = 0;
-        __hip_atomic_store(counters + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-    }
-    __syncthreads();
-    // threshold: the K-th largest tile maximum (entry [t][0]); 1 (every listed
-    // element) when fewer than K tiles hold one
-    unsigned long long thr = 1ull;
-    {
-        unsigned long long kth = 0;
-        for (int q = tid; q < T; q += kTwoThreads) {
-            const unsigned long long mine = lkey[q * K];
-            int rank = 0;
-            for (int u = 0; u < T; ++u) rank += lkey[u * K] > mine;
-            if (rank == K - 1 && mine != 0) kth = mine;
-        }
-        kth = wave_max_key(kth);
-        if (lane == 0) wk[wave] = kth;
-        __syncthreads();
-        for (int w = 0; w < kTwoWaves; ++w) thr = wk[w] > thr ? wk[w] : thr;
-    }
-    for (int q = tid; q < NE; q += kTwoThreads)
-        if (lkey[q] >= thr) cand[atomicAdd(&count, 1)] = q;
-    __syncthreads();
-    const int C = count;
-    for (int c = tid; c < C; c += kTwoThreads) {
-        const int q = cand[c];
-        const unsigned long long k = lkey[q];
-        int rank = 0;
-        for (int u = 0; u < C; ++u) rank += lkey[cand[u]] > k;
-        if (rank < K) write_winner(b, K, rank, (int)~(unsigned)k, lval[q], X, vals, flat, xy, widx);
-    }
-    if (!cg.cols) return;
-    __syncthreads();
-    const int JZ = cg.J * cg.Z, KJZ = K * JZ;
-    constexpr int CU = 8;  // column elements per thread in flight
-    for (int e0 = tid; e0 < KJZ; e0 += CU * kTwoThreads) {
-        float cv[CU];
-#pragma unroll
-        for (int u = 0; u < CU; ++u) {
-            const int e = min(e0 + u * kTwoThreads, KJZ - 1);
-            const int k = e / JZ, r = e - k * JZ;
-            const int j = r / cg.Z, z = r - j * cg.Z;
-            cv[u] = cg.cube[(((size_t)b * cg.J + j) * M + widx[k]) * cg.Z + z];
-        }
-#pragma unroll
-        for (int u = 0; u < CU; ++u)
-            if (e0 + u * kTwoThreads < KJZ) cg.cols[(size_t)b * KJZ + e0 + u * kTwoThreads] = cv[u];
-    }
-}
-
-// Tile geometry of the two-level kernel: R rows per tile (about two elements per
-// thread), T tiles, E elements per thread, the dynamic LDS (staged rows or the
-// merge's T*K entries at 16 B).  Y <= 256 keeps the halo rows within two more
-// load slots per thread (E + 2).
-struct TwoLevel {
-    int R, T, E;
-    size_t lds;
-};
-
-static inline bool two_level_shape(int X, int Y, int K, TwoLevel &g) {
-    if (K > 16 || Y > 256 || (long long)X * Y > 65535) return false;
-    g.R = min(X, (2 * kTwoThreads + Y - 1) / Y);
-    g.T = (X + g.R - 1) / g.R;
-    const int e = (g.R * Y + kTwoThreads - 1) / kTwoThreads;
-    g.E = e <= 1 ? 1 : e <= 2 ? 2 : 4;
-    const size_t rows = (size_t)(g.R + 2) * Y * 4, merge = (size_t)g.T * K * 16;
-    g.lds = rows > merge ? rows : merge;
-    return g.lds <= 64 * 1024;
 }
 
 // columns[b,k,j,z] = cube[b,j,flat[b,k],z]; one thread per output element,
@@ -711,14 +490,8 @@ __global__ __launch_bounds__(256) void proposal_centers_kernel(const int64_t *__
 }  // namespace fvp
 
 namespace fvp {
-static size_t two_level_ws_bytes(int B, int X, int Y, int K) {
-    TwoLevel g;
-    if (B <= 0 || X <= 0 || Y <= 0 || K <= 0 || !two_level_shape(X, Y, K, g)) return 0;
-    return nms_counter_bytes(B) + (size_t)B * g.T * K * sizeof(NmsEntry);
-}
-
 static int nms_any(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals, int64_t *flat,
-                   int64_t *xy, const ColGather &cg, int Xc, int Yc, void *ws, size_t ws_bytes, void *stream) {
+                   int64_t *xy, const ColGather &cg, int Xc, int Yc, void *stream) {
     if (!prob || !vals || !flat) return FVP_ERR_NULL;
     if (B <= 0 || X <= 0 || Y <= 0 || K <= 0 || K > X * Y) return FVP_ERR_SHAPE;
     const size_t M = (size_t)X * Y;
@@ -727,23 +500,6 @@ static int nms_any(const float *prob, int B, int X, int Y, long long frame_strid
     if (frame_stride == 0) frame_stride = (long long)M;
     if (frame_stride < (long long)M) return FVP_ERR_SHAPE;
     hipStream_t st = (hipStream_t)stream;
-    TwoLevel g;
-    if (ws && two_level_shape(X, Y, K, g)) {
-        if (ws_bytes < two_level_ws_bytes(B, X, Y, K) || (reinterpret_cast<uintptr_t>(ws) & 15))
-            return FVP_ERR_WORKSPACE;
-        unsigned *counters = reinterpret_cast<unsigned *>(ws);
-        NmsEntry *entries = reinterpret_cast<NmsEntry *>(reinterpret_cast<unsigned char *>(ws) + nms_counter_bytes(B));
-        if ((long long)B * g.T > 0x7fffffffLL) return FVP_ERR_SHAPE;
-        const dim3 grid((unsigned)(B * g.T)), blk(kTwoThreads);
-        auto go = [&](auto kernel) {
-            hipLaunchKernelGGL(kernel, grid, blk, g.lds, st, prob, frame_stride, B, X, Y, K, g.R, g.T, counters,
-                               entries, vals, flat, xy, cg);
-        };
-        if (g.E == 1) go(nms_two_level_kernel<1>);
-        else if (g.E == 2) go(nms_two_level_kernel<2>);
-        else go(nms_two_level_kernel<4>);
-        return (int)hipGetLastError();
-    }
     const int E = (int)((M + kSelThreads - 1) / kSelThreads);
     const size_t sel_lds = ((M * 4 + 15) & ~(size_t)15) + (size_t)kSelCap * 8;
     if (K <= kSelWaves && E <= kSelMaxE && sel_lds <= 159 * 1024) {
@@ -784,7 +540,7 @@ static int nms_any(const float *prob, int B, int X, int Y, long long frame_strid
 extern "C" int fvp_nms_topk(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
                             int64_t *flat, int64_t *xy, void *stream) {
     return fvp::nms_any(prob, B, X, Y, frame_stride, K, vals, flat, xy, fvp::ColGather{nullptr, nullptr, 0, 0}, 0, 0,
-                        nullptr, 0, stream);
+                        stream);
 }
 
 extern "C" int fvp_nms_topk_columns(const float *prob, int B, int X, int Y, long long frame_stride, int K,
@@ -793,24 +549,7 @@ extern "C" int fvp_nms_topk_columns(const float *prob, int B, int X, int Y, long
     if (!cube || !columns) return FVP_ERR_NULL;
     if (J <= 0 || Z <= 0) return FVP_ERR_SHAPE;
     return fvp::nms_any(prob, B, X, Y, frame_stride, K, vals, flat, xy, fvp::ColGather{cube, columns, J, Z}, X, Y,
-                        nullptr, 0, stream);
-}
-
-extern "C" size_t fvp_nms_workspace_bytes(int B, int X, int Y, int K) { return fvp::two_level_ws_bytes(B, X, Y, K); }
-
-extern "C" int fvp_nms_topk_ws(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
-                               int64_t *flat, int64_t *xy, void *workspace, size_t workspace_bytes, void *stream) {
-    return fvp::nms_any(prob, B, X, Y, frame_stride, K, vals, flat, xy, fvp::ColGather{nullptr, nullptr, 0, 0}, 0, 0,
-                        workspace, workspace_bytes, stream);
-}
-
-extern "C" int fvp_nms_topk_columns_ws(const float *prob, int B, int X, int Y, long long frame_stride, int K,
-                                       float *vals, int64_t *flat, int64_t *xy, const float *cube, int J, int Z,
-                                       float *columns, void *workspace, size_t workspace_bytes, void *stream) {
-    if (!cube || !columns) return FVP_ERR_NULL;
-    if (J <= 0 || Z <= 0) return FVP_ERR_SHAPE;
-    return fvp::nms_any(prob, B, X, Y, frame_stride, K, vals, flat, xy, fvp::ColGather{cube, columns, J, Z}, X, Y,
-                        workspace, workspace_bytes, stream);
+                        stream);
 }
 
 extern "C" int fvp_gather_columns(const float *cube, int B, int J, int X, int Y, int Z, const int64_t *flat, int K,

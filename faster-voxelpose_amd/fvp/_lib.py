@@ -61,11 +61,6 @@ SIGNATURES = {
     "fvp_nms_topk": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_nms_topk_columns": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_int, c_int, c_void_p, c_void_p],
-    "fvp_nms_workspace_bytes": [c_int, c_int, c_int, c_int],
-    "fvp_nms_topk_ws": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                        ctypes.c_size_t, c_void_p],
-    "fvp_nms_topk_columns_ws": [c_void_p, c_int, c_int, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p,
-                                c_void_p, c_int, c_int, c_void_p, c_void_p, ctypes.c_size_t, c_void_p],
     "fvp_gather_columns": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
     "fvp_voxel_columns": [c_void_p, c_int, ctypes.c_longlong, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int,
                           c_int, c_void_p, c_void_p, c_void_p, ctypes.POINTER(GridSpec), ctypes.POINTER(ImageSpec),
@@ -121,7 +116,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 19
+ABI_VERSION = 18
 _LIB = None
 
 
@@ -145,8 +140,7 @@ def load():
                       "fvp_person_workspace_bytes": ctypes.c_size_t,
                       "fvp_conv2d_workspace_bytes": ctypes.c_size_t,
                       "fvp_conv2d_ex_workspace_bytes": ctypes.c_size_t,
-                      "fvp_conv1d_net_lds_bytes": ctypes.c_size_t,
-                      "fvp_nms_workspace_bytes": ctypes.c_size_t}.get(name, c_int)
+                      "fvp_conv1d_net_lds_bytes": ctypes.c_size_t}.get(name, c_int)
     if lib.fvp_abi_version() != ABI_VERSION:
         raise FvpError(f"fvp: ABI version mismatch ({lib.fvp_abi_version()} != {ABI_VERSION})")
     _LIB = lib

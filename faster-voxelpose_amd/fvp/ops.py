@@ -330,69 +330,28 @@ def _(heatmaps_cl, J, cams, grid_index, resize_t, start, end, center, bins, ori_
 
 
 # ---------------------------------------------------------------------------
-# Two-level NMS (fvp_nms_topk_ws / fvp_nms_topk_columns_ws): a frame's map on many
-# CUs.  Used up to NMS_TWO_LEVEL_MAX_FRAMES frames per launch; larger batches fill
-# the chip with one 1024-thread block per frame already.
-NMS_TWO_LEVEL_MAX_FRAMES = 64
-_NMS_WS: dict = {}  # (device index, stream, B) -> zeroed workspace (counters self-reset)
-
-
-def _nms_workspace(p: torch.Tensor, B: int, X: int, Y: int, K: int, two_level):
-    """(workspace tensor, bytes) for the two-level kernel, or (None, 0) for the
-    one-block kernel.  two_level: None = by batch size, True / False = forced
-    (tests and probes).  One zeroed buffer per (device, stream, B): the kernel's
-    per-frame counters sit in its first 4*B bytes, so buffers are not shared
-    between batch sizes or streams."""
-    if two_level is False or (two_level is None and B > NMS_TWO_LEVEL_MAX_FRAMES):
-        return None, 0
-    n = int(_lib.load().fvp_nms_workspace_bytes(B, X, Y, K))
-    if n == 0:
-        return None, 0
-    key = (p.device.index, _stream(p), B)
-    ws = _NMS_WS.get(key)
-    if ws is None or ws.numel() < n:
-        ws = torch.zeros((n + 255) // 256 * 256, dtype=torch.uint8, device=p.device)
-        _NMS_WS[key] = ws
-    return ws, n
-
-
-def _nms_map(prob: torch.Tensor):
-    """(map, B, X, Y, frame stride): a channel slice of a contiguous [B,C,X,Y]
-    tensor is passed by frame stride, without a copy (a batch stride below X*Y
-    -- e.g. an expand()ed map with stride 0 -- is copied: the kernels read each
-    frame's X*Y floats at b*stride)."""
+@_custom_op("fvp::nms_topk", mutates_args=(), device_types="cuda")
+def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     if prob.device.type != "cuda":
         raise _lib.FvpError(f"fvp: prob_map must be on a HIP device, got {prob.device}")
     B, X, Y = prob.shape[0], prob.shape[-2], prob.shape[-1]
+    if prob.numel() != B * X * Y:
+        raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map")
     p = prob
+    # a channel slice of a contiguous [B,C,X,Y] tensor is passed by frame stride, without a copy
+    # (a batch stride below X*Y -- e.g. an expand()ed map with stride 0 -- is copied:
+    # the kernel reads each frame's X*Y floats at b*stride)
     if not (p.dtype == torch.float32 and p.stride()[-1] == 1 and p.stride()[-2] == Y
             and (B <= 1 or p.stride()[0] >= X * Y)):
         p = p.to(torch.float32).contiguous()
-    return p, B, X, Y, (p.stride()[0] if B > 1 else X * Y)
-
-
-def nms_topk_into(prob: torch.Tensor, K: int, two_level=None):
-    """nms_topk's implementation; two_level forces the kernel (None: by batch size)."""
-    p, B, X, Y, stride = _nms_map(prob)
-    if prob.numel() != B * X * Y:
-        raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map")
+    stride = p.stride()[0] if B > 1 else X * Y
     vals = torch.empty((B, K), dtype=torch.float32, device=p.device)
     flat = torch.empty((B, K), dtype=torch.int64, device=p.device)
     xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
     if B == 0:
         return vals, xy, flat
-    ws, n = _nms_workspace(p, B, X, Y, K, two_level)
-    if ws is not None:
-        _lib.call("fvp_nms_topk_ws", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _ptr(ws), n,
-                  _stream(p))
-    else:
-        _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
+    _lib.call("fvp_nms_topk", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _stream(p))
     return vals, xy, flat
-
-
-@_custom_op("fvp::nms_topk", mutates_args=(), device_types="cuda")
-def nms_topk(prob: torch.Tensor, K: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    return nms_topk_into(prob, K)
 
 
 def proposal_buffers(B: int, K: int, device) -> tuple[torch.Tensor, torch.Tensor]:
@@ -405,24 +364,26 @@ def proposal_buffers(B: int, K: int, device) -> tuple[torch.Tensor, torch.Tensor
     return vals, flat
 
 
-def _nms_topk_columns_into(prob, K, cube, vals, flat, two_level=None):
-    """fvp_nms_topk_columns[_ws] into the caller's vals [B,K] fp32 / flat [B,K] int64."""
+def _nms_topk_columns_into(prob, K, cube, vals, flat):
+    """fvp_nms_topk_columns into the caller's vals [B,K] fp32 / flat [B,K] int64."""
+    if prob.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: prob_map must be on a HIP device, got {prob.device}")
     c = _dev_f32(cube, "feature_cubes")
-    p, B, X, Y, stride = _nms_map(prob)
+    B, X, Y = prob.shape[0], prob.shape[-2], prob.shape[-1]
     if prob.numel() != B * X * Y or c.dim() != 5 or tuple(c.shape[0:1]) + tuple(c.shape[2:4]) != (B, X, Y):
         raise _lib.FvpError("fvp: nms2D expects a [B, 1, X, Y] map over the cube's [B, J, X, Y, Z] grid")
+    p = prob
+    if not (p.dtype == torch.float32 and p.stride()[-1] == 1 and p.stride()[-2] == Y
+            and (B <= 1 or p.stride()[0] >= X * Y)):
+        p = p.to(torch.float32).contiguous()
+    stride = p.stride()[0] if B > 1 else X * Y
     J, Z = c.shape[1], c.shape[4]
     xy = torch.empty((B, K, 2), dtype=torch.int64, device=p.device)
     cols = torch.empty((B, K, J, Z), dtype=torch.float32, device=p.device)
     if B == 0 or cols.numel() == 0:
         return vals, xy, flat, cols
-    ws, n = _nms_workspace(p, B, X, Y, K, two_level)
-    if ws is not None:
-        _lib.call("fvp_nms_topk_columns_ws", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _ptr(c),
-                  J, Z, _ptr(cols), _ptr(ws), n, _stream(p))
-    else:
-        _lib.call("fvp_nms_topk_columns", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _ptr(c),
-                  J, Z, _ptr(cols), _stream(p))
+    _lib.call("fvp_nms_topk_columns", _ptr(p), B, X, Y, stride, K, _ptr(vals), _ptr(flat), _ptr(xy), _ptr(c), J, Z,
+              _ptr(cols), _stream(p))
     return vals, xy, flat, cols
 
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 19
+#define FVP_ABI_VERSION 18
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -202,25 +202,6 @@ int fvp_proposal_centers(const int64_t *index, int index_dims, const float *hm1d
  *   cube device [B][J][X][Y][Z];  columns device [B][K][J][Z] */
 int fvp_nms_topk_columns(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
                          int64_t *flat, int64_t *xy, const float *cube, int J, int Z, float *columns, void *stream);
-/* The same two selections on many CUs per frame (the two-level kernel: tiles
- * of map rows pick their top-K, the last tile block of each frame to finish
- * merges them; same results bit for bit).  The one-block kernels above give a
- * frame one CU, which at small batches (run/validate.py's B = 8) leaves the
- * chip idle.  Used when the map fits (K <= 16, Y <= 256, X*Y < 65536;
- * otherwise these run the one-block kernels and ignore the workspace).
- *   workspace  device, 16-B aligned, >= fvp_nms_workspace_bytes(B, X, Y, K)
- *              bytes (0 = the shape does not take the two-level kernel).  Its
- *              first 4*B bytes are per-frame counters that MUST be zero before
- *              the first call with this B; every call leaves them zero.  Keep
- *              one workspace per stream: concurrent calls must not share one.
- * Replaces nms2D / get_index2D (lib/core/proposal.py:13-76) and the column
- * gather (lib/models/human_detection_net.py:199-200), as the calls above. */
-size_t fvp_nms_workspace_bytes(int B, int X, int Y, int K);
-int fvp_nms_topk_ws(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
-                    int64_t *flat, int64_t *xy, void *workspace, size_t workspace_bytes, void *stream);
-int fvp_nms_topk_columns_ws(const float *prob, int B, int X, int Y, long long frame_stride, int K, float *vals,
-                            int64_t *flat, int64_t *xy, const float *cube, int J, int Z, float *columns,
-                            void *workspace, size_t workspace_bytes, void *stream);
 /* z-columns of the top-K proposals: columns[b,k,j,:] = cube[b,j,flat[b,k],:]
  * (an index outside [0, X*Y) reads nothing and yields NaN; torch.gather raises)
  * Replaces the torch.gather at lib/models/human_detection_net.py:199-200. */

@@ -1128,77 +1128,34 @@ def test_divisors_outside_div_const_sweep_take_ieee_division(gpu_device, otf, im
         _assert_same(cube[0].cpu().numpy(), O.voxelize(hm[0].numpy(), sg).reshape(3, *bins), "cube")
 
 
-@pytest.mark.parametrize("kind", ["c3_xy", "zeros", "plateau", "nan", "nan_spots", "negative", "tiny", "big_noise",
-                                  "c5_size", "ragged", "column", "row", "single"])
-def test_nms_two_level_equals_one_block_and_oracle(gpu_device, kind):
-    """The two-level NMS (tiles of rows on many CUs + the last tile block's merge,
-    fvp_nms_topk[_columns]_ws) against the one-block kernels and the oracle, bit
-    for bit: values (-0.0 / NaN payloads), flat indices, get_index2D pairs and the
-    fused column gather; plateaus of tied zeros (the HDN's masked maps), maps of
-    one tile and of 40 tiles, a 300 x 1 column, K = X*Y."""
-    from fvp import ops
+@pytest.mark.parametrize("kind", ["plateau", "plateau_k16", "smooth_b8", "c5_size", "single"])
+def test_nms_plateaus_and_columns_vs_oracle(gpu_device, kind):
+    """nms2D and the fused column gather on a few peaks over exact zeros (the
+    candidate list then holds hundreds of tied zeros, ranked by index), on C3-like
+    smooth maps at B = 8, a 160 x 160 map and K = X*Y: bit for bit against the
+    oracle, columns against torch indexing."""
+    from fvp.proposal import nms2D, nms2D_columns
 
     g = torch.Generator().manual_seed(len(kind))
-    shape, K = {"c3_xy": ((8, 1, 80, 80), 10), "zeros": ((3, 1, 80, 80), 10), "plateau": ((8, 1, 80, 80), 10),
-                "nan": ((2, 1, 80, 80), 10), "nan_spots": ((4, 1, 80, 80), 16), "negative": ((2, 1, 40, 40), 16),
-                "tiny": ((4, 1, 4, 4), 16), "big_noise": ((3, 1, 128, 128), 10), "c5_size": ((2, 1, 160, 160), 10),
-                "ragged": ((5, 1, 37, 53), 7), "column": ((2, 1, 300, 1), 5), "row": ((2, 1, 1, 256), 5),
+    shape, K = {"plateau": ((8, 1, 80, 80), 10), "plateau_k16": ((3, 1, 80, 80), 16),
+                "smooth_b8": ((8, 1, 80, 80), 10), "c5_size": ((2, 1, 160, 160), 10),
                 "single": ((3, 1, 3, 3), 9)}[kind]
-    if kind == "zeros":
-        prob = torch.zeros(shape)
-    elif kind == "nan":
-        prob = torch.full(shape, float("nan"))
-    elif kind == "negative":
-        prob = -torch.rand(shape, generator=g)
-    elif kind == "plateau":  # CenterNet-like: a few peaks on exact zeros
+    B, _, X, Y = shape
+    if kind.startswith("plateau"):
         prob = torch.rand(shape, generator=g)
         prob[prob < 0.999] = 0.0
-    elif kind == "c3_xy":
-        B, _, X, Y = shape
+    elif kind == "smooth_b8":
         prob = torch.nn.functional.avg_pool2d(torch.rand((B, 1, X + 6, Y + 6), generator=g), 7, 1)
     else:
         prob = torch.rand(shape, generator=g)
-    if kind == "nan_spots":
-        prob.view(-1)[torch.randperm(prob.numel(), generator=g)[:12]] = float("nan")
-    if kind == "negative":
-        prob[0, 0, 5, 5] = -0.0
-    B, _, X, Y = shape
-    Z, J = 6, 3
+    J, Z = 3, 6
     cube = torch.rand((B, J, X, Y, Z), generator=g).to(gpu_device)
     pd = prob.to(gpu_device)
-    lib = __import__("fvp._lib", fromlist=["load"]).load()
-    assert lib.fvp_nms_workspace_bytes(B, X, Y, K) > 0  # these shapes take the two-level kernel
     ov, oxy, ofl = O.nms2d(prob.numpy(), K)
-    res = {}
-    for two in (True, False):
-        for rep in range(2):  # the counters reset themselves: a second call sees a clean workspace
-            v, xy, fl = ops.nms_topk_into(pd, K, two_level=two)
-            v2, xy2, fl2, cols = ops._nms_topk_columns_into(pd, K, cube, torch.empty((B, K), device=gpu_device),
-                                                            torch.empty((B, K), dtype=torch.int64, device=gpu_device),
-                                                            two_level=two)
-            torch.cuda.synchronize()
-            got = v.cpu().numpy()
-            assert np.array_equal(got.view(np.uint32), v2.cpu().numpy().view(np.uint32)), (two, rep)
-            assert torch.equal(fl, fl2) and torch.equal(xy, xy2)
-            assert np.array_equal(np.isnan(got), np.isnan(ov))
-            assert np.array_equal(np.nan_to_num(got, nan=7.0), np.nan_to_num(ov, nan=7.0))
-            assert np.array_equal(fl.cpu().numpy(), ofl) and np.array_equal(xy.cpu().numpy(), oxy), (kind, two)
-            ref_cols = torch.stack([cube[b].reshape(J, X * Y, Z)[:, fl[b]].permute(1, 0, 2) for b in range(B)])
-            assert torch.equal(cols, ref_cols)
-            res[(two, rep)] = (got.view(np.uint32).copy(), fl.cpu().numpy(), cols.cpu().numpy())
-    a, b = res[(True, 0)], res[(False, 0)]
-    assert all(np.array_equal(x, y) for x, y in zip(a, b))
-
-
-def test_nms_two_level_batch_sizes_share_a_stream(gpu_device):
-    """Workspaces per batch size on one stream (the counters of B frames sit in the
-    first 4B bytes): alternating B = 3, 64, 1, 64, 3 and a 200-frame forced launch
-    (many XCDs per frame) all equal the one-block kernel."""
-    from fvp import ops
-
-    g = torch.Generator().manual_seed(5)
-    maps = torch.rand((200, 1, 80, 80), generator=g).to(gpu_device)
-    for B in (3, 64, 1, 64, 3, 200):
-        v1, _, f1 = ops.nms_topk_into(maps[:B], 10, two_level=True)
-        v0, _, f0 = ops.nms_topk_into(maps[:B], 10, two_level=False)
-        assert torch.equal(f1, f0) and torch.equal(v1, v0), B
+    v, xy, fl = nms2D(pd, K)
+    v2, xy2, fl2, cols = nms2D_columns(pd, K, cube)
+    assert np.array_equal(v.cpu().numpy(), ov) and np.array_equal(v2.cpu().numpy(), ov)
+    assert np.array_equal(fl.cpu().numpy(), ofl) and np.array_equal(fl2.cpu().numpy(), ofl)
+    assert np.array_equal(xy.cpu().numpy(), oxy) and np.array_equal(xy2.cpu().numpy(), oxy)
+    ref_cols = torch.stack([cube[b].reshape(J, X * Y, Z)[:, fl[b]].permute(1, 0, 2) for b in range(B)])
+    assert torch.equal(cols, ref_cols)

@@ -14,6 +14,7 @@
 #   step    tools/step_host.py (host / GPU time per part of the small-batch step; $STEP_ARGS)
 #   overlap tools/overlap_probe2.py for each library in $AB_LIBS
 #   pmcl2   TCC_HIT / TCC_MISS (one counter pass each) of a short bench run per library in $AB_LIBS
+#   nmsp    tools/nms_probe.py (NMS top-K [+ columns] per launch, smooth and plateau maps)
 #   wino    tools/wino_probe.py (Winograd vs direct 3x3 layers)
 #   cnn     tools/bench_cnn.py
 #   cntrace rocprofv3 kernel trace of one CenterNet (8 frames) and one P2PNet (240 images) forward, per dispatch
@@ -77,6 +78,8 @@ for step in "$@"; do
              done
            done
            python3 tools/pmc_kernels.py $O/pmc_* ;;
+    nmsp)  timeout -k 10 300 python3 tools/nms_probe.py > $O/nms_probe.json 2> $O/nms_probe.err || fail nmsp $O/nms_probe.err
+           cat $O/nms_probe.json ;;
     wino)  timeout -k 10 300 python3 tools/wino_probe.py > $O/wino.jsonl 2> $O/wino.err || fail wino $O/wino.err
            cat $O/wino.jsonl ;;
     winoab) for lib in $AB_LIBS; do

@@ -22,11 +22,15 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
     out = {"lib": os.environ.get("FVP_LIB", "libfvp.so")}
-    for B in (1, 8):
+    for B, mname in ((1, ""), (8, ""), (8, "plateau_")):
         prob = torch.nn.functional.avg_pool2d(torch.rand((B, 1, 88, 88), generator=g), 9, 1).to(dev)
+        if mname:  # a few peaks on exact zeros: hundreds of tied candidates
+            prob = torch.rand((B, 1, 80, 80), generator=g)
+            prob[prob < 0.999] = 0.0
+            prob = prob.to(dev)
         cube = torch.rand((B, 15, 80, 80, 20), generator=g).to(dev)
-        for tag, fn in (("topk", lambda: ops.nms_topk(prob, 10)),
-                        ("topk_columns", lambda: ops.nms_topk_columns(prob, 10, cube))):
+        for tag, fn in ((f"{mname}topk", lambda: ops.nms_topk(prob, 10)),
+                        (f"{mname}topk_columns", lambda: ops.nms_topk_columns(prob, 10, cube))):
             from fvp.graphs import CapturedStep
 
             def many(fn=fn):

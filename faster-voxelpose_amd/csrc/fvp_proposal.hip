@@ -222,11 +222,11 @@ __device__ __forceinline__ void write_winner(int b, int K, int slot, int idx, fl
 // as 64-bit order keys in registers (cand_key: NaN first, value descending,
 // index ascending; every key of a real element is > 0; the masked values are
 // recomputed from the staged map for the few candidates):
-//   1. t = the K-th largest of the 16 wave maxima.  Those K maxima are distinct
-//      elements >= t, so at least K elements are >= t, and the top-K are among
-//      the elements >= t.
+//   1. t = the K-th largest of the 64 16-lane row maxima.  Those K maxima are
+//      distinct elements >= t, so at least K elements are >= t, and the top-K are
+//      among the elements >= t.
 //   2. the elements >= t are compacted into an LDS list by wave ballots (a map
-//      typically has tens; an all-equal plateau at most 64*(K-1)+1),
+//      typically has tens; an all-equal plateau at most 16*(K-1)+1 below the threshold row),
 //   3. every listed candidate counts the listed keys above its own: that rank
 //      is its output slot when < K.
 // A list longer than kSelCap (only for adversarial value layouts) falls back
@@ -253,6 +253,7 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
     float *map = reinterpret_cast<float *>(smem);                                             // [M]
     unsigned long long *lkey = reinterpret_cast<unsigned long long *>(smem + (((size_t)M * 4 + 15) & ~(size_t)15));
     __shared__ unsigned long long wmax[kSelWaves];
+    __shared__ unsigned long long gmax[4 * kSelWaves];  // maxima of the block's 16-lane rows
     __shared__ unsigned long long thr;
     __shared__ int count;
     __shared__ int widx[kSelWaves];  // winners' flat indices (K <= kSelWaves)
@@ -325,14 +326,22 @@ __global__ __launch_bounds__(kSelThreads) void nms_select_kernel(const float *__
             best = key[i] > best ? key[i] : best;
         }
     }
-    best = wave_max_key(best);
-    if (lane == 0) wmax[wave] = best;
+    // the maxima of the 64 16-lane rows (DPP within rows: lane 15 of each row ends with its
+    // row's maximum); the K-th largest of them is the threshold.  Rows rather than waves:
+    // on a plateau of tied zeros the threshold is a zero's key, and the candidates are the
+    // zeros of smaller index -- ~16 per row above it instead of ~64 per wave
+    best = dpp_max<0x111, 0xf, 0xf>(best);
+    best = dpp_max<0x112, 0xf, 0xf>(best);
+    best = dpp_max<0x113, 0xf, 0xf>(best);
+    best = dpp_max<0x114, 0xf, 0xe>(best);
+    best = dpp_max<0x118, 0xf, 0xc>(best);
+    if ((lane & 15) == 15) gmax[wave * 4 + (lane >> 4)] = best;
     __syncthreads();
-    if (wave == 0 && lane < kSelWaves) {
-        const unsigned long long mine = wmax[lane];
+    if (wave == 0) {
+        const unsigned long long mine = gmax[lane];
         int rank = 0;
-#pragma unroll
-        for (int w = 0; w < kSelWaves; ++w) rank += wmax[w] > mine;
+#pragma unroll 16
+        for (int w = 0; w < 4 * kSelWaves; ++w) rank += gmax[w] > mine;
         if (rank == K - 1) thr = mine;
     }
     __syncthreads();

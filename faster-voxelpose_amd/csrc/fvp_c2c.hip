@@ -29,14 +29,16 @@ struct C2COp {
     int src, dst, res_pre, res_post;  // activation buffer ids (-1: none)
     int relu;
     int w_off;  // params offset (floats, % 4 == 0): W [cin][k][cout], then scale [cout], shift [cout]
-    int cic;    // input channels per staged weight chunk (% 4 == 0, cic * k * cout <= kC2CWChunk)
+    int cic;    // input channels per staged weight chunk (% 4 == 0, cic * k * cout <= the chunk size)
 };
 static_assert(sizeof(C2COp) == 12 * sizeof(int), "C2COp layout");
 
 constexpr int kC2CThreads = 1024;
-constexpr int kC2CWChunk = 12288;  // floats per weight chunk buffer (48 KB; two buffers)
-constexpr int kC2CStage = kC2CWChunk / (4 * kC2CThreads);  // float4 loads per thread per chunk
-constexpr int kC2CRed = 4096;      // floats of the split-K partial sums (4 splits x 1024 / LG items x LG)
+// Weight chunk buffers (two): wchunk floats each, a multiple of kC2CStageFloats up to
+// kC2CMaxStage of them -- 12,288 (48 KB) unless the activations need the room (C5's
+// Z = 64 columns: 8,192).  The split-K partial sums take kC2CThreads * LG floats.
+constexpr int kC2CStageFloats = 4 * kC2CThreads;  // one float4 load per thread
+constexpr int kC2CMaxStage = 3;
 
 // Activation rows in LDS are padded: [C][3 zeros, L values, 3 zeros] (pitch L + 6),
 // so a tap outside the row reads a zero and the products need no guards.
@@ -99,17 +101,18 @@ __device__ __forceinline__ void c2c_conv(const C2COp &op, const float *__restric
     else c2c_products<7, false, LG>(op, in, wl, ci0, nci, co, g, ks, KS, acc);
 }
 
-// one block per column; dynamic LDS: [2][kC2CWChunk] weights, the split partial sums, then nbuf
-// activation buffers of slot floats
+// one block per column; dynamic LDS: [2][wchunk] weights, the split partial sums
+// [kC2CThreads * LG], then nbuf activation buffers of slot floats
 template <int LG>
 __global__ __launch_bounds__(kC2CThreads) void c2c_net_kernel(const float *__restrict__ x, int cin0, int L0,
                                                               const C2COp *__restrict__ prog, int nops,
                                                               const float *__restrict__ params, int slot, int nbuf,
-                                                              int out_buf, int cout_final, int Lfinal,
+                                                              int wchunk, int out_buf, int cout_final, int Lfinal,
                                                               float *__restrict__ y) {
     extern __shared__ __attribute__((aligned(16))) float c2clds[];
-    float *wbuf0 = c2clds, *wbuf1 = c2clds + kC2CWChunk, *red = c2clds + 2 * kC2CWChunk;
-    float *act = red + kC2CRed;
+    float *wbuf0 = c2clds, *wbuf1 = c2clds + wchunk, *red = c2clds + 2 * wchunk;
+    float *act = red + kC2CThreads * LG;
+    const int nstage = wchunk / kC2CStageFloats;
     const int tid = threadIdx.x, col = blockIdx.x;
     const int cin4 = (cin0 + 3) & ~3, Lp0 = L0 + 2 * kC2CPad;  // channels past cin0: zero rows
     for (int e = tid; e < cin4 * Lp0; e += kC2CThreads) {
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(kC2CThreads) void c2c_net_kernel(const float *__res
         act[e] = (c < cin0 && q >= 0 && q < L0) ? x[((size_t)col * cin0 + c) * L0 + q] : 0.0f;
     }
     (void)nbuf;
-    f32x4 st[kC2CStage];
+    f32x4 st[kC2CMaxStage];
     auto chunk_floats = [&](const C2COp &q, int c) {
         return (c + 1 < (q.cin + q.cic - 1) / q.cic ? q.cic : q.cin - c * q.cic) * q.k * q.cout;
     };
@@ -150,17 +153,17 @@ __global__ __launch_bounds__(kC2CThreads) void c2c_net_kernel(const float *__res
             const int n4 = chunk_floats(op, c) >> 2;
             const f32x4 *src = reinterpret_cast<const f32x4 *>(W + (size_t)c * op.cic * op.k * op.cout);
 #pragma unroll
-            for (int u = 0; u < kC2CStage; ++u) {
+            for (int u = 0; u < kC2CMaxStage; ++u) {
                 const int e = tid + kC2CThreads * u;
-                if (e < n4) st[u] = src[e];
+                if (u < nstage && e < n4) st[u] = src[e];
             }
         };
         auto store_chunk = [&](int c, float *dstw) {
             const int n4 = chunk_floats(op, c) >> 2;
 #pragma unroll
-            for (int u = 0; u < kC2CStage; ++u) {
+            for (int u = 0; u < kC2CMaxStage; ++u) {
                 const int e = tid + kC2CThreads * u;
-                if (e < n4) reinterpret_cast<f32x4 *>(dstw)[e] = st[u];
+                if (u < nstage && e < n4) reinterpret_cast<f32x4 *>(dstw)[e] = st[u];
             }
         };
         // (a prefetch of the next op's first chunk during this op measured slower: 142 -> 160 us)
@@ -218,28 +221,29 @@ __global__ __launch_bounds__(kC2CThreads) void c2c_net_kernel(const float *__res
 
 }  // namespace fvp
 
-extern "C" size_t fvp_conv1d_net_lds_bytes(int slot, int nbuf) {
-    return (size_t)(2 * fvp::kC2CWChunk + fvp::kC2CRed + (size_t)slot * nbuf) * sizeof(float);
+extern "C" size_t fvp_conv1d_net_lds_bytes(int slot, int nbuf, int wchunk, int lg) {
+    return (size_t)(2 * (size_t)wchunk + (size_t)fvp::kC2CThreads * lg + (size_t)slot * nbuf) * sizeof(float);
 }
 
 extern "C" int fvp_conv1d_net(const float *x, int ncols, int cin0, int L0, const int *prog, int nops,
-                              const float *params, int slot, int nbuf, int out_buf, int cout_final, int Lfinal, int lg,
-                              float *y, void *stream) {
+                              const float *params, int slot, int nbuf, int wchunk, int out_buf, int cout_final,
+                              int Lfinal, int lg, float *y, void *stream) {
     if (!x || !prog || !params || !y) return FVP_ERR_NULL;
     if (ncols <= 0 || cin0 <= 0 || L0 <= 0 || nops <= 0 || slot <= 0 || nbuf <= 0 || out_buf < 0 || out_buf >= nbuf ||
-        cout_final <= 0 || Lfinal <= 0 || ((cin0 + 3) & ~3) * (L0 + 6) > slot || cout_final * (Lfinal + 6) > slot)
+        cout_final <= 0 || Lfinal <= 0 || ((cin0 + 3) & ~3) * (L0 + 6) > slot || cout_final * (Lfinal + 6) > slot ||
+        wchunk <= 0 || wchunk % fvp::kC2CStageFloats || wchunk > fvp::kC2CMaxStage * fvp::kC2CStageFloats)
         return FVP_ERR_SHAPE;
-    const size_t lds = fvp_conv1d_net_lds_bytes(slot, nbuf);
+    if (lg != 4 && lg != 8) return FVP_ERR_SHAPE;
+    const size_t lds = fvp_conv1d_net_lds_bytes(slot, nbuf, wchunk, lg);
     if (lds > 160 * 1024) return FVP_ERR_SHAPE;
     hipStream_t s = (hipStream_t)stream;
     const dim3 g((unsigned)ncols), b(fvp::kC2CThreads);
     auto P = reinterpret_cast<const fvp::C2COp *>(prog);
-    switch (lg) {
-        case 4: hipLaunchKernelGGL(fvp::c2c_net_kernel<4>, g, b, lds, s, x, cin0, L0, P, nops, params, slot, nbuf,
-                                   out_buf, cout_final, Lfinal, y); break;
-        case 8: hipLaunchKernelGGL(fvp::c2c_net_kernel<8>, g, b, lds, s, x, cin0, L0, P, nops, params, slot, nbuf,
-                                   out_buf, cout_final, Lfinal, y); break;
-        default: return FVP_ERR_SHAPE;
-    }
+    if (lg == 4)
+        hipLaunchKernelGGL(fvp::c2c_net_kernel<4>, g, b, lds, s, x, cin0, L0, P, nops, params, slot, nbuf, wchunk,
+                           out_buf, cout_final, Lfinal, y);
+    else
+        hipLaunchKernelGGL(fvp::c2c_net_kernel<8>, g, b, lds, s, x, cin0, L0, P, nops, params, slot, nbuf, wchunk,
+                           out_buf, cout_final, Lfinal, y);
     return (int)hipGetLastError();
 }

@@ -94,9 +94,9 @@ SIGNATURES = {
     "fvp_conv2d_ex_workspace_bytes": [c_int] * 13,
     "fvp_conv2d_geom": [c_int] * 10 + [ctypes.POINTER(c_int)],
     "fvp_maxpool_pad_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "fvp_conv1d_net_lds_bytes": [c_int, c_int],
+    "fvp_conv1d_net_lds_bytes": [c_int, c_int, c_int, c_int],
     "fvp_conv1d_net": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                       c_int, c_void_p, c_void_p],
+                       c_int, c_int, c_void_p, c_void_p],
     "fvp_conv_front7_f32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_front7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_stem7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -116,7 +116,7 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 _LIB = None
 
 

@@ -527,11 +527,14 @@ class Net1D:
     as [cin][k][cout] followed by its folded BN scale and shift.  ``None`` from
     ``build`` when the module has another shape or the buffers exceed LDS."""
 
-    W_CHUNK = 12288  # floats per weight chunk (csrc/fvp_c2c.hip kC2CWChunk)
+    # floats per weight chunk buffer (csrc/fvp_c2c.hip: two buffers, multiples of 4096 up
+    # to 12288): the largest whose LDS total fits -- C5's Z = 64 columns take 8192
+    W_CHUNKS = (12288, 8192, 4096)
 
-    def __init__(self):
+    def __init__(self, wchunk: int = 12288):
         self.ops, self.params, self.off = [], [], 0
         self.free, self.nbuf, self.slot = [], 0, 0
+        self.wchunk = wchunk
 
     def _buf(self, C, L):
         self.slot = max(self.slot, C * (L + 6) + 16)  # rows [3 zeros, L, 3 zeros]; slack for the last row's reads
@@ -585,7 +588,7 @@ class Net1D:
         if cin < C:  # the input's zero rows past its channels (the network input padded to 4)
             w = torch.cat([w, w.new_zeros((C - cin, k, cout))])
             cin = C
-        cic = min(cin, (self.W_CHUNK // (k * cout)) // 4 * 4)  # 4 channels per product step
+        cic = min(cin, (self.wchunk // (k * cout)) // 4 * 4)  # 4 channels per product step
         if cic < 4 or (cic * k * cout) % 4 or ((cin % cic) * k * cout) % 4:
             raise ValueError("weight chunk alignment")
         sc, sh = self._fold(conv, bn)
@@ -620,7 +623,17 @@ class Net1D:
             # reference fails at `x + skip_x2` (cnns_1d.py) and so does the per-layer path
             # (ConvLayer's res_post shape assert) -- the one-launch net must not run it
             return None
-        n = cls()
+        for wchunk in cls.W_CHUNKS:
+            n = cls._build(module, cin0, L0, wchunk)
+            if n is not False:
+                return n
+        return None
+
+    @classmethod
+    def _build(cls, module, cin0: int, L0: int, wchunk: int):
+        """The net with weight chunks of `wchunk` floats; None if the module has another
+        shape, False if its LDS total exceeds the CU's 160 KB at this chunk size."""
+        n = cls(wchunk)
         try:
             cin4 = (cin0 + 3) // 4 * 4
             x = n._buf(cin4, L0)
@@ -660,9 +673,9 @@ class Net1D:
         lg = next((g for g in (4, 8) if all(c * -(-Lo // g) <= 1024 for c, Lo in shapes)), None)
         if lg is None:
             return None
-        lds = _lib.load().fvp_conv1d_net_lds_bytes(n.slot, n.nbuf)
+        lds = _lib.load().fvp_conv1d_net_lds_bytes(n.slot, n.nbuf, n.wchunk, lg)
         if lds > 160 * 1024:
-            return None
+            return False
         dev = module.output_hm.weight.device
         n.prog = torch.tensor(n.ops, dtype=torch.int32, device=dev).contiguous()
         n.param = torch.cat(n.params).contiguous().to(dev)
@@ -675,8 +688,8 @@ class Net1D:
         y = torch.empty((N, self.cout, self.Lout), dtype=torch.float32, device=x.device)
         if N:
             _lib.call("fvp_conv1d_net", _ptr(x), N, self.cin0, self.L0, _ptr(self.prog), len(self.ops),
-                      _ptr(self.param), self.slot, self.nbuf, self.out_buf, self.cout, self.Lout, self.lg, _ptr(y),
-                      _stream(y))
+                      _ptr(self.param), self.slot, self.nbuf, self.wchunk, self.out_buf, self.cout, self.Lout,
+                      self.lg, _ptr(y), _stream(y))
         return y
 
 

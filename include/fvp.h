@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 18
+#define FVP_ABI_VERSION 19
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -433,13 +433,16 @@ int fvp_conv3x3_wino_plan(int N, int H, int W, int Cpo, int *plan);
  * relu, w_off, cic}; params: device fp32, at w_off (% 4 == 0) W [cin][k][cout]
  * then the folded BN scale [cout] and shift [cout]; a conv's weights stream
  * through LDS in chunks of cic input channels (cic * k * cout % 4 == 0,
- * <= 12288 floats).  out = act(scale * sum W x + shift (+ res_pre)) (+ res_post);
+ * <= wchunk floats; wchunk in {4096, 8192, 12288}: two chunk buffers share the
+ * LDS with the activations, so longer columns take smaller chunks).
+ * out = act(scale * sum W x + shift (+ res_pre)) (+ res_post);
  * the input is buffer 0, the output buffer out_buf.  lg in {4, 8}:
  * output positions per thread item, cout * ceil(Lout / lg) <= 1024 for every
  * conv.  fvp/cnn.py Net1D builds the program. */
-size_t fvp_conv1d_net_lds_bytes(int slot, int nbuf);
+size_t fvp_conv1d_net_lds_bytes(int slot, int nbuf, int wchunk, int lg);
 int fvp_conv1d_net(const float *x, int ncols, int cin0, int L0, const int *prog, int nops, const float *params,
-                   int slot, int nbuf, int out_buf, int cout_final, int Lfinal, int lg, float *y, void *stream);
+                   int slot, int nbuf, int wchunk, int out_buf, int cout_final, int Lfinal, int lg, float *y,
+                   void *stream);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
 int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf

@@ -82,10 +82,13 @@ def test_conv_geometry_host():
     assert lib.fvp_conv_front7_f32(1, 1, 17, 64, 64, 1, 1, 1, 1, None) == 1002
     assert lib.fvp_conv_front7_f32(None, 1, 15, 64, 64, 1, 1, 1, 1, None) == 1001
     # the one-launch 1-D net: NULLs, a slot too small for the input, an lg it has no kernel for
-    assert lib.fvp_conv1d_net(None, 80, 15, 20, 1, 25, 1, 1424, 6, 0, 1, 20, 4, 1, None) == 1001
-    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 100, 6, 0, 1, 20, 4, 1, None) == 1002
-    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 0, 1, 20, 3, 1, None) == 1002
-    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 6, 1, 20, 4, 1, None) == 1002
+    assert lib.fvp_conv1d_net(None, 80, 15, 20, 1, 25, 1, 1424, 6, 12288, 0, 1, 20, 4, 1, None) == 1001
+    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 100, 6, 12288, 0, 1, 20, 4, 1, None) == 1002
+    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 12288, 0, 1, 20, 3, 1, None) == 1002
+    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 12288, 6, 1, 20, 4, 1, None) == 1002
+    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 6000, 0, 1, 20, 4, 1, None) == 1002   # chunk % 4096
+    assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 16384, 0, 1, 20, 4, 1, None) == 1002  # > 3 stages
+    assert lib.fvp_conv1d_net_lds_bytes(2832, 6, 8192, 4) == (2 * 8192 + 4096 + 2832 * 6) * 4
     # FVP_CONV_F32_KC (fp32 LDS-DMA kernel): not with bf16 operands, Cpi % 16 only
     conv = lambda cpi, flags: lib.fvp_conv2d_nhwc_ex(1, 1, 8, 8, cpi, 1, 3, 3, 16, 128, 1, 1, None, None, 0,
                                                       0, 1, 1, 1, 1, flags, 0, 1, None, 0, None)

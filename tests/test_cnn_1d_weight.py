@@ -142,7 +142,8 @@ def test_transposed_conv1d_and_pool1d_vs_torch(gpu_device):
 def test_c2c_large_batch_vs_torch(gpu_device, N, L):
     """N columns (80 = 8 frames x K=10) at the C2 / C3 (Z=20), C4 (Z=32) and C5
     (Z=64) column lengths, through the one-launch net (fvp_conv1d_net, the AUTO
-    path) and the per-layer kernels: both against torch's C2CNet."""
+    path; Z = 64 with 8,192-float weight chunks) and the per-layer kernels: both
+    against torch's C2CNet."""
     from fvp import cnn
     from fvp.cnn import FvpCNN
 
@@ -153,8 +154,9 @@ def test_c2c_large_batch_vs_torch(gpu_device, N, L):
         ref = c2c(x)
     net = FvpCNN(c2c)
     y = net(x)
-    if L <= 32:  # (Z = 64 exceeds the one-launch net's LDS: the per-layer kernels run)
-        assert net.net1d[(15, L)] is not None, "the one-launch path was not taken"
+    n1 = net.net1d[(15, L)]
+    assert n1 is not None, "the one-launch path was not taken"
+    assert n1.wchunk == (8192 if L == 64 else 12288)  # (Z = 64: smaller weight chunks make room)
     _close(y.cpu().numpy(), ref.cpu().numpy(), f"C2CNet one launch, {N} columns of {L}")
     per_layer = FvpCNN(c2c, algo=cnn.CONV_PER_TAP)(x)
     _close(per_layer.cpu().numpy(), ref.cpu().numpy(), f"C2CNet per layer, {N} columns of {L}")

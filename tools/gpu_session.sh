@@ -14,6 +14,8 @@
 #   step    tools/step_host.py (host / GPU time per part of the small-batch step; $STEP_ARGS)
 #   overlap tools/overlap_probe2.py for each library in $AB_LIBS
 #   pmcl2   TCC_HIT / TCC_MISS (one counter pass each) of a short bench run per library in $AB_LIBS
+#   c2c     tools/c2c_probe.py at Z = 20 / 32 / 64 (one-launch C2CNet vs per-layer kernels)
+#   pipe5   tools/bench_pipeline.py at C5 (8 frames: the HDN with Z = 64 columns)
 #   nmsp    tools/nms_probe.py (NMS top-K [+ columns] per launch, smooth and plateau maps)
 #   wino    tools/wino_probe.py (Winograd vs direct 3x3 layers)
 #   cnn     tools/bench_cnn.py
@@ -78,6 +80,13 @@ for step in "$@"; do
              done
            done
            python3 tools/pmc_kernels.py $O/pmc_* ;;
+    c2c)   : > $O/c2c.jsonl
+           for L in 20 32 64; do
+             timeout -k 10 120 python3 tools/c2c_probe.py --L $L >> $O/c2c.jsonl 2> $O/c2c.err || fail c2c $O/c2c.err
+           done
+           cat $O/c2c.jsonl ;;
+    pipe5) timeout -k 10 300 python3 tools/bench_pipeline.py --workload c5 --frames 8 --steps 5 > $O/pipeline_c5.jsonl 2> $O/pipeline_c5.err || fail pipe5 $O/pipeline_c5.err
+           cut -c1-400 $O/pipeline_c5.jsonl ;;
     nmsp)  timeout -k 10 300 python3 tools/nms_probe.py > $O/nms_probe.json 2> $O/nms_probe.err || fail nmsp $O/nms_probe.err
            cat $O/nms_probe.json ;;
     wino)  timeout -k 10 300 python3 tools/wino_probe.py > $O/wino.jsonl 2> $O/wino.err || fail wino $O/wino.err

@@ -37,16 +37,32 @@ def run(args):
 
     dev = torch.device("cuda:0")
     J = 15
-    if args.net == "p2p":
-        m, hw = cnn_arch.P2PNet(J, J).eval(), (64, 64)
-    else:
-        m, hw = cnn_arch.CenterNet(J, 1).eval(), (80, 80)
-    m.load_state_dict(synthetic.seeded_state_dict(m, 11))
     algo = {"auto": cnn.CONV_AUTO, "dma": cnn.CONV_DMA, "halo": cnn.CONV_HALO, "pertap": cnn.CONV_PER_TAP,
             "nosplit": cnn.CONV_PER_TAP_NOSPLIT}[args.algo]
-    f = cnn.FvpCNN(m.to(dev), torch.bfloat16 if args.bf16 else torch.float32, algo=algo)
-    x = torch.rand((args.images, J) + hw, device=dev)
-    fwd = (lambda: f(x)) if args.net == "p2p" else (lambda: f.from_xy(x))
+    dt = torch.bfloat16 if args.bf16 else torch.float32
+    if args.net == "backbone":  # PoseResNet-50 on --images views of the Panoptic IMAGE_SIZE (960 x 512)
+        from fvp.backbone import FvpPoseResNet
+
+        m = cnn_arch.PoseResNet(50, J).eval()
+        m.load_state_dict(synthetic.seeded_state_dict(m, 21))
+        f = FvpPoseResNet(m.to(dev), dt)
+        x = torch.randn((args.images, 3, 512, 960), device=dev)
+        fwd = lambda: f.forward_nhwc(x)  # noqa: E731
+    elif args.net == "c2c":  # C2CNet on --images z-columns of 15 x --length
+        m = cnn_arch.C2CNet(J, 1).eval()
+        m.load_state_dict(synthetic.seeded_state_dict(m, 14))
+        f = cnn.FvpCNN(m.to(dev), dt, algo=algo)
+        x = torch.rand((args.images, J, args.length), device=dev)
+        fwd = lambda: f(x)  # noqa: E731
+    else:
+        if args.net == "p2p":
+            m, hw = cnn_arch.P2PNet(J, J).eval(), (64, 64)
+        else:
+            m, hw = cnn_arch.CenterNet(J, 1).eval(), (80, 80)
+        m.load_state_dict(synthetic.seeded_state_dict(m, 11))
+        f = cnn.FvpCNN(m.to(dev), dt, algo=algo)
+        x = torch.rand((args.images, J) + hw, device=dev)
+        fwd = (lambda: f(x)) if args.net == "p2p" else (lambda: f.from_xy(x))
     with torch.no_grad():
         for _ in range(args.iters):
             fwd()
@@ -108,13 +124,29 @@ def pmc(args):
             r["lds_conflict_frac"] = round(r.get("SQ_LDS_BANK_CONFLICT", 0) / r["SQ_LDS_IDX_ACTIVE"], 3)
     for r in rows:
         print(json.dumps(r))
+    # the whole forward: MFMA busy over the GPU-active time of its dispatches (each
+    # dispatch's GRBM_GUI_ACTIVE counts that dispatch), the ratio of MFMA-busy to
+    # SQ-busy cycles as rocprofv3 sums them, and the MFMA work actually issued
+    # (SQ_INSTS_VALU_MFMA_MOPS_F32 in units of 512 FLOPs) against the direct-conv
+    # FLOPs that the TF/s figures of tools/bench_cnn.py count
+    tot = {c: sum(r.get(c, 0.0) for r in rows) for c in
+           ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F32")}
+    out = {"forward": True, "dispatches": len(rows), **{k: v for k, v in tot.items() if v}}
+    if tot["GRBM_GUI_ACTIVE"]:
+        out["mfma_busy"] = round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
+    if tot["SQ_BUSY_CYCLES"]:
+        out["mfma_busy_per_sq_busy"] = round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] / tot["SQ_BUSY_CYCLES"], 4)
+    if tot["SQ_INSTS_VALU_MFMA_MOPS_F32"]:
+        out["mfma_gflop_issued"] = round(tot["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512 / 1e9, 3)
+    print(json.dumps(out))
 
 
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
     r = sub.add_parser("run")
-    r.add_argument("--net", choices=["p2p", "centernet"], default="centernet")
+    r.add_argument("--net", choices=["p2p", "centernet", "c2c", "backbone"], default="centernet")
+    r.add_argument("--length", type=int, default=20, help="c2c: column length Z")
     r.add_argument("--images", type=int, default=8)
     r.add_argument("--bf16", action="store_true")
     r.add_argument("--algo", choices=["auto", "dma", "halo", "pertap", "nosplit"], default="auto")

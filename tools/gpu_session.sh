@@ -16,6 +16,8 @@
 #   pmcl2   TCC_HIT / TCC_MISS (one counter pass each) of a short bench run per library in $AB_LIBS
 #   c2c     tools/c2c_probe.py at Z = 20 / 32 / 64 (one-launch C2CNet vs per-layer kernels)
 #   pipe5   tools/bench_pipeline.py at C5 (8 frames: the HDN with Z = 64 columns)
+#   pipetrace rocprofv3 kernel stats of tools/bench_pipeline.py (heatmaps -> poses, C3 B = 8)
+#   pmcfwd  tools/pmc_forwards.sh (MFMA busy / ops of the shipped CNN forwards)
 #   nmsp    tools/nms_probe.py (NMS top-K [+ columns] per launch, smooth and plateau maps)
 #   wino    tools/wino_probe.py (Winograd vs direct 3x3 layers)
 #   cnn     tools/bench_cnn.py
@@ -87,6 +89,14 @@ for step in "$@"; do
            cat $O/c2c.jsonl ;;
     pipe5) timeout -k 10 300 python3 tools/bench_pipeline.py --workload c5 --frames 8 --steps 5 > $O/pipeline_c5.jsonl 2> $O/pipeline_c5.err || fail pipe5 $O/pipeline_c5.err
            cut -c1-400 $O/pipeline_c5.jsonl ;;
+    pipetrace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pipetrace -o run -- python3 tools/bench_pipeline.py --steps 5 > $O/pipetrace.log 2>&1 || fail pipetrace $O/pipetrace.log
+           python3 -c "
+import csv,sys
+r=list(csv.DictReader(open('$O/pipetrace/run_kernel_stats.csv')))
+r.sort(key=lambda x:-float(x['TotalDurationNs']))
+for x in r[:30]: print(f\"{x['Name'][:80]:80s} {x['Calls']:>6s} {float(x['AverageNs'])/1e3:9.1f} us {float(x['Percentage']):6.2f} %\")
+" | tee $O/pipetrace_top.txt ;;
+    pmcfwd) OUT=$OUT/pmcfwd timeout -k 10 1200 bash tools/pmc_forwards.sh || fail pmcfwd /dev/null ;;
     nmsp)  timeout -k 10 300 python3 tools/nms_probe.py > $O/nms_probe.json 2> $O/nms_probe.err || fail nmsp $O/nms_probe.err
            cat $O/nms_probe.json ;;
     wino)  timeout -k 10 300 python3 tools/wino_probe.py > $O/wino.jsonl 2> $O/wino.err || fail wino $O/wino.err

@@ -1514,6 +1514,54 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw_tiled_kernel(const float *__
     }
 }
 
+// 1x1 convolution of NHWC activations written straight to NCHW:
+// out[n][co][p] = act(scale[co] * sum_ci in[n][p][ci] W[ci][co] + shift[co]).  P2PNet's
+// output layer (cnns_2d.py:185-232, Conv2d(32, J, 1)) feeds soft-argmax and WeightNet in
+// the reference's NCHW layout; the GEMM kernels write NHWC, and the layout pass after
+// them re-read and re-wrote the whole map.  A thread owns one pixel: its CIN4 float4 of
+// input in registers, the weights [co][ci] in LDS (float4 broadcast reads), Cout outputs
+// stored plane by plane (consecutive threads, consecutive pixels: coalesced rows).
+template <int CIN4>
+__global__ __launch_bounds__(256) void conv1x1_nchw_kernel(const float *__restrict__ in, int HW, int Cpi,
+                                                           const float *__restrict__ w, int ldw, int Cout,
+                                                           const float *__restrict__ scale,
+                                                           const float *__restrict__ shift, int relu, long long npix,
+                                                           float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float wl[64 * 4 * CIN4];  // [co][ci]
+    __shared__ float ss[2 * 64];
+    const int tid = threadIdx.x;
+    for (int e = tid; e < Cout * 4 * CIN4; e += 256) {
+        const int co = e / (4 * CIN4), ci = e - co * (4 * CIN4);
+        wl[e] = w[(size_t)ci * ldw + co];
+    }
+    for (int e = tid; e < Cout; e += 256) {
+        ss[e] = scale[e];
+        ss[64 + e] = shift[e];
+    }
+    __syncthreads();
+    const long long pix = (long long)blockIdx.x * 256 + tid;
+    if (pix >= npix) return;
+    f32x4 xv[CIN4];
+    const float *px = in + (size_t)pix * Cpi;
+#pragma unroll
+    for (int q = 0; q < CIN4; ++q) xv[q] = *reinterpret_cast<const f32x4 *>(px + 4 * q);
+    const long long n = pix / HW, p = pix - n * HW;
+    float *o = out + (size_t)n * Cout * HW + p;
+    for (int co = 0; co < Cout; ++co) {
+        const f32x4 *wr = reinterpret_cast<const f32x4 *>(wl + co * 4 * CIN4);
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < CIN4; ++q) {
+            const f32x4 wv = wr[q];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc = __builtin_fmaf(xv[q][k], wv[k], acc);
+        }
+        float v = acc * ss[co] + ss[64 + co];
+        if (relu) v = fmaxf(v, 0.0f);
+        o[(size_t)co * HW] = v;
+    }
+}
+
 }  // namespace fvp
 
 namespace fvp {
@@ -1981,5 +2029,27 @@ extern "C" int fvp_nhwc_to_nchw(const float *in, int N, int C, int H, int W, int
     }
     hipLaunchKernelGGL(fvp::nhwc_to_nchw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, in, out, N, C, HW, Cp);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_conv1x1_nchw(const float *in, int N, int H, int W, int Cpi, int Cin, const float *w, int ldw,
+                                int Cout, const float *scale, const float *shift, int relu, float *out,
+                                void *stream) {
+    if (!in || !w || !scale || !shift || !out) return FVP_ERR_NULL;
+    if (N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cpi < Cin || Cpi % 4 || Cout <= 0 || Cout > 64 || ldw < Cout)
+        return FVP_ERR_SHAPE;
+    // float4s read per pixel: 4, 8 or 16 (<= the pitch); w holds that many rows, zero past Cin
+    const int cin4 = (Cin + 3) / 4, t4 = cin4 <= 4 ? 4 : cin4 <= 8 ? 8 : 16;
+    if (cin4 > 16 || 4 * t4 > Cpi || (reinterpret_cast<uintptr_t>(in) & 15)) return FVP_ERR_SHAPE;
+    const long long npix = (long long)N * H * W;
+    const dim3 g((unsigned)((npix + 255) / 256)), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    auto go = [&](auto c) {
+        hipLaunchKernelGGL(fvp::conv1x1_nchw_kernel<decltype(c)::value>, g, b, 0, st, in, H * W, Cpi, w, ldw, Cout,
+                           scale, shift, relu, npix, out);
+    };
+    if (t4 == 4) go(std::integral_constant<int, 4>{});
+    else if (t4 == 8) go(std::integral_constant<int, 8>{});
+    else go(std::integral_constant<int, 16>{});
     return (int)hipGetLastError();
 }

@@ -114,6 +114,8 @@ SIGNATURES = {
     "fvp_conv3x3_wino_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "fvp_conv1x1_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                         c_int, c_void_p, c_void_p],
 }
 
 ABI_VERSION = 19

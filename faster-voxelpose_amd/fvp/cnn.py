@@ -789,6 +789,30 @@ class FvpCNN:
             x = c(x, relu)
         return x
 
+    def _head_nchw(self, y: Act) -> torch.Tensor:
+        """The output 1x1 conv (cnns_2d.py:209) straight into NCHW (fvp_conv1x1_nchw): no
+        NHWC output and layout pass.  Other heads / dtypes: the GEMM, then to_nchw."""
+        o = self.out
+        if (o.mode != 0 or (o.KH, o.KW) != (1, 1) or y.t.dtype != torch.float32 or o.bf16 or o.Cout > 64
+                or y.Cp != o.Cpi or o.Cpi % 4 or (o.Cin + 3) // 4 > 16):
+            return to_nchw(o(y, relu=False))
+        t4 = 4 if o.Cin <= 16 else 8 if o.Cin <= 32 else 16
+        if 4 * t4 > o.Cpi or o.wpack.shape[1] < 4 * t4:
+            return to_nchw(o(y, relu=False))
+        out = torch.empty((y.N, o.Cout, y.H, y.W), dtype=torch.float32, device=y.t.device)
+        _lib.call("fvp_conv1x1_nchw", _ptr(y.t), y.N, y.H, y.W, y.Cp, o.Cin, _ptr(o.wpack), o.Cpo_w, o.Cout,
+                  _ptr(o.scale), _ptr(o.shift), 0, _ptr(out), _stream(out))
+        return out
+
+    def one_launch_for(self, x: torch.Tensor) -> bool:
+        """True when a C2CNet call on x runs as ONE fvp_conv1d_net launch (Net1D)."""
+        if self.kind != "c2c" or not self.one_launch or x.dim() != 3:
+            return False
+        key = tuple(x.shape[1:])
+        if key not in self.net1d:
+            self.net1d[key] = Net1D.build(self.module, *key)
+        return self.net1d[key] is not None
+
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
         if self.kind == "c2c":  # [N, C, L] as [N, C, 1, L]
@@ -801,7 +825,7 @@ class FvpCNN:
             y = self.out(self.encdec(self.front(to_nhwc(x.unsqueeze(2)))), relu=False)
             return to_nchw(y).squeeze(2)
         if self.kind == "p2p":
-            return to_nchw(self.out(self.encdec(self._front(x)), relu=False))
+            return self._head_nchw(self.encdec(self._front(x)))
         if self.kind == "centernet":
             return self.from_xy(x)
         return to_nchw(self.plan(to_nhwc(x)))
@@ -885,8 +909,8 @@ class GraphedCNN:
 
     def _run(self, method: str, x: torch.Tensor):
         fn = getattr(self.net, method)
-        if torch.cuda.is_current_stream_capturing() or not x.is_cuda:
-            return fn(x)
+        if torch.cuda.is_current_stream_capturing() or not x.is_cuda or self.net.one_launch_for(x):
+            return fn(x)  # (a one-launch net gains nothing from a graph but the copies in and out)
         key = (method, tuple(x.shape), x.dtype, x.device)
         hit = self._graphs.get(key)
         if hit is None and len(self._graphs) >= self.max_shapes:
@@ -911,11 +935,27 @@ class GraphedCNN:
         return self._run("from_xy", xy)
 
 
+def _tensor_sig(module: nn.Module) -> tuple:
+    """(storage, version) of every parameter and buffer of ``module``'s tree.  The walk
+    goes over a cached list of the submodules -- re-listed when a module's children
+    change -- and their parameter / buffer dicts: module.parameters()' generator walk
+    with its name prefixes and memo set cost ~4x more host time per call (C2CNet,
+    P2PNet: 156 tensors in 91 modules), paid on every fused forward."""
+    mods = getattr(module, "_fvp_mods", None)
+    shape = tuple(id(c) for m in mods for c in m._modules.values()) if mods is not None else None
+    if mods is None or shape != getattr(module, "_fvp_mods_shape", None):
+        mods = list(module.modules())
+        object.__setattr__(module, "_fvp_mods", mods)
+        object.__setattr__(module, "_fvp_mods_shape", tuple(id(c) for m in mods for c in m._modules.values()))
+    return tuple((t.data_ptr(), t._version) for m in mods for d in (m._parameters, m._buffers)
+                 for t in d.values() if t is not None)
+
+
 def cached(module: nn.Module, dtype=torch.float32, algo: int | None = None, graphs: bool = False):
     """FvpCNN (or FvpWeightNet) for ``module``, rebuilt whenever its parameters
     or buffers change (storage or in-place version), e.g. after load_state_dict,
     or the precision / kernel choice asked for differs."""
-    sig = (dtype, algo) + tuple((t.data_ptr(), t._version) for t in list(module.parameters()) + list(module.buffers()))
+    sig = (dtype, algo) + _tensor_sig(module)
     hit = getattr(module, "_fvp_cnn", None)
     if hit is None or hit[0] != sig:
         net = FvpWeightNet(module) if hasattr(module, "heatmap_feature_net") else FvpCNN(module, dtype, algo)

@@ -71,23 +71,28 @@ def fused_jln_forward(self, meta, heatmaps, proposal_centers, mask, cameras, res
 
 
 def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_transform, all_fused, all_pose, first):
+    from . import cnn, integration
+
     sub_meta = dict(meta)
     sub_meta["seq"] = [meta["seq"][first]] * heatmaps.shape[0]
+    # the CNN wrappers' staleness checks (host work) before the sync below, while the
+    # GPU still runs the HDN: after it the GPU waits for every host step
+    opts = integration.options_of(self)
+    use = opts.cnn and not self.conv_net.training
+    conv = cnn.cached(self.conv_net, opts.cnn_dtype) if use else self.conv_net
+    wnet = cnn.cached(self.weight_net) if use and not self.weight_net.training else self.weight_net
     idx = mask.nonzero()  # the batch's one host sync; the scatters below index with it (no further syncs)
     planes, offset, _ = self.project_layer.forward_batch(heatmaps, sub_meta, proposal_centers, mask, cameras,
                                                          resize_transform, idx=idx)
     P = planes.shape[0] // 3
     if P == 0:
         return
-    from . import cnn, integration
-
-    opts = integration.options_of(self)
-    use = opts.cnn and not self.conv_net.training
-    conv = cnn.cached(self.conv_net, opts.cnn_dtype) if use else self.conv_net
-    features = torch.stack(torch.chunk(conv(planes), 3), dim=0)                    # [3,P,J,S,S]
+    out = conv(planes)                                                              # [3P,J,S,S]
+    # torch.stack(torch.chunk(out, 3)) of joint_localization_net.py: a view for a contiguous
+    # [3P, ...] tensor (chunk k, row p = row k*P + p), no copy
+    features = out.reshape((3, P) + tuple(out.shape[1:]))                           # [3,P,J,S,S]
     pose, maxprob = ops.soft_argmax(features, self.project_layer.center_grid, offset,
                                     float(self.soft_argmax_layer.beta))
-    wnet = cnn.cached(self.weight_net) if use and not self.weight_net.training else self.weight_net
     weights = wnet(features)                                                        # [3P,J,1]
     fused, confs = ops.fuse_poses(pose, weights, maxprob)
     fi, ki = idx[:, 0], idx[:, 1]  # mask's (frame, proposal) pairs in mask order, as the boolean scatters

@@ -443,6 +443,13 @@ size_t fvp_conv1d_net_lds_bytes(int slot, int nbuf, int wchunk, int lg);
 int fvp_conv1d_net(const float *x, int ncols, int cin0, int L0, const int *prog, int nops, const float *params,
                    int slot, int nbuf, int wchunk, int out_buf, int cout_final, int Lfinal, int lg, float *y,
                    void *stream);
+/* 1x1 convolution of NHWC activations [N][H][W][Cpi] (16-B aligned) written NCHW:
+ * out[n][co][y][x] = act(scale[co] * sum_ci in[n][y][x][ci] w[ci * ldw + co] + shift[co]),
+ * Cout <= 64; 4, 8 or 16 float4s of input are read per pixel (<= Cpi), so w holds
+ * that many rows (zero past Cin; the padded GEMM weights of fvp/cnn.py do).
+ * P2PNet's output layer (lib/models/cnns_2d.py:185-232) without the NHWC -> NCHW pass. */
+int fvp_conv1x1_nchw(const float *in, int N, int H, int W, int Cpi, int Cin, const float *w, int ldw, int Cout,
+                     const float *scale, const float *shift, int relu, float *out, void *stream);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
 int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf

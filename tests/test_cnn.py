@@ -448,3 +448,29 @@ def test_bf16_p2pnet_vs_reference(gpu_device):
     y = FvpCNN(p2p.to(gpu_device), torch.bfloat16)(torch.from_numpy(x_p2p).to(gpu_device))
     err = float(np.abs(y.cpu().numpy() - d["y_p2p"]).max()) / float(np.abs(d["y_p2p"]).max())
     assert err <= 5e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,hw", [(32, 15, (64, 64)), (15, 1, (9, 13)), (50, 64, (5, 7)), (16, 33, (3, 3))])
+def test_head_1x1_writes_nchw_vs_torch(gpu_device, cin, cout, hw):
+    """fvp_conv1x1_nchw (P2PNet's output layer straight into NCHW, FvpCNN._head_nchw)
+    against torch's conv2d of the same weights, and the GEMM + layout-pass path."""
+    import torch.nn as nn
+
+    from fvp import cnn, synthetic
+
+    conv = nn.Conv2d(cin, cout, 1).eval()
+    conv.load_state_dict(synthetic.seeded_state_dict(conv, cin + cout))
+    conv = conv.to(gpu_device)
+    x = torch.rand((3, cin) + hw, generator=torch.Generator().manual_seed(cout)).to(gpu_device)
+    with torch.no_grad():
+        ref = conv(x)
+    layer = cnn.ConvLayer(conv, None)
+    a = cnn.to_nhwc(x, layer.Cpi)
+    f = cnn.FvpCNN.__new__(cnn.FvpCNN)
+    f.out = layer
+    got = f._head_nchw(a)
+    gemm = cnn.to_nchw(layer(a, relu=False))
+    torch.cuda.synchronize()
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"1x1 head {cin}->{cout}")
+    _close(got.cpu().numpy(), gemm.cpu().numpy(), f"1x1 head vs GEMM {cin}->{cout}")

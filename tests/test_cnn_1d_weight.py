@@ -238,3 +238,37 @@ def test_graphed_c2c_equals_eager(gpu_device):
     for got, ref in outs:  # earlier results survive later replays
         assert torch.equal(got, ref)
     assert len(g._graphs) == 2 and g.eager_calls == 1  # (8, 20): the third shape, past max_shapes
+
+
+def test_cached_signature_tracks_every_change():
+    """fvp.cnn.cached rebuilds its wrapper when the module's weights change: the
+    fast walk (_tensor_sig) must see in-place writes, load_state_dict, a
+    reassigned Parameter, a replaced submodule and BatchNorm statistics, and
+    stay equal when nothing changed."""
+    import torch.nn as nn
+
+    import cnn_arch
+    from fvp import synthetic
+    from fvp.cnn import _tensor_sig
+
+    m = cnn_arch.C2CNet(15, 1).eval()
+    s0 = _tensor_sig(m)
+    assert _tensor_sig(m) == s0 and len(s0) == len(list(m.parameters())) + len(list(m.buffers()))
+    with torch.no_grad():
+        m.output_hm.weight.add_(1.0)  # in place: version
+    s1 = _tensor_sig(m)
+    assert s1 != s0
+    m.load_state_dict(synthetic.seeded_state_dict(m, 3))
+    s2 = _tensor_sig(m)
+    assert s2 != s1
+    m.output_hm.weight = nn.Parameter(m.output_hm.weight.detach().clone())  # reassigned: storage
+    s3 = _tensor_sig(m)
+    assert s3 != s2
+    bn = next(x for x in m.modules() if isinstance(x, nn.BatchNorm1d))
+    bn.running_mean.add_(0.5)
+    s4 = _tensor_sig(m)
+    assert s4 != s3
+    m.output_hm = nn.Conv1d(32, 1, 1)  # a replaced submodule: the walk is re-listed
+    s5 = _tensor_sig(m)
+    assert s5 != s4 and len(s5) == len(list(m.parameters())) + len(list(m.buffers()))
+    assert _tensor_sig(m) == s5

@@ -226,8 +226,13 @@ def test_graphed_c2c_equals_eager(gpu_device):
 
     c2c, _, _, _ = _nets()
     c2c = c2c.to(gpu_device)
-    eager = cnn.FvpCNN(c2c)
-    g = cnn.GraphedCNN(cnn.FvpCNN(c2c), max_shapes=2)
+    # the per-layer kernels (a launch-bound chain: what the graphs are for); the one-launch
+    # net (AUTO) runs eagerly inside GraphedCNN -- a graph of one kernel only adds copies
+    eager = cnn.FvpCNN(c2c, algo=cnn.CONV_PER_TAP)
+    g = cnn.GraphedCNN(cnn.FvpCNN(c2c, algo=cnn.CONV_PER_TAP), max_shapes=2)
+    one = cnn.GraphedCNN(cnn.FvpCNN(c2c))
+    x1 = torch.rand((80, 15, 20), generator=torch.Generator().manual_seed(4)).to(gpu_device)
+    assert torch.equal(one(x1), cnn.FvpCNN(c2c)(x1)) and not one._graphs and one.eager_calls == 0
     gen = torch.Generator().manual_seed(3)
     outs = []
     for n, L in ((80, 20), (80, 20), (30, 32), (8, 20), (80, 20), (30, 32)):

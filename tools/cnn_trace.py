@@ -87,7 +87,7 @@ def parse(args):
         cur.append(r)
     if cur:
         iters.append(cur)
-    iters = [it for it in iters if len(it) >= 3]
+    iters = [it for it in iters if len(it) >= args.min_dispatches]
     last = iters[-1]
     busy = [sum(e - s for s, e, _ in it) / 1e3 for it in iters]
     span = [(it[-1][1] - it[0][0]) / 1e3 for it in iters]
@@ -153,6 +153,8 @@ def main():
     r.add_argument("--iters", type=int, default=8)
     p = sub.add_parser("parse")
     p.add_argument("dir")
+    p.add_argument("--min-dispatches", type=int, default=3,
+                   help="groups with fewer dispatches are setup work, not forwards (1 for the one-launch C2CNet)")
     m = sub.add_parser("pmc")
     m.add_argument("dir")
     m.add_argument("--per-forward", type=int, default=37)

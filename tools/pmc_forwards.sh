@@ -8,10 +8,11 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 O=gpurun_out/${OUT:-pmcfwd}; mkdir -p $O
 P="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE"
-for spec in "p2p 240 26" "centernet 8 26" "c2c 80 1" "backbone 40 ${BB_DISPATCHES:-62}"; do
+# (third field: the fewest dispatches a forward has -- trace groups below it are setup work)
+for spec in "p2p 240 10" "centernet 8 10" "c2c 80 1" "backbone 40 10"; do
   set -- $spec; net=$1; n=$2; per=$3
   timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/tr_$net -o run -- python3 tools/cnn_trace.py run --net $net --images $n > $O/tr_$net.log 2>&1 || { echo "trace $net failed"; tail -20 $O/tr_$net.log; exit 1; }
-  python3 tools/cnn_trace.py parse $O/tr_$net > $O/trace_$net.json || exit 1
+  python3 tools/cnn_trace.py parse $O/tr_$net --min-dispatches $per > $O/trace_$net.json || exit 1
   timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/pmc_$net -o run -- python3 tools/cnn_trace.py run --net $net --images $n --iters 3 > $O/pmc_$net.log 2>&1 || { echo "pmc $net failed"; tail -20 $O/pmc_$net.log; exit 1; }
   per=$(python3 -c "import json; print(json.load(open('$O/trace_$net.json'))['dispatches'])")
   python3 tools/cnn_trace.py pmc $O/pmc_$net --per-forward $per > $O/pmc_$net.jsonl || exit 1

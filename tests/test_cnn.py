@@ -474,3 +474,25 @@ def test_head_1x1_writes_nchw_vs_torch(gpu_device, cin, cout, hw):
     torch.cuda.synchronize()
     _close(got.cpu().numpy(), ref.cpu().numpy(), f"1x1 head {cin}->{cout}")
     _close(got.cpu().numpy(), gemm.cpu().numpy(), f"1x1 head vs GEMM {cin}->{cout}")
+
+
+@pytest.mark.gpu
+def test_graphed_centernet_equals_eager(gpu_device):
+    """CenterNet replayed from a hipGraph per batch shape (GraphedCNN.from_xy,
+    FvpOptions.center_graphs): bit-identical to the eager launches, new inputs
+    copied in, both outputs cloned out (not aliased across calls)."""
+    from fvp import cnn
+
+    _, cn, _, _ = _nets()
+    cn = cn.to(gpu_device)
+    eager = cnn.FvpCNN(cn)
+    g = cnn.GraphedCNN(cnn.FvpCNN(cn))
+    gen = torch.Generator().manual_seed(9)
+    outs = []
+    for b in (8, 8, 3, 8):
+        xy = torch.rand((b, 15, 80, 80), generator=gen).to(gpu_device)
+        outs.append((g.from_xy(xy), eager.from_xy(xy)))
+    torch.cuda.synchronize()
+    for (gh, gs), (eh, es) in outs:
+        assert torch.equal(gh, eh) and torch.equal(gs, es)
+    assert len(g._graphs) == 2 and g.eager_calls == 0

@@ -73,10 +73,7 @@ class FvpOptions:
       fast or faster).  Default from the environment variable
       FVP_RECOMPUTE_COLUMNS (0 / 1) when set.
     c2c_graphs: with cnn, the launch-bound 1-D C2CNet replays from a
-      hipGraph per column-batch shape (fvp.cnn.GraphedCNN) when it does not run
-      as one launch (fvp.cnn.Net1D).
-    center_graphs: with cnn, CenterNet (26 launches at a few frames) replays
-      from a hipGraph per batch shape the same way.
+      hipGraph per column-batch shape (fvp.cnn.GraphedCNN).
     share_layout: fused_hdn_forward lays planar fp32 heatmaps out channels-last
       ONCE for the batch (fvp.heatmaps.to_channels_last) and attaches the copy
       to the heatmaps tensor, so its own gather and the JLN's person planes
@@ -89,7 +86,6 @@ class FvpOptions:
     recompute_columns: bool | None = dataclasses.field(default_factory=_env_recompute)
     recompute_cube_bytes: int = 512 << 20
     c2c_graphs: bool = True
-    center_graphs: bool = True
     share_layout: bool = True
 
 
@@ -181,7 +177,7 @@ def center_net_from_xy(center_net, xy: torch.Tensor, opts: FvpOptions = DEFAULT_
     """CenterNet.forward (cnns_2d.py:280-295) minus its first line, fed with
     the xy max-plane the voxelize kernel already produced."""
     if opts.cnn and not center_net.training:
-        return fvp_cnn.cached(center_net, opts.cnn_dtype, graphs=opts.center_graphs).from_xy(xy)
+        return fvp_cnn.cached(center_net, opts.cnn_dtype).from_xy(xy)
     x = center_net.front_layers(xy)
     x = center_net.encoder_decoder(x)
     return center_net.output_hm(x), center_net.output_size(x)

@@ -36,8 +36,6 @@ def main():
     ap.add_argument("--torch-cnn", action="store_true", help="CNNs on torch's convolution instead of fvp")
     ap.add_argument("--bf16", action="store_true", help="fvp CNNs with bf16 operands (opt-in precision)")
     ap.add_argument("--views", action="store_true", help="start from the images: PoseResNet-50 backbone first")
-    ap.add_argument("--center-graphs", choices=["on", "off"], default="on",
-                    help="CenterNet replayed from a hipGraph (FvpOptions.center_graphs)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -97,8 +95,7 @@ def main():
     jl.soft_argmax_layer = jln.SoftArgmaxLayer(AttrDict.wrap({"NETWORK": {"BETA": 100}}))
     for net in (hdn, jl):
         integration.set_options(net, cnn=not args.torch_cnn,
-                                cnn_dtype=torch.bfloat16 if args.bf16 else torch.float32,
-                                center_graphs=args.center_graphs == "on")
+                                cnn_dtype=torch.bfloat16 if args.bf16 else torch.float32)
     backbone = None
     if args.views:
         from fvp.backbone import FvpPoseResNet
@@ -159,7 +156,6 @@ def main():
         "ms_per_batch_repeats": [round(r[0], 3) for r in reps], "frames": B, "proposals_per_frame": K,
         "hdn_ms": round(hdn_ms, 3), "jln_ms": round(jln_ms, 3),
         "cnn": "torch (MIOpen)" if args.torch_cnn else ("fvp bf16 MFMA" if args.bf16 else "fvp fp32 MFMA"),
-        "center_graphs": args.center_graphs == "on" and not args.torch_cnn,
         "config": f"{w.name}: {len(cams[seq])} cams, J={J}, {w.voxels_per_axis} whole grid, 64^3 per person; "
                   "CenterNet/C2CNet/P2PNet/WeightNet reference architectures with seeded weights"}))
 

@@ -73,7 +73,8 @@ class FvpOptions:
       fast or faster).  Default from the environment variable
       FVP_RECOMPUTE_COLUMNS (0 / 1) when set.
     c2c_graphs: with cnn, the launch-bound 1-D C2CNet replays from a
-      hipGraph per column-batch shape (fvp.cnn.GraphedCNN).
+      hipGraph per column-batch shape (fvp.cnn.GraphedCNN) when it does not run
+      as one launch (fvp.cnn.Net1D).
     share_layout: fused_hdn_forward lays planar fp32 heatmaps out channels-last
       ONCE for the batch (fvp.heatmaps.to_channels_last) and attaches the copy
       to the heatmaps tensor, so its own gather and the JLN's person planes

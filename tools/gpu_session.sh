@@ -46,7 +46,8 @@ for step in "$@"; do
     jln)   timeout -k 10 300 python3 tools/bench_jln.py --frames 32 --steps 10 > $O/jln.json 2> $O/jln.err || fail jln $O/jln.err
            cut -c1-300 $O/jln.json ;;
     all)   for wl in c1 c2 c3 c4 c5; do
-             timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 2 --traffic off --cpu-baseline on > $O/all_$wl.json 2> $O/all_$wl.err || fail all_$wl $O/all_$wl.err
+             tr=off; case $wl in c4|c5) tr=auto;; esac  # (C4 / C5: the FETCH / WRITE counters too)
+             timeout -k 10 600 python bench.py --workload $wl --steps 10 --warmup 2 --traffic $tr --cpu-baseline on > $O/all_$wl.json 2> $O/all_$wl.err || fail all_$wl $O/all_$wl.err
              echo "$wl: $(cut -c1-200 $O/all_$wl.json)"
            done
            for wb in c4:32 c5:32; do

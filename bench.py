@@ -270,7 +270,8 @@ def tap_floor_ceiling(n_vox, V, J, H, W, elem, layout_pass, copy_gbs, alg_per_fr
             layout_bytes += V * js * H * W * elem + table
     t_taps = wave_loads * TAP_CYCLES_PER_WAVELOAD / (CUS * CLOCK_HZ)
     t_layout = layout_bytes / (copy_gbs * 1e9) if (layout_pass and copy_gbs) else 0.0
-    t = t_taps + t_layout
+    # (the HBM roof itself bounds the op where the taps are few: C1's one camera)
+    t = max(t_taps + t_layout, alg_per_frame / (HBM_PEAK_GBS * 1e9))
     frac = alg_per_frame / t / (HBM_PEAK_GBS * 1e9)
     return {"frac": round(frac, 4),
             "us_per_frame": round(t * 1e6, 3), "tap_floor_us_per_frame": round(t_taps * 1e6, 3),

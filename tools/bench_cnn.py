@@ -19,11 +19,29 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 MFMA_F32_PEAK_TF = 157.3
 
 
+def _pmc_forward(d, net):
+    """The forward totals tools/pmc_forwards.sh wrote for `net` (pmc_<net>.jsonl, last
+    line) and the image count of that run (trace_<net>.json is the same batch)."""
+    if not d:
+        return None
+    f = os.path.join(d, f"pmc_{net}.jsonl")
+    if not os.path.exists(f):
+        return None
+    tot = json.loads(open(f).read().splitlines()[-1])
+    if "mfma_gflop_issued" not in tot:
+        return None
+    images = {"p2p": 240, "centernet": 8}[net]  # tools/pmc_forwards.sh batch sizes
+    return dict(tot, images=images, file=os.path.relpath(f, REPO))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--proposals", type=int, default=40, help="JLN proposals in the batch (4 frames x 10)")
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--pmc-dir", default=None,
+                    help="tools/pmc_forwards.sh output: add the measured MFMA work issued and MFMA-busy share "
+                         "of the same forwards to the P2PNet / CenterNet lines")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -102,9 +120,20 @@ def main():
                          "fvp_graph_ms": round(t_g, 4), "fvp_graph_tflops": round(fl / (t_g * 1e-3) / 1e12, 2),
                          "fvp_tflops": round(fl / (t_f * 1e-3) / 1e12, 2),
                          "mfma_frac_of_f32_peak": round(fl / (t_f * 1e-3) / 1e12 / MFMA_F32_PEAK_TF, 4),
+                         "flops_counted": "direct convolution (Winograd layers issue fewer: mfma_issued)",
                          "speedup_vs_torch": round(t_t / t_f, 3),
                          "bf16_ms": round(t_b, 4), "bf16_tflops": round(fl / (t_b * 1e-3) / 1e12, 2),
                          "bf16_frac_of_bf16_peak": round(fl / (t_b * 1e-3) / 1e12 / 2500.0, 4)}
+            pmc = _pmc_forward(args.pmc_dir, "p2p" if p2p_line else "centernet")
+            if pmc:  # the measured MFMA work of the same network per image, at this line's time
+                per_img = pmc["mfma_gflop_issued"] / pmc["images"]
+                issued = per_img * int(x.shape[0])
+                out[name]["mfma_issued"] = {
+                    "gflop": round(issued, 3), "tflops": round(issued / (t_f * 1e-3) / 1e3, 2),
+                    "frac_of_f32_peak": round(issued / (t_f * 1e-3) / 1e3 / MFMA_F32_PEAK_TF, 4),
+                    "mfma_busy": pmc["mfma_busy"], "mfma_busy_per_sq_busy": pmc.get("mfma_busy_per_sq_busy"),
+                    "source": f"{pmc['file']} (SQ_INSTS_VALU_MFMA_MOPS_F32 x 512 over {pmc['images']} images; "
+                              "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE))"}
         # C2CNet on the K z-columns of every frame; WeightNet on the 3K joint-feature stacks
         c2c = cnn_arch.C2CNet(J, 1).eval()
         c2c.load_state_dict(synthetic.seeded_state_dict(c2c, 14))

@@ -110,7 +110,7 @@ for l in open(sys.argv[1]):
     d=json.loads(l); print(f\"{d['layer']:24s} direct {d['direct']['us']:8.1f} wino {d['wino']['us']:8.1f} x{d['speedup']:.2f} err {d['wino']['err']:.2e}\")
 " $O/wino_$lib.jsonl
            done ;;
-    cnn)   timeout -k 10 300 python3 tools/bench_cnn.py > $O/cnn.jsonl 2> $O/cnn.err || fail cnn $O/cnn.err
+    cnn)   timeout -k 10 300 python3 tools/bench_cnn.py ${PMCDIR:+--pmc-dir $PMCDIR} $( [ -z "${PMCDIR:-}" ] && [ -d $O/pmcfwd ] && echo --pmc-dir $O/pmcfwd ) > $O/cnn.jsonl 2> $O/cnn.err || fail cnn $O/cnn.err
            cut -c1-400 $O/cnn.jsonl ;;
     cntrace) for nt in centernet:8 p2p:240; do
              net=${nt%%:*}; im=${nt##*:}

@@ -49,7 +49,9 @@ def fused_jln_forward(self, meta, heatmaps, proposal_centers, mask, cameras, res
     all_pose_preds [3,B,K,J,2]); proposal_centers[..., 4] of valid proposals is
     overwritten with the confidences, as in the reference (:180)."""
     if self.training:
-        return self._fvp_original_forward(meta, heatmaps, proposal_centers, mask, cameras, resize_transform)
+        out = self._fvp_original_forward(meta, heatmaps, proposal_centers, mask, cameras, resize_transform)
+        release_shared(heatmaps)
+        return out
     device = heatmaps.device
     B, K = proposal_centers.shape[:2]
     J = heatmaps.shape[2]

@@ -89,6 +89,14 @@ def test_conv_geometry_host():
     assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 6000, 0, 1, 20, 4, 1, None) == 1002   # chunk % 4096
     assert lib.fvp_conv1d_net(1, 80, 15, 20, 1, 25, 1, 1424, 6, 16384, 0, 1, 20, 4, 1, None) == 1002  # > 3 stages
     assert lib.fvp_conv1d_net_lds_bytes(2832, 6, 8192, 4) == (2 * 8192 + 4096 + 2832 * 6) * 4
+    # the 1x1 head writing NCHW: NULLs, Cout > 64, a pitch too small for the float4s read, misalignment
+    head = lambda p, cpi, cin, cout: lib.fvp_conv1x1_nchw(p, 1, 8, 8, cpi, cin, 16, cout, cout, 16, 16, 0, 16, None)
+    assert head(None, 16, 16, 15) == 1001
+    assert head(16, 16, 16, 65) == 1002
+    assert head(16, 16, 20, 15) == 1002   # Cin > pitch
+    assert head(16, 20, 20, 15) == 1002   # 8 float4s per pixel but a 20-float pitch
+    assert head(16, 18, 16, 15) == 1002   # pitch % 4
+    assert head(20, 16, 16, 15) == 1002   # input not 16-B aligned
     # FVP_CONV_F32_KC (fp32 LDS-DMA kernel): not with bf16 operands, Cpi % 16 only
     conv = lambda cpi, flags: lib.fvp_conv2d_nhwc_ex(1, 1, 8, 8, cpi, 1, 3, 3, 16, 128, 1, 1, None, None, 0,
                                                       0, 1, 1, 1, 1, flags, 0, 1, None, 0, None)

@@ -1562,6 +1562,166 @@ __global__ __launch_bounds__(256) void conv1x1_nchw_kernel(const float *__restri
     }
 }
 
+// P2PNet's tail in one launch (cnns_2d.py:178-180, 209): y = ReLU(BN(ConvTranspose2d(k 2, s 2)(x)))
+// + skip, then the 1x1 output conv z = Wh y + b written NCHW.  The two-kernel path writes y
+// (126 MB per 240 planes of 64^2 x 32) and reads it back for the head; here y lives in LDS only.
+// Item = 32 input pixels of one row (-> 2 output rows x 64 pixels); 256 threads; each block walks
+// items blockIdx.x, + gridDim.x, ... with the next item's loads in flight during this one's GEMMs
+// (one item per block, loads then GEMMs, ran the launch at 92 us = the memory time plus the
+// matrix-core time: blocks started together stay in step, profiles/round6/up2_head/):
+//   0. x [32 px][Cpi] and the item's skip [2 rows][64 px][32] -> LDS (16-B loads, branch-free so
+//      all are in flight at once), channels permuted to [s][kq][c4] (c = 16 s + 4 c4 + kq) so
+//      that one ds_read_b128 gives a lane the 4 channels of 4 successive v_mfma_f32_16x16x4f32
+//   1. GEMM [32 px] x [Cpi] x [4 classes x 32 co] on the matrix cores: wave w owns pixel tile
+//      w & 1 and column tiles 4 (w >> 1) .. + 3; the weights' B fragments (wd: [Cpi/16][4 kq]
+//      [128 n][4 c4], n = (2 ry + rx) 32 + co) loaded once per block for the first 4 K steps
+//   2. epilogue: * scale + shift, ReLU, + the staged skip -> y, in place in LDS
+//   3. head GEMM [128 out px] x [32] x [16] (wh: [2][4 kq][16 j][4 c4]), * hscale + hshift
+//   4. z through LDS to rows of 64 contiguous floats per plane
+constexpr int kUpY = 36;    // y LDS pitch (conflict-free b128 reads)
+constexpr int kUpZ = 132;   // z LDS pitch
+__host__ __device__ constexpr int up2_x_pitch(int Cpi) { return Cpi + 4; }
+__host__ __device__ constexpr int up2_lds_floats(int Cpi) { return 32 * up2_x_pitch(Cpi) + 128 * kUpY + 16 * kUpZ; }
+__global__ __launch_bounds__(256) void up2_head_nchw_kernel(const float *__restrict__ in, int N, int H, int W,
+                                                            int Cpi, const float *__restrict__ wd,
+                                                            const float *__restrict__ scale,
+                                                            const float *__restrict__ shift,
+                                                            const float *__restrict__ skip, int Cps, int Cs,
+                                                            const float *__restrict__ wh,
+                                                            const float *__restrict__ hscale,
+                                                            const float *__restrict__ hshift, int J,
+                                                            float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int XP = up2_x_pitch(Cpi);
+    float *const xl = lds, *const yl = lds + 32 * XP, *const zl = yl + 128 * kUpY;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int l16 = lane & 15, cm = lane >> 4;
+    const int segs = W >> 5, items = N * H * segs;
+    const int Ho = 2 * H, Wo = 2 * W;
+    const int nq = Cpi >> 2, nx = 32 * nq;  // nx <= 1024
+    const int mt = wave & 1, nt0 = (wave >> 1) * 4;
+    const int ks = Cpi >> 4;
+    // the block's constants: the first KB K steps' weight fragments (in registers: 80.5 us against
+    // 86-87.5 for loading them per item at 3 blocks per CU), BN and head scales
+    constexpr int KB = 4;
+    f32x4 bw[4][4];
+#pragma unroll
+    for (int s = 0; s < KB; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            bw[s][i] = *reinterpret_cast<const f32x4 *>(
+                wd + (((size_t)min(s, ks - 1) * 4 + cm) * 128 + 16 * (nt0 + i) + l16) * 4);
+    f32x4 hw2[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) hw2[s] = *reinterpret_cast<const f32x4 *>(wh + ((s * 4 + cm) * 16 + l16) * 4);
+    float sc[4], sh[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int co = (16 * (nt0 + i) + l16) & 31;
+        sc[i] = scale[co];
+        sh[i] = shift[co];
+    }
+    const float hs = hscale[min(l16, J - 1)], hb = hshift[min(l16, J - 1)];
+
+    // an item's loads go out one item ahead of its GEMMs (two ahead, in a second register set,
+    // measured no faster: 82.5 vs 80.1 us)
+    auto load = [&](int item, f32x4 (&xv)[4], f32x4 (&sv)[4]) {
+        // every address clamped into the tensors, values selected at the LDS writes
+        const int xs = item % segs, yy = (item / segs) % H, n = item / (segs * H);
+        const float *__restrict__ src = in + (((size_t)n * H + yy) * W + xs * 32) * Cpi;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = min(tid + 256 * u, nx - 1);
+            const int px = e / nq, q = e - px * nq;
+            xv[u] = *reinterpret_cast<const f32x4 *>(src + (size_t)px * Cpi + 4 * q);
+            const int e2 = tid + 256 * u, qo = e2 >> 3, p4 = min(e2 & 7, (Cs - 1) >> 2);  // (a quad that exists)
+            const int oy = 2 * yy + (qo >> 6), ox = 64 * xs + (qo & 63);
+            sv[u] = *reinterpret_cast<const f32x4 *>(skip + (((size_t)n * Ho + oy) * Wo + ox) * Cps + 4 * p4);
+        }
+    };
+    auto body = [&](int item, f32x4 (&xv)[4], f32x4 (&sv)[4]) {
+        // 0. this item's loads -> LDS, then the next item's loads go out
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + 256 * u;
+            if (e < nx) {
+                const int px = e / nq, q = e - px * nq;  // channels 4q + kq = (s = q >> 2, c4 = q & 3, kq)
+                float *d = xl + px * XP + (q >> 2) * 16 + (q & 3);
+#pragma unroll
+                for (int kq = 0; kq < 4; ++kq) d[kq * 4] = xv[u][kq];
+            }
+            const int qo = e >> 3, p4 = e & 7;
+            float *d = yl + qo * kUpY + (p4 >> 2) * 16 + (p4 & 3);
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) d[kq * 4] = 4 * p4 + kq < Cs ? sv[u][kq] : 0.0f;
+        }
+        __syncthreads();  // (B1) x and skip staged; the last item's stores have read z
+        const int xs = item % segs, yy = (item / segs) % H, n = item / (segs * H);
+        if (item + (int)gridDim.x < items) load(item + gridDim.x, xv, sv);
+        // 1. the deconvolution GEMM
+        f32x4 acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto step = [&](int s, const f32x4 (&bv)[4]) {
+            const f32x4 av = *reinterpret_cast<const f32x4 *>(xl + (16 * mt + l16) * XP + s * 16 + cm * 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k], bv[i][k], acc[i], 0, 0, 0);
+        };
+#pragma unroll
+        for (int s = 0; s < KB; ++s)
+            if (s < ks) step(s, bw[s]);
+        for (int s = KB; s < ks; ++s) {
+            f32x4 bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                bv[i] = *reinterpret_cast<const f32x4 *>(wd + (((size_t)s * 4 + cm) * 128 + 16 * (nt0 + i) + l16) * 4);
+            step(s, bv);
+        }
+        // 2. BN, ReLU, + skip -> y[q][co] in place, q = 64 ry + 2 px + rx
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int nn = 16 * (nt0 + i) + l16, cls = nn >> 5, co = nn & 31;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int px = 16 * mt + 4 * cm + r;
+                float *yp = yl + (64 * (cls >> 1) + 2 * px + (cls & 1)) * kUpY + (co >> 4) * 16 + (co & 3) * 4 +
+                            ((co >> 2) & 3);
+                *yp = fmaxf(acc[i][r] * sc[i] + sh[i], 0.0f) + *yp;
+            }
+        }
+        __syncthreads();  // (B2) y complete; x read
+        // 3. the head: wave w owns output-pixel tiles 2w, 2w + 1
+        f32x4 z[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const f32x4 av =
+                    *reinterpret_cast<const f32x4 *>(yl + (16 * (2 * wave + h) + l16) * kUpY + s * 16 + cm * 4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) z[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k], hw2[s][k], z[h], 0, 0, 0);
+            }
+        if (l16 < J) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) zl[l16 * kUpZ + 16 * (2 * wave + h) + 4 * cm + r] = z[h][r] * hs + hb;
+        }
+        __syncthreads();  // (B3) z complete; y read
+        // 4. NCHW rows: plane j, output rows 2yy, 2yy + 1, columns 64 xs .. 64 xs + 63
+        for (int e = tid; e < J * 128; e += 256) {
+            const int j = e >> 7, q = e & 127;
+            out[(((size_t)n * J + j) * Ho + 2 * yy + (q >> 6)) * Wo + 64 * xs + (q & 63)] = zl[j * kUpZ + q];
+        }
+    };
+    f32x4 xv[4], sv[4];
+    if ((int)blockIdx.x < items) load(blockIdx.x, xv, sv);
+    for (int item = blockIdx.x; item < items; item += gridDim.x) body(item, xv, sv);
+}
+
 }  // namespace fvp
 
 namespace fvp {
@@ -2051,5 +2211,31 @@ extern "C" int fvp_conv1x1_nchw(const float *in, int N, int H, int W, int Cpi, i
     if (t4 == 4) go(std::integral_constant<int, 4>{});
     else if (t4 == 8) go(std::integral_constant<int, 8>{});
     else go(std::integral_constant<int, 16>{});
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_up2_head_nchw(const float *in, int N, int H, int W, int Cpi, const float *wd, const float *scale,
+                                 const float *shift, const float *skip, int Cps, int Cs, const float *wh,
+                                 const float *hscale, const float *hshift, int J, float *out, void *stream) {
+    if (!in || !wd || !scale || !shift || !skip || !wh || !hscale || !hshift || !out) return FVP_ERR_NULL;
+    if (N <= 0 || H <= 0 || W <= 0 || W % 32 || Cpi <= 0 || Cpi % 16 || Cpi > 128 || Cs <= 0 || Cs > 32 ||
+        Cps < Cs || Cps % 4 || J <= 0 || J > 16 || (reinterpret_cast<uintptr_t>(in) & 15) ||
+        (reinterpret_cast<uintptr_t>(skip) & 15))
+        return FVP_ERR_SHAPE;
+    const long long items = (long long)N * H * (W / 32);
+    if (items > 0x7fffffffLL || (long long)N * J * 4 * H * W > (1LL << 40)) return FVP_ERR_SHAPE;
+    // the blocks walk the items in turn: as many as are resident at once (VGPRs, LDS)
+    const size_t lds = (size_t)fvp::up2_lds_floats(Cpi) * sizeof(float);
+    int dev = 0, cus = 256, per_cu = 2;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fvp::up2_head_nchw_kernel, 256, lds) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 2;
+    const long long slots = (long long)cus * per_cu;
+    const long long blocks = items < slots ? items : slots;
+    hipLaunchKernelGGL(fvp::up2_head_nchw_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, in, N, H,
+                       W, Cpi, wd, scale, shift, skip, Cps, Cs, wh, hscale, hshift, J, out);
     return (int)hipGetLastError();
 }

@@ -116,9 +116,11 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv1x1_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          c_int, c_void_p, c_void_p],
+    "fvp_up2_head_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                          c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 _LIB = None
 
 

@@ -502,21 +502,28 @@ class _Plan:
             for i, sub in enumerate(p):
                 x = sub(x, res_post if i == len(p) - 1 else None)
             return x
-        if k == "encdec":  # EncoderDecorder.forward (cnns_2d.py:156-180)
-            skip_x1 = p["skip_res1"](x)
-            x = p["encoder_pool1"](x)
-            x = p["encoder_res1"](x)
-            skip_x2 = p["skip_res2"](x)
-            x = p["encoder_pool2"](x)
-            x = p["encoder_res2"](x)
-            x = p["mid_res"](x)
-            x = p["decoder_res2"](x)
-            x = p["decoder_upsample2"](x, res_post=skip_x2)  # x = upsample(x) + skip_x2
-            x = p["decoder_res1"](x)
-            x = p["decoder_upsample1"](x, res_post=skip_x1)  # x = upsample(x) + skip_x1
+        if k == "encdec":
             assert res_post is None
-            return x
+            x, skip_x1 = self.until_last_upsample(x)
+            return p["decoder_upsample1"](x, res_post=skip_x1)  # x = upsample(x) + skip_x1
         raise AssertionError(k)
+
+    def until_last_upsample(self, x: Act) -> tuple:
+        """EncoderDecorder.forward (cnns_2d.py:156-180) up to its last upsample:
+        (decoder_res1's output, skip_x1)."""
+        assert self.kind == "encdec"
+        p = self.parts
+        skip_x1 = p["skip_res1"](x)
+        x = p["encoder_pool1"](x)
+        x = p["encoder_res1"](x)
+        skip_x2 = p["skip_res2"](x)
+        x = p["encoder_pool2"](x)
+        x = p["encoder_res2"](x)
+        x = p["mid_res"](x)
+        x = p["decoder_res2"](x)
+        x = p["decoder_upsample2"](x, res_post=skip_x2)  # x = upsample(x) + skip_x2
+        x = p["decoder_res1"](x)
+        return x, skip_x1
 
 
 class Net1D:
@@ -728,6 +735,7 @@ class FvpCNN:
             self.front = _Plan(module.front_layers, dtype, algo=algo)
             self.encdec = _Plan(module.encoder_decoder, dtype, algo=algo)
             self.out = ConvLayer(module.output_layer, None, dtype, algo=algo)
+            self.tail = self._compile_tail() if dtype == torch.float32 and algo in (None, CONV_AUTO) else None
         else:
             self.kind = "plain"
             self.plan = _Plan(module, dtype, algo=algo)
@@ -767,6 +775,49 @@ class FvpCNN:
             wp = torch.zeros((49, 16, 16), dtype=torch.float32, device=w.device)
             wp[:, :c.Cout, :c.Cin] = w.permute(2, 3, 0, 1).reshape(49, c.Cout, c.Cin)
             self.front7 = ("fvp_conv_front7_f32", wp.contiguous(), c)
+
+    def _compile_tail(self):
+        """P2PNet's decoder_upsample1 (+ skip_x1) and output layer as ONE fvp_up2_head_nchw
+        launch: (wd, deconv ConvLayer, wh) packed as include/fvp.h describes, or None where
+        the layers are not ConvTranspose2d(k 2, s 2) -> <= 32 channels -> 1x1 conv to <= 16."""
+        up = self.encdec.parts["decoder_upsample1"]
+        if up.kind != "seq" or len(up.parts) != 1 or not up.parts[0][1]:
+            return None
+        c = up.parts[0][0]
+        conv = self.module.encoder_decoder.decoder_upsample1.block[0]
+        head = self.module.output_layer
+        if not (isinstance(conv, nn.ConvTranspose2d) and conv.kernel_size == (2, 2) and conv.stride == (2, 2)
+                and conv.padding == (0, 0) and conv.output_padding == (0, 0) and conv.groups == 1
+                and conv.dilation == (1, 1) and conv.out_channels <= 32 and c.Cpi % 16 == 0 and c.Cpi <= 128
+                and isinstance(head, nn.Conv2d) and head.kernel_size == (1, 1) and head.stride == (1, 1)
+                and head.padding == (0, 0) and head.groups == 1 and head.in_channels == conv.out_channels
+                and head.out_channels <= 16 and self.out.Cpo >= head.out_channels):
+            return None
+        w = conv.weight.detach().float()  # [Cin][Cout][2][2]
+        cin, cout = w.shape[:2]
+        wf = torch.zeros((c.Cpi, 4, 32), dtype=torch.float32, device=w.device)  # [ci][2 ry + rx][co]
+        wf[:cin, :, :cout] = w.permute(0, 2, 3, 1).reshape(cin, 4, cout)
+        # ci = 16 s + 4 c4 + kq -> [s][kq][n = class * 32 + co][c4]
+        wd = wf.reshape(c.Cpi // 16, 4, 4, 128).permute(0, 2, 3, 1).contiguous()
+        h = head.weight.detach().float()[:, :, 0, 0]  # [J][Cout]
+        hf = torch.zeros((32, 16), dtype=torch.float32, device=h.device)
+        hf[:cout, :h.shape[0]] = h.t()
+        wh = hf.reshape(2, 4, 4, 16).permute(0, 2, 3, 1).contiguous()  # [s][kq][j][c4]
+        return wd, c, wh, h.shape[0]
+
+    def _tail_nchw(self, x: Act, skip: Act):
+        """decoder_upsample1(x) + skip, then the output layer, NCHW (fvp_up2_head_nchw);
+        None where this input does not fit the kernel."""
+        wd, c, wh, J = self.tail
+        if (x.t.dtype != torch.float32 or skip.t.dtype != torch.float32 or x.Cp != c.Cpi or x.W % 32
+                or not x.t.is_contiguous() or not skip.t.is_contiguous() or skip.C > 32 or skip.C < c.Cout or skip.Cp % 4
+                or tuple(skip.t.shape[:3]) != (x.N, 2 * x.H, 2 * x.W)):
+            return None
+        out = torch.empty((x.N, J, 2 * x.H, 2 * x.W), dtype=torch.float32, device=x.t.device)
+        _lib.call("fvp_up2_head_nchw", _ptr(x.t), x.N, x.H, x.W, x.Cp, _ptr(wd), _ptr(c.scale), _ptr(c.shift),
+                  _ptr(skip.t), skip.Cp, c.Cout, _ptr(wh), _ptr(self.out.scale), _ptr(self.out.shift), J,
+                  _ptr(out), _stream(out))
+        return out
 
     def _front(self, x: torch.Tensor) -> Act:
         """front_layers(x) for NCHW fp32 maps x."""
@@ -825,7 +876,14 @@ class FvpCNN:
             y = self.out(self.encdec(self.front(to_nhwc(x.unsqueeze(2)))), relu=False)
             return to_nchw(y).squeeze(2)
         if self.kind == "p2p":
-            return self._head_nchw(self.encdec(self._front(x)))
+            f = self._front(x)
+            if self.tail is not None:
+                y, skip_x1 = self.encdec.until_last_upsample(f)
+                out = self._tail_nchw(y, skip_x1)
+                if out is not None:
+                    return out
+                return self._head_nchw(self.encdec.parts["decoder_upsample1"](y, res_post=skip_x1))
+            return self._head_nchw(self.encdec(f))
         if self.kind == "centernet":
             return self.from_xy(x)
         return to_nchw(self.plan(to_nhwc(x)))

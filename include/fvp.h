@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 19
+#define FVP_ABI_VERSION 20
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -450,6 +450,19 @@ int fvp_conv1d_net(const float *x, int ncols, int cin0, int L0, const int *prog,
  * P2PNet's output layer (lib/models/cnns_2d.py:185-232) without the NHWC -> NCHW pass. */
 int fvp_conv1x1_nchw(const float *in, int N, int H, int W, int Cpi, int Cin, const float *w, int ldw, int Cout,
                      const float *scale, const float *shift, int relu, float *out, void *stream);
+/* P2PNet's tail in one launch (lib/models/cnns_2d.py:178-180 and 209): the
+ * decoder's last Upsample2DBlock plus its skip and the output 1x1 conv,
+ *   y[n][2y+ry][2x+rx][co] = max(scale[co] * sum_ci in[n][y][x][ci] W[ci][co][ry][rx] + shift[co], 0)
+ *                            + (co < Cs ? skip[n][2y+ry][2x+rx][co] : 0)      (co < 32)
+ *   out[n][j][oy][ox] = hscale[j] * sum_co y[n][oy][ox][co] Wh[j][co] + hshift[j]  (j < J <= 16)
+ * with y never written to memory.  in: NHWC [N][H][W][Cpi] (16-B aligned, Cpi % 16 == 0, <= 128,
+ * W % 32 == 0); skip: NHWC [N][2H][2W][Cps] (16-B aligned, Cps % 4 == 0); wd: [Cpi/16][4][128][4] with
+ * wd[s][kq][(2 ry + rx) 32 + co][c4] = W[16 s + 4 c4 + kq][co][ry][rx] (zero past Cin / Cout);
+ * wh: [2][4][16][4], wh[s][kq][j][c4] = Wh[j][16 s + 4 c4 + kq]; out: NCHW [N][J][2H][2W]
+ * (fvp/cnn.py FvpCNN packs both). */
+int fvp_up2_head_nchw(const float *in, int N, int H, int W, int Cpi, const float *wd, const float *scale,
+                      const float *shift, const float *skip, int Cps, int Cs, const float *wh, const float *hscale,
+                      const float *hshift, int J, float *out, void *stream);
 /* Output size of a geometry (host only): out_hw = {Ho, Wo}; FVP_ERR_SHAPE if invalid. */
 int fvp_conv2d_geom(int H, int W, int Cpi, int KH, int KW, int mode, int sy, int sx, int py, int px, int *out_hw);
 /* MaxPool2d(K, S, P) of NHWC activations (C % 4 == 0) with implicit -inf

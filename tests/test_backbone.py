@@ -97,6 +97,17 @@ def test_conv_geometry_host():
     assert head(16, 20, 20, 15) == 1002   # 8 float4s per pixel but a 20-float pitch
     assert head(16, 18, 16, 15) == 1002   # pitch % 4
     assert head(20, 16, 16, 15) == 1002   # input not 16-B aligned
+    # P2PNet's fused tail: NULLs, W % 32, Cpi % 16 / > 128, skip channels, J > 16
+    tail = lambda p, w, cpi, cps, cs, j: lib.fvp_up2_head_nchw(p, 1, 4, w, cpi, 16, 16, 16, 16, cps, cs, 16, 16, 16,
+                                                               j, 16, None)
+    assert tail(None, 32, 64, 32, 32, 15) == 1001
+    assert tail(16, 48, 64, 32, 32, 15) == 1002
+    assert tail(16, 32, 40, 32, 32, 15) == 1002
+    assert tail(16, 32, 144, 32, 32, 15) == 1002
+    assert tail(16, 32, 64, 16, 32, 15) == 1002   # skip pitch < its channels
+    assert tail(16, 32, 64, 64, 33, 15) == 1002   # > 32 upsampled channels
+    assert tail(16, 32, 64, 32, 32, 17) == 1002
+    assert tail(20, 32, 64, 32, 32, 15) == 1002   # input not 16-B aligned
     # FVP_CONV_F32_KC (fp32 LDS-DMA kernel): not with bf16 operands, Cpi % 16 only
     conv = lambda cpi, flags: lib.fvp_conv2d_nhwc_ex(1, 1, 8, 8, cpi, 1, 3, 3, 16, 128, 1, 1, None, None, 0,
                                                       0, 1, 1, 1, 1, flags, 0, 1, None, 0, None)

@@ -496,3 +496,49 @@ def test_graphed_centernet_equals_eager(gpu_device):
     for (gh, gs), (eh, es) in outs:
         assert torch.equal(gh, eh) and torch.equal(gs, es)
     assert len(g._graphs) == 2 and g.eager_calls == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,cin,cout,h,w,j", [(3, 64, 32, 32, 32, 15), (2, 48, 20, 3, 64, 16), (1, 128, 32, 2, 32, 1)])
+def test_p2p_tail_one_launch_vs_torch(gpu_device, n, cin, cout, h, w, j):
+    """fvp_up2_head_nchw (FvpCNN._tail_nchw): P2PNet's last Upsample2DBlock + skip_x1 +
+    output layer in one launch, against torch's modules of the same weights, and
+    against the two-launch path (the deconvolution GEMM, then fvp_conv1x1_nchw)."""
+    import types
+
+    import torch.nn as nn
+
+    import cnn_arch
+    from fvp import cnn, synthetic
+
+    up = cnn_arch.Upsample2DBlock(cin, cout, 2, 2).eval()
+    head = nn.Conv2d(cout, j, 1).eval()
+    for m, seed in ((up, cin), (head, j)):
+        m.load_state_dict(synthetic.seeded_state_dict(m, seed))
+    with torch.no_grad():  # non-trivial BN statistics
+        bn = up.block[1]
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+    up, head = up.to(gpu_device), head.to(gpu_device)
+    g = torch.Generator().manual_seed(n * 7 + cin)
+    x = (torch.rand((n, cin, h, w), generator=g) - 0.3).to(gpu_device)
+    skip = torch.rand((n, cout, 2 * h, 2 * w), generator=g).to(gpu_device)
+    with torch.no_grad():
+        ref = head(up(x) + skip)
+    f = cnn.FvpCNN.__new__(cnn.FvpCNN)
+    f.module = types.SimpleNamespace(encoder_decoder=types.SimpleNamespace(decoder_upsample1=up), output_layer=head)
+    f.encdec = types.SimpleNamespace(parts={"decoder_upsample1": cnn._Plan(up)})
+    f.out = cnn.ConvLayer(head, None)
+    f.tail = f._compile_tail()
+    assert f.tail is not None
+    c = f.tail[1]
+    xa, sa = cnn.to_nhwc(x, c.Cpi), cnn.to_nhwc(skip, 32)
+    got = f._tail_nchw(xa, sa)
+    assert got is not None and got.shape == (n, j, 2 * h, 2 * w)
+    two = f._head_nchw(f.encdec.parts["decoder_upsample1"](xa, res_post=sa))
+    torch.cuda.synchronize()
+    _close(got.cpu().numpy(), ref.cpu().numpy(), f"up2 + head {cin}->{cout}->{j}")
+    _close(got.cpu().numpy(), two.cpu().numpy(), f"up2 + head vs two launches {cin}->{cout}->{j}")
+    # the whole P2PNet takes this path (64^2 planes: 32-pixel rows into the last upsample)
+    p2p = cnn_arch.P2PNet(15, 15).eval().to(gpu_device)
+    assert cnn.FvpCNN(p2p).tail is not None

@@ -825,9 +825,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
     // kOOB, which the range check turns into zeros.  Per row, the input offset
     // of tap (0, 0) and a bit mask of the taps inside the image are decoded
     // once (quotients by a float reciprocal + one correction: M < 2^24).
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(a.in, (unsigned)((size_t)a.N * a.H * a.W * a.Cpi * ES));
-    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(reinterpret_cast<const char *>(wb) + (size_t)g * a.Cpo_w * Ktot * ES,
-                                                   (unsigned)((size_t)a.Cpo_w * Ktot * ES));
+    const u32x4 ra = uniform_rsrc4(a.in, (unsigned)((size_t)a.N * a.H * a.W * a.Cpi * ES));
+    const u32x4 rb = uniform_rsrc4(reinterpret_cast<const char *>(wb) + (size_t)g * a.Cpo_w * Ktot * ES,
+                                   (unsigned)((size_t)a.Cpo_w * Ktot * ES));
     const int HWm = a.Hm * a.Wm;
     const float inv_hw = 1.0f / (float)HWm, inv_w = 1.0f / (float)a.Wm;
     auto qdiv = [](int n, int d, float inv) {
@@ -861,18 +861,19 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_dma_kernel(ConvArgs a, const 
         const int r = (wave * NBI + i) * RPI + lane / SPR;
         vob[i] = (n0 + r) * (int)Ktot * ES + (slot ^ swz(r)) * 16;
     }
-    typedef __attribute__((address_space(3))) void *lds_ptr;
+    typedef __attribute__((address_space(3))) char *lds_cp;
+    const unsigned lds0 = (unsigned)(size_t)(lds_cp)lds;  // the stage buffers' LDS byte address
     auto issue = [&](int ks, int tap, int d, int buf) {
-        char *sa = lds + buf * STAGE;
+        const unsigned sa = lds0 + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < NAI; ++i) {
             const unsigned vo = (tmask[i] >> tap) & 1u ? (unsigned)(voa[i] + d) : kOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(sa + (wave * NAI + i) * 1024), 16, vo, 0, 0, 0);
+            lds_dma16(ra, __builtin_amdgcn_readfirstlane(sa + (wave * NAI + i) * 1024), vo);
         }
 #pragma unroll
         for (int i = 0; i < NBI; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(sa + ABYTES + (wave * NBI + i) * 1024), 16,
-                                                     (unsigned)(vob[i] + ks * RB), 0, 0, 0);
+            lds_dma16(rb, __builtin_amdgcn_readfirstlane(sa + ABYTES + (wave * NBI + i) * 1024),
+                      (unsigned)(vob[i] + ks * RB));
     };
     f32x16 acc[TM][TN];
 #pragma unroll

@@ -23,6 +23,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *base,
     return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// The same descriptor as four SGPR words, for the inline-asm LDS-DMA below.
+__device__ __forceinline__ u32x4 uniform_rsrc4(const void *base, unsigned bytes) {
+    const unsigned long long p = (unsigned long long)base;
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((unsigned)p);
+    r.y = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32)) & 0xffffu;  // stride 0
+    r.z = __builtin_amdgcn_readfirstlane(bytes);
+    r.w = 0x00020000u;
+    return r;
+}
+
+// One 16-B piece per lane of a global -> LDS copy (buffer_load_dwordx4 ... lds) into the wave's
+// 1-KiB run at LDS byte address lds_base (M0; wave-uniform).  Inline asm rather than
+// __builtin_amdgcn_raw_ptr_buffer_load_lds: the compiler then does not track the copy as an LDS
+// write, so it puts no s_waitcnt vmcnt(0) before the LDS reads of the OTHER stage buffer (with
+// the builtin it drained the next stage's copies before every step's reads: a double buffer
+// with no overlap).  The caller orders it with counted vmcnt waits and barriers.
+__device__ __forceinline__ void lds_dma16(u32x4 rsrc, unsigned lds_base, unsigned voffset) {
+    asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voffset), "s"(rsrc), "{m0}"(lds_base) : "memory");
+}
+
 // -- layout pass ----------------------------------------------------------------
 // thread = (pixel, joint quad q): reads joints 4q..4q+3 of one pixel (the lanes
 // of a wave cover 64/LPV consecutive pixels -> coalesced plane reads), writes

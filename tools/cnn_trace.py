@@ -135,7 +135,10 @@ def pmc(args):
     if tot["GRBM_GUI_ACTIVE"]:
         out["mfma_busy"] = round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
     if tot["SQ_BUSY_CYCLES"]:
-        out["mfma_busy_per_sq_busy"] = round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] / tot["SQ_BUSY_CYCLES"], 4)
+        # SQ_BUSY_CYCLES counts per shader engine (32 on MI355X: 8 XCDs x 4), SQ_VALU_MFMA_BUSY_CYCLES
+        # per SIMD (rocprofv3 --list-avail): the MFMA-busy share of the SIMD cycles in which the
+        # engines had waves is the ratio over the 32 SIMDs of an engine
+        out["mfma_busy_per_sq_busy"] = round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot["SQ_BUSY_CYCLES"] * 32), 4)
     if tot["SQ_INSTS_VALU_MFMA_MOPS_F32"]:
         out["mfma_gflop_issued"] = round(tot["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512 / 1e9, 3)
     print(json.dumps(out))

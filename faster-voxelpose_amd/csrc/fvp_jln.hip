@@ -263,6 +263,66 @@ __global__ __launch_bounds__(256) void weight_net_kernel(const float *__restrict
     if (threadIdx.x == 0) out[blockIdx.x] = 1.0f / (1.0f + expf(-(part + b2[0])));
 }
 
+// torch.nonzero of a [rows][cols] bool mask in one launch (the JLN's one host sync reads `count`):
+// idx[i] = (row, col) of the i-th true entry in row-major order, as nonzero returns them.  One
+// 1,024-thread block: per 1,024-entry tile a wave-ballot prefix, the waves' totals in LDS, and a
+// running base (rocprim's nonzero took 6 launches and a fill for the same, ~30 us at C3 B = 8).
+__global__ __launch_bounds__(1024) void mask_nonzero_kernel(const unsigned char *__restrict__ mask, int n, int cols,
+                                                            long long *__restrict__ idx, int *__restrict__ count) {
+    __shared__ int wtot[16];
+    __shared__ int base_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) base_s = 0;
+    __syncthreads();
+    for (int t0 = 0; t0 < n; t0 += 1024) {
+        const int e = t0 + tid;
+        const bool on = e < n && mask[e] != 0;
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(on);
+        const int before = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        if (lane == 0) wtot[wave] = (int)__builtin_popcountll(bal);
+        __syncthreads();
+        int off = base_s;
+        for (int w = 0; w < wave; ++w) off += wtot[w];
+        if (on) {
+            idx[2 * (size_t)(off + before)] = e / cols;
+            idx[2 * (size_t)(off + before) + 1] = e % cols;
+        }
+        __syncthreads();  // every wave has read base_s and wtot
+        if (tid == 0) {
+            int tot = 0;
+            for (int w = 0; w < 16; ++w) tot += wtot[w];
+            base_s += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *count = base_s;
+}
+
+// The JLN's three boolean scatters (joint_localization_net.py:176-180) in one launch:
+// all_fused[b,k] = fused[p], all_pose[:, b, k] = pose[:, p], centers[b, k, conf_col] = confs[p]
+// for the P (b, k) pairs of idx; thread = (p, joint).
+__global__ __launch_bounds__(256) void scatter_poses_kernel(const long long *__restrict__ idx, int P, int B, int K,
+                                                            int J, const float *__restrict__ fused,
+                                                            const float *__restrict__ pose,
+                                                            const float *__restrict__ confs,
+                                                            float *__restrict__ all_fused, float *__restrict__ all_pose,
+                                                            float *__restrict__ centers, long long cs0, long long cs1,
+                                                            int conf_col) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= (long long)P * J) return;
+    const int p = (int)(gid / J), j = (int)(gid - (long long)p * J);
+    const long long b = idx[2 * p], k = idx[2 * p + 1];
+    const size_t bkj = ((size_t)b * K + k) * J + j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) all_fused[bkj * 3 + c] = fused[((size_t)p * J + j) * 3 + c];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            all_pose[(((size_t)pl * B * K) * J + bkj) * 2 + c] = pose[((((size_t)pl * P) + p) * J + j) * 2 + c];
+    if (j == 0 && centers) centers[b * cs0 + k * cs1 + conf_col] = confs[p];
+}
+
 }  // namespace fvp
 
 extern "C" int fvp_soft_argmax(const float *features, int P, int J, int S2, const float *center_grid,
@@ -311,5 +371,26 @@ extern "C" int fvp_weight_net(const float *features, int Nimg, int H, int W, con
     else
         hipLaunchKernelGGL(fvp::weight_net_kernel<64>, dim3((unsigned)Nimg), dim3(256), lds, st, features, H, W,
                            conv_w, scale, shift, C, fc1_w, fc1_b, Hd, fc2_w, fc2_b, out);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_mask_nonzero(const unsigned char *mask, int rows, int cols, long long *idx, int *count,
+                                void *stream) {
+    if (!mask || !idx || !count) return FVP_ERR_NULL;
+    if (rows < 0 || cols <= 0 || (long long)rows * cols > (1LL << 24)) return FVP_ERR_SHAPE;
+    hipLaunchKernelGGL(fvp::mask_nonzero_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mask, rows * cols, cols,
+                       idx, count);
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_scatter_poses(const long long *idx, int P, int B, int K, int J, const float *fused,
+                                 const float *pose, const float *confs, float *all_fused, float *all_pose,
+                                 float *centers, long long cs0, long long cs1, int conf_col, void *stream) {
+    if (P == 0) return FVP_OK;
+    if (!idx || !fused || !pose || !all_fused || !all_pose || (centers && !confs)) return FVP_ERR_NULL;
+    if (P < 0 || B <= 0 || K <= 0 || J <= 0 || P > B * K) return FVP_ERR_SHAPE;
+    const long long n = (long long)P * J;
+    hipLaunchKernelGGL(fvp::scatter_poses_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       idx, P, B, K, J, fused, pose, confs, all_fused, all_pose, centers, cs0, cs1, conf_col);
     return (int)hipGetLastError();
 }

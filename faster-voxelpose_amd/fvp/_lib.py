@@ -116,11 +116,14 @@ SIGNATURES = {
     "fvp_nhwc_to_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_conv1x1_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          c_int, c_void_p, c_void_p],
+    "fvp_mask_nonzero": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "fvp_scatter_poses": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p, ctypes.c_longlong, ctypes.c_longlong, c_int, c_void_p],
     "fvp_up2_head_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                           c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 _LIB = None
 
 

@@ -83,7 +83,8 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
     use = opts.cnn and not self.conv_net.training
     conv = cnn.cached(self.conv_net, opts.cnn_dtype) if use else self.conv_net
     wnet = cnn.cached(self.weight_net) if use and not self.weight_net.training else self.weight_net
-    idx = mask.nonzero()  # the batch's one host sync; the scatters below index with it (no further syncs)
+    # mask.nonzero() in one launch: the batch's one host sync; the scatters below index with it
+    idx = ops.mask_nonzero(mask) if mask.is_cuda and mask.dim() == 2 and mask.dtype == torch.bool else mask.nonzero()
     planes, offset, _ = self.project_layer.forward_batch(heatmaps, sub_meta, proposal_centers, mask, cameras,
                                                          resize_transform, idx=idx)
     P = planes.shape[0] // 3
@@ -97,7 +98,13 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
                                     float(self.soft_argmax_layer.beta))
     weights = wnet(features)                                                        # [3P,J,1]
     fused, confs = ops.fuse_poses(pose, weights, maxprob)
-    fi, ki = idx[:, 0], idx[:, 1]  # mask's (frame, proposal) pairs in mask order, as the boolean scatters
-    all_fused[fi, ki] = fused
-    all_pose[:, fi, ki] = pose
-    proposal_centers[fi, ki, 4] = confs
+    # mask's (frame, proposal) pairs in mask order, as the boolean scatters: one launch
+    # (all_fused[fi, ki] = fused; all_pose[:, fi, ki] = pose; proposal_centers[fi, ki, 4] = confs)
+    if (proposal_centers.dtype == torch.float32 and proposal_centers.stride(2) == 1 and all_fused.is_contiguous()
+            and all_pose.is_contiguous()):
+        ops.scatter_poses(idx, fused, pose, confs, all_fused, all_pose, proposal_centers, 4)
+    else:
+        fi, ki = idx[:, 0], idx[:, 1]
+        all_fused[fi, ki] = fused
+        all_pose[:, fi, ki] = pose
+        proposal_centers[fi, ki, 4] = confs

@@ -733,6 +733,41 @@ def _(pose, weights, maxprob):
     return pose.new_empty((P, J, 3)), pose.new_empty((P,))
 
 
+def mask_nonzero(mask: torch.Tensor) -> torch.Tensor:
+    """``mask.nonzero()`` of a 2-D bool mask on the device in one launch (fvp_mask_nonzero): the
+    [count, 2] int64 (row, col) pairs in row-major order.  Reading the count is the one host
+    sync, as in torch.nonzero.  Eager only (the count sizes the result)."""
+    if mask.dim() != 2 or mask.dtype != torch.bool or mask.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: mask_nonzero takes a 2-D bool device tensor, got {tuple(mask.shape)} {mask.dtype}")
+    m = mask.contiguous()
+    rows, cols = m.shape
+    idx = torch.empty((rows * cols, 2), dtype=torch.int64, device=m.device)
+    count = torch.empty((1,), dtype=torch.int32, device=m.device)
+    if rows * cols == 0:
+        return idx
+    _lib.call("fvp_mask_nonzero", _ptr(m), rows, cols, _ptr(idx), _ptr(count), _stream(m))
+    return idx[:int(count.item())]
+
+
+def scatter_poses(idx: torch.Tensor, fused: torch.Tensor, pose: torch.Tensor, confs: torch.Tensor,
+                  all_fused: torch.Tensor, all_pose: torch.Tensor, centers: torch.Tensor, conf_col: int = 4) -> None:
+    """The JLN's result scatters in one launch (fvp_scatter_poses): all_fused[b, k] = fused,
+    all_pose[:, b, k] = pose, centers[b, k, conf_col] = confs for (b, k) = idx rows."""
+    P = idx.shape[0]
+    if P == 0:
+        return
+    B, K, J = all_fused.shape[:3]
+    for t, shape in ((fused, (P, J, 3)), (pose, (3, P, J, 2)), (confs, (P,)), (all_pose, (3, B, K, J, 2))):
+        if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous():
+            raise _lib.FvpError(f"fvp: scatter_poses operand {tuple(t.shape)} {t.dtype} != {shape} float32")
+    if (not all_fused.is_contiguous() or centers.dtype != torch.float32 or centers.dim() != 3
+            or centers.stride(2) != 1 or idx.dtype != torch.int64 or idx.dim() != 2 or idx.shape[1] != 2):
+        raise _lib.FvpError("fvp: scatter_poses layouts")
+    idx = idx.contiguous()  # (torch.nonzero's result is a transposed view on the device)
+    _lib.call("fvp_scatter_poses", _ptr(idx), P, B, K, J, _ptr(fused), _ptr(pose), _ptr(confs), _ptr(all_fused),
+              _ptr(all_pose), _ptr(centers), centers.stride(0), centers.stride(1), conf_col, _stream(all_fused))
+
+
 def nms_topk_columns_joint(prob: torch.Tensor, K: int, cube: torch.Tensor):
     """nms_topk_columns with vals / flat in one buffer (proposal_buffers), so
     fvp.parallel.gather_proposals sends them as they are -- eager only: a

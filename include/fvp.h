@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 20
+#define FVP_ABI_VERSION 21
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -299,6 +299,18 @@ int fvp_soft_argmax(const float *features, int P, int J, int S2, const float *ce
  *   weights device [3P][J] (WeightNet output);  fused [P][J][3], confs [P] (either may be NULL) */
 int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob, int P, int J,
                    float *fused, float *confs, void *stream);
+/* torch.nonzero of a [rows][cols] bool mask (uint8, contiguous), one launch:
+ * idx [rows*cols][2] int64 receives the (row, col) of the true entries in
+ * row-major order (the first *count rows are written), count device int
+ * (joint_localization_net.py:136-137's boolean selections as indices). */
+int fvp_mask_nonzero(const unsigned char *mask, int rows, int cols, long long *idx, int *count, void *stream);
+/* The JLN's result scatters (joint_localization_net.py:176-180) in one launch:
+ * for p < P with (b, k) = idx[p]: all_fused [B][K][J][3] <- fused [P][J][3],
+ * all_pose [3][B][K][J][2] <- pose [3][P][J][2], and (centers non-NULL)
+ * centers[b * cs0 + k * cs1 + conf_col] <- confs[p]. */
+int fvp_scatter_poses(const long long *idx, int P, int B, int K, int J, const float *fused, const float *pose,
+                      const float *confs, float *all_fused, float *all_pose, float *centers, long long cs0,
+                      long long cs1, int conf_col, void *stream);
 
 /* Dense 2-D convolution on the fp32 matrix cores (v_mfma_f32_32x32x2_f32),
  * implicit GEMM over NHWC activations, for the HDN / JLN CNNs

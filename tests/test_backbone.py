@@ -97,6 +97,13 @@ def test_conv_geometry_host():
     assert head(16, 20, 20, 15) == 1002   # 8 float4s per pixel but a 20-float pitch
     assert head(16, 18, 16, 15) == 1002   # pitch % 4
     assert head(20, 16, 16, 15) == 1002   # input not 16-B aligned
+    # the JLN's nonzero / scatters: NULLs and sizes before any launch
+    assert lib.fvp_mask_nonzero(None, 2, 2, 16, 16, None) == 1001
+    assert lib.fvp_mask_nonzero(16, 2, 0, 16, 16, None) == 1002
+    assert lib.fvp_mask_nonzero(16, 1 << 13, 1 << 12, 16, 16, None) == 1002
+    assert lib.fvp_scatter_poses(None, 0, 1, 1, 1, None, None, None, None, None, None, 7, 7, 4, None) == 0  # P = 0
+    assert lib.fvp_scatter_poses(16, 3, 1, 2, 15, 16, 16, 16, 16, 16, None, 7, 7, 4, None) == 1002          # P > B K
+    assert lib.fvp_scatter_poses(16, 1, 1, 2, 15, 16, 16, None, 16, 16, 16, 14, 7, 4, None) == 1001         # confs
     # P2PNet's fused tail: NULLs, W % 32, Cpi % 16 / > 128, skip channels, J > 16
     tail = lambda p, w, cpi, cps, cs, j: lib.fvp_up2_head_nchw(p, 1, 4, w, cpi, 16, 16, 16, 16, cps, cs, 16, 16, 16,
                                                                j, 16, None)

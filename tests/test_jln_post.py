@@ -86,3 +86,44 @@ def test_empty_batch_is_a_no_op(gpu_device):
     pose, maxprob = ops.soft_argmax(f, grid, None, 100.0)
     fused, confs = ops.fuse_poses(pose, torch.zeros((0, 15, 1), device=gpu_device), maxprob)
     assert pose.shape == (3, 0, 15, 2) and fused.shape == (0, 15, 3) and confs.shape == (0,)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,cols,p", [(8, 10, 0.5), (1, 1, 1.0), (3, 7, 0.0), (32, 10, 1.0), (40, 97, 0.3),
+                                         (1, 3000, 0.01)])
+def test_mask_nonzero_matches_torch(gpu_device, rows, cols, p):
+    """fvp_mask_nonzero (the JLN's one sync): exactly torch.nonzero's (row, col) pairs, in
+    its row-major order, over one and several 1,024-entry tiles, empty and full masks."""
+    from fvp import ops
+
+    g = torch.Generator().manual_seed(rows * cols)
+    mask = (torch.rand((rows, cols), generator=g) < p).to(gpu_device)
+    got = ops.mask_nonzero(mask)
+    assert torch.equal(got, mask.nonzero())
+    assert torch.equal(ops.mask_nonzero(mask.t()), mask.t().nonzero())  # a non-contiguous view
+
+
+@pytest.mark.gpu
+def test_scatter_poses_matches_index_put(gpu_device):
+    """fvp_scatter_poses: the three boolean scatters of joint_localization_net.py:176-180
+    (all_fused, all_pose, the confidence column of proposal_centers) bit for bit."""
+    from fvp import ops
+
+    B, K, J = 4, 10, 15
+    g = torch.Generator().manual_seed(5)
+    mask = (torch.rand((B, K), generator=g) < 0.6).to(gpu_device)
+    idx = mask.nonzero()
+    P = idx.shape[0]
+    fused = torch.randn((P, J, 3), generator=g).to(gpu_device)
+    pose = torch.randn((3, P, J, 2), generator=g).to(gpu_device)
+    confs = torch.rand((P,), generator=g).to(gpu_device)
+    centers = torch.randn((B, K, 7), generator=g).to(gpu_device)
+    af, ap, ce = torch.zeros((B, K, J, 3), device=gpu_device), torch.zeros((3, B, K, J, 2), device=gpu_device), \
+        centers.clone()
+    ops.scatter_poses(idx, fused, pose, confs, af, ap, ce, 4)
+    rf, rp, rc = torch.zeros_like(af), torch.zeros_like(ap), centers.clone()
+    rf[mask] = fused
+    rp[:, mask] = pose
+    rc[mask, 4] = confs
+    torch.cuda.synchronize()
+    assert torch.equal(af, rf) and torch.equal(ap, rp) and torch.equal(ce, rc)

@@ -267,8 +267,13 @@ __global__ __launch_bounds__(256) void weight_net_kernel(const float *__restrict
 // idx[i] = (row, col) of the i-th true entry in row-major order, as nonzero returns them.  One
 // 1,024-thread block: per 1,024-entry tile a wave-ballot prefix, the waves' totals in LDS, and a
 // running base (rocprim's nonzero took 6 launches and a fill for the same, ~30 us at C3 B = 8).
+// Optionally (the JLN's selection, so that nothing but views remains after the sync): frame_of[i] =
+// row (int32) and rowdst[i][0..width) = rowsrc[row * rs0 + col * rs1 + 0..width).
 __global__ __launch_bounds__(1024) void mask_nonzero_kernel(const unsigned char *__restrict__ mask, int n, int cols,
-                                                            long long *__restrict__ idx, int *__restrict__ count) {
+                                                            long long *__restrict__ idx, int *__restrict__ count,
+                                                            int *__restrict__ frame_of,
+                                                            const float *__restrict__ rowsrc, long long rs0,
+                                                            long long rs1, int width, float *__restrict__ rowdst) {
     __shared__ int wtot[16];
     __shared__ int base_s;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -284,8 +289,12 @@ __global__ __launch_bounds__(1024) void mask_nonzero_kernel(const unsigned char 
         int off = base_s;
         for (int w = 0; w < wave; ++w) off += wtot[w];
         if (on) {
-            idx[2 * (size_t)(off + before)] = e / cols;
-            idx[2 * (size_t)(off + before) + 1] = e % cols;
+            const int i = off + before, r = e / cols, c = e - r * cols;
+            idx[2 * (size_t)i] = r;
+            idx[2 * (size_t)i + 1] = c;
+            if (frame_of) frame_of[i] = r;
+            if (rowdst)
+                for (int q = 0; q < width; ++q) rowdst[(size_t)i * width + q] = rowsrc[r * rs0 + c * rs1 + q];
         }
         __syncthreads();  // every wave has read base_s and wtot
         if (tid == 0) {
@@ -374,12 +383,22 @@ extern "C" int fvp_weight_net(const float *features, int Nimg, int H, int W, con
     return (int)hipGetLastError();
 }
 
+extern "C" int fvp_mask_select(const unsigned char *mask, int rows, int cols, long long *idx, int *count,
+                               int *frame_of, const float *rowsrc, long long rs0, long long rs1, int width,
+                               float *rowdst, void *stream);
+
 extern "C" int fvp_mask_nonzero(const unsigned char *mask, int rows, int cols, long long *idx, int *count,
                                 void *stream) {
-    if (!mask || !idx || !count) return FVP_ERR_NULL;
-    if (rows < 0 || cols <= 0 || (long long)rows * cols > (1LL << 24)) return FVP_ERR_SHAPE;
+    return fvp_mask_select(mask, rows, cols, idx, count, nullptr, nullptr, 0, 0, 0, nullptr, stream);
+}
+
+extern "C" int fvp_mask_select(const unsigned char *mask, int rows, int cols, long long *idx, int *count,
+                               int *frame_of, const float *rowsrc, long long rs0, long long rs1, int width,
+                               float *rowdst, void *stream) {
+    if (!mask || !idx || !count || (rowdst && !rowsrc)) return FVP_ERR_NULL;
+    if (rows < 0 || cols <= 0 || (long long)rows * cols > (1LL << 24) || (rowdst && width <= 0)) return FVP_ERR_SHAPE;
     hipLaunchKernelGGL(fvp::mask_nonzero_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, mask, rows * cols, cols,
-                       idx, count);
+                       idx, count, frame_of, rowsrc, rs0, rs1, width, rowdst);
     return (int)hipGetLastError();
 }
 

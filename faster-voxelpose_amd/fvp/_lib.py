@@ -117,6 +117,8 @@ SIGNATURES = {
     "fvp_conv1x1_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                          c_int, c_void_p, c_void_p],
     "fvp_mask_nonzero": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "fvp_mask_select": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
+                        ctypes.c_longlong, c_int, c_void_p, c_void_p],
     "fvp_scatter_poses": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, ctypes.c_longlong, ctypes.c_longlong, c_int, c_void_p],
     "fvp_up2_head_nchw": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,

@@ -83,10 +83,17 @@ def _jln_batch(self, meta, heatmaps, proposal_centers, mask, cameras, resize_tra
     use = opts.cnn and not self.conv_net.training
     conv = cnn.cached(self.conv_net, opts.cnn_dtype) if use else self.conv_net
     wnet = cnn.cached(self.weight_net) if use and not self.weight_net.training else self.weight_net
-    # mask.nonzero() in one launch: the batch's one host sync; the scatters below index with it
-    idx = ops.mask_nonzero(mask) if mask.is_cuda and mask.dim() == 2 and mask.dtype == torch.bool else mask.nonzero()
+    # mask.nonzero(), its frames and the selected proposal rows in one launch: the batch's one host
+    # sync (only views after it); the scatters below index with idx
+    sel = None
+    if (mask.is_cuda and mask.dim() == 2 and mask.dtype == torch.bool and proposal_centers.dtype == torch.float32
+            and proposal_centers.dim() == 3 and proposal_centers.stride(2) == 1):
+        sel = ops.mask_select(mask, proposal_centers)
+        idx = sel[0]
+    else:
+        idx = mask.nonzero()
     planes, offset, _ = self.project_layer.forward_batch(heatmaps, sub_meta, proposal_centers, mask, cameras,
-                                                         resize_transform, idx=idx)
+                                                         resize_transform, idx=idx, sel=sel)
     P = planes.shape[0] // 3
     if P == 0:
         return

@@ -749,6 +749,30 @@ def mask_nonzero(mask: torch.Tensor) -> torch.Tensor:
     return idx[:int(count.item())]
 
 
+def mask_select(mask: torch.Tensor, rows: torch.Tensor) -> tuple:
+    """(idx, frame_of, selected) for a [B, K] bool mask and rows [B, K, W] float32 (last dim
+    contiguous): ``mask.nonzero()``, its frame column as int32 and ``rows[mask]``, all from one
+    launch (fvp_mask_select); the count read is the one host sync, the results are views."""
+    if mask.dim() != 2 or mask.dtype != torch.bool or mask.device.type != "cuda":
+        raise _lib.FvpError(f"fvp: mask_select takes a 2-D bool device tensor, got {tuple(mask.shape)} {mask.dtype}")
+    if (rows.dim() != 3 or tuple(rows.shape[:2]) != tuple(mask.shape) or rows.dtype != torch.float32
+            or rows.stride(2) != 1 or rows.device != mask.device):
+        raise _lib.FvpError(f"fvp: mask_select rows {tuple(rows.shape)} {rows.dtype} for a mask {tuple(mask.shape)}")
+    m = mask.contiguous()
+    B, K = m.shape
+    W = rows.shape[2]
+    idx = torch.empty((B * K, 2), dtype=torch.int64, device=m.device)
+    frame_of = torch.empty((B * K,), dtype=torch.int32, device=m.device)
+    sel = torch.empty((B * K, W), dtype=torch.float32, device=m.device)
+    count = torch.empty((1,), dtype=torch.int32, device=m.device)
+    if B * K == 0:
+        return idx, frame_of, sel
+    _lib.call("fvp_mask_select", _ptr(m), B, K, _ptr(idx), _ptr(count), _ptr(frame_of), _ptr(rows), rows.stride(0),
+              rows.stride(1), W, _ptr(sel), _stream(m))
+    n = int(count.item())
+    return idx[:n], frame_of[:n], sel[:n]
+
+
 def scatter_poses(idx: torch.Tensor, fused: torch.Tensor, pose: torch.Tensor, confs: torch.Tensor,
                   all_fused: torch.Tensor, all_pose: torch.Tensor, centers: torch.Tensor, conf_col: int = 4) -> None:
     """The JLN's result scatters in one launch (fvp_scatter_poses): all_fused[b, k] = fused,

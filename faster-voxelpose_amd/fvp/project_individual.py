@@ -174,19 +174,23 @@ class ProjectLayer(nn.Module):
                                       proposal_centers, None, False, True)
         return planes, offset
 
-    def forward_batch(self, heatmaps, meta, proposal_centers, mask, cameras, resize_transform, idx=None):
+    def forward_batch(self, heatmaps, meta, proposal_centers, mask, cameras, resize_transform, idx=None, sel=None):
         """Every valid proposal of the batch in one launch per sequence (the
         reference loops frames and proposals with host syncs,
         joint_localization_net.py:148-151, project_individual.py:272-275).
         proposal_centers [B,K,7], mask [B,K] bool.  Returns (planes [3P,J,S,S]
         in (frame, proposal) order of ``mask``, offset [P,3], frame_of [P]).
-        idx: ``mask.nonzero()`` if the caller already has it (its one host sync)."""
+        idx: ``mask.nonzero()`` if the caller already has it (its one host sync); sel: the
+        (idx, frame_of int32, proposal_centers[mask]) triple of ops.mask_select instead."""
         ops.forward_only(heatmaps, proposal_centers)
         seqs = list(meta["seq"])[: heatmaps.shape[0]]
-        if idx is None:
-            idx = mask.nonzero()  # one host sync for the whole batch
-        frame_of = idx[:, 0].to(torch.int32)
-        props = proposal_centers[idx[:, 0], idx[:, 1]]
+        if sel is not None:
+            idx, frame_of, props = sel
+        else:
+            if idx is None:
+                idx = mask.nonzero()  # one host sync for the whole batch
+            frame_of = idx[:, 0].to(torch.int32)
+            props = proposal_centers[idx[:, 0], idx[:, 1]]
         uniq = list(dict.fromkeys(seqs))
         if len(uniq) == 1:
             _, planes, offset = self._run(heatmaps, 0, meta, cameras, resize_transform, props, frame_of, False, True)

@@ -304,6 +304,12 @@ int fvp_fuse_poses(const float *pose, const float *weights, const float *maxprob
  * row-major order (the first *count rows are written), count device int
  * (joint_localization_net.py:136-137's boolean selections as indices). */
 int fvp_mask_nonzero(const unsigned char *mask, int rows, int cols, long long *idx, int *count, void *stream);
+/* The same, plus (each optional) frame_of [rows*cols] int32 = the row of each selected entry and
+ * rowdst [rows*cols][width] = rowsrc[row * rs0 + col * rs1 + 0 .. width) (floats): the JLN's
+ * selected frames and proposal rows (joint_localization_net.py:140-151) from the same launch,
+ * so that after its one host sync only views remain. */
+int fvp_mask_select(const unsigned char *mask, int rows, int cols, long long *idx, int *count, int *frame_of,
+                    const float *rowsrc, long long rs0, long long rs1, int width, float *rowdst, void *stream);
 /* The JLN's result scatters (joint_localization_net.py:176-180) in one launch:
  * for p < P with (b, k) = idx[p]: all_fused [B][K][J][3] <- fused [P][J][3],
  * all_pose [3][B][K][J][2] <- pose [3][P][J][2], and (centers non-NULL)

@@ -127,3 +127,21 @@ def test_scatter_poses_matches_index_put(gpu_device):
     rc[mask, 4] = confs
     torch.cuda.synchronize()
     assert torch.equal(af, rf) and torch.equal(ap, rp) and torch.equal(ce, rc)
+
+
+@pytest.mark.gpu
+def test_mask_select_matches_torch(gpu_device):
+    """fvp_mask_select: nonzero, its frame column as int32 and the selected proposal rows (a
+    strided view too) exactly as torch computes them."""
+    from fvp import ops
+
+    g = torch.Generator().manual_seed(11)
+    for B, K, p in ((8, 10, 0.4), (3, 5, 0.0), (2, 700, 0.5)):
+        mask = (torch.rand((B, K), generator=g) < p).to(gpu_device)
+        big = torch.randn((B, K, 9), generator=g).to(gpu_device)
+        rows = big[:, :, 1:8]  # last dim contiguous, rows strided
+        idx, frame_of, sel = ops.mask_select(mask, rows)
+        ref = mask.nonzero()
+        assert torch.equal(idx, ref)
+        assert torch.equal(frame_of, ref[:, 0].to(torch.int32))
+        assert torch.equal(sel, rows[mask])

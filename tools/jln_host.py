@@ -42,8 +42,16 @@ def main():
     grid = layer._seq_grid(hm, 0, meta, cams, rt)
     a = layer._args()
     ws_bytes = _lib.load().fvp_person_workspace_bytes(*hm.shape)
+    sel = ops.mask_select(mask, allp)
+    from fvp.heatmaps import channels_last_of
     pieces = {
         "forward_batch (launch, after the sync)": lambda: layer.forward_batch(hm, meta, allp, mask, cams, rt),
+        "forward_batch(sel=mask_select(...)) (the JLN's path)":
+            lambda: layer.forward_batch(hm, meta, allp, mask, cams, rt, idx=sel[0], sel=sel),
+        "ops.mask_select (incl. its sync)": lambda: ops.mask_select(mask, allp),
+        "ops.forward_only": lambda: ops.forward_only(hm, allp),
+        "channels_last_of": lambda: channels_last_of(hm),
+        "layer._otf": lambda: layer._otf(hm.shape[1]),
         "mask.nonzero()": lambda: mask.nonzero(),
         "frame_of = idx[:,0].to(int32)": lambda: idx[:, 0].to(torch.int32),
         "props = allp[idx[:,0], idx[:,1]]": lambda: allp[idx[:, 0], idx[:, 1]],

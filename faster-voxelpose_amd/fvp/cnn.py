@@ -843,16 +843,22 @@ class FvpCNN:
     def _head_nchw(self, y: Act) -> torch.Tensor:
         """The output 1x1 conv (cnns_2d.py:209) straight into NCHW (fvp_conv1x1_nchw): no
         NHWC output and layout pass.  Other heads / dtypes: the GEMM, then to_nchw."""
-        o = self.out
+        out = self._conv1x1_nchw(y, 0, self.out)
+        return out if out is not None else to_nchw(self.out(y, relu=False))
+
+    @staticmethod
+    def _conv1x1_nchw(y: Act, c0: int, o: "ConvLayer"):
+        """1x1 conv `o` of channels c0 .. c0 + o.Cin - 1 of y, written NCHW by fvp_conv1x1_nchw;
+        None where the kernel does not apply (its float4 reads must stay inside the pixel)."""
         if (o.mode != 0 or (o.KH, o.KW) != (1, 1) or y.t.dtype != torch.float32 or o.bf16 or o.Cout > 64
-                or y.Cp != o.Cpi or o.Cpi % 4 or (o.Cin + 3) // 4 > 16):
-            return to_nchw(o(y, relu=False))
+                or c0 % 4 or o.Cpi % 4 or (o.Cin + 3) // 4 > 16 or not y.t.is_contiguous()):
+            return None
         t4 = 4 if o.Cin <= 16 else 8 if o.Cin <= 32 else 16
-        if 4 * t4 > o.Cpi or o.wpack.shape[1] < 4 * t4:
-            return to_nchw(o(y, relu=False))
+        if c0 + 4 * t4 > y.Cp or o.wpack.shape[1] < 4 * t4 or c0 + o.Cin > y.C:
+            return None
         out = torch.empty((y.N, o.Cout, y.H, y.W), dtype=torch.float32, device=y.t.device)
-        _lib.call("fvp_conv1x1_nchw", _ptr(y.t), y.N, y.H, y.W, y.Cp, o.Cin, _ptr(o.wpack), o.Cpo_w, o.Cout,
-                  _ptr(o.scale), _ptr(o.shift), 0, _ptr(out), _stream(out))
+        _lib.call("fvp_conv1x1_nchw", _ptr(y.t) + 4 * c0, y.N, y.H, y.W, y.Cp, o.Cin, _ptr(o.wpack), o.Cpo_w,
+                  o.Cout, _ptr(o.scale), _ptr(o.shift), 0, _ptr(out), _stream(out))
         return out
 
     def one_launch_for(self, x: torch.Tensor) -> bool:
@@ -894,8 +900,16 @@ class FvpCNN:
         f = self.encdec(self._front(xy))
         if self.heads is None:
             return to_nchw(self._run_seq(self.hm, f)), to_nchw(self._run_seq(self.size, f))
-        c3, c1, n_hm = self.heads  # both heads as one 3x3 and one 1x1 launch
-        y = c1(c3(f, relu=True), relu=False)
+        c3, c1, n_hm = self.heads  # both heads' 3x3 convs as one launch
+        t = c3(f, relu=True)
+        # each head's 1x1 conv on its half of the merged channels, written NCHW (no GEMM
+        # into NHWC and two layout passes)
+        h1, s1 = self.hm[-1][0], self.size[-1][0]
+        hm = self._conv1x1_nchw(t, 0, h1)
+        size = self._conv1x1_nchw(t, h1.Cin, s1) if hm is not None else None
+        if size is not None:
+            return hm, size
+        y = c1(t, relu=False)
         return to_nchw(Act(y.t, n_hm)), to_nchw_from(y, n_hm, y.C - n_hm)
 
 

@@ -43,6 +43,12 @@ CONV_WINO = 6
 WINO_AUTO = os.environ.get("FVP_CONV_WINO", "1") != "0"
 DEFAULT_ALGO = CONV_AUTO if os.environ.get("FVP_F32_DMA", "1") != "0" else CONV_AUTO_NO_DMA
 FVP_CONV_F32_KC = 8
+# fp32 1x1 stride-1 layers with K >= BLAS_1X1_MIN_K input channels and no residual
+# (the ResNet bottleneck's reducing conv1) as one library GEMM with the BN scale
+# folded into the weights and bias + ReLU in its epilogue (torch._addmm_activation:
+# hipBLASLt); FVP_BLAS_1X1=0 keeps them on the fvp kernels (the A/B arm).
+BLAS_1X1 = os.environ.get("FVP_BLAS_1X1", "1") != "0"
+BLAS_1X1_MIN_K = 512
 
 
 _CUS = {}
@@ -178,6 +184,18 @@ class ConvLayer:
         self.shift = torch.zeros(self.Cpo, device=dev)
         self.scale[:cout] = scale
         self.shift[:cout] = shift
+        self.blas_w = None  # [Cout][Cin] weights * BN scale for the library-GEMM 1x1 path
+        if (not self.bf16 and self.mode == 0 and (self.KH, self.KW) == (1, 1) and self.stride == (1, 1)
+                and self.pad == (0, 0) and cin >= BLAS_1X1_MIN_K and cin == self.Cpi and cout == self.Cpo):
+            self.blas_w = (w[:, :, 0, 0] * scale[:, None]).contiguous()
+
+    def _blas(self, x: "Act", relu: bool, res_pre, res_post, out, pool) -> bool:
+        """Whether this call runs as the library GEMM (1x1 fp32 layer built with AUTO, no
+        residual or pooling, fp32 matmul precision "highest" so the result is a plain fp32 GEMM)."""
+        return (BLAS_1X1 and self.blas_w is not None and self.algo == CONV_AUTO and res_pre is None
+                and res_post is None and not pool
+                and x.t.dtype == torch.float32 and x.t.is_contiguous() and out.is_contiguous()
+                and torch.get_float32_matmul_precision() == "highest")
 
     def geom(self) -> tuple:
         return (self.mode, self.stride[0], self.stride[1], self.pad[0], self.pad[1])
@@ -205,6 +223,13 @@ class ConvLayer:
         for r in (res_pre, res_post):
             assert r is None or (tuple(r.t.shape) == tuple(out.shape) and r.t.dtype == odt), \
                 (None if r is None else (r.t.shape, r.t.dtype), out.shape)
+        if self._blas(x, relu, res_pre, res_post, out, pool):
+            a, o = x.t.view(-1, self.Cpi), out.view(-1, self.Cpo)
+            if relu:
+                torch._addmm_activation(self.shift, a, self.blas_w.t(), out=o)
+            else:
+                torch.addmm(self.shift, a, self.blas_w.t(), out=o)
+            return Act(out, self.Cout)
         flags, wp = 0, self.wpack
         if self.bf16:  # FVP_CONV_BF16 | _IN | _OUT (include/fvp.h)
             flags = 1 | (2 if x.t.dtype == torch.bfloat16 else 0) | (4 if odt == torch.bfloat16 else 0)

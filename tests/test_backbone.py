@@ -172,6 +172,31 @@ def test_strided_conv_matches_torch(gpu_device, conv_kernel, cin, cout, k, s, p,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,relu", [(512, 128, True), (1024, 256, True), (2048, 512, False)])
+def test_blas_1x1_matches_torch(gpu_device, cin, cout, relu):
+    """AUTO's library-GEMM path for the Bottleneck's reducing 1x1 (resnet.py:60-62):
+    BN scale folded into the weights, bias (+ ReLU) in the GEMM epilogue."""
+    from fvp import cnn
+
+    torch.manual_seed(cin + cout)
+    conv, bn = nn.Conv2d(cin, cout, 1, bias=False).to(gpu_device).eval(), nn.BatchNorm2d(cout).to(gpu_device).eval()
+    x = torch.randn((3, cin, 10, 14), device=gpu_device)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        ref = bn(conv(x))
+        ref = torch.relu(ref) if relu else ref
+        layer = cnn.ConvLayer(conv, bn)
+        xa = cnn.to_nhwc(x, layer.Cpi)
+        out = torch.empty((3, 10, 14, cout), device=gpu_device)
+        assert layer.blas_w is not None and layer._blas(xa, relu, None, None, out, False) == cnn.BLAS_1X1
+        got = cnn.to_nchw(layer(xa, relu=relu))
+    assert _rel_err(got.cpu().numpy(), ref.cpu().numpy()) <= 2e-5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,hw", [(2048, 256, (3, 4)), (256, 256, (12, 16)), (48, 32, (5, 7))])
 def test_deconv4_matches_torch(gpu_device, conv_kernel, cin, cout, hw):
     """ConvTranspose2d(4, 2, 1) (resnet.py:173-180) as four parity GEMMs."""

@@ -1118,6 +1118,130 @@ __global__ __launch_bounds__(256, 2) void conv_stem7_bf16_kernel(const float *__
     }
 }
 
+// ---- the same stem on the fp32 matrix cores (the default precision) --------
+// 7x7 / s2 / p3, C <= 3 NCHW planes -> 64 channels + BN + ReLU, fp32 NHWC64
+// out.  The generic path converts the images to a 4-channel NHWC pitch first
+// and walks K = 49 taps x 4 channels, a quarter of it the zero channel (1.42 +
+// 0.1 ms per 40 images).  Here K is the 147 real (tap, channel) pairs in the
+// order kk = ky * 21 + kx * 3 + c, padded to 148 = 37 steps of
+// v_mfma_f32_16x16x4f32 with the weights as the A operand: the halo keeps the
+// three planes interleaved ([row][x][c], 207-float rows), so within a kernel
+// row kk - 21 ky is the lane's offset from its pixel (6 j for output column j)
+// and a step whose four kk straddle two rows only adds the row step (186
+// floats) on the lanes past the seam.  Persistent blocks (2 per CU) walk 8 x 32
+// output tiles: the [148][64] weights are staged once per block, and the next
+// tile's halo is loaded into registers during the current tile's MFMAs.  Wave
+// w owns output rows 2w, 2w + 1 x 32 columns (4 pixel tiles) x the 64 channels
+// (4 channel tiles): per step 4 A + 4 B reads for 16 MFMAs.  D[co][pixel]:
+// lane -> pixel, its 4 registers -> 4 consecutive channels, one 16-B store.
+constexpr int kS32TH = 8, kS32TW = 32, kS32HR = 2 * kS32TH + 5, kS32HX = 2 * kS32TW + 5;  // 21 x 69 halo
+constexpr int kS32RP = kS32HX * 3;                           // halo row pitch (floats)
+constexpr int kS32Halo = kS32HR * kS32RP;                    // 4,347 floats
+constexpr int kS32HU = (kS32Halo + 255) / 256;               // halo floats per thread
+constexpr int kS32K = 148, kS32WP = 80;                      // weight rows [kk][co], conflict-free pitch
+constexpr int kS32HaloLds = (kS32Halo + 3) / 4 * 4;
+
+__global__ __launch_bounds__(256, 2) void conv_stem7_f32_kernel(const float *__restrict__ img, int C, int H, int W,
+                                                                 int Ho, int Wo, int tiles_x, int tiles_y,
+                                                                 int ntiles, const float *__restrict__ wpk,
+                                                                 const float *__restrict__ scale,
+                                                                 const float *__restrict__ shift,
+                                                                 float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float lds[kS32HaloLds + kS32K * kS32WP];
+    float *halo = lds, *wl = lds + kS32HaloLds;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int j = lane & 15, g = lane >> 4;
+    const int per_img = tiles_x * tiles_y;
+    for (int e = t; e < kS32K * kS32WP / 4; e += 256)
+        reinterpret_cast<f32x4 *>(wl)[e] = reinterpret_cast<const f32x4 *>(wpk)[e];
+    float hv[kS32HU];
+    auto origin = [&](int tile, int &n, int &oy0, int &ox0) {
+        n = tile / per_img;
+        const int tr = tile - n * per_img, ty = tr / tiles_x;
+        oy0 = ty * kS32TH;
+        ox0 = (tr - ty * tiles_x) * kS32TW;
+    };
+    // halo float e <- plane c = e / (HR * HX), row r, column x (consecutive threads: consecutive x)
+    auto load_halo = [&](int tile) {
+        int n, oy0, ox0;
+        origin(tile, n, oy0, ox0);
+        const float *__restrict__ src = img + (size_t)n * C * H * W;
+#pragma unroll
+        for (int u = 0; u < kS32HU; ++u) {
+            const int e = t + 256 * u;
+            const int c = e / (kS32HR * kS32HX), rem = e - c * (kS32HR * kS32HX);
+            const int r = rem / kS32HX, xx = rem - r * kS32HX;
+            const int y = 2 * oy0 - 3 + r, x = 2 * ox0 - 3 + xx;
+            const bool in = e < kS32Halo && c < C && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+            hv[u] = in ? src[((size_t)c * H + y) * W + x] : 0.0f;
+        }
+    };
+    f32x4 sc[4], sh[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        sc[c] = *reinterpret_cast<const f32x4 *>(scale + 16 * c + 4 * g);
+        sh[c] = *reinterpret_cast<const f32x4 *>(shift + 16 * c + 4 * g);
+    }
+    // the lane's extra row step on a seam step, by the seam's first lane group (1, 2, 3)
+    const int seam1 = g >= 1 ? kS32RP - 21 : 0, seam2 = g >= 2 ? kS32RP - 21 : 0, seam3 = g >= 3 ? kS32RP - 21 : 0;
+    const float *wlane = wl + g * kS32WP + j;
+    const float *hlane = halo + 4 * wave * kS32RP + 6 * j + g;
+    int tile = blockIdx.x;
+    if (tile < ntiles) load_halo(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        __syncthreads();  // every wave is past the previous tile's halo reads (and the weights are stored)
+#pragma unroll
+        for (int u = 0; u < kS32HU; ++u) {
+            const int e = t + 256 * u;
+            if (e < kS32Halo) {
+                const int c = e / (kS32HR * kS32HX), rem = e - c * (kS32HR * kS32HX);
+                halo[rem * 3 + c] = hv[u];  // [row][x][c]: row * 207 + x * 3 + c = rem * 3 + c
+            }
+        }
+        if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);  // in flight during the MFMAs
+        __syncthreads();
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < kS32K / 4; ++s) {
+            const int kk0 = 4 * s, ky0 = kk0 / 21, seam = 21 * (ky0 + 1) - kk0;  // lanes g >= seam: next row
+            const int step = seam == 1 ? seam1 : seam == 2 ? seam2 : seam == 3 ? seam3 : 0;
+            const int boff = kk0 + ky0 * (kS32RP - 21);
+            f32x4 a, b;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[c] = wlane[kk0 * kS32WP + 16 * c];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {  // pixel tile p: output row 2w + (p >> 1), columns 16 (p & 1) ..
+                const float v = hlane[(p >> 1) * 2 * kS32RP + (p & 1) * 96 + boff + step];
+                b[p] = (s == kS32K / 4 - 1 && g == 3) ? 0.0f : v;  // kk = 147: the zero K row
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) acc[c][p] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b[p], acc[c][p], 0, 0, 0);
+        }
+        int n, oy0, ox0;
+        origin(tile, n, oy0, ox0);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int oy = oy0 + 2 * wave + (p >> 1), ox = ox0 + 16 * (p & 1) + j;
+            if (oy < Ho && ox < Wo) {
+                float *o = out + (((size_t)n * Ho + oy) * Wo + ox) * 64 + 4 * g;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    f32x4 v;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v[k] = fmaxf(acc[c][p][k] * sc[c][k] + sh[c][k], 0.0f);
+                    *reinterpret_cast<f32x4 *>(o + 16 * c) = v;
+                }
+            }
+        }
+    }
+}
+
 // ---- the CNNs' 7x7 J -> 16 front conv on bf16 MFMA, from the NCHW maps -------
 // Basic2DBlock(J, 16, 7) of P2PNet / CenterNet (cnns_2d.py:12-29, 185-232,
 // 235-295): 7x7, stride 1, pad 3, C <= 16 input planes -> 16 channels + BN +
@@ -2145,6 +2269,25 @@ extern "C" int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W,
     hipLaunchKernelGGL(fvp::conv_stem7_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, C,
                        H, W, Ho, Wo, tx, ty, ntiles, reinterpret_cast<const __bf16 *>(wpack), scale, shift,
                        reinterpret_cast<__bf16 *>(out));
+    return (int)hipGetLastError();
+}
+
+extern "C" int fvp_conv_stem7_f32(const float *img, int N, int C, int H, int W, const float *wpack, const float *scale,
+                                  const float *shift, float *out, void *stream) {
+    if (!img || !wpack || !scale || !shift || !out) return FVP_ERR_NULL;
+    if (N <= 0 || C < 1 || C > 3 || H < 1 || W < 1) return FVP_ERR_SHAPE;
+    if (((uintptr_t)wpack | (uintptr_t)scale | (uintptr_t)shift | (uintptr_t)out) & 15) return FVP_ERR_SHAPE;
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2*3 - 7) / 2 + 1
+    const int tx = (Wo + fvp::kS32TW - 1) / fvp::kS32TW, ty = (Ho + fvp::kS32TH - 1) / fvp::kS32TH;
+    if ((long long)N * tx * ty > 0x7fffffffLL) return FVP_ERR_SHAPE;
+    const int ntiles = N * tx * ty;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;  // persistent: 2 blocks per CU walk the tiles
+    hipLaunchKernelGGL(fvp::conv_stem7_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, img, C,
+                       H, W, Ho, Wo, tx, ty, ntiles, wpack, scale, shift, out);
     return (int)hipGetLastError();
 }
 

@@ -100,6 +100,7 @@ SIGNATURES = {
     "fvp_conv_front7_f32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_front7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_conv_stem7_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fvp_conv_stem7_f32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fvp_maxpool_pad_nhwc_bf16": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool2_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "fvp_maxpool_nhwc": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
@@ -125,7 +126,7 @@ SIGNATURES = {
                           c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
 }
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 _LIB = None
 
 

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .cnn import Act, ConvLayer, maxpool_pad, to_nchw, to_nhwc
+from .cnn import CONV_AUTO, Act, ConvLayer, maxpool_pad, to_nchw, to_nhwc
 from .ops import _ptr, _stream
 from .heatmaps import ChannelsLastHeatmaps
 
@@ -89,13 +89,18 @@ class FvpPoseResNet:
         # bf16: the 7x7/s2/p3 -> 64 stem runs its own kernel straight from the
         # NCHW images (fvp_conv_stem7_bf16), weights packed [64][7][8][4]
         c1 = module.conv1
-        self.stem7 = None
-        if (dtype == torch.bfloat16 and tuple(c1.kernel_size) == (7, 7) and tuple(c1.stride) == (2, 2)
-                and tuple(c1.padding) == (3, 3) and c1.out_channels == 64 and c1.groups == 1
-                and tuple(c1.dilation) == (1, 1)):
+        self.stem7 = self.stem7_f32 = None
+        stem7 = (tuple(c1.kernel_size) == (7, 7) and tuple(c1.stride) == (2, 2) and tuple(c1.padding) == (3, 3)
+                 and c1.out_channels == 64 and c1.groups == 1 and tuple(c1.dilation) == (1, 1))
+        if stem7 and dtype == torch.bfloat16:
             w = torch.zeros((64, 7, 8, 4), dtype=torch.float32, device=c1.weight.device)
             w[:, :, :7, :c1.in_channels] = c1.weight.detach().float().permute(0, 2, 3, 1)
             self.stem7 = w.reshape(64, 224).to(torch.bfloat16).contiguous()
+        elif stem7 and c1.in_channels <= 3 and (algo is None or algo == CONV_AUTO):
+            # fp32 (fvp_conv_stem7_f32): row kk = 21 ky + 3 kx + c of [148][80], column co
+            w = torch.zeros((7, 7, 3, 80), dtype=torch.float32, device=c1.weight.device)
+            w[:, :, :c1.in_channels, :64] = c1.weight.detach().float().permute(2, 3, 1, 0)
+            self.stem7_f32 = torch.cat([w.reshape(147, 80), w.new_zeros((1, 80))]).contiguous()
         mp = module.maxpool
         k, s, p = (mp.kernel_size, mp.stride, mp.padding)
         k, s, p = (v if isinstance(v, int) else v[0] for v in (k, s, p))
@@ -136,6 +141,8 @@ class FvpPoseResNet:
             raise _lib.FvpError(f"fvp: images must be on a HIP device, got {images.device}")
         if self.stem7 is not None:
             x = self._stem7(images)
+        elif self.stem7_f32 is not None:
+            x = self._stem7_f32(images)
         else:
             x = self.stem(to_nhwc(images, RGB_PITCH), relu=True)
         x = maxpool_pad(x, *self.pool)
@@ -150,6 +157,14 @@ class FvpPoseResNet:
         N, C, H, W = x.shape
         out = torch.empty((N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64), dtype=torch.bfloat16, device=x.device)
         _lib.call("fvp_conv_stem7_bf16", _ptr(x), N, C, H, W, _ptr(self.stem7), _ptr(self.stem.scale),
+                  _ptr(self.stem.shift), _ptr(out), _stream(out))
+        return Act(out, 64)
+
+    def _stem7_f32(self, images: torch.Tensor) -> Act:
+        x = images.float().contiguous()
+        N, C, H, W = x.shape
+        out = torch.empty((N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64), device=x.device)
+        _lib.call("fvp_conv_stem7_f32", _ptr(x), N, C, H, W, _ptr(self.stem7_f32), _ptr(self.stem.scale),
                   _ptr(self.stem.shift), _ptr(out), _stream(out))
         return Act(out, 64)
 

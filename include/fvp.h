@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define FVP_ABI_VERSION 21
+#define FVP_ABI_VERSION 22
 /* Joints per heatmap set: the voxelize and person kernels run up to 32 joints
  * per pass (one channels-last pixel of 32 floats per tap) and more in joint
  * slices of 32. */
@@ -496,6 +496,15 @@ int fvp_maxpool_pad_nhwc(const float *in, int N, int H, int W, int C, int K, int
  * (bf16 operands, fp32 accumulation). */
 int fvp_conv_stem7_bf16(const float *img, int N, int C, int H, int W, const void *wpack, const float *scale,
                         const float *shift, void *out, void *stream);
+/* The same stem on the fp32 matrix cores (exact fp32 products, fp32 sums; the
+ * default precision), C <= 3 NCHW fp32 images -> fp32 NHWC [N][Ho][Wo][64]:
+ * K = the 147 (tap, channel) pairs kk = 21 ky + 3 kx + c plus one zero row.
+ * wpack: fp32 [148][80] = W[co][c][ky][kx] at (kk, co), zero for co >= 64,
+ * c >= C and kk = 147; scale / shift: fp32 [64] (BN folded).  wpack, scale,
+ * shift and out 16-B aligned.  Replaces the NHWC conversion + the generic
+ * 4-channel-pitch conv of resnet.py:105-107 (fvp/backbone.py). */
+int fvp_conv_stem7_f32(const float *img, int N, int C, int H, int W, const float *wpack, const float *scale,
+                       const float *shift, float *out, void *stream);
 /* The CNNs' front Basic2DBlock (cnns_2d.py: 7x7, stride 1, pad 3, C <= 16
  * planes -> 16 channels) + BN + ReLU on bf16 MFMA, straight from the NCHW
  * fp32 maps [N][C][H][W] to bf16 NHWC [N][H][W][16].  wpack: bf16

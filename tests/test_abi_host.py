@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), "ctypes table out of sync with include/fvp.h"
-    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 21
+    assert lib.fvp_abi_version() == _lib.ABI_VERSION == 22
     assert lib.fvp_status_string(0) == b"success"
 
 

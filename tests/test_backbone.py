@@ -77,6 +77,9 @@ def test_conv_geometry_host():
     assert lib.fvp_conv_stem7_bf16(1, 1, 5, 64, 64, 1, 1, 1, 1, None) == 1002      # > 4 input channels
     assert lib.fvp_conv_stem7_bf16(1, 0, 3, 64, 64, 1, 1, 1, 1, None) == 1002      # N = 0
     assert lib.fvp_conv_stem7_bf16(None, 1, 3, 64, 64, 1, 1, 1, 1, None) == 1001
+    assert lib.fvp_conv_stem7_f32(16, 1, 4, 64, 64, 16, 16, 16, 16, None) == 1002   # > 3 input channels (fp32)
+    assert lib.fvp_conv_stem7_f32(16, 1, 3, 64, 64, 16, 16, 16, 20, None) == 1002   # out not 16-B aligned
+    assert lib.fvp_conv_stem7_f32(None, 1, 3, 64, 64, 16, 16, 16, 16, None) == 1001
     assert lib.fvp_conv_front7_bf16(1, 1, 17, 64, 64, 1, 1, 1, 1, None) == 1002     # > 16 input planes
     assert lib.fvp_conv_front7_bf16(None, 1, 15, 64, 64, 1, 1, 1, 1, None) == 1001
     assert lib.fvp_conv_front7_f32(1, 1, 17, 64, 64, 1, 1, 1, 1, None) == 1002
@@ -287,6 +290,37 @@ def test_stem7_bf16_vs_torch(gpu_device, cin, hw):
     assert got.shape == ref.shape
     err = float((got - ref).abs().max()) / float(ref.abs().max())
     assert err <= 2e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,hw", [(3, (512, 960)), (3, (37, 70)), (2, (21, 33)), (1, (64, 100))])
+def test_stem7_f32_vs_torch(gpu_device, cin, hw):
+    """fvp_conv_stem7_f32 (the fp32 backbone's 7x7/s2/p3 -> 64 + BN + ReLU from
+    NCHW images, K = the 147 real (tap, channel) pairs): within 2e-5 of the
+    output scale of torch's fp32 conv, ragged tiles included; an Inf pixel
+    reaches no output outside the windows that hold it (the padded K row reads
+    no image data)."""
+    import cnn_arch
+    from fvp import synthetic
+    from fvp.backbone import FvpPoseResNet
+
+    m = cnn_arch.PoseResNet(18, 15).eval()
+    m.conv1 = nn.Conv2d(cin, 64, 7, 2, 3, bias=False)
+    m.load_state_dict(synthetic.seeded_state_dict(m, 5 + cin))
+    m = m.to(gpu_device)
+    bb = FvpPoseResNet(m)
+    assert bb.stem7_f32 is not None
+    x = torch.rand((2, cin) + hw, generator=torch.Generator().manual_seed(cin)).to(gpu_device)
+    if hw == (37, 70):
+        x[1, cin - 1, 20, 41] = float("inf")
+    got = bb._stem7_f32(x).t.permute(0, 3, 1, 2).cpu()
+    with torch.no_grad():  # on the CPU: MIOpen's conv spreads an Inf beyond the windows that hold it
+        ref = torch.relu(m.bn1.cpu()(m.conv1.cpu()(x.cpu())))
+    assert got.shape == ref.shape
+    fin = torch.isfinite(ref)
+    assert int((~fin).sum()) <= 4 * 4 * 64  # only the windows over the Inf pixel
+    err = float((got - ref)[fin].abs().max()) / float(ref[fin].abs().max())
+    assert err <= 2e-5, err
 
 
 @pytest.mark.gpu

@@ -212,14 +212,15 @@ def test_deconv4_matches_torch(gpu_device, conv_kernel, cin, cout, hw):
 
 
 @pytest.mark.gpu
-def test_maxpool_pad_matches_torch(gpu_device):
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (3, 1, 1), (2, 2, 0)])  # (3, 2, 1): the stem's 32-bit kernel
+def test_maxpool_pad_matches_torch(gpu_device, k, s, p):
     from fvp.cnn import maxpool_pad, to_nchw, to_nhwc
 
     x = torch.randn((2, 64, 35, 45), device=gpu_device)
     x[0, 3, 0, 0] = float("nan")
     x[1, 5] = -float("inf")
-    got = to_nchw(maxpool_pad(to_nhwc(x), 3, 2, 1))
-    ref = F.max_pool2d(x, 3, 2, 1)
+    got = to_nchw(maxpool_pad(to_nhwc(x), k, s, p))
+    ref = F.max_pool2d(x, k, s, p)
     torch.cuda.synchronize()
     assert got.shape == ref.shape
     assert torch.equal(torch.nan_to_num(got, 7.0), torch.nan_to_num(ref, 7.0))

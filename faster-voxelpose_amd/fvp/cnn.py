@@ -43,12 +43,15 @@ CONV_WINO = 6
 WINO_AUTO = os.environ.get("FVP_CONV_WINO", "1") != "0"
 DEFAULT_ALGO = CONV_AUTO if os.environ.get("FVP_F32_DMA", "1") != "0" else CONV_AUTO_NO_DMA
 FVP_CONV_F32_KC = 8
-# fp32 1x1 stride-1 layers with K >= BLAS_1X1_MIN_K input channels and no residual
-# (the ResNet bottleneck's reducing conv1) as one library GEMM with the BN scale
-# folded into the weights and bias + ReLU in its epilogue (torch._addmm_activation:
-# hipBLASLt); FVP_BLAS_1X1=0 keeps them on the fvp kernels (the A/B arm).
+# fp32 1x1 stride-1 layers without a residual as one library GEMM with the BN scale
+# folded into the weights and bias (+ ReLU) in its epilogue (torch._addmm_activation:
+# hipBLASLt) where that measured faster (tools/gemm_probe.py, tools/thin_gemm_probe.py):
+# K >= BLAS_1X1_MIN_K input channels (the ResNet Bottleneck's reducing conv1), or
+# K >= 64 on launches of >= BLAS_1X1_MIN_M pixels (the first stage at 40 x 128 x 240:
+# 64 -> 256 downsample 0.62 -> 0.50 ms, 256 -> 64 0.43 -> 0.39); FVP_BLAS_1X1=0 keeps
+# them on the fvp kernels (the A/B arm).
 BLAS_1X1 = os.environ.get("FVP_BLAS_1X1", "1") != "0"
-BLAS_1X1_MIN_K = 512
+BLAS_1X1_MIN_K, BLAS_1X1_MIN_M = 512, 1 << 20
 
 
 _CUS = {}
@@ -186,7 +189,7 @@ class ConvLayer:
         self.shift[:cout] = shift
         self.blas_w = None  # [Cout][Cin] weights * BN scale for the library-GEMM 1x1 path
         if (not self.bf16 and self.mode == 0 and (self.KH, self.KW) == (1, 1) and self.stride == (1, 1)
-                and self.pad == (0, 0) and cin >= BLAS_1X1_MIN_K and cin == self.Cpi and cout == self.Cpo):
+                and self.pad == (0, 0) and cin >= 64 and cin == self.Cpi and cout == self.Cpo):
             self.blas_w = (w[:, :, 0, 0] * scale[:, None]).contiguous()
 
     def _blas(self, x: "Act", relu: bool, res_pre, res_post, out, pool) -> bool:
@@ -194,6 +197,7 @@ class ConvLayer:
         residual or pooling, fp32 matmul precision "highest" so the result is a plain fp32 GEMM)."""
         return (BLAS_1X1 and self.blas_w is not None and self.algo == CONV_AUTO and res_pre is None
                 and res_post is None and not pool
+                and (self.Cpi >= BLAS_1X1_MIN_K or x.N * x.H * x.W >= BLAS_1X1_MIN_M)
                 and x.t.dtype == torch.float32 and x.t.is_contiguous() and out.is_contiguous()
                 and torch.get_float32_matmul_precision() == "highest")
 

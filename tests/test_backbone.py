@@ -175,15 +175,19 @@ def test_strided_conv_matches_torch(gpu_device, conv_kernel, cin, cout, k, s, p,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cin,cout,relu", [(512, 128, True), (1024, 256, True), (2048, 512, False)])
-def test_blas_1x1_matches_torch(gpu_device, cin, cout, relu):
-    """AUTO's library-GEMM path for the Bottleneck's reducing 1x1 (resnet.py:60-62):
-    BN scale folded into the weights, bias (+ ReLU) in the GEMM epilogue."""
+@pytest.mark.parametrize("cin,cout,relu,nhw", [(512, 128, True, (3, 10, 14)), (1024, 256, True, (3, 10, 14)),
+                                               (2048, 512, False, (3, 10, 14)), (64, 256, False, (1, 1024, 1024)),
+                                               (256, 64, True, (2, 512, 1024))])
+def test_blas_1x1_matches_torch(gpu_device, cin, cout, relu, nhw):
+    """AUTO's library-GEMM path for the 1x1 layers without a residual (resnet.py:60-62
+    reducing conv1, :132-137 the first stage's downsample): BN scale folded into the
+    weights, bias (+ ReLU) in the GEMM epilogue; K >= 512, or >= 2^20 pixels."""
     from fvp import cnn
 
     torch.manual_seed(cin + cout)
     conv, bn = nn.Conv2d(cin, cout, 1, bias=False).to(gpu_device).eval(), nn.BatchNorm2d(cout).to(gpu_device).eval()
-    x = torch.randn((3, cin, 10, 14), device=gpu_device)
+    n, h, w = nhw
+    x = torch.randn((n, cin, h, w), device=gpu_device)
     with torch.no_grad():
         bn.running_mean.uniform_(-0.2, 0.2)
         bn.running_var.uniform_(0.5, 1.5)
@@ -193,7 +197,7 @@ def test_blas_1x1_matches_torch(gpu_device, cin, cout, relu):
         ref = torch.relu(ref) if relu else ref
         layer = cnn.ConvLayer(conv, bn)
         xa = cnn.to_nhwc(x, layer.Cpi)
-        out = torch.empty((3, 10, 14, cout), device=gpu_device)
+        out = torch.empty((n, h, w, cout), device=gpu_device)
         assert layer.blas_w is not None and layer._blas(xa, relu, None, None, out, False) == cnn.BLAS_1X1
         got = cnn.to_nchw(layer(xa, relu=relu))
     assert _rel_err(got.cpu().numpy(), ref.cpu().numpy()) <= 2e-5

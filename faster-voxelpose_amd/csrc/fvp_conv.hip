@@ -2009,8 +2009,12 @@ static int conv_launch(const float *in, int N, int H, int W, int Cpi, const void
     auto dma = [&](auto f32) {
         constexpr bool F = decltype(f32)::value;
         constexpr int E = F ? 4 : 2;
-        // 32-column tiles (4 waves of 32 x 32) for the <= 32-channel layers, 128-B rows only
-        const int BN = Ntot > 64 ? 128 : (Ntot > 32 || Cpi * E % 128) ? 64 : 32;
+        // 32-column tiles (4 waves of 32 x 32) for the <= 32-channel layers, 128-B rows only.
+        // fp32 takes 64-column tiles where bf16 takes 128: 4 waves and 48 KB of LDS per
+        // block, 3 blocks per CU instead of 2 of 8 waves -- PoseResNet-50 fp32 layers
+        // 31.02 -> 30.53 ms (3x3/s2 512->512 at 32 x 60: 0.85 -> 0.73 ms, the 1x1
+        // expand layers 3-7 %; profiles/round6/dma_bn64/)
+        const int BN = Ntot > 64 ? (F ? 64 : 128) : (Ntot > 32 || Cpi * E % 128) ? 64 : 32;
         const dim3 gr((unsigned)((M + 127) / 128), (unsigned)((Ntot + BN - 1) / BN), (unsigned)G);
         if (BN == 32) {
             hipLaunchKernelGGL((fvp::conv_dma_kernel<32, 128 / E, 4, F>), gr, dim3(256), 0, st, a, wpack);

@@ -298,6 +298,9 @@ class ConvLayer:
                 # mostly empty stays on the halo kernel (3x3 512->512 at 16x30: 600
                 # blocks on 512 slots, 0.83 vs 0.89 ms; P2PNet's 3x3 128->128 at 16x16,
                 # 480 blocks: DMA 0.175 vs 0.191 ms)
+                # (the rule was measured with 128-column tiles above 64 columns; the fp32
+                # kernel now runs 64-column tiles there, 3 blocks per CU -- faster on every
+                # layer it kept, so the same choices stand)
                 ncols = self.nq * self.Cpo
                 bn = 128 if ncols > 64 else 64
                 blocks = -(-M // 128) * -(-ncols // bn) * self.G
